@@ -1,0 +1,163 @@
+/*
+ * pacmann.h — C ABI of libpacmann.so, the MI355X (gfx950) implementation of
+ * Pacmann's two data-parallel inner loops (wuwuz/Pacmann):
+ *
+ *   1. PianoPIR: AES-128-MMO PRF set expansion + 64-bit XOR database fold
+ *      (client hint preprocessing, server answer, online hint search and
+ *      refresh, 16-way batch PIR), bit-exact with the pianopir Go code + aes_amd64.s.
+ *   2. graphann: batched L2 / uint32 inner-product distance evaluation that
+ *      drives the degree-m beam search, bit-exact with l2_distance_amd64.s.
+ *
+ * The entry points replace the reference's Go package surfaces at method /
+ * batch granularity (never per PRF or per 640-B XOR: a launch per leaf would
+ * cost more than the Go assembly it replaces).  Each function cites the
+ * reference interface it stands in for.  All pointers are HOST pointers;
+ * device memory is owned by the library behind opaque handles.  Input host
+ * buffers are copied and never retained; output buffers are caller-allocated.
+ * Every function returns 0 on success or a negative PM_E* code; the message
+ * is in pm_last_error() (thread-local).  The library never aborts the process
+ * (the reference's log.Fatalf paths return PM_EINVAL instead).
+ *
+ * Threading: one handle per host thread; handles are not thread-safe (the
+ * reference's PianoPIRClient is not either, pir.go:91-121).
+ */
+#ifndef PACMANN_H
+#define PACMANN_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PM_OK 0
+#define PM_EINVAL -1   /* bad argument / reference log.Fatalf condition   */
+#define PM_EHIP -2     /* HIP runtime error                              */
+#define PM_ENOMEM -3   /* device allocation failed                       */
+
+/* Per-sub-query status codes (pianopir/pir.go:354-471 error returns). */
+#define PM_Q_OK 0          /* answered through PIR                             */
+#define PM_Q_EBUDGET 1     /* "exceed the maximum number of queries" :386-391  */
+#define PM_Q_ECHUNK 2      /* "too many queries in chunk" :396-400             */
+#define PM_Q_ENOHIT 3      /* "no hit hint in the primary hint table" :416-419 */
+#define PM_Q_ERANGE 4      /* idx out of range (:373-378 log.Fatalf)           */
+
+typedef struct pm_ctx pm_ctx;
+typedef struct pm_pir pm_pir;           /* PianoPIR             (pir.go:473-477)       */
+typedef struct pm_batchpir pm_batchpir; /* SimpleBatchPianoPIR  (batch-pir.go:40-53)   */
+typedef struct pm_graph pm_graph;       /* GraphANNFrontend + PIRGraphInfo / BasicGraphInfo */
+
+/* ---- context ----------------------------------------------------------- */
+int         pm_ctx_create(int device, pm_ctx** out);
+void        pm_ctx_destroy(pm_ctx* ctx);
+const char* pm_last_error(void);
+int         pm_ctx_sync(pm_ctx* ctx);
+/* Per-kernel timing with HIP events recorded on the stream each kernel runs
+ * on.  Names: "prep_offsets", "prep_fold", "prep_repl", "hint_match",
+ * "resolve", "answer", "decode", "l2_rows", "ip_scan", "prf". */
+int pm_timing_enable(pm_ctx* ctx, int on);
+int pm_timing_reset(pm_ctx* ctx);
+int pm_timing_get(pm_ctx* ctx, const char* kernel, uint64_t* launches, double* total_ms,
+                  double* alg_bytes);
+
+/* ---- leaf primitives, batched ----------------------------------------- */
+/* expandKeyAsm (pianopir/aes_amd64.s:87-126): FIPS-197 AES-128 key schedule. */
+int pm_expand_key(const uint8_t key[16], uint32_t round_keys[44]);
+/* PRFEvalWithLongKeyAndTag (pianopir/util.go:157-165) over n (tag, x) pairs on
+ * the GPU: out[i] = low64_LE(AES_k(B) ^ B), B = LE64((tag<<35)+x) || 0^8. */
+int pm_prf_batch(pm_ctx* ctx, const uint32_t round_keys[44], const uint64_t* tags,
+                 const uint64_t* xs, uint64_t n, uint64_t* out);
+/* L2Dist (graphann/build_graph.go:119-127 -> l2_distance_amd64.s:4-36) of one
+ * query against nrows rows (row-major nrows x dim), bit-exact. */
+int pm_l2_batch(pm_ctx* ctx, const float* query, const float* rows, uint64_t nrows,
+                uint64_t dim, float* out);
+/* InnerProduct (l2_distance_amd64.s:39-68) of one query against nrows rows:
+ * per-row uint32 dot products mod 2^32 (per_row may be NULL) and their
+ * wrapping sum. */
+int pm_ip_batch(pm_ctx* ctx, const uint32_t* query, const uint32_t* rows, uint64_t nrows,
+                uint64_t dim, uint32_t* per_row, uint32_t* sum);
+/* TestInnerProduct scan (graphann/graphann_test.go:249-283) fully on device:
+ * fills vectors[i*D+j] = i+j in HBM, query[j] = j, then sums the N row dot
+ * products mod 2^32.  scan_ms = device time of the scan kernel alone. */
+int pm_ip_bench(pm_ctx* ctx, uint64_t N, uint64_t D, uint32_t* sum, double* scan_ms);
+
+/* ---- PianoPIR (pianopir/pir.go) --------------------------------------- */
+typedef struct {
+  uint64_t DBEntryByteNum, DBEntrySize, DBSize, ChunkSize, SetSize, ThreadNum, FailureProbLog2;
+  uint64_t MaxQueryNum, PrimaryHintNum, MaxQueryPerChunk, FinishedQueryNum;
+} pm_pir_config;
+
+/* NewPianoPIR(DBSize, DBEntryByteNum, rawDB, FailureProbLog2) (pir.go:479-514).
+ * seed drives the key / replacement / dummy streams that the
+ * reference draws from time-seeded math/rand (pir.go:132,208,305,366). */
+int    pm_pir_create(pm_ctx* ctx, uint64_t DBSize, uint64_t DBEntryByteNum, const uint64_t* rawDB,
+                     uint64_t FailureProbLog2, uint64_t seed, pm_pir** out);
+void   pm_pir_destroy(pm_pir* h);
+int    pm_pir_preprocessing(pm_pir* h);          /* PianoPIR.Preprocessing      pir.go:516-518 */
+int    pm_pir_dummy_preprocessing(pm_pir* h);    /* PianoPIR.DummyPreprocessing pir.go:520-523 */
+/* PianoPIR.Query(idx, realQuery) (pir.go:525-533); *status = PM_Q_* */
+int    pm_pir_query(pm_pir* h, uint64_t idx, int real, uint64_t* out, int* status);
+int    pm_pir_config_get(pm_pir* h, pm_pir_config* cfg);   /* PianoPIR.Config  pir.go:546-548 */
+double pm_pir_local_storage(pm_pir* h);                    /* LocalStorageSize pir.go:178-190 */
+double pm_pir_comm_per_query(pm_pir* h);                   /* CommCostPerQuery pir.go:539-544 */
+/* PianoPIRServer.PrivateQuery (pir.go:65-88), batched: nq offset sets of
+ * SetSize uint32 each -> nq entries of DBEntrySize words. */
+int    pm_pir_server_answer(pm_pir* h, const uint32_t* offsets, uint64_t nq, uint64_t* out);
+
+/* ---- SimpleBatchPianoPIR (pianopir/batch-pir.go) ---------------------- */
+typedef struct {
+  uint64_t DBEntryByteNum, DBEntrySize, DBSize, BatchSize, PartitionNum, PartitionSize,
+           ThreadNum, FailureProbLog2;
+  uint64_t FinishedBatchNum, QueriesMadeInPartition, SupportBatchNum, PrepCount;
+  double   LocalStorage, PreprocessingTime, CommOnline, CommOffline;
+} pm_batchpir_stats;
+
+/* NewSimpleBatchPianoPIR (batch-pir.go:55-93) */
+int  pm_batchpir_create(pm_ctx* ctx, uint64_t DBSize, uint64_t DBEntryByteNum, uint64_t BatchSize,
+                        const uint64_t* rawDB, uint64_t FailureProbLog2, uint64_t seed,
+                        pm_batchpir** out);
+void pm_batchpir_destroy(pm_batchpir* h);
+int  pm_batchpir_preprocessing(pm_batchpir* h);         /* batch-pir.go:119-155 */
+int  pm_batchpir_dummy_preprocessing(pm_batchpir* h);   /* batch-pir.go:157-166 */
+/* Query (batch-pir.go:170-248): out = n x DBEntrySize words; dropped or failed
+ * ids get an all-zero entry exactly like the reference. */
+int  pm_batchpir_query(pm_batchpir* h, const uint64_t* ids, uint64_t n, uint64_t* out);
+int  pm_batchpir_stats_get(pm_batchpir* h, pm_batchpir_stats* s);
+int  pm_batchpir_subconfig(pm_batchpir* h, uint64_t partition, pm_pir_config* cfg);
+
+/* State export of one partition's client (test hook; sizes from the config):
+ * round_keys[44], primary_tag[PH], primary_parity[PH*E], primary_pp[PH],
+ * backup_tag[SS*Qpc], backup_parity[SS*Qpc*E], repl_idx[SS*Qpc],
+ * repl_val[SS*Qpc*E], hist[SS].  Any pointer may be NULL. */
+int pm_pir_export(pm_pir* h, uint32_t* round_keys, uint64_t* primary_tag, uint64_t* primary_parity,
+                  uint64_t* primary_pp, uint64_t* backup_tag, uint64_t* backup_parity,
+                  uint64_t* repl_idx, uint64_t* repl_val, uint64_t* hist);
+int pm_batchpir_export(pm_batchpir* h, uint64_t partition, uint32_t* round_keys,
+                       uint64_t* primary_tag, uint64_t* primary_parity, uint64_t* primary_pp,
+                       uint64_t* backup_tag, uint64_t* backup_parity, uint64_t* repl_idx,
+                       uint64_t* repl_val, uint64_t* hist);
+
+/* ---- graphann (graphann/search.go) over PIRGraphInfo (private-search.go) */
+/* PIRGraphInfo{N,Dim,M,graph,vectors,skipPrep,NonPrivateMode} (private-search.go:336-353)
+ * wrapped in a GraphANNFrontend (search.go:69-72).  vectors: n x dim f32,
+ * graph: n x m uint32.  nonprivate=1 gives BasicGraphInfo-style direct access
+ * (private-search.go:445-455).  search_seed drives the host id stream that the
+ * reference draws from global math/rand. */
+int  pm_graph_create(pm_ctx* ctx, uint64_t n, uint64_t dim, uint64_t m, const float* vectors,
+                     const uint32_t* graph, int nonprivate, int skip_prep, uint64_t pir_seed,
+                     uint64_t search_seed, pm_graph** out);
+void pm_graph_destroy(pm_graph* g);
+int  pm_graph_preprocess(pm_graph* g);   /* GraphANNFrontend.Preprocess  search.go:74-81 */
+/* GraphANNFrontend.SearchKNN (search.go:114-234); ids/steps: k entries, -1 padded */
+int  pm_search_knn(pm_graph* g, const float* query, int k, int max_step, int parallel,
+                   int benchmarking, int64_t* ids, int64_t* steps);
+/* private-search.go:216-240 query loop incl. the maintenance trigger (:226-232) */
+int  pm_search_loop(pm_graph* g, const float* queries, uint64_t q, int k, int step, int parallel,
+                    int benchmarking, int64_t* answers, double* online_s, double* maintenance_s);
+int  pm_graph_counts(pm_graph* g, uint64_t* total_queries, uint64_t* succ_queries);
+pm_batchpir* pm_graph_pir(pm_graph* g);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PACMANN_H */

@@ -1,0 +1,464 @@
+"""pacmann_amd — MI355X-native PianoPIR + graphann hot path (libpacmann.so).
+
+Python mirror of the reference's Go package surfaces, bound through the C ABI
+in include/pacmann.h.  Names, argument meaning and error behaviour follow the
+reference so that tests read like pianopir/pir_test.go:
+
+    pir = SimpleBatchPianoPIR(DBSize, DBEntryByteNum, BatchSize, rawDB, FailureProbLog2)
+    pir.Preprocessing()
+    responses, err = pir.Query(batch)
+
+There is no CPU fallback: constructing any handle without a built
+libpacmann.so or without a HIP device raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+import numpy as np
+
+__all__ = [
+    "Context", "PianoPIR", "SimpleBatchPianoPIR", "PIRGraphInfo", "GraphANNFrontend",
+    "lib", "expand_key", "prf_batch", "l2_batch", "ip_batch", "ip_bench", "LIB_PATH",
+    "QueryError",
+]
+
+LIB_PATH = Path(__file__).resolve().parent / "libpacmann.so"
+_lib = None
+
+u8p = C.POINTER(C.c_uint8)
+u32p = C.POINTER(C.c_uint32)
+u64p = C.POINTER(C.c_uint64)
+i64p = C.POINTER(C.c_int64)
+f32p = C.POINTER(C.c_float)
+vp = C.c_void_p
+u64 = C.c_uint64
+dbl = C.c_double
+
+
+class PirConfig(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in (
+        "DBEntryByteNum DBEntrySize DBSize ChunkSize SetSize ThreadNum FailureProbLog2 "
+        "MaxQueryNum PrimaryHintNum MaxQueryPerChunk FinishedQueryNum").split()]
+
+    def asdict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+class BatchStats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in (
+        "DBEntryByteNum DBEntrySize DBSize BatchSize PartitionNum PartitionSize ThreadNum "
+        "FailureProbLog2 FinishedBatchNum QueriesMadeInPartition SupportBatchNum PrepCount").split()] + \
+        [(n, C.c_double) for n in "LocalStorage PreprocessingTime CommOnline CommOffline".split()]
+
+    def asdict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+# name -> (restype, argtypes) ; every exported symbol of include/pacmann.h
+SIGNATURES = {
+    "pm_ctx_create": (C.c_int, [C.c_int, C.POINTER(vp)]),
+    "pm_ctx_destroy": (None, [vp]),
+    "pm_last_error": (C.c_char_p, []),
+    "pm_ctx_sync": (C.c_int, [vp]),
+    "pm_timing_enable": (C.c_int, [vp, C.c_int]),
+    "pm_timing_reset": (C.c_int, [vp]),
+    "pm_timing_get": (C.c_int, [vp, C.c_char_p, u64p, C.POINTER(dbl), C.POINTER(dbl)]),
+    "pm_expand_key": (C.c_int, [u8p, u32p]),
+    "pm_prf_batch": (C.c_int, [vp, u32p, u64p, u64p, u64, u64p]),
+    "pm_l2_batch": (C.c_int, [vp, f32p, f32p, u64, u64, f32p]),
+    "pm_ip_batch": (C.c_int, [vp, u32p, u32p, u64, u64, u32p, u32p]),
+    "pm_ip_bench": (C.c_int, [vp, u64, u64, u32p, C.POINTER(dbl)]),
+    "pm_pir_create": (C.c_int, [vp, u64, u64, u64p, u64, u64, C.POINTER(vp)]),
+    "pm_pir_destroy": (None, [vp]),
+    "pm_pir_preprocessing": (C.c_int, [vp]),
+    "pm_pir_dummy_preprocessing": (C.c_int, [vp]),
+    "pm_pir_query": (C.c_int, [vp, u64, C.c_int, u64p, C.POINTER(C.c_int)]),
+    "pm_pir_config_get": (C.c_int, [vp, C.POINTER(PirConfig)]),
+    "pm_pir_local_storage": (C.c_double, [vp]),
+    "pm_pir_comm_per_query": (C.c_double, [vp]),
+    "pm_pir_server_answer": (C.c_int, [vp, u32p, u64, u64p]),
+    "pm_batchpir_create": (C.c_int, [vp, u64, u64, u64, u64p, u64, u64, C.POINTER(vp)]),
+    "pm_batchpir_destroy": (None, [vp]),
+    "pm_batchpir_preprocessing": (C.c_int, [vp]),
+    "pm_batchpir_dummy_preprocessing": (C.c_int, [vp]),
+    "pm_batchpir_query": (C.c_int, [vp, u64p, u64, u64p]),
+    "pm_batchpir_stats_get": (C.c_int, [vp, C.POINTER(BatchStats)]),
+    "pm_batchpir_subconfig": (C.c_int, [vp, u64, C.POINTER(PirConfig)]),
+    "pm_pir_export": (C.c_int, [vp, u32p, u64p, u64p, u64p, u64p, u64p, u64p, u64p, u64p]),
+    "pm_batchpir_export": (C.c_int, [vp, u64, u32p, u64p, u64p, u64p, u64p, u64p, u64p, u64p, u64p]),
+    "pm_graph_create": (C.c_int, [vp, u64, u64, u64, f32p, u32p, C.c_int, C.c_int, u64, u64, C.POINTER(vp)]),
+    "pm_graph_destroy": (None, [vp]),
+    "pm_graph_preprocess": (C.c_int, [vp]),
+    "pm_search_knn": (C.c_int, [vp, f32p, C.c_int, C.c_int, C.c_int, C.c_int, i64p, i64p]),
+    "pm_search_loop": (C.c_int, [vp, f32p, u64, C.c_int, C.c_int, C.c_int, C.c_int, i64p,
+                                 C.POINTER(dbl), C.POINTER(dbl)]),
+    "pm_graph_counts": (C.c_int, [vp, u64p, u64p]),
+    "pm_graph_pir": (vp, [vp]),
+}
+
+Q_OK, Q_EBUDGET, Q_ECHUNK, Q_ENOHIT, Q_ERANGE = range(5)
+_QERR = {
+    Q_EBUDGET: "exceed the maximum number of queries",
+    Q_ECHUNK: "too many queries in chunk",
+    Q_ENOHIT: "no hit hint in the primary hint table",
+    Q_ERANGE: "idx is out of range",
+}
+
+
+class QueryError(Exception):
+    """Recoverable per-query error (the reference's `error` return value)."""
+
+    def __init__(self, code: int):
+        super().__init__(_QERR.get(code, f"status {code}"))
+        self.code = code
+
+
+def lib() -> C.CDLL:
+    """Load libpacmann.so; raises if it has not been built (no fallback)."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise RuntimeError(f"{LIB_PATH} is missing: run `python -m pacmann_amd.build` "
+                               "(there is no CPU fallback)")
+        L = C.CDLL(str(LIB_PATH))
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(rc: int):
+    if rc != 0:
+        raise RuntimeError(f"libpacmann error {rc}: {lib().pm_last_error().decode()}")
+
+
+def _p(a: np.ndarray, t):
+    return a.ctypes.data_as(t)
+
+
+def _u64(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.uint64))
+
+
+class Context:
+    """One HIP device + stream (pm_ctx)."""
+
+    def __init__(self, device: int = 0):
+        h = vp()
+        _check(lib().pm_ctx_create(device, C.byref(h)))
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().pm_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sync(self):
+        _check(lib().pm_ctx_sync(self.h))
+
+    def timing(self, on: bool):
+        _check(lib().pm_timing_enable(self.h, int(on)))
+
+    def timing_reset(self):
+        _check(lib().pm_timing_reset(self.h))
+
+    def timing_get(self, kernel: str):
+        n = C.c_uint64()
+        ms = C.c_double()
+        by = C.c_double()
+        _check(lib().pm_timing_get(self.h, kernel.encode(), C.byref(n), C.byref(ms), C.byref(by)))
+        return n.value, ms.value, by.value
+
+
+_default_ctx: Context | None = None
+
+
+def default_context() -> Context:
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context(0)
+    return _default_ctx
+
+
+# ---------------------------------------------------------------------------
+# leaf batches
+# ---------------------------------------------------------------------------
+def expand_key(key: bytes) -> np.ndarray:
+    rk = np.zeros(44, dtype=np.uint32)
+    kb = (C.c_uint8 * 16).from_buffer_copy(bytes(key))
+    _check(lib().pm_expand_key(kb, _p(rk, u32p)))
+    return rk
+
+
+def prf_batch(rk: np.ndarray, tags, xs, ctx: Context | None = None) -> np.ndarray:
+    ctx = ctx or default_context()
+    rk = np.ascontiguousarray(rk, dtype=np.uint32)
+    t, x = _u64(tags), _u64(xs)
+    out = np.zeros(len(t), dtype=np.uint64)
+    _check(lib().pm_prf_batch(ctx.h, _p(rk, u32p), _p(t, u64p), _p(x, u64p), len(t), _p(out, u64p)))
+    return out
+
+
+def l2_batch(query, rows, ctx: Context | None = None) -> np.ndarray:
+    ctx = ctx or default_context()
+    q = np.ascontiguousarray(query, dtype=np.float32)
+    r = np.ascontiguousarray(rows, dtype=np.float32).reshape(-1, q.shape[0])
+    out = np.zeros(r.shape[0], dtype=np.float32)
+    _check(lib().pm_l2_batch(ctx.h, _p(q, f32p), _p(r, f32p), r.shape[0], q.shape[0], _p(out, f32p)))
+    return out
+
+
+def ip_batch(query, rows, per_row: bool = True, ctx: Context | None = None):
+    ctx = ctx or default_context()
+    q = np.ascontiguousarray(query, dtype=np.uint32)
+    r = np.ascontiguousarray(rows, dtype=np.uint32).reshape(-1, q.shape[0])
+    pr = np.zeros(max(1, r.shape[0]), dtype=np.uint32)
+    s = C.c_uint32()
+    _check(lib().pm_ip_batch(ctx.h, _p(q, u32p), _p(r, u32p), r.shape[0], q.shape[0],
+                             _p(pr, u32p) if per_row else None, C.byref(s)))
+    return (pr[: r.shape[0]] if per_row else None), s.value
+
+
+def ip_bench(N: int, D: int, ctx: Context | None = None):
+    """TestInnerProduct's scan fully on device; returns (sum, scan_ms)."""
+    ctx = ctx or default_context()
+    s = C.c_uint32()
+    ms = C.c_double()
+    _check(lib().pm_ip_bench(ctx.h, N, D, C.byref(s), C.byref(ms)))
+    return s.value, ms.value
+
+
+# ---------------------------------------------------------------------------
+# PianoPIR / SimpleBatchPianoPIR
+# ---------------------------------------------------------------------------
+def _export(fn, h, cfg: PirConfig, *pre):
+    E, PH, SS, Q = cfg.DBEntrySize, cfg.PrimaryHintNum, cfg.SetSize, cfg.MaxQueryPerChunk
+    nb = SS * Q
+    st = {
+        "round_keys": np.zeros(44, np.uint32),
+        "primary_tag": np.zeros(PH, np.uint64), "primary_parity": np.zeros(PH * E, np.uint64),
+        "primary_pp": np.zeros(PH, np.uint64), "backup_tag": np.zeros(nb, np.uint64),
+        "backup_parity": np.zeros(nb * E, np.uint64), "repl_idx": np.zeros(nb, np.uint64),
+        "repl_val": np.zeros(nb * E, np.uint64), "hist": np.zeros(SS, np.uint64),
+    }
+    _check(fn(h, *pre, _p(st["round_keys"], u32p), *[_p(st[k], u64p) for k in (
+        "primary_tag", "primary_parity", "primary_pp", "backup_tag", "backup_parity",
+        "repl_idx", "repl_val", "hist")]))
+    return st
+
+
+class PianoPIR:
+    """pianopir.PianoPIR (pir.go:473-548) on the GPU."""
+
+    def __init__(self, DBSize: int, DBEntryByteNum: int, rawDB, FailureProbLog2: int,
+                 seed: int = 1, ctx: Context | None = None):
+        self.ctx = ctx or default_context()
+        db = _u64(rawDB)
+        if db.size != DBSize * (DBEntryByteNum // 8):   # pir.go:483-485 log.Fatalf
+            raise ValueError(f"Piano PIR len(rawDB) = {db.size}; want {DBSize * (DBEntryByteNum // 8)}")
+        h = vp()
+        _check(lib().pm_pir_create(self.ctx.h, DBSize, DBEntryByteNum, _p(db, u64p), FailureProbLog2,
+                                   seed, C.byref(h)))
+        self.h = h
+        self.E = DBEntryByteNum // 8
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().pm_pir_destroy(self.h)
+            self.h = None
+
+    def Preprocessing(self):
+        _check(lib().pm_pir_preprocessing(self.h))
+
+    def DummyPreprocessing(self):
+        _check(lib().pm_pir_dummy_preprocessing(self.h))
+
+    def Query(self, idx: int, realQuery: bool = True):
+        """Returns (entry, err) like the Go method; err is None or QueryError."""
+        out = np.zeros(self.E, dtype=np.uint64)
+        st = C.c_int()
+        _check(lib().pm_pir_query(self.h, idx, int(realQuery), _p(out, u64p), C.byref(st)))
+        return out, (None if st.value == Q_OK else QueryError(st.value))
+
+    def Config(self) -> dict:
+        c = PirConfig()
+        _check(lib().pm_pir_config_get(self.h, C.byref(c)))
+        return c.asdict()
+
+    def LocalStorageSize(self) -> float:
+        return lib().pm_pir_local_storage(self.h)
+
+    def CommCostPerQuery(self) -> float:
+        return lib().pm_pir_comm_per_query(self.h)
+
+    def PrivateQuery(self, offsets) -> np.ndarray:
+        """Server answer(s) for one ([SetSize]) or many ([nq, SetSize]) offset sets."""
+        o = np.ascontiguousarray(np.asarray(offsets, dtype=np.uint32))
+        ss = self.Config()["SetSize"]
+        o2 = o.reshape(-1, ss)
+        out = np.zeros((o2.shape[0], self.E), dtype=np.uint64)
+        _check(lib().pm_pir_server_answer(self.h, _p(o2, u32p), o2.shape[0], _p(out, u64p)))
+        return out[0] if o.ndim == 1 else out
+
+    def export_state(self) -> dict:
+        c = PirConfig()
+        _check(lib().pm_pir_config_get(self.h, C.byref(c)))
+        return _export(lib().pm_pir_export, self.h, c)
+
+
+class SimpleBatchPianoPIR:
+    """pianopir.SimpleBatchPianoPIR (batch-pir.go:40-276) on the GPU."""
+
+    def __init__(self, DBSize: int, DBEntryByteNum: int, BatchSize: int, rawDB,
+                 FailureProbLog2: int, seed: int = 1, ctx: Context | None = None, _handle=None):
+        self.ctx = ctx or default_context()
+        self.E = DBEntryByteNum // 8
+        self._owned = _handle is None
+        if _handle is not None:
+            self.h = _handle
+            return
+        db = _u64(rawDB)
+        if db.size != DBSize * self.E:   # batch-pir.go:57-59 log.Fatalf
+            raise ValueError(f"BatchPIR: len(rawDB) = {db.size}; want {DBSize * self.E}")
+        h = vp()
+        _check(lib().pm_batchpir_create(self.ctx.h, DBSize, DBEntryByteNum, BatchSize, _p(db, u64p),
+                                        FailureProbLog2, seed, C.byref(h)))
+        self.h = h
+
+    def __del__(self):
+        if getattr(self, "h", None) and self._owned:
+            lib().pm_batchpir_destroy(self.h)
+        self.h = None
+
+    def Preprocessing(self):
+        _check(lib().pm_batchpir_preprocessing(self.h))
+
+    def DummyPreprocessing(self):
+        _check(lib().pm_batchpir_dummy_preprocessing(self.h))
+
+    def Query(self, idx):
+        """Returns (responses [len(idx), DBEntrySize] uint64, err=None)."""
+        ids = _u64(idx).ravel()
+        out = np.zeros((len(ids), self.E), dtype=np.uint64)
+        _check(lib().pm_batchpir_query(self.h, _p(ids, u64p), len(ids), _p(out, u64p)))
+        return out, None
+
+    def stats(self) -> dict:
+        s = BatchStats()
+        _check(lib().pm_batchpir_stats_get(self.h, C.byref(s)))
+        return s.asdict()
+
+    def Config(self) -> dict:
+        s = self.stats()
+        return {k: s[k] for k in ("DBEntryByteNum DBEntrySize DBSize BatchSize PartitionNum "
+                                  "PartitionSize ThreadNum FailureProbLog2").split()}
+
+    def SubConfig(self, i: int) -> dict:
+        c = PirConfig()
+        _check(lib().pm_batchpir_subconfig(self.h, i, C.byref(c)))
+        return c.asdict()
+
+    def LocalStorageSize(self) -> float:
+        return self.stats()["LocalStorage"]
+
+    def CommCostPerBatchOnline(self) -> int:
+        return int(self.stats()["CommOnline"])
+
+    def CommCostPerBatchOffline(self) -> int:
+        return int(self.stats()["CommOffline"])
+
+    def PreprocessingTime(self) -> float:
+        return self.stats()["PreprocessingTime"]
+
+    @property
+    def FinishedBatchNum(self) -> int:
+        return self.stats()["FinishedBatchNum"]
+
+    @property
+    def SupportBatchNum(self) -> int:
+        return self.stats()["SupportBatchNum"]
+
+    def export_state(self, partition: int) -> dict:
+        return _export(lib().pm_batchpir_export, self.h, self._cfg(partition), partition)
+
+    def _cfg(self, i):
+        c = PirConfig()
+        _check(lib().pm_batchpir_subconfig(self.h, i, C.byref(c)))
+        return c
+
+
+# ---------------------------------------------------------------------------
+# graphann
+# ---------------------------------------------------------------------------
+class PIRGraphInfo:
+    """PIRGraphInfo (private-search.go:336-531) wrapped in GraphANNFrontend
+    (graphann/search.go:69-245).  nonprivate=True gives BasicGraphInfo-style
+    direct vertex access."""
+
+    def __init__(self, vectors, graph, nonprivate: bool = False, skip_prep: bool = False,
+                 pir_seed: int = 1, search_seed: int = 1, ctx: Context | None = None):
+        self.ctx = ctx or default_context()
+        v = np.ascontiguousarray(vectors, dtype=np.float32)
+        g = np.ascontiguousarray(graph, dtype=np.uint32)
+        self.N, self.Dim = v.shape
+        self.M = g.shape[1]
+        h = vp()
+        _check(lib().pm_graph_create(self.ctx.h, self.N, self.Dim, self.M, _p(v, f32p), _p(g, u32p),
+                                     int(nonprivate), int(skip_prep), pir_seed, search_seed,
+                                     C.byref(h)))
+        self.h = h
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().pm_graph_destroy(self.h)
+            self.h = None
+
+    def GetMetadata(self):
+        return self.N, self.Dim, self.M
+
+    def Preprocess(self):
+        _check(lib().pm_graph_preprocess(self.h))
+
+    @property
+    def PIR(self) -> SimpleBatchPianoPIR | None:
+        hp = lib().pm_graph_pir(self.h)
+        if not hp:
+            return None
+        return SimpleBatchPianoPIR(0, self.Dim * 4 + self.M * 4, 0, None, 0, ctx=self.ctx,
+                                   _handle=vp(hp))
+
+    def counts(self):
+        t, s = C.c_uint64(), C.c_uint64()
+        _check(lib().pm_graph_counts(self.h, C.byref(t), C.byref(s)))
+        return t.value, s.value
+
+    def SearchKNN(self, query, k: int, maxStep: int, parallel: int, benchmarking: bool = False):
+        q = np.ascontiguousarray(query, dtype=np.float32)
+        ids = np.zeros(k, dtype=np.int64)
+        steps = np.zeros(k, dtype=np.int64)
+        _check(lib().pm_search_knn(self.h, _p(q, f32p), k, maxStep, parallel, int(benchmarking),
+                                   _p(ids, i64p), _p(steps, i64p)))
+        return ids, steps
+
+    def SearchLoop(self, queries, k: int, step: int, parallel: int, benchmarking: bool = False):
+        """private-search.go:216-240: returns (answers [q,k], online_s, maintenance_s)."""
+        qs = np.ascontiguousarray(queries, dtype=np.float32)
+        ans = np.zeros((qs.shape[0], k), dtype=np.int64)
+        on, mt = C.c_double(), C.c_double()
+        _check(lib().pm_search_loop(self.h, _p(qs, f32p), qs.shape[0], k, step, parallel,
+                                    int(benchmarking), _p(ans, i64p), C.byref(on), C.byref(mt)))
+        return ans, on.value, mt.value
+
+
+GraphANNFrontend = PIRGraphInfo

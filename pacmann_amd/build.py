@@ -1,0 +1,48 @@
+"""Build libpacmann.so (hand-written HIP for gfx950) in-tree.
+
+    python -m pacmann_amd.build
+
+The .so lands next to this file (pacmann_amd/libpacmann.so) so that it travels
+to the GPU box with the repo snapshot.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+LIB = PKG / "libpacmann.so"
+SOURCES = [CSRC / "pm_kernels.hip", CSRC / "pm_engine.cpp"]
+HEADERS = [CSRC / "pm_internal.h", CSRC / "pm_aes.h", ROOT / "include" / "pacmann.h"]
+
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = [
+    "-x", "hip", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+    # bit-exact fp32 L2: no FMA contraction, IEEE denormals (l2_distance_amd64.s order)
+    "-ffp-contract=off", "-fno-gpu-flush-denormals-to-zero",
+    "-Wall", "-Werror=return-type",
+]
+
+
+def needs_build() -> bool:
+    if not LIB.exists():
+        return True
+    t = LIB.stat().st_mtime
+    return any(p.stat().st_mtime > t for p in SOURCES + HEADERS)
+
+
+def build(force: bool = False, verbose: bool = True) -> Path:
+    if force or needs_build():
+        cmd = [HIPCC, *FLAGS, "-o", str(LIB), *map(str, SOURCES)]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True, cwd=CSRC)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

@@ -1,0 +1,1074 @@
+// pm_engine.cpp — host side of libpacmann.so: the PianoPIR / SimpleBatchPianoPIR
+// engine (device-resident DB, hints and client state; batched steps), the
+// graphann beam search over PIRGraphInfo, and the extern "C" boundary of
+// include/pacmann.h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/pacmann.h"
+#include "pm_aes.h"
+#include "pm_internal.h"
+
+using namespace pm;
+
+// ---------------------------------------------------------------------------
+// errors
+// ---------------------------------------------------------------------------
+static thread_local std::string g_err;
+static int fail(int code, const std::string& msg) { g_err = msg; return code; }
+#define HIPCHK(x)                                                                         \
+  do {                                                                                    \
+    hipError_t e_ = (x);                                                                  \
+    if (e_ != hipSuccess)                                                                 \
+      return fail(PM_EHIP, std::string(#x) + ": " + hipGetErrorString(e_));               \
+  } while (0)
+#define CHK(x)            \
+  do {                    \
+    int r_ = (x);         \
+    if (r_ != 0) return r_; \
+  } while (0)
+
+extern "C" const char* pm_last_error(void) { return g_err.c_str(); }
+
+// ---------------------------------------------------------------------------
+// host AES-128 key schedule (FIPS-197 §5.2; expandKeyAsm, aes_amd64.s:87-126)
+// ---------------------------------------------------------------------------
+static constexpr AesTables kAes{};
+extern "C" int pm_expand_key(const uint8_t key[16], uint32_t rk[44]) {
+  uint8_t w[176];
+  memcpy(w, key, 16);
+  uint8_t rcon = 1;
+  for (int i = 16; i < 176; i += 4) {
+    uint8_t t[4] = {w[i - 4], w[i - 3], w[i - 2], w[i - 1]};
+    if (i % 16 == 0) {
+      uint8_t u = t[0];
+      t[0] = kAes.sbox[t[1]] ^ rcon; t[1] = kAes.sbox[t[2]]; t[2] = kAes.sbox[t[3]]; t[3] = kAes.sbox[u];
+      rcon = AesTables::gmul(rcon, 2);
+    }
+    for (int k = 0; k < 4; ++k) w[i + k] = w[i - 16 + k] ^ t[k];
+  }
+  memcpy(rk, w, 176);   // little-endian word view, as the GPU and AESENC read it
+  return 0;
+}
+static void derive_key(uint64_t seed, uint64_t part, uint64_t epoch, uint8_t key[16]) {
+  uint64_t r1 = hash4(seed, DOM_KEY, part, epoch, 0), r2 = hash4(seed, DOM_KEY, part, epoch, 1);
+  memcpy(key, &r1, 8);
+  memcpy(key + 8, &r2, 8);
+}
+
+// ---------------------------------------------------------------------------
+// context, device buffers, timing
+// ---------------------------------------------------------------------------
+struct DevBuf {
+  void* p = nullptr;
+  size_t n = 0;
+  ~DevBuf() { if (p) (void)hipFree(p); }
+  int reserve(size_t bytes) {
+    if (bytes <= n) return 0;
+    if (p) { (void)hipFree(p); p = nullptr; n = 0; }
+    if (bytes == 0) return 0;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess) return fail(PM_ENOMEM, "hipMalloc(" + std::to_string(bytes) + "): " + hipGetErrorString(e));
+    n = bytes;
+    return 0;
+  }
+  template <class T> T* as() const { return (T*)p; }
+};
+struct HostBuf {   // pinned staging
+  void* p = nullptr;
+  size_t n = 0;
+  ~HostBuf() { if (p) (void)hipHostFree(p); }
+  int reserve(size_t bytes) {
+    if (bytes <= n) return 0;
+    if (p) { (void)hipHostFree(p); p = nullptr; n = 0; }
+    hipError_t e = hipHostMalloc(&p, bytes, 0);
+    if (e != hipSuccess) return fail(PM_ENOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+    n = bytes;
+    return 0;
+  }
+  template <class T> T* as() const { return (T*)p; }
+};
+
+struct TimedLaunch { std::string name; hipEvent_t a, b; double bytes; };
+
+struct pm_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool timing = false;
+  std::vector<TimedLaunch> launches;
+  std::vector<hipEvent_t> pool;
+  hipEvent_t ev() {
+    if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
+    hipEvent_t e; (void)hipEventCreate(&e); return e;
+  }
+  // Bracket a launch with events on the stream it runs on (when enabled).
+  template <class F> void timed(const char* name, double bytes, F&& f) {
+    if (!timing) { f(); return; }
+    TimedLaunch t{name, ev(), ev(), bytes};
+    (void)hipEventRecord(t.a, stream);
+    f();
+    (void)hipEventRecord(t.b, stream);
+    launches.push_back(t);
+  }
+  ~pm_ctx() {
+    for (auto& t : launches) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
+    for (auto e : pool) (void)hipEventDestroy(e);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+extern "C" int pm_ctx_create(int device, pm_ctx** out) {
+  if (!out) return fail(PM_EINVAL, "out is NULL");
+  int n = 0;
+  HIPCHK(hipGetDeviceCount(&n));
+  if (device < 0 || device >= n) return fail(PM_EINVAL, "no such HIP device " + std::to_string(device));
+  HIPCHK(hipSetDevice(device));
+  pm_ctx* c = new pm_ctx();
+  c->device = device;
+  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) { delete c; return fail(PM_EHIP, hipGetErrorString(e)); }
+  *out = c;
+  return 0;
+}
+extern "C" void pm_ctx_destroy(pm_ctx* c) { if (c) { (void)hipSetDevice(c->device); delete c; } }
+extern "C" int pm_ctx_sync(pm_ctx* c) { HIPCHK(hipStreamSynchronize(c->stream)); HIPCHK(hipGetLastError()); return 0; }
+extern "C" int pm_timing_enable(pm_ctx* c, int on) { c->timing = on != 0; return 0; }
+extern "C" int pm_timing_reset(pm_ctx* c) {
+  HIPCHK(hipStreamSynchronize(c->stream));
+  for (auto& t : c->launches) { c->pool.push_back(t.a); c->pool.push_back(t.b); }
+  c->launches.clear();
+  return 0;
+}
+extern "C" int pm_timing_get(pm_ctx* c, const char* name, uint64_t* launches, double* total_ms,
+                             double* bytes) {
+  HIPCHK(hipStreamSynchronize(c->stream));
+  uint64_t n = 0; double ms = 0, by = 0;
+  for (auto& t : c->launches) {
+    if (t.name != name) continue;
+    float x = 0;
+    HIPCHK(hipEventElapsedTime(&x, t.a, t.b));
+    ++n; ms += x; by += t.bytes;
+  }
+  if (launches) *launches = n;
+  if (total_ms) *total_ms = ms;
+  if (bytes) *bytes = by;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// PianoPIR engine: P partitions (P = 1 for PianoPIR, BatchSize/2 for the batch)
+// ---------------------------------------------------------------------------
+struct PartHost {
+  PmPart d{};
+  uint64_t epoch_ctr = 0, fqn = 0, dummy_ctr = 0;
+  uint64_t maxq64 = 0;
+  std::unordered_map<uint64_t, std::vector<uint64_t>> cache;   // localCache (pir.go:120)
+};
+
+struct Engine {
+  pm_ctx* ctx = nullptr;
+  bool is_batch = false;
+  uint64_t N = 0, E = 0, Ebytes = 0, F = 0, seed = 0;
+  uint64_t B = 0, P = 1, PS = 0;
+  bool skipPrep = false;
+  // SimpleBatchPianoPIR stats (batch-pir.go:46-52)
+  uint64_t FBN = 0, QMIP = 0, Support = 0, prepCount = 0;
+  double prepTime = 0, storage = 0, commOn = 0, commOff = 0;
+
+  DevBuf db, parts_d, tag, pp, parity, ridx, rval, hist, fqn;
+  DevBuf offs, bits, subs_d, sb_d, res_d, qoffs, ans, out, dist, qvec;
+  HostBuf in_h, out_h;
+  std::vector<PartHost> parts;
+  uint32_t maxH = 0, maxPH = 0, maxSS = 0, maxRepl = 0;
+
+  // per-step host view
+  std::vector<PmSub> subs;
+  std::vector<uint32_t> sb;
+  std::vector<uint64_t> sub_gid;   // global id per sub (REAL) for mapping
+  PmRes* res_h = nullptr;
+  uint64_t* out_h_words = nullptr;
+  float* dist_h = nullptr;
+};
+
+// NewPianoPIR parameterisation (pir.go:479-514) + NewPianoPIRClient (:130-175)
+static void part_params(PartHost& ph, uint64_t N, uint64_t F) {
+  uint64_t target = (uint64_t)(2 * std::sqrt((double)N));
+  uint64_t cs = 1;
+  while (cs < target) cs *= 2;
+  uint64_t ss = (uint64_t)std::ceil((double)N / (double)cs);
+  ss = (ss + 3) / 4 * 4;
+  const uint64_t thr = 8;   // PianoPIRConfig.ThreadNum (pir.go:502)
+  uint64_t maxq = (uint64_t)(std::sqrt((double)N) * std::log((double)N));
+  uint64_t k = (uint64_t)std::ceil(std::log(2.0) * (double)(F + 1));
+  uint64_t phn = (k * cs + thr - 1) / thr * thr;
+  uint64_t qpc = 3 * (uint64_t)((double)maxq / (double)ss);
+  qpc = (qpc + thr - 1) / thr * thr;
+  ph.d.N = N;
+  ph.d.CS = (uint32_t)cs;
+  uint32_t lg = 0; while ((1ull << lg) < cs) ++lg;
+  ph.d.log2CS = lg;
+  ph.d.SS = (uint32_t)ss;
+  ph.d.PH = (uint32_t)phn;
+  ph.d.Qpc = (uint32_t)qpc;
+  ph.d.H = (uint32_t)(phn + ss * qpc);
+  ph.maxq64 = maxq;
+  ph.d.MaxQ = (uint32_t)std::min<uint64_t>(maxq, 0xffffffffu);
+}
+
+static double part_storage(const PartHost& p, uint64_t Ebytes) {   // LocalStorageSize pir.go:178-190
+  double s = 0;
+  s = s + (double)p.d.PH * 8;
+  s = s + (double)p.d.PH * (double)Ebytes;
+  s = s + (double)p.d.PH * 8;
+  double tb = (double)p.d.SS * (double)p.d.Qpc;
+  s = s + tb * 8;
+  s = s + tb * (double)Ebytes;
+  s = s + tb * 8;
+  s = s + tb * (double)Ebytes;
+  return s;
+}
+static double part_comm(const PartHost& p, uint64_t E) { return (double)((uint64_t)p.d.SS * 4 + E * 8); }
+
+static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, uint64_t B,
+                         const uint64_t* rawDB, uint64_t F, uint64_t seed, bool batch) {
+  if (!ctx) return fail(PM_EINVAL, "ctx is NULL");
+  if (!rawDB && N) return fail(PM_EINVAL, "rawDB is NULL");
+  if (N == 0) return fail(PM_EINVAL, "DBSize must be > 0");
+  if (Ebytes < 8) return fail(PM_EINVAL, "DBEntryByteNum must be >= 8");
+  HIPCHK(hipSetDevice(ctx->device));
+  g->ctx = ctx; g->is_batch = batch;
+  g->N = N; g->Ebytes = Ebytes; g->E = Ebytes / 8; g->F = F; g->seed = seed;
+  if (batch) {
+    g->B = B;
+    g->P = B / 2;   // BatchSize / RealQueryPerPartition (batch-pir.go:62)
+    if (g->P == 0) return fail(PM_EINVAL, "BatchSize must be >= 2");
+    g->PS = (N + g->P - 1) / g->P;
+  } else {
+    g->P = 1; g->PS = N;
+  }
+  g->parts.resize(g->P);
+  uint64_t off_tag = 0, off_pp = 0, off_par = 0, off_ridx = 0, off_rval = 0, off_hist = 0;
+  for (uint64_t i = 0; i < g->P; ++i) {
+    PartHost& ph = g->parts[i];
+    uint64_t start = i * g->PS, end = std::min((i + 1) * g->PS, N);
+    if (end <= start) return fail(PM_EINVAL, "empty partition (DBSize too small for BatchSize)");
+    part_params(ph, end - start, F);
+    if (ph.d.CS > 32768) return fail(PM_EINVAL, "ChunkSize > 32768 unsupported (16-bit prep offsets)");
+    if ((uint64_t)ph.d.H >= (1ull << 29)) return fail(PM_EINVAL, "tag space >= 2^29 (util.go:161)");
+    ph.d.row0 = start; ph.d.seed = seed; ph.d.idx = i;
+    g->maxH = std::max(g->maxH, ph.d.H);
+    g->maxPH = std::max(g->maxPH, ph.d.PH);
+    g->maxSS = std::max(g->maxSS, ph.d.SS);
+    g->maxRepl = std::max(g->maxRepl, ph.d.SS * ph.d.Qpc);
+    // carve offsets (elements)
+    ph.d.tag = (uint32_t*)(uintptr_t)off_tag; off_tag += ph.d.H;
+    ph.d.pp = (uint32_t*)(uintptr_t)off_pp; off_pp += ph.d.PH;
+    ph.d.parity = (uint64_t*)(uintptr_t)off_par; off_par += (uint64_t)ph.d.H * g->E;
+    ph.d.ridx = (uint32_t*)(uintptr_t)off_ridx; off_ridx += (uint64_t)ph.d.SS * ph.d.Qpc;
+    ph.d.rval = (uint64_t*)(uintptr_t)off_rval; off_rval += (uint64_t)ph.d.SS * ph.d.Qpc * g->E;
+    ph.d.hist = (uint32_t*)(uintptr_t)off_hist; off_hist += ph.d.SS;
+  }
+  CHK(g->db.reserve(N * g->E * 8));
+  HIPCHK(hipMemcpy(g->db.p, rawDB, N * g->E * 8, hipMemcpyHostToDevice));
+  CHK(g->tag.reserve(off_tag * 4));
+  CHK(g->pp.reserve(off_pp * 4));
+  CHK(g->parity.reserve(off_par * 8));
+  CHK(g->ridx.reserve(off_ridx * 4));
+  CHK(g->rval.reserve(off_rval * 8));
+  CHK(g->hist.reserve(off_hist * 4));
+  CHK(g->fqn.reserve(g->P * 4));
+  CHK(g->parts_d.reserve(g->P * sizeof(PmPart)));
+  for (uint64_t i = 0; i < g->P; ++i) {
+    PmPart& d = g->parts[i].d;
+    d.tag = g->tag.as<uint32_t>() + (uintptr_t)d.tag;
+    d.pp = g->pp.as<uint32_t>() + (uintptr_t)d.pp;
+    d.parity = g->parity.as<uint64_t>() + (uintptr_t)d.parity;
+    d.ridx = g->ridx.as<uint32_t>() + (uintptr_t)d.ridx;
+    d.rval = g->rval.as<uint64_t>() + (uintptr_t)d.rval;
+    d.hist = g->hist.as<uint32_t>() + (uintptr_t)d.hist;
+    d.fqn = g->fqn.as<uint32_t>() + i;
+  }
+  HIPCHK(hipMemsetAsync(g->fqn.p, 0, g->P * 4, ctx->stream));
+  HIPCHK(hipMemsetAsync(g->hist.p, 0, off_hist * 4, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+static int upload_parts(Engine* g) {
+  std::vector<PmPart> v(g->P);
+  for (uint64_t i = 0; i < g->P; ++i) v[i] = g->parts[i].d;
+  HIPCHK(hipMemcpyAsync(g->parts_d.p, v.data(), g->P * sizeof(PmPart), hipMemcpyHostToDevice,
+                        g->ctx->stream));
+  HIPCHK(hipStreamSynchronize(g->ctx->stream));   // v goes out of scope
+  return 0;
+}
+
+// Client.Preprocessing (pir.go:267-301) for partitions [p0, p1): Initialization
+// (new key, reset state) then, unless skipPrep, the full hint fold.
+static int engine_prep(Engine* g, uint64_t p0, uint64_t p1) {
+  pm_ctx* c = g->ctx;
+  hipStream_t st = c->stream;
+  for (uint64_t i = p0; i < p1; ++i) {
+    PartHost& ph = g->parts[i];
+    uint8_t key[16];
+    derive_key(g->seed, i, ph.epoch_ctr, key);
+    ph.d.epoch = ph.epoch_ctr++;
+    pm_expand_key(key, ph.d.rk);
+    ph.fqn = 0;
+    ph.cache.clear();
+  }
+  CHK(upload_parts(g));
+  const PmPart* dp = g->parts_d.as<PmPart>() + p0;
+  const int np = (int)(p1 - p0);
+  c->timed("prep_init", 0, [&] { pmk::prep_init(st, dp, np, g->maxH, g->maxRepl, (uint32_t)g->E, g->skipPrep); });
+  if (g->skipPrep) {   // DummyPreprocessing (pir.go:520-523): zero hints
+    for (uint64_t i = p0; i < p1; ++i) {
+      const PmPart& d = g->parts[i].d;
+      HIPCHK(hipMemsetAsync(d.parity, 0, (uint64_t)d.H * g->E * 8, st));
+      HIPCHK(hipMemsetAsync(d.rval, 0, (uint64_t)d.SS * d.Qpc * g->E * 8, st));
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    return 0;
+  }
+  // group partitions so the 16-bit offset scratch stays within budget
+  const uint64_t per = (uint64_t)g->maxH * g->maxSS;
+  const uint64_t budget = 1ull << 30;
+  uint64_t group = std::max<uint64_t>(1, budget / (per * 2));
+  group = std::min<uint64_t>(group, (uint64_t)np);
+  CHK(g->offs.reserve(group * per * 2));
+  for (uint64_t a = p0; a < p1; a += group) {
+    const uint64_t b = std::min(p1, a + group);
+    const PmPart* dpa = g->parts_d.as<PmPart>() + a;
+    const int n = (int)(b - a);
+    double aes = 0, fold = 0, repl = 0;
+    for (uint64_t i = a; i < b; ++i) {
+      const PmPart& d = g->parts[i].d;
+      aes += (double)d.H * d.SS;
+      // algorithmic fold bytes: hpc * SS pairs of one E-word entry
+      fold += ((double)d.PH + (double)(d.SS - 1) * d.Qpc) * d.SS * (double)g->E * 8;
+      repl += (double)d.SS * d.Qpc * g->E * 8 * 2;
+    }
+    c->timed("prep_offsets", aes, [&] {
+      pmk::prep_offsets(st, dpa, n, g->maxH, g->maxSS, g->offs.as<uint16_t>(), per);
+    });
+    c->timed("prep_fold", fold, [&] {
+      pmk::prep_fold(st, dpa, n, g->maxH, g->maxSS, g->offs.as<uint16_t>(), per, g->db.as<uint64_t>(),
+                     (uint32_t)g->E);
+    });
+    c->timed("prep_repl", repl, [&] { pmk::prep_repl(st, dpa, n, g->maxRepl, g->db.as<uint64_t>(), (uint32_t)g->E); });
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(st));
+  return 0;
+}
+
+// One batched step: the sub-queries in g->subs (partition-major, ranges in
+// g->sb).  HOSTCACHE rows are provided in `cached` (nsub x E, only those rows
+// read).  Results land in g->res_h / g->out_h_words (/ g->dist_h if q != NULL).
+static int engine_step(Engine* g, const std::vector<std::vector<uint64_t>>& cached, const float* q,
+                       uint32_t dim) {
+  pm_ctx* c = g->ctx;
+  hipStream_t st = c->stream;
+  const uint32_t nsub = (uint32_t)g->subs.size();
+  if (nsub == 0) return 0;
+  const uint64_t E = g->E;
+  const uint32_t words = (g->maxPH + 63) / 64;
+  CHK(g->subs_d.reserve(nsub * sizeof(PmSub)));
+  CHK(g->sb_d.reserve((g->P + 1) * 4));
+  CHK(g->bits.reserve((uint64_t)nsub * words * 8));
+  CHK(g->res_d.reserve(nsub * sizeof(PmRes)));
+  CHK(g->qoffs.reserve((uint64_t)nsub * g->maxSS * 4));
+  CHK(g->ans.reserve((uint64_t)nsub * E * 8));
+  CHK(g->out.reserve((uint64_t)nsub * E * 8));
+  CHK(g->dist.reserve((uint64_t)nsub * 4));
+  // pinned staging: subs | sb | cached rows
+  const size_t in_bytes = nsub * sizeof(PmSub) + (g->P + 1) * 4 + 16;
+  bool any_cached = false;
+  for (auto& s : g->subs) any_cached |= (s.kind == SUB_HOSTCACHE);
+  const size_t cached_bytes = any_cached ? (size_t)nsub * E * 8 : 0;
+  CHK(g->in_h.reserve(in_bytes + cached_bytes));
+  char* ip = g->in_h.as<char>();
+  memcpy(ip, g->subs.data(), nsub * sizeof(PmSub));
+  memcpy(ip + nsub * sizeof(PmSub), g->sb.data(), (g->P + 1) * 4);
+  HIPCHK(hipMemcpyAsync(g->subs_d.p, ip, nsub * sizeof(PmSub), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(g->sb_d.p, ip + nsub * sizeof(PmSub), (g->P + 1) * 4, hipMemcpyHostToDevice, st));
+  if (any_cached) {
+    uint64_t* cw = (uint64_t*)(ip + in_bytes);
+    for (uint32_t s = 0; s < nsub; ++s)
+      if (g->subs[s].kind == SUB_HOSTCACHE) {
+        memcpy(cw + (uint64_t)s * E, cached[s].data(), E * 8);
+        HIPCHK(hipMemcpyAsync(g->out.as<uint64_t>() + (uint64_t)s * E, cw + (uint64_t)s * E, E * 8,
+                              hipMemcpyHostToDevice, st));
+      }
+  }
+  const PmPart* dp = g->parts_d.as<PmPart>();
+  const PmSub* ds = g->subs_d.as<PmSub>();
+  const uint32_t* dsb = g->sb_d.as<uint32_t>();
+  PmRes* dr = g->res_d.as<PmRes>();
+  uint32_t nreal = 0;
+  for (auto& s : g->subs) nreal += s.kind == SUB_REAL;
+  double match_aes = (double)nreal * g->maxPH;
+  c->timed("hint_match", match_aes, [&] { pmk::hint_match(st, dp, ds, nsub, g->maxPH, g->bits.as<uint64_t>(), words); });
+  c->timed("resolve", 0, [&] {
+    pmk::resolve(st, dp, (int)g->P, ds, dsb, g->bits.as<uint64_t>(), words, dr, g->qoffs.as<uint32_t>(), g->maxSS);
+  });
+  double ans_bytes = 0;
+  for (auto& s : g->subs)
+    if (s.kind == SUB_REAL || s.kind == SUB_DUMMY) {
+      const PmPart& d = g->parts[s.part].d;
+      ans_bytes += (double)d.SS * (E * 8 + 4) + E * 8;
+    }
+  c->timed("answer", ans_bytes, [&] {
+    pmk::answer(st, dp, ds, dr, nsub, g->qoffs.as<uint32_t>(), g->maxSS, g->db.as<uint64_t>(), (uint32_t)E,
+                g->ans.as<uint64_t>());
+  });
+  c->timed("decode", 0, [&] {
+    pmk::decode(st, dp, (int)g->P, ds, dsb, dr, g->ans.as<uint64_t>(), (uint32_t)E, g->out.as<uint64_t>());
+  });
+  if (q) {
+    HIPCHK(hipMemcpyAsync(g->qvec.p, q, dim * 4, hipMemcpyHostToDevice, st));
+    c->timed("l2_rows", (double)nsub * dim * 4, [&] {
+      pmk::l2_rows(st, (const float*)g->out.p, E * 2, nsub, nullptr, g->qvec.as<float>(), dim, g->dist.as<float>());
+    });
+  }
+  HIPCHK(hipGetLastError());
+  const size_t ob = nsub * sizeof(PmRes) + (size_t)nsub * E * 8 + (size_t)nsub * 4;
+  CHK(g->out_h.reserve(ob));
+  char* op = g->out_h.as<char>();
+  HIPCHK(hipMemcpyAsync(op, dr, nsub * sizeof(PmRes), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(op + nsub * sizeof(PmRes), g->out.p, (size_t)nsub * E * 8, hipMemcpyDeviceToHost, st));
+  if (q)
+    HIPCHK(hipMemcpyAsync(op + nsub * sizeof(PmRes) + (size_t)nsub * E * 8, g->dist.p, nsub * 4,
+                          hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  g->res_h = (PmRes*)op;
+  g->out_h_words = (uint64_t*)(op + nsub * sizeof(PmRes));
+  g->dist_h = q ? (float*)(op + nsub * sizeof(PmRes) + (size_t)nsub * E * 8) : nullptr;
+  // host mirrors: FinishedQueryNum and localCache (pir.go:469-470)
+  for (uint32_t s = 0; s < nsub; ++s) {
+    if (g->res_h[s].status != ST_OK) continue;
+    PartHost& ph = g->parts[g->subs[s].part];
+    ph.fqn++;
+    const uint64_t* w = g->out_h_words + (uint64_t)s * E;
+    ph.cache[g->subs[s].idx] = std::vector<uint64_t>(w, w + E);
+  }
+  return 0;
+}
+
+// Append one sub-query of partition p to the step being built.
+static void add_sub(Engine* g, uint32_t p, bool real, uint64_t local, uint64_t gid,
+                    std::vector<std::vector<uint64_t>>& cached) {
+  PartHost& ph = g->parts[p];
+  PmSub s{p, SUB_NONE, 0};
+  if (!real) {
+    s.kind = SUB_DUMMY; s.idx = ph.dummy_ctr++;
+  } else {
+    s.kind = SUB_REAL; s.idx = local;
+    auto it = ph.cache.find(local);
+    if (it != ph.cache.end()) { s.kind = SUB_HOSTCACHE; cached.resize(g->subs.size() + 1); cached.back() = it->second; }
+  }
+  g->subs.push_back(s);
+  g->sub_gid.push_back(gid);
+  if (cached.size() < g->subs.size()) cached.resize(g->subs.size());
+}
+static void begin_step(Engine* g) {
+  g->subs.clear(); g->sub_gid.clear();
+  g->sb.assign(g->P + 1, 0);
+}
+static void close_partition(Engine* g, uint32_t p) {   // sub_begin[p+1] = current size
+  for (uint64_t i = p + 1; i <= g->P; ++i) g->sb[i] = (uint32_t)g->subs.size();
+}
+
+// ---------------------------------------------------------------------------
+// PianoPIR C ABI
+// ---------------------------------------------------------------------------
+struct pm_pir { Engine e; };
+struct pm_batchpir { Engine e; };
+
+extern "C" int pm_pir_create(pm_ctx* ctx, uint64_t DBSize, uint64_t DBEntryByteNum, const uint64_t* rawDB,
+                             uint64_t F, uint64_t seed, pm_pir** out) {
+  if (!out) return fail(PM_EINVAL, "out is NULL");
+  pm_pir* h = new pm_pir();
+  int r = engine_create(ctx, &h->e, DBSize, DBEntryByteNum, 0, rawDB, F, seed, false);
+  if (r) { delete h; return r; }
+  *out = h;
+  return 0;
+}
+extern "C" void pm_pir_destroy(pm_pir* h) { delete h; }
+extern "C" int pm_pir_preprocessing(pm_pir* h) { return engine_prep(&h->e, 0, 1); }
+// Initialization only (pir.go:520-523); skipPrep stays set for later preprocessing.
+extern "C" int pm_pir_dummy_preprocessing(pm_pir* h) {
+  h->e.skipPrep = true;
+  return engine_prep(&h->e, 0, 1);
+}
+
+static int status_to_api(uint32_t st) {
+  switch (st) {
+    case ST_OK: case ST_DUP: case ST_CACHED: case ST_DUMMY: return PM_Q_OK;
+    case ST_EBUDGET: return PM_Q_EBUDGET;
+    case ST_ECHUNK: return PM_Q_ECHUNK;
+    case ST_ENOHIT: return PM_Q_ENOHIT;
+    default: return PM_Q_ERANGE;
+  }
+}
+
+// PianoPIR.Query (pir.go:525-533) -> Client.Query (:354-471)
+extern "C" int pm_pir_query(pm_pir* h, uint64_t idx, int real, uint64_t* out, int* status) {
+  Engine* g = &h->e;
+  PartHost& ph = g->parts[0];
+  if (ph.fqn == ph.maxq64) CHK(engine_prep(g, 0, 1));
+  memset(out, 0, g->E * 8);
+  if (real && idx >= ph.d.N) { if (status) *status = PM_Q_ERANGE; return 0; }
+  std::vector<std::vector<uint64_t>> cached;
+  begin_step(g);
+  add_sub(g, 0, real != 0, idx, idx, cached);
+  close_partition(g, 0);
+  if (g->subs[0].kind == SUB_HOSTCACHE) {   // local cache hit (pir.go:381-383)
+    memcpy(out, cached[0].data(), g->E * 8);
+    if (status) *status = PM_Q_OK;
+    return 0;
+  }
+  CHK(engine_step(g, cached, nullptr, 0));
+  const uint32_t st = g->res_h[0].status;
+  if (st == ST_OK || st == ST_DUP) memcpy(out, g->out_h_words, g->E * 8);
+  if (status) *status = status_to_api(st);
+  return 0;
+}
+extern "C" int pm_pir_config_get(pm_pir* h, pm_pir_config* c) {
+  const Engine& g = h->e; const PartHost& p = g.parts[0];
+  c->DBEntryByteNum = g.Ebytes; c->DBEntrySize = g.E; c->DBSize = p.d.N; c->ChunkSize = p.d.CS;
+  c->SetSize = p.d.SS; c->ThreadNum = 8; c->FailureProbLog2 = g.F; c->MaxQueryNum = p.maxq64;
+  c->PrimaryHintNum = p.d.PH; c->MaxQueryPerChunk = p.d.Qpc; c->FinishedQueryNum = p.fqn;
+  return 0;
+}
+extern "C" double pm_pir_local_storage(pm_pir* h) { return part_storage(h->e.parts[0], h->e.Ebytes); }
+extern "C" double pm_pir_comm_per_query(pm_pir* h) { return part_comm(h->e.parts[0], h->e.E); }
+
+extern "C" int pm_pir_server_answer(pm_pir* h, const uint32_t* offsets, uint64_t nq, uint64_t* out) {
+  Engine* g = &h->e;
+  pm_ctx* c = g->ctx;
+  const PmPart& d = g->parts[0].d;
+  if (nq == 0) return 0;
+  CHK(g->qoffs.reserve(nq * d.SS * 4));
+  CHK(g->ans.reserve(nq * g->E * 8));
+  CHK(upload_parts(g));
+  HIPCHK(hipMemcpyAsync(g->qoffs.p, offsets, nq * d.SS * 4, hipMemcpyHostToDevice, c->stream));
+  c->timed("answer", (double)nq * (d.SS * (g->E * 8 + 4) + g->E * 8), [&] {
+    pmk::server_answer(c->stream, g->parts_d.as<PmPart>(), g->qoffs.as<uint32_t>(), (uint32_t)nq, d.SS,
+                       g->db.as<uint64_t>(), (uint32_t)g->E, g->ans.as<uint64_t>());
+  });
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out, g->ans.p, nq * g->E * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+static int engine_export(Engine* g, uint64_t p, uint32_t* rk, uint64_t* pt, uint64_t* par, uint64_t* ppo,
+                         uint64_t* bt, uint64_t* bpar, uint64_t* ri, uint64_t* rv, uint64_t* hist) {
+  if (p >= g->P) return fail(PM_EINVAL, "partition out of range");
+  const PmPart& d = g->parts[p].d;
+  const uint64_t E = g->E, nb = (uint64_t)d.SS * d.Qpc;
+  HIPCHK(hipStreamSynchronize(g->ctx->stream));
+  if (rk) memcpy(rk, d.rk, 44 * 4);
+  auto widen = [&](uint64_t* dst, const uint32_t* src, uint64_t n) -> int {
+    if (!dst) return 0;
+    std::vector<uint32_t> t(n);
+    HIPCHK(hipMemcpy(t.data(), src, n * 4, hipMemcpyDeviceToHost));
+    for (uint64_t i = 0; i < n; ++i) dst[i] = t[i];
+    return 0;
+  };
+  CHK(widen(pt, d.tag, d.PH));
+  CHK(widen(ppo, d.pp, d.PH));
+  CHK(widen(bt, d.tag + d.PH, nb));
+  CHK(widen(ri, d.ridx, nb));
+  CHK(widen(hist, d.hist, d.SS));
+  if (par) HIPCHK(hipMemcpy(par, d.parity, (uint64_t)d.PH * E * 8, hipMemcpyDeviceToHost));
+  if (bpar) HIPCHK(hipMemcpy(bpar, d.parity + (uint64_t)d.PH * E, nb * E * 8, hipMemcpyDeviceToHost));
+  if (rv) HIPCHK(hipMemcpy(rv, d.rval, nb * E * 8, hipMemcpyDeviceToHost));
+  return 0;
+}
+extern "C" int pm_pir_export(pm_pir* h, uint32_t* rk, uint64_t* pt, uint64_t* par, uint64_t* pp,
+                             uint64_t* bt, uint64_t* bpar, uint64_t* ri, uint64_t* rv, uint64_t* hist) {
+  return engine_export(&h->e, 0, rk, pt, par, pp, bt, bpar, ri, rv, hist);
+}
+
+// ---------------------------------------------------------------------------
+// SimpleBatchPianoPIR C ABI (batch-pir.go)
+// ---------------------------------------------------------------------------
+static void record_stats(Engine* g, double t) {   // RecordStats batch-pir.go:110-117
+  g->prepTime = t;
+  double s = 0; for (auto& p : g->parts) s += part_storage(p, g->Ebytes);
+  g->storage = (double)(uint64_t)s;
+  double on = 0; for (auto& p : g->parts) on += part_comm(p, g->E) * 2.0;
+  g->commOn = (double)(uint64_t)on;
+  g->Support = g->parts[0].maxq64 / 2;
+  double dbBytes = (double)g->N * (double)g->Ebytes;
+  g->commOff = (double)(uint64_t)(dbBytes / (double)g->Support);
+}
+extern "C" int pm_batchpir_create(pm_ctx* ctx, uint64_t DBSize, uint64_t DBEntryByteNum, uint64_t BatchSize,
+                                  const uint64_t* rawDB, uint64_t F, uint64_t seed, pm_batchpir** out) {
+  if (!out) return fail(PM_EINVAL, "out is NULL");
+  pm_batchpir* h = new pm_batchpir();
+  int r = engine_create(ctx, &h->e, DBSize, DBEntryByteNum, BatchSize, rawDB, F, seed, true);
+  if (r) { delete h; return r; }
+  *out = h;
+  return 0;
+}
+extern "C" void pm_batchpir_destroy(pm_batchpir* h) { delete h; }
+static int batch_prep(Engine* g) {   // Preprocessing (batch-pir.go:119-155)
+  g->FBN = 0; g->QMIP = 0;
+  auto t0 = std::chrono::steady_clock::now();
+  CHK(engine_prep(g, 0, g->P));
+  double t = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  g->prepCount++;
+  record_stats(g, t);
+  return 0;
+}
+extern "C" int pm_batchpir_preprocessing(pm_batchpir* h) { return batch_prep(&h->e); }
+extern "C" int pm_batchpir_dummy_preprocessing(pm_batchpir* h) {   // batch-pir.go:157-166
+  h->e.skipPrep = true;
+  CHK(engine_prep(&h->e, 0, h->e.P));
+  record_stats(&h->e, 0);
+  return 0;
+}
+
+// Query (batch-pir.go:170-248).  Partitions whose FinishedQueryNum cannot reach
+// MaxQueryNum inside this batch run as one fused step; the rest replay the
+// reference's per-sub-query re-preprocessing check (pir.go:527-530) one
+// sub-query at a time.
+static int batch_query(Engine* g, const uint64_t* idx, uint64_t n, uint64_t* out, const float* q,
+                       uint32_t dim, float* dist_out) {
+  const uint64_t E = g->E, P = g->P;
+  for (uint64_t i = 0; i < n; ++i)
+    if (idx[i] >= g->N) return fail(PM_EINVAL, "id " + std::to_string(idx[i]) + " >= DBSize");
+  const uint64_t qn = n / P;
+  std::vector<std::vector<uint64_t>> pq(P);
+  for (uint64_t i = 0; i < n; ++i) pq[idx[i] / g->PS].push_back(idx[i]);
+  for (auto& v : pq) while (v.size() < qn) v.push_back(kDefaultValue);
+  // responses[id] = last response made for it (batch-pir.go:187,213)
+  std::unordered_map<uint64_t, std::pair<std::vector<uint64_t>, float>> responses;
+  auto collect = [&]() {
+    for (size_t s = 0; s < g->subs.size(); ++s) {
+      const PmSub& sb = g->subs[s];
+      if (sb.kind != SUB_REAL && sb.kind != SUB_HOSTCACHE) continue;
+      const uint64_t* w = g->out_h_words + (uint64_t)s * E;
+      responses[g->sub_gid[s]] = {std::vector<uint64_t>(w, w + E), g->dist_h ? g->dist_h[s] : 0.0f};
+    }
+  };
+  std::vector<std::vector<uint64_t>> cached;
+  // fast partitions, in rounds of at most kStepPerPart sub-queries per
+  // partition (the resolve kernel tracks that many refreshed hints per step)
+  std::vector<bool> slow(P, false);
+  for (uint64_t p = 0; p < P; ++p) {
+    uint64_t nreal = 0;
+    for (uint64_t j = 0; j < qn; ++j) nreal += pq[p][j] != kDefaultValue;
+    const PartHost& ph = g->parts[p];
+    slow[p] = qn && ph.fqn + nreal >= ph.maxq64;
+  }
+  const uint64_t kStepPerPart = 256;
+  for (uint64_t j0 = 0; j0 < qn; j0 += kStepPerPart) {
+    const uint64_t j1 = std::min(qn, j0 + kStepPerPart);
+    cached.clear();
+    begin_step(g);
+    for (uint64_t p = 0; p < P; ++p) {
+      if (!slow[p])
+        for (uint64_t j = j0; j < j1; ++j) {
+          const uint64_t id = pq[p][j];
+          add_sub(g, (uint32_t)p, id != kDefaultValue, id - p * g->PS, id, cached);
+        }
+      close_partition(g, (uint32_t)p);
+    }
+    if (!g->subs.empty()) { CHK(engine_step(g, cached, q, dim)); collect(); }
+  }
+  for (uint64_t p = 0; p < P; ++p) {
+    if (!slow[p]) continue;
+    for (uint64_t j = 0; j < qn; ++j) {
+      PartHost& ph = g->parts[p];
+      if (ph.fqn == ph.maxq64) CHK(engine_prep(g, p, p + 1));
+      cached.clear();
+      begin_step(g);
+      const uint64_t id = pq[p][j];
+      add_sub(g, (uint32_t)p, id != kDefaultValue, id - p * g->PS, id, cached);
+      close_partition(g, (uint32_t)p);
+      CHK(engine_step(g, cached, q, dim));
+      collect();
+    }
+  }
+  for (uint64_t i = 0; i < n; ++i) {
+    auto it = responses.find(idx[i]);
+    if (it != responses.end()) {
+      memcpy(out + i * E, it->second.first.data(), E * 8);
+      if (dist_out) dist_out[i] = it->second.second;
+    } else {
+      memset(out + i * E, 0, E * 8);
+      if (dist_out) dist_out[i] = 0;
+    }
+  }
+  if (g->QMIP >= g->parts[0].maxq64 - 2) {
+    CHK(batch_prep(g));
+  } else {
+    g->FBN += n / g->B;
+    g->QMIP += qn;
+  }
+  return 0;
+}
+extern "C" int pm_batchpir_query(pm_batchpir* h, const uint64_t* ids, uint64_t n, uint64_t* out) {
+  return batch_query(&h->e, ids, n, out, nullptr, 0, nullptr);
+}
+extern "C" int pm_batchpir_stats_get(pm_batchpir* h, pm_batchpir_stats* s) {
+  const Engine& g = h->e;
+  s->DBEntryByteNum = g.Ebytes; s->DBEntrySize = g.E; s->DBSize = g.N; s->BatchSize = g.B;
+  s->PartitionNum = g.P; s->PartitionSize = g.PS; s->ThreadNum = 1; s->FailureProbLog2 = g.F;
+  s->FinishedBatchNum = g.FBN; s->QueriesMadeInPartition = g.QMIP; s->SupportBatchNum = g.Support;
+  s->PrepCount = g.prepCount; s->LocalStorage = g.storage; s->PreprocessingTime = g.prepTime;
+  s->CommOnline = g.commOn; s->CommOffline = g.commOff;
+  return 0;
+}
+extern "C" int pm_batchpir_subconfig(pm_batchpir* h, uint64_t p, pm_pir_config* c) {
+  const Engine& g = h->e;
+  if (p >= g.P) return fail(PM_EINVAL, "partition out of range");
+  const PartHost& ph = g.parts[p];
+  c->DBEntryByteNum = g.Ebytes; c->DBEntrySize = g.E; c->DBSize = ph.d.N; c->ChunkSize = ph.d.CS;
+  c->SetSize = ph.d.SS; c->ThreadNum = 8; c->FailureProbLog2 = g.F; c->MaxQueryNum = ph.maxq64;
+  c->PrimaryHintNum = ph.d.PH; c->MaxQueryPerChunk = ph.d.Qpc; c->FinishedQueryNum = ph.fqn;
+  return 0;
+}
+extern "C" int pm_batchpir_export(pm_batchpir* h, uint64_t p, uint32_t* rk, uint64_t* pt, uint64_t* par,
+                                  uint64_t* pp, uint64_t* bt, uint64_t* bpar, uint64_t* ri, uint64_t* rv,
+                                  uint64_t* hist) {
+  return engine_export(&h->e, p, rk, pt, par, pp, bt, bpar, ri, rv, hist);
+}
+
+// ---------------------------------------------------------------------------
+// leaf batches
+// ---------------------------------------------------------------------------
+extern "C" int pm_prf_batch(pm_ctx* c, const uint32_t rk[44], const uint64_t* tags, const uint64_t* xs,
+                            uint64_t n, uint64_t* out) {
+  if (n == 0) return 0;
+  DevBuf drk, dt, dx, dout;
+  CHK(drk.reserve(176)); CHK(dt.reserve(n * 8)); CHK(dx.reserve(n * 8)); CHK(dout.reserve(n * 8));
+  hipStream_t st = c->stream;
+  HIPCHK(hipMemcpyAsync(drk.p, rk, 176, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(dt.p, tags, n * 8, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(dx.p, xs, n * 8, hipMemcpyHostToDevice, st));
+  c->timed("prf", (double)n, [&] { pmk::prf_batch(st, drk.as<uint32_t>(), dt.as<uint64_t>(), dx.as<uint64_t>(), n, dout.as<uint64_t>()); });
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out, dout.p, n * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  return 0;
+}
+extern "C" int pm_l2_batch(pm_ctx* c, const float* q, const float* rows, uint64_t nrows, uint64_t dim,
+                           float* out) {
+  if (nrows == 0) return 0;
+  if (dim == 0) return fail(PM_EINVAL, "dim must be > 0");
+  DevBuf dq, dr, dout;
+  CHK(dq.reserve(dim * 4)); CHK(dr.reserve(nrows * dim * 4)); CHK(dout.reserve(nrows * 4));
+  hipStream_t st = c->stream;
+  HIPCHK(hipMemcpyAsync(dq.p, q, dim * 4, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(dr.p, rows, nrows * dim * 4, hipMemcpyHostToDevice, st));
+  c->timed("l2_rows", (double)nrows * dim * 4, [&] {
+    pmk::l2_rows(st, dr.as<float>(), dim, nrows, nullptr, dq.as<float>(), (uint32_t)dim, dout.as<float>());
+  });
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out, dout.p, nrows * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  return 0;
+}
+extern "C" int pm_ip_batch(pm_ctx* c, const uint32_t* q, const uint32_t* rows, uint64_t nrows, uint64_t dim,
+                           uint32_t* per_row, uint32_t* sum) {
+  if (dim == 0) return fail(PM_EINVAL, "dim must be > 0");
+  DevBuf dq, dr, dpr, ds;
+  CHK(dq.reserve(dim * 4)); CHK(dr.reserve(std::max<uint64_t>(1, nrows * dim * 4)));
+  CHK(dpr.reserve(std::max<uint64_t>(4, nrows * 4))); CHK(ds.reserve(4));
+  hipStream_t st = c->stream;
+  HIPCHK(hipMemcpyAsync(dq.p, q, dim * 4, hipMemcpyHostToDevice, st));
+  if (nrows) HIPCHK(hipMemcpyAsync(dr.p, rows, nrows * dim * 4, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemsetAsync(ds.p, 0, 4, st));
+  c->timed("ip_scan", (double)nrows * dim * 4, [&] {
+    pmk::ip_rows(st, dr.as<uint32_t>(), nrows, dq.as<uint32_t>(), (uint32_t)dim, per_row ? dpr.as<uint32_t>() : nullptr,
+                 ds.as<uint32_t>());
+  });
+  HIPCHK(hipGetLastError());
+  if (per_row && nrows) HIPCHK(hipMemcpyAsync(per_row, dpr.p, nrows * 4, hipMemcpyDeviceToHost, st));
+  uint32_t s = 0;
+  HIPCHK(hipMemcpyAsync(&s, ds.p, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (sum) *sum = s;
+  return 0;
+}
+extern "C" int pm_ip_bench(pm_ctx* c, uint64_t N, uint64_t D, uint32_t* sum, double* scan_ms) {
+  if (D == 0 || D % 4 || D > 4096) return fail(PM_EINVAL, "D must be a multiple of 4 and <= 4096");
+  DevBuf dv, dq, ds;
+  CHK(dv.reserve(N * D * 4)); CHK(dq.reserve(D * 4)); CHK(ds.reserve(4));
+  std::vector<uint32_t> q(D);
+  for (uint64_t j = 0; j < D; ++j) q[j] = (uint32_t)j;
+  hipStream_t st = c->stream;
+  HIPCHK(hipMemcpyAsync(dq.p, q.data(), D * 4, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemsetAsync(ds.p, 0, 4, st));
+  pmk::ip_fill(st, dv.as<uint32_t>(), N, (uint32_t)D);
+  hipEvent_t a, b;
+  HIPCHK(hipEventCreate(&a)); HIPCHK(hipEventCreate(&b));
+  HIPCHK(hipEventRecord(a, st));
+  c->timed("ip_scan", (double)N * D * 4, [&] { pmk::ip_rows(st, dv.as<uint32_t>(), N, dq.as<uint32_t>(), (uint32_t)D, nullptr, ds.as<uint32_t>()); });
+  HIPCHK(hipEventRecord(b, st));
+  HIPCHK(hipGetLastError());
+  uint32_t s = 0;
+  HIPCHK(hipMemcpyAsync(&s, ds.p, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, a, b));
+  (void)hipEventDestroy(a); (void)hipEventDestroy(b);
+  if (sum) *sum = s;
+  if (scan_ms) *scan_ms = ms;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// graphann: GraphANNFrontend over PIRGraphInfo / BasicGraphInfo
+// ---------------------------------------------------------------------------
+struct SplitMix {   // host id stream standing in for Go's global math/rand
+  uint64_t s;
+  uint64_t next() { s += 0x9e3779b97f4a7c15ULL; uint64_t z = s;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL; z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31); }
+  uint64_t intn(uint64_t n) { return next() % n; }
+};
+struct VD { float dist; int64_t id; };
+struct Known { std::vector<int64_t> nb; float dist; };
+
+struct pm_graph {
+  pm_ctx* ctx = nullptr;
+  uint64_t n = 0, dim = 0, m = 0;
+  bool nonprivate = false, skipPrep = false;
+  uint64_t pir_seed = 0;
+  SplitMix rng{0};
+  std::vector<float> vectors;
+  std::vector<uint32_t> graph;
+  DevBuf dvec, dq, dids, ddist;
+  pm_batchpir* pir = nullptr;
+  std::vector<uint64_t> start;   // StartVertices ids
+  DevBuf dstart;
+  uint64_t total = 0, succ = 0;
+  ~pm_graph() { delete pir; }
+};
+
+extern "C" int pm_graph_create(pm_ctx* ctx, uint64_t n, uint64_t dim, uint64_t m, const float* vectors,
+                               const uint32_t* graph, int nonprivate, int skip_prep, uint64_t pir_seed,
+                               uint64_t search_seed, pm_graph** out) {
+  if (!ctx || !out || !vectors || !graph) return fail(PM_EINVAL, "NULL argument");
+  if (n == 0 || dim == 0 || m == 0) return fail(PM_EINVAL, "n, dim, m must be > 0");
+  if ((dim * 4 + m * 4) % 8) return fail(PM_EINVAL, "(4*dim + 4*m) must be a multiple of 8");
+  HIPCHK(hipSetDevice(ctx->device));
+  pm_graph* g = new pm_graph();
+  g->ctx = ctx; g->n = n; g->dim = dim; g->m = m; g->nonprivate = nonprivate; g->skipPrep = skip_prep;
+  g->pir_seed = pir_seed; g->rng.s = search_seed;
+  g->vectors.assign(vectors, vectors + n * dim);
+  g->graph.assign(graph, graph + n * m);
+  int r = g->dvec.reserve(n * dim * 4);
+  if (!r) r = g->dq.reserve(dim * 4);
+  if (r) { delete g; return r; }
+  hipError_t e = hipMemcpy(g->dvec.p, vectors, n * dim * 4, hipMemcpyHostToDevice);
+  if (e != hipSuccess) { delete g; return fail(PM_EHIP, hipGetErrorString(e)); }
+  *out = g;
+  return 0;
+}
+extern "C" void pm_graph_destroy(pm_graph* g) { delete g; }
+extern "C" pm_batchpir* pm_graph_pir(pm_graph* g) { return g->pir; }
+extern "C" int pm_graph_counts(pm_graph* g, uint64_t* t, uint64_t* s) { *t = g->total; *s = g->succ; return 0; }
+
+// PIRGraphInfo.Preprocess (private-search.go:355-412) + GetStartVertex (:508-531)
+extern "C" int pm_graph_preprocess(pm_graph* g) {
+  {   // the PIR is built in non-private mode too (private-search.go:405)
+    const uint64_t ebytes = g->dim * 4 + g->m * 4, E = ebytes / 8;
+    std::vector<uint64_t> raw(g->n * E);
+    for (uint64_t i = 0; i < g->n; ++i) {
+      uint8_t* e = (uint8_t*)&raw[i * E];
+      memcpy(e, &g->vectors[i * g->dim], g->dim * 4);
+      memcpy(e + g->dim * 4, &g->graph[i * g->m], g->m * 4);
+    }
+    delete g->pir; g->pir = nullptr;
+    CHK(pm_batchpir_create(g->ctx, g->n, ebytes, g->m, raw.data(), 8, g->pir_seed, &g->pir));
+    if (g->skipPrep) CHK(pm_batchpir_dummy_preprocessing(g->pir));
+    else CHK(pm_batchpir_preprocessing(g->pir));
+  }
+  const uint64_t target = (uint64_t)std::sqrt((double)g->n);
+  std::unordered_map<uint64_t, bool> added;
+  g->start.clear();
+  for (uint64_t i = 0; i < target; ++i) {
+    uint64_t x = g->rng.intn(g->n);
+    while (added.count(x)) x = g->rng.intn(g->n);
+    added[x] = true;
+    g->start.push_back(x);
+  }
+  std::vector<uint32_t> ids(g->start.begin(), g->start.end());
+  CHK(g->dstart.reserve(std::max<size_t>(4, ids.size() * 4)));
+  if (!ids.empty()) HIPCHK(hipMemcpy(g->dstart.p, ids.data(), ids.size() * 4, hipMemcpyHostToDevice));
+  return 0;
+}
+
+// container/heap (Go stdlib) restated: up / down / Push / Pop on a min-heap.
+static void heap_up(std::vector<VD>& h, int64_t j) {
+  for (;;) { int64_t i = (j - 1) / 2; if (i == j || !(h[j].dist < h[i].dist)) break; std::swap(h[i], h[j]); j = i; }
+}
+static void heap_down(std::vector<VD>& h, int64_t i0, int64_t n) {
+  int64_t i = i0;
+  for (;;) {
+    int64_t j1 = 2 * i + 1; if (j1 >= n || j1 < 0) break;
+    int64_t j = j1, j2 = j1 + 1;
+    if (j2 < n && h[j2].dist < h[j1].dist) j = j2;
+    if (!(h[j].dist < h[i].dist)) break;
+    std::swap(h[i], h[j]); i = j;
+  }
+}
+static void heap_push(std::vector<VD>& h, VD x) { h.push_back(x); heap_up(h, (int64_t)h.size() - 1); }
+static VD heap_pop(std::vector<VD>& h) {
+  int64_t n = (int64_t)h.size() - 1; std::swap(h[0], h[n]); heap_down(h, 0, n);
+  VD r = h.back(); h.pop_back(); return r;
+}
+
+// GetVertexInfo (private-search.go:441-506) with the L2 distance of every
+// returned vector to `q` computed on the GPU (k_l2_rows) next to the decode.
+static int get_vertex_info(pm_graph* g, const std::vector<int64_t>& ids, const float* q,
+                           std::vector<std::vector<int64_t>>& nbs, std::vector<float>& dist) {
+  g->total += ids.size();
+  const uint64_t n = ids.size();
+  nbs.assign(n, {});
+  dist.assign(n, 0.0f);
+  if (g->nonprivate) {
+    std::vector<uint32_t> u(ids.begin(), ids.end());
+    for (uint64_t i = 0; i < n; ++i)
+      nbs[i].assign(&g->graph[(uint64_t)ids[i] * g->m], &g->graph[(uint64_t)ids[i] * g->m] + g->m);
+    if (q && n) {
+      hipStream_t st = g->ctx->stream;
+      CHK(g->dids.reserve(n * 4)); CHK(g->ddist.reserve(n * 4));
+      HIPCHK(hipMemcpyAsync(g->dids.p, u.data(), n * 4, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(g->dq.p, q, g->dim * 4, hipMemcpyHostToDevice, st));
+      g->ctx->timed("l2_rows", (double)n * g->dim * 4, [&] {
+        pmk::l2_rows(st, g->dvec.as<float>(), g->dim, n, g->dids.as<uint32_t>(), g->dq.as<float>(), (uint32_t)g->dim, g->ddist.as<float>());
+      });
+      HIPCHK(hipMemcpyAsync(dist.data(), g->ddist.p, n * 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+    }
+    return 0;
+  }
+  Engine* e = &g->pir->e;
+  const uint64_t E = e->E;
+  std::vector<uint64_t> qi(ids.begin(), ids.end()), resp(n * E);
+  if (q) CHK(e->qvec.reserve(g->dim * 4));
+  CHK(batch_query(e, qi.data(), n, resp.data(), q, (uint32_t)g->dim, q ? dist.data() : nullptr));
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint8_t* b = (const uint8_t*)&resp[i * E];
+    nbs[i].resize(g->m);
+    bool correct = true;
+    for (uint64_t j = 0; j < g->m; ++j) {
+      uint32_t t; memcpy(&t, b + (g->dim + j) * 4, 4);
+      nbs[i][j] = (int64_t)t;
+      if (t != g->graph[(uint64_t)ids[i] * g->m + j]) correct = false;
+    }
+    if (correct) g->succ++;
+  }
+  return 0;
+}
+
+// SearchKNN (graphann/search.go:114-234).  Same tie rules as oracle/pm_oracle.cpp.
+extern "C" int pm_search_knn(pm_graph* g, const float* query, int k, int max_step, int parallel,
+                             int benchmarking, int64_t* ids_out, int64_t* steps_out) {
+  if (!g->pir && !g->nonprivate) return fail(PM_EINVAL, "pm_graph_preprocess not called");
+  const int64_t n = (int64_t)g->n, m = (int64_t)g->m;
+  std::unordered_map<int64_t, int64_t> reach;
+  std::unordered_map<int64_t, Known> known;
+  std::vector<VD> heap;
+  hipStream_t st = g->ctx->stream;
+  if (!benchmarking) {
+    const uint64_t ns = g->start.size();
+    std::vector<float> d(ns);
+    if (ns) {
+      CHK(g->ddist.reserve(ns * 4));
+      HIPCHK(hipMemcpyAsync(g->dq.p, query, g->dim * 4, hipMemcpyHostToDevice, st));
+      g->ctx->timed("l2_rows", (double)ns * g->dim * 4, [&] {
+        pmk::l2_rows(st, g->dvec.as<float>(), g->dim, ns, g->dstart.as<uint32_t>(), g->dq.as<float>(), (uint32_t)g->dim, g->ddist.as<float>());
+      });
+      HIPCHK(hipMemcpyAsync(d.data(), g->ddist.p, ns * 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+    }
+    std::vector<std::pair<VD, size_t>> fs;
+    for (size_t i = 0; i < ns; ++i) fs.push_back({{d[i], (int64_t)g->start[i]}, i});
+    std::stable_sort(fs.begin(), fs.end(), [](const auto& a, const auto& b) { return a.first.dist < b.first.dist; });
+    for (size_t i = 0; (int64_t)heap.size() < parallel && i < fs.size(); ++i) {
+      const int64_t id = fs[i].first.id;
+      if (known.count(id)) continue;
+      Known kv;
+      kv.nb.assign(&g->graph[(uint64_t)id * g->m], &g->graph[(uint64_t)id * g->m] + g->m);
+      kv.dist = fs[i].first.dist;
+      known[id] = std::move(kv);
+      heap_push(heap, fs[i].first);
+      reach[id] = 0;
+    }
+  }
+  std::vector<std::vector<int64_t>> nbs;
+  std::vector<float> dist;
+  for (int step = 0; step < max_step; ++step) {
+    std::vector<int64_t> batch;
+    for (int r = 0; r < parallel; ++r) {
+      if (heap.empty() || benchmarking) {
+        for (int64_t i = 0; i < m; ++i) batch.push_back((int64_t)g->rng.intn((uint64_t)n));
+      } else {
+        VD it = heap_pop(heap);
+        const Known& v = known[it.id];
+        batch.insert(batch.end(), v.nb.begin(), v.nb.end());
+      }
+    }
+    CHK(get_vertex_info(g, batch, benchmarking ? nullptr : query, nbs, dist));
+    if (benchmarking) continue;
+    for (size_t i = 0; i < batch.size(); ++i) {
+      const int64_t id = batch[i];
+      if (known.count(id)) continue;
+      bool ok = false;
+      for (auto x : nbs[i]) if (x != 0) { ok = true; break; }
+      if (!ok) continue;
+      reach[id] = step;
+      known[id] = Known{std::move(nbs[i]), dist[i]};
+      heap_push(heap, {dist[i], id});
+    }
+  }
+  std::vector<VD> all;
+  all.reserve(known.size());
+  for (auto& kv : known) all.push_back({kv.second.dist, kv.first});
+  std::sort(all.begin(), all.end(), [](const VD& a, const VD& b) {
+    return a.dist < b.dist || (a.dist == b.dist && a.id < b.id); });
+  for (int i = 0; i < k; ++i) {
+    if (i >= (int)all.size()) { ids_out[i] = -1; if (steps_out) steps_out[i] = -1; }
+    else { ids_out[i] = all[i].id; if (steps_out) steps_out[i] = reach[all[i].id]; }
+  }
+  return 0;
+}
+
+// private-search.go:216-240
+extern "C" int pm_search_loop(pm_graph* g, const float* queries, uint64_t q, int k, int step, int parallel,
+                              int benchmarking, int64_t* answers, double* online_s, double* maint_s) {
+  std::vector<int64_t> steps(k);
+  double maint = 0;
+  auto t0 = std::chrono::steady_clock::now();
+  for (uint64_t i = 0; i < q; ++i) {
+    CHK(pm_search_knn(g, queries + i * g->dim, k, step, parallel, benchmarking, answers + i * k, steps.data()));
+    if (g->pir) {
+      Engine* e = &g->pir->e;
+      if (e->FBN + (uint64_t)step * (uint64_t)parallel + 10 >= e->Support) {
+        auto a = std::chrono::steady_clock::now();
+        CHK(batch_prep(e));
+        maint += std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count();
+      }
+    }
+  }
+  double total = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  if (online_s) *online_s = total - maint;
+  if (maint_s) *maint_s = maint;
+  return 0;
+}

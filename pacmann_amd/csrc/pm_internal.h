@@ -1,0 +1,107 @@
+// pm_internal.h — shared host/device definitions for libpacmann.so (gfx950).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+namespace pm {
+
+constexpr uint32_t kDefaultProgramPoint = 0x7fffffffu;   // pir.go:15
+constexpr uint64_t kDefaultValue = 0xdeadbeefULL;        // batch-pir.go:15
+constexpr uint16_t kSkip = 0xffffu;                      // prep offset sentinel: backup hint's own chunk
+constexpr int kBlock = 256;
+
+// Randomness streams; identical spec to oracle/pm_oracle.cpp.
+enum : uint64_t { DOM_KEY = 1, DOM_REPL = 2, DOM_DUMMY = 3 };
+__host__ __device__ inline uint64_t sm64(uint64_t x) {
+  uint64_t z = x + 0x9e3779b97f4a7c15ULL;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+__host__ __device__ inline uint64_t hash4(uint64_t seed, uint64_t dom, uint64_t a, uint64_t b,
+                                          uint64_t c) {
+  uint64_t h = sm64(seed + dom);
+  h = sm64(h ^ a);
+  h = sm64(h ^ b);
+  return sm64(h ^ c);
+}
+
+// One PianoPIR instance ("partition") as the device sees it.  Parameters
+// follow NewPianoPIR / NewPianoPIRClient (pir.go:130-175, 479-514).
+// Hint index space h in [0, H): h < PH primary hints, h >= PH backup hint
+// (g, j) with h = PH + g*Qpc + j (backupShortTag[g][j], pir.go:244-251).
+struct PmPart {
+  uint64_t N;        // DBSize of this sub-PIR
+  uint64_t row0;     // first global DB row of this partition
+  uint64_t seed;     // randomness seed (keys, replacement, dummy)
+  uint64_t epoch;    // preprocessing epoch in use
+  uint64_t idx;      // partition index (stream domain)
+  uint32_t CS, log2CS, SS, PH, Qpc, H, MaxQ, pad;
+  uint32_t rk[44];   // expanded AES-128 key (expandKeyAsm layout)
+  // client state, device-resident
+  uint32_t* tag;     // [H]   short tags (primary tags mutate on refresh)
+  uint32_t* pp;      // [PH]  primaryProgramPoint
+  uint64_t* parity;  // [H*E] primary parities then backup parities
+  uint32_t* ridx;    // [SS*Qpc] replacementIdx
+  uint64_t* rval;    // [SS*Qpc*E] replacementVal
+  uint32_t* hist;    // [SS]  QueryHistogram
+  uint32_t* fqn;     // [1]   FinishedQueryNum
+};
+
+// Sub-query kinds / statuses for one batched step.
+enum : uint32_t { SUB_NONE = 0, SUB_REAL = 1, SUB_DUMMY = 2, SUB_HOSTCACHE = 3 };
+enum : uint32_t {
+  ST_OK = 0, ST_EBUDGET = 1, ST_ECHUNK = 2, ST_ENOHIT = 3, ST_ERANGE = 4,
+  ST_DUMMY = 8, ST_CACHED = 9, ST_DUP = 10, ST_SKIP = 11
+};
+struct PmSub {
+  uint32_t part, kind;
+  uint64_t idx;   // local index in the partition (REAL) / dummy counter (DUMMY)
+};
+// Per-sub-query resolution record written by the resolve kernel.
+struct PmRes {
+  uint32_t status, hit, chunk, ing;   // ing = in-group index (QueryHistogram before)
+  uint32_t ref, pad0, pad1, pad2;     // ST_DUP: earlier sub-query holding the response
+};
+
+struct Launch {   // per-step scalar launch arguments
+  const uint64_t* db;
+  uint32_t E, EX;   // words per entry, XOR width (E & ~3, xorSlices semantics)
+};
+
+}  // namespace pm
+
+// Kernel launchers (pm_kernels.hip).  All asynchronous on `st`.
+namespace pmk {
+using namespace pm;
+void prep_init(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxH, uint32_t maxRepl,
+               uint32_t E, bool zero_state);
+void prep_offsets(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxH, uint32_t maxSS,
+                  uint16_t* offs, uint64_t offs_stride);
+void prep_fold(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxH, uint32_t maxSS,
+               const uint16_t* offs, uint64_t offs_stride, const uint64_t* db, uint32_t E);
+void prep_repl(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxRepl,
+               const uint64_t* db, uint32_t E);
+void hint_match(hipStream_t st, const PmPart* dparts, const PmSub* subs, uint32_t nsub,
+                uint32_t maxPH, uint64_t* bits, uint32_t words);
+void resolve(hipStream_t st, const PmPart* dparts, int nparts, const PmSub* subs,
+             const uint32_t* sub_begin, const uint64_t* bits, uint32_t words, PmRes* res,
+             uint32_t* qoffs, uint32_t maxSS);
+void answer(hipStream_t st, const PmPart* dparts, const PmSub* subs, const PmRes* res,
+            uint32_t nsub, const uint32_t* qoffs, uint32_t maxSS, const uint64_t* db, uint32_t E,
+            uint64_t* ans);
+void decode(hipStream_t st, const PmPart* dparts, int nparts, const PmSub* subs,
+            const uint32_t* sub_begin, const PmRes* res, const uint64_t* ans, uint32_t E,
+            uint64_t* out);
+void server_answer(hipStream_t st, const PmPart* dpart, const uint32_t* offs, uint32_t nq,
+                   uint32_t SS, const uint64_t* db, uint32_t E, uint64_t* out);
+void l2_rows(hipStream_t st, const float* rows, uint64_t row_stride_floats, uint64_t nrows,
+             const uint32_t* row_ids, const float* q, uint32_t dim, float* out);
+void ip_rows(hipStream_t st, const uint32_t* rows, uint64_t nrows, const uint32_t* q, uint32_t dim,
+             uint32_t* per_row, uint32_t* sum);
+void ip_fill(hipStream_t st, uint32_t* rows, uint64_t N, uint32_t D);
+void prf_batch(hipStream_t st, const uint32_t* rk, const uint64_t* tags, const uint64_t* xs,
+               uint64_t n, uint64_t* out);
+}  // namespace pmk

@@ -1,0 +1,30 @@
+"""Test configuration.  `-m gpu` tests need an MI355X and call libpacmann.so
+through its C ABI; everything else runs on CPU (oracle KATs, host logic,
+ABI symbol checks, gloo multi-rank tests)."""
+import os
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+if str(ROOT) not in sys.path:
+    sys.path.insert(0, str(ROOT))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu)")
+    config.addinivalue_line("markers", "slow: long-running test")
+
+
+@pytest.fixture(scope="session")
+def ctx():
+    import pacmann_amd as pm
+    return pm.default_context()
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    from oracle import oracle as O
+    O.lib()
+    return O

@@ -1,0 +1,46 @@
+"""Seeded synthetic inputs shaped like the reference's workloads.
+
+No dataset or network exists on either machine: SIFT1M-shaped data are a
+clustered mixture with integer values in [0,255] (bvecs semantics,
+graphann/loader.go:46-51); graphs are exact kNN graphs (small n) or uniform
+random degree-m graphs like private-search.go:54-69 `genRandomGraph`.
+"""
+import numpy as np
+
+
+def clustered_vectors(n, d, centers=None, sigma=20.0, seed=0):
+    rng = np.random.default_rng(seed)
+    k = centers or max(1, min(1000, n // 64))
+    c = rng.uniform(0, 255, size=(k, d)).astype(np.float32)
+    out = np.empty((n, d), dtype=np.float32)
+    step = 1 << 18
+    for a in range(0, n, step):
+        b = min(n, a + step)
+        lab = rng.integers(0, k, size=b - a)
+        x = c[lab] + rng.normal(0, sigma, size=(b - a, d)).astype(np.float32)
+        out[a:b] = np.clip(np.rint(x), 0, 255)
+    return out
+
+
+def knn_graph(v, m):
+    """Exact m-NN graph (no self loops) by brute force; small n only."""
+    n = v.shape[0]
+    sq = (v.astype(np.float64) ** 2).sum(1)
+    g = np.empty((n, m), dtype=np.uint32)
+    for a in range(0, n, 1024):
+        b = min(n, a + 1024)
+        d2 = sq[a:b, None] + sq[None, :] - 2.0 * v[a:b].astype(np.float64) @ v.T.astype(np.float64)
+        d2[np.arange(b - a), np.arange(a, b)] = np.inf
+        g[a:b] = np.argpartition(d2, m, axis=1)[:, :m]
+    return g
+
+
+def random_graph(n, m, seed=0):
+    """genRandomGraph (private-search.go:54-69): uniform ids, no self loops."""
+    rng = np.random.default_rng(seed)
+    g = rng.integers(0, n, size=(n, m), dtype=np.int64)
+    self_loop = g == np.arange(n)[:, None]
+    while self_loop.any():
+        g[self_loop] = rng.integers(0, n, size=int(self_loop.sum()))
+        self_loop = g == np.arange(n)[:, None]
+    return g.astype(np.uint32)

@@ -1,0 +1,283 @@
+"""GPU parity: libpacmann.so (HIP, gfx950) against the CPU oracle, bit-exact.
+
+Every test calls the product through its C ABI (pacmann_amd -> libpacmann.so)
+and the restatement through oracle/liboracle.so on identical seeded inputs.
+Integer / byte / index results must match bit for bit; the fp32 L2 distances
+too (the kernel reproduces l2_distance_amd64.s's accumulation order), so the
+tolerance written here is zero ulp.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SEED = 20240501
+
+
+def rand_db(n, e, seed=1):
+    return np.random.default_rng(seed).integers(0, 2**64, size=n * e, dtype=np.uint64)
+
+
+# ---------------------------------------------------------------------------
+# leaf primitives
+# ---------------------------------------------------------------------------
+def test_prf_known_answer(ctx):
+    import pacmann_amd as pm
+    rk = pm.expand_key(bytes(range(16)))
+    out = pm.prf_batch(rk, [5], [7], ctx)
+    assert int(out[0]) == 0x821E9920390BACED
+
+
+def test_prf_batch_matches_oracle(ctx, oracle):
+    import pacmann_amd as pm
+    rng = np.random.default_rng(3)
+    for trial in range(4):
+        key = rng.bytes(16)
+        rk = pm.expand_key(key)
+        assert np.array_equal(rk, oracle.expand_key(key))
+        n = 200_003
+        tags = rng.integers(0, 2**29, size=n, dtype=np.uint64)
+        xs = rng.integers(0, 2**35, size=n, dtype=np.uint64)
+        assert np.array_equal(pm.prf_batch(rk, tags, xs, ctx), oracle.prf_batch(rk, tags, xs))
+
+
+@pytest.mark.parametrize("dim", [8, 16, 128, 192, 13, 100, 3])
+def test_l2_batch_bitexact(ctx, oracle, dim):
+    import pacmann_amd as pm
+    rng = np.random.default_rng(dim)
+    rows = rng.standard_normal((1000, dim)).astype(np.float32) * 37
+    q = rng.standard_normal(dim).astype(np.float32)
+    got = pm.l2_batch(q, rows, ctx)
+    want = oracle.l2_batch(q, rows)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))   # 0 ulp
+
+
+def test_l2_msmarco_golden(ctx):
+    """Real d=192 vectors from the reference's validation fixture."""
+    import pacmann_amd as pm
+    from tests.golden_io import load_golden
+    g = load_golden("l2_msmarco")
+    for qi in range(g["queries"].shape[0]):
+        got = pm.l2_batch(g["queries"][qi], g["documents"], ctx)
+        assert np.array_equal(got.view(np.uint32), g["dist"][qi].view(np.uint32))
+
+
+def test_ip_batch(ctx, oracle):
+    import pacmann_amd as pm
+    rng = np.random.default_rng(5)
+    for dim in (128, 192, 7):
+        rows = rng.integers(0, 2**32, size=(3001, dim), dtype=np.uint32)
+        q = rng.integers(0, 2**32, size=dim, dtype=np.uint32)
+        per, s = pm.ip_batch(q, rows, True, ctx)
+        want = np.array([oracle.inner_product(r, q) for r in rows], dtype=np.uint32)
+        assert np.array_equal(per, want)
+        assert s == int(want.astype(np.uint64).sum() % 2**32)
+        _, s2 = pm.ip_batch(q, rows, False, ctx)
+        assert s2 == s
+
+
+def ip_closed_form(N, D=128):
+    sj = D * (D - 1) // 2
+    sj2 = (D - 1) * D * (2 * D - 1) // 6
+    return (sj * N * (N - 1) // 2 + sj2 * N) % 2**32
+
+
+def test_ip_bench_closed_form(ctx, oracle):
+    import pacmann_amd as pm
+    s, ms = pm.ip_bench(1_000_000, 128, ctx)
+    assert s == ip_closed_form(1_000_000)
+    assert s == oracle.inner_product_bench(1_000_000, 128, 8)
+
+
+@pytest.mark.slow
+def test_ip_bench_full_size(ctx):
+    """graphann_test.go:249-283 at N=1e8, D=128 (51.2 GB in HBM)."""
+    import pacmann_amd as pm
+    s, ms = pm.ip_bench(100_000_000, 128, ctx)
+    assert s == 1_178_525_696 == ip_closed_form(100_000_000)
+
+
+# ---------------------------------------------------------------------------
+# PianoPIR
+# ---------------------------------------------------------------------------
+STATE_KEYS = ["round_keys", "primary_tag", "primary_parity", "primary_pp", "backup_tag",
+              "backup_parity", "repl_idx", "repl_val", "hist"]
+
+
+def assert_state_equal(a, b):
+    for k in STATE_KEYS:
+        assert np.array_equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize("N,E,F", [(18750, 4, 40), (5000, 6, 8), (3000, 5, 8), (2000, 2, 8),
+                                   (62500, 80, 8)])
+def test_pir_preprocessing_state(ctx, oracle, N, E, F):
+    import pacmann_amd as pm
+    db = rand_db(N, E, seed=N)
+    g = pm.PianoPIR(N, E * 8, db, F, seed=SEED, ctx=ctx)
+    o = oracle.PianoPIR(N, E * 8, db, F, seed=SEED)
+    assert g.Config() == o.Config()
+    g.Preprocessing()
+    o.Preprocessing()
+    assert_state_equal(g.export_state(), o.export_state())
+
+
+@pytest.mark.parametrize("N,E,F", [(18750, 4, 40), (5000, 6, 8), (3000, 5, 8)])
+def test_pir_query_sequence(ctx, oracle, N, E, F):
+    """TestPIRBasic (pir_test.go:9-58) + bit-exact parity of every response,
+    status and the final client state, through one re-preprocessing."""
+    import pacmann_amd as pm
+    db = rand_db(N, E, seed=7 * N)
+    g = pm.PianoPIR(N, E * 8, db, F, seed=SEED, ctx=ctx)
+    o = oracle.PianoPIR(N, E * 8, db, F, seed=SEED)
+    g.Preprocessing()
+    o.Preprocessing()
+    maxq = g.Config()["MaxQueryNum"]
+    rng = np.random.default_rng(N)
+    ids = rng.integers(0, N, size=maxq + 40)
+    ids[5::17] = ids[3]   # repeats exercise the local cache
+    EX = E & ~3
+    for i, idx in enumerate(ids):
+        real = (i % 13) != 6
+        got, err = g.Query(int(idx), real)
+        want, st = o.Query(int(idx), real)
+        assert (err.code if err else 0) == st, i
+        assert np.array_equal(got, want), i
+        if real and st == 0:   # property of TestPIRBasic
+            assert np.array_equal(got[:EX], db[idx * E: idx * E + EX])
+    assert g.Config()["FinishedQueryNum"] == o.Config()["FinishedQueryNum"]
+    assert_state_equal(g.export_state(), o.export_state())
+
+
+def test_pir_server_answer(ctx, oracle):
+    import pacmann_amd as pm
+    N, E = 40000, 8
+    db = rand_db(N, E, 11)
+    g = pm.PianoPIR(N, E * 8, db, 8, seed=SEED, ctx=ctx)
+    o = oracle.PianoPIR(N, E * 8, db, 8, seed=SEED)
+    cfg = g.Config()
+    rng = np.random.default_rng(1)
+    offs = rng.integers(0, cfg["ChunkSize"], size=(37, cfg["SetSize"]), dtype=np.uint32)
+    got = g.PrivateQuery(offs)
+    for i in range(offs.shape[0]):
+        assert np.array_equal(got[i], o.PrivateQuery(offs[i]))
+
+
+def test_pir_dummy_preprocessing(ctx, oracle):
+    import pacmann_amd as pm
+    N, E = 9000, 4
+    db = rand_db(N, E, 12)
+    g = pm.PianoPIR(N, E * 8, db, 8, seed=SEED, ctx=ctx)
+    o = oracle.PianoPIR(N, E * 8, db, 8, seed=SEED)
+    g.DummyPreprocessing()
+    o.DummyPreprocessing()
+    assert_state_equal(g.export_state(), o.export_state())
+    for idx in np.random.default_rng(2).integers(0, N, size=50):
+        got, err = g.Query(int(idx), True)
+        want, st = o.Query(int(idx), True)
+        assert (err.code if err else 0) == st
+        assert np.array_equal(got, want)
+
+
+# ---------------------------------------------------------------------------
+# SimpleBatchPianoPIR
+# ---------------------------------------------------------------------------
+def test_batch_pir_basic(ctx, oracle):
+    """TestBatchPIRBasic (pir_test.go:60-202) with the GPU path, plus
+    bit-exact parity against the oracle for every response."""
+    import pacmann_amd as pm
+    N, E, B = 1_000_000, 16, 32
+    db = np.repeat(np.arange(N, dtype=np.uint64), E)   # rawDB[i*16+j] = i
+    g = pm.SimpleBatchPianoPIR(N, E * 8, B, db, 20, seed=SEED, ctx=ctx)
+    o = oracle.SimpleBatchPianoPIR(N, E * 8, B, db, 20, seed=SEED)
+    g.Preprocessing()
+    o.Preprocessing()
+    cfg = g.Config()
+    P, PS = cfg["PartitionNum"], cfg["PartitionSize"]
+    rng = np.random.default_rng(4)
+    # (a) one query per partition
+    q1 = np.array([p * PS + rng.integers(0, min(PS, N - p * PS)) for p in range(P)], np.uint64)
+    # (b) four per partition
+    q2 = np.array([p * PS + rng.integers(0, min(PS, N - p * PS)) for p in range(P) for _ in range(4)],
+                  np.uint64)
+    for q in (q1, q2):
+        got, _ = g.Query(q)
+        want, _ = o.Query(q)
+        assert np.array_equal(got, want)
+        assert np.array_equal(got, db.reshape(N, E)[q])
+    # (c) 32 distinct ids all in partition 0: first QueryPerPartition correct, rest zero
+    q3 = rng.choice(PS, size=B, replace=False).astype(np.uint64)
+    got, _ = g.Query(q3)
+    want, _ = o.Query(q3)
+    assert np.array_equal(got, want)
+    assert np.array_equal(got[:2], db.reshape(N, E)[q3[:2]])
+    assert not got[2:].any()
+
+
+@pytest.mark.parametrize("N,E,B,n", [(200_000, 80, 32, 96), (50_000, 12, 8, 24), (30_000, 6, 32, 200)])
+def test_batch_pir_sequence(ctx, oracle, N, E, B, n):
+    """Many batches (duplicates, drops, dummies) through the batch layer's
+    re-preprocessing trigger (batch-pir.go:239-245) and, for the last case,
+    the per-sub-query FinishedQueryNum == MaxQueryNum path (pir.go:527-530)."""
+    import pacmann_amd as pm
+    db = rand_db(N, E, N + E)
+    g = pm.SimpleBatchPianoPIR(N, E * 8, B, db, 8, seed=SEED, ctx=ctx)
+    o = oracle.SimpleBatchPianoPIR(N, E * 8, B, db, 8, seed=SEED)
+    g.Preprocessing()
+    o.Preprocessing()
+    rng = np.random.default_rng(N)
+    maxq = g.SubConfig(0)["MaxQueryNum"]
+    nb = int(maxq // max(1, n // g.Config()["PartitionNum"])) + 8
+    for b in range(min(nb, 400)):
+        q = rng.integers(0, N, size=n, dtype=np.uint64)
+        q[7::11] = q[1]
+        got, _ = g.Query(q)
+        want, _ = o.Query(q)
+        assert np.array_equal(got, want), b
+    sg, so = g.stats(), o.stats()
+    for k in ("FinishedBatchNum", "QueriesMadeInPartition", "SupportBatchNum", "PrepCount",
+              "LocalStorage", "CommOnline", "CommOffline"):
+        assert sg[k] == so[k], k
+    for p in range(g.Config()["PartitionNum"]):
+        assert_state_equal(g.export_state(p), o.sub(p).export_state())
+
+
+# ---------------------------------------------------------------------------
+# graphann beam search over PIR
+# ---------------------------------------------------------------------------
+def small_graph(n=4096, d=128, m=32, seed=0):
+    from tests.datagen import clustered_vectors, knn_graph
+    v = clustered_vectors(n, d, seed=seed)
+    return v, knn_graph(v, m)
+
+
+@pytest.mark.parametrize("nonprivate,bench", [(False, False), (True, False), (False, True)])
+def test_search_knn_matches_oracle(ctx, oracle, nonprivate, bench):
+    import pacmann_amd as pm
+    v, graph = small_graph()
+    qs = v[:20] + np.float32(3.0)
+    g = pm.PIRGraphInfo(v, graph, nonprivate=nonprivate, skip_prep=bench, pir_seed=5, search_seed=9, ctx=ctx)
+    o = oracle.Graph(v, graph, nonprivate=nonprivate, skip_prep=bench, pir_seed=5, search_seed=9)
+    g.Preprocess()
+    o.Preprocess()
+    for q in qs:
+        gi, gs = g.SearchKNN(q, 10, 20, 3, bench)
+        oi, os_ = o.SearchKNN(q, 10, 20, 3, bench)
+        assert np.array_equal(gi, oi)
+        assert np.array_equal(gs, os_)
+    assert g.counts() == o.counts()
+
+
+def test_search_loop_with_maintenance(ctx, oracle):
+    import pacmann_amd as pm
+    v, graph = small_graph(n=2048, seed=1)
+    qs = v[::37][:30] + np.float32(1.0)
+    g = pm.PIRGraphInfo(v, graph, pir_seed=6, search_seed=2, ctx=ctx)
+    o = oracle.Graph(v, graph, pir_seed=6, search_seed=2)
+    g.Preprocess()
+    o.Preprocess()
+    ga, _, gm = g.SearchLoop(qs, 10, 20, 3)
+    oa, _, om = o.SearchLoop(qs, 10, 20, 3)
+    assert np.array_equal(ga, oa)
+    assert g.PIR.stats()["PrepCount"] == o.pir().stats()["PrepCount"] > 1
+    assert g.counts() == o.counts()
