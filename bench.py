@@ -1,0 +1,165 @@
+"""bench.py — private queries/sec on the SIFT1M-shaped private search (1 MI355X per rank).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+
+Workload (BASELINE.json configs[1], the metric's config): n = 1e6 vectors,
+d = 128, degree m = 32 graph, k = 10, step = 20, parallel = 3, batch PIR with
+BatchSize = m = 32 (16 partitions) and FailureProbLog2 = 8, exactly the
+private-search.go harness (run-private-search.sh flags).  Data are synthetic
+(no dataset in the image): a clustered SIFT-like mixture with integer values in
+[0,255] and a uniform random degree-32 graph (private-search.go:54-69).
+
+One step = one private query (GraphANNFrontend.SearchKNN over PIRGraphInfo,
+20 batch-PIR rounds of 96 ids) plus, whenever the harness trigger fires
+(private-search.go:226-232), the full hint re-preprocessing — so `value` is
+q / (online + maintenance) wall time, the reference's own accounting.
+
+Multi-GPU: one process per GPU (torch.distributed.run); every rank runs an
+independent client + server replica on its own GPU and query stream (queries
+are independent units, no data-path exchange), so scaling is weak and `value`
+is the sum of queries over the max of the ranks' times.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+N, DIM, M, K_TOP, STEP, PARALLEL, F = 1_000_000, 128, 32, 10, 20, 3, 8
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+METRIC = "private queries/sec + PIR-scan HBM GB/s, SIFT1M d=128 at 1/2/4/8 GPUs"
+KERNELS = ["prep_offsets", "prep_fold", "prep_repl", "hint_match", "resolve", "answer", "decode",
+           "l2_rows"]
+
+
+def make_data(rank: int):
+    from tests.datagen import clustered_vectors, random_graph
+    v = clustered_vectors(N, DIM, seed=100 + rank)
+    g = random_graph(N, M, seed=200 + rank)
+    return v, g
+
+
+def make_queries(v, n, seed):
+    rng = np.random.default_rng(seed)
+    idx = rng.integers(0, v.shape[0], size=n)
+    q = v[idx] + rng.normal(0, 8, size=(n, v.shape[1])).astype(np.float32)
+    return np.clip(np.rint(q), 0, 255).astype(np.float32)
+
+
+def dist_init():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws == 1:
+        return None, 0, 1, 0
+    import torch.distributed as dist
+    dist.init_process_group("gloo")   # control plane only: barrier + max of timings
+    return dist, dist.get_rank(), ws, int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def cpu_baseline(v, g, queries):
+    """The oracle (single-thread C++ restatement of the Go/AVX path) on a bounded
+    sample of the same workload: one preprocessing, then 46 queries = two
+    23-query maintenance windows, value = q / (online + maintenance)."""
+    from oracle import oracle as O
+    og = O.Graph(v, g, pir_seed=11, search_seed=12)
+    t0 = time.perf_counter()
+    og.Preprocess()
+    prep = time.perf_counter() - t0
+    nq = 46
+    _, online, maint = og.SearchLoop(queries[:nq], K_TOP, STEP, PARALLEL)
+    return {"value": nq / (online + maint), "unit": "queries/s", "cores": 1, "kind": "port",
+            "sample": f"{nq} SIFT1M-shaped private queries (2 maintenance windows) after one "
+                      f"{prep:.2f}s preprocessing; online {online:.2f}s + maintenance {maint:.2f}s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    dist, rank, ws, local = dist_init()
+    import pacmann_amd as pm
+
+    ctx = pm.Context(local)
+    v, g = make_data(rank)
+    queries = make_queries(v, args.warmup + args.steps + 64, seed=300 + rank)
+    gi = pm.PIRGraphInfo(v, g, pir_seed=11 + rank, search_seed=12 + rank, ctx=ctx)
+    gi.Preprocess()   # GraphANNFrontend.Preprocess: DB packing + first hint preprocessing
+    if args.warmup:
+        gi.SearchLoop(queries[:args.warmup], K_TOP, STEP, PARALLEL)
+
+    ctx.timing_reset()
+    ctx.timing(True)
+    if dist:
+        dist.barrier()
+    ctx.sync()
+    t0 = time.perf_counter()
+    _, online, maint = gi.SearchLoop(queries[args.warmup:args.warmup + args.steps], K_TOP, STEP, PARALLEL)
+    ctx.sync()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ctx.timing(False)
+
+    ktime = {k: ctx.timing_get(k) for k in KERNELS}
+    if dist:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    total_q = args.steps * ws
+    value = total_q / elapsed
+    # dominant kernel by device time in the timed region; PIR-scan = the fold
+    dom = max(KERNELS, key=lambda k: ktime[k][1])
+    fold_n, fold_ms, fold_bytes = ktime["prep_fold"]
+    ans_n, ans_ms, ans_bytes = ktime["answer"]
+
+    def roof(name):
+        n, ms, by = ktime[name]
+        if n == 0 or ms == 0:
+            return None
+        ach = (by / n) / (ms / n / 1e3) / 1e9
+        return {"bound": "hbm", "kernel": name, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                "launches": n, "avg_ms": round(ms / n, 4), "alg_bytes_per_launch": by / n}
+
+    stats = gi.PIR.stats()
+    out = {
+        "metric": METRIC, "value": round(value, 2), "unit": "queries/s", "n_gpus": ws,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+        "data": "synthetic (clustered SIFT-like uint8-valued f32 vectors, uniform random degree-32 graph)",
+        "config": {"workload": "SIFT1M-shaped private graph search over 16-partition batch PianoPIR",
+                   "n": N, "dim": DIM, "m": M, "k": K_TOP, "step": STEP, "parallel": PARALLEL,
+                   "batch_size": M, "failure_prob_log2": F, "parallelism": f"replicas{ws}"},
+        "roofline": roof(dom) if dom in ("prep_fold", "answer") else roof("prep_fold"),
+        "online_s_per_query": round(online / args.steps, 6),
+        "maintenance_s_per_query": round(maint / args.steps, 6),
+        "preprocessing_s": round(stats["PreprocessingTime"], 6),
+        "pir_answer": roof("answer"),
+        "kernel_ms": {k: round(ktime[k][1], 3) for k in KERNELS},
+        "dominant_kernel": dom,
+    }
+    if not args.no_cpu_baseline and ws == 1:
+        out["cpu_baseline"] = cpu_baseline(v, g, queries[args.warmup + args.steps:])
+    print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

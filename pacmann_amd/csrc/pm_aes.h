@@ -53,6 +53,10 @@ struct AesTables {
 
 constexpr int kTeLdsWords = 256 * 32;   // 32 KiB replicated Te0
 
+// Device copy of the tables (one per translation unit; read only by aes_lds_init).
+static constexpr AesTables kAesTablesHost{};
+static __device__ const AesTables g_aes = kAesTablesHost;
+
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
 
 // Fill the replicated table.  Call with the whole block, then __syncthreads().

@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -81,14 +83,18 @@ struct DevBuf {
   }
   template <class T> T* as() const { return (T*)p; }
 };
-struct HostBuf {   // pinned staging
+// Pinned host memory the GPU reads (step descriptor) and writes (results)
+// zero-copy.  It must be fine-grained (coherent): with the default
+// coarse-grained allocation the GPU may serve the descriptor from a stale L2
+// line and the host may read result rows before the device writes land.
+struct HostBuf {
   void* p = nullptr;
   size_t n = 0;
   ~HostBuf() { if (p) (void)hipHostFree(p); }
   int reserve(size_t bytes) {
     if (bytes <= n) return 0;
     if (p) { (void)hipHostFree(p); p = nullptr; n = 0; }
-    hipError_t e = hipHostMalloc(&p, bytes, 0);
+    hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocCoherent | hipHostMallocMapped);
     if (e != hipSuccess) return fail(PM_ENOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
     n = bytes;
     return 0;
@@ -101,7 +107,9 @@ struct TimedLaunch { std::string name; hipEvent_t a, b; double bytes; };
 struct pm_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  bool timing = false;
+  int timing = 0;   // 0 off, 1 preprocessing / leaf kernels, 2 also the per-step kernels
+  bool debug_sync = false;   // PM_DEBUG_SYNC=1: synchronise after every launch (fault triage)
+  std::string last_kernel;
   std::vector<TimedLaunch> launches;
   std::vector<hipEvent_t> pool;
   hipEvent_t ev() {
@@ -109,8 +117,15 @@ struct pm_ctx {
     hipEvent_t e; (void)hipEventCreate(&e); return e;
   }
   // Bracket a launch with events on the stream it runs on (when enabled).
-  template <class F> void timed(const char* name, double bytes, F&& f) {
-    if (!timing) { f(); return; }
+  template <class F> void timed(const char* name, double bytes, F&& f, int level = 1) {
+    last_kernel = name;
+    if (debug_sync) {
+      f();
+      hipError_t e = hipStreamSynchronize(stream);
+      if (e != hipSuccess) fprintf(stderr, "[pm] kernel %s failed: %s\n", name, hipGetErrorString(e));
+      return;
+    }
+    if (timing < level) { f(); return; }
     TimedLaunch t{name, ev(), ev(), bytes};
     (void)hipEventRecord(t.a, stream);
     f();
@@ -132,6 +147,8 @@ extern "C" int pm_ctx_create(int device, pm_ctx** out) {
   HIPCHK(hipSetDevice(device));
   pm_ctx* c = new pm_ctx();
   c->device = device;
+  const char* dbg = getenv("PM_DEBUG_SYNC");
+  c->debug_sync = dbg && dbg[0] == '1';
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e != hipSuccess) { delete c; return fail(PM_EHIP, hipGetErrorString(e)); }
   *out = c;
@@ -139,7 +156,7 @@ extern "C" int pm_ctx_create(int device, pm_ctx** out) {
 }
 extern "C" void pm_ctx_destroy(pm_ctx* c) { if (c) { (void)hipSetDevice(c->device); delete c; } }
 extern "C" int pm_ctx_sync(pm_ctx* c) { HIPCHK(hipStreamSynchronize(c->stream)); HIPCHK(hipGetLastError()); return 0; }
-extern "C" int pm_timing_enable(pm_ctx* c, int on) { c->timing = on != 0; return 0; }
+extern "C" int pm_timing_enable(pm_ctx* c, int on) { c->timing = on; return 0; }
 extern "C" int pm_timing_reset(pm_ctx* c) {
   HIPCHK(hipStreamSynchronize(c->stream));
   for (auto& t : c->launches) { c->pool.push_back(t.a); c->pool.push_back(t.b); }
@@ -169,7 +186,7 @@ struct PartHost {
   PmPart d{};
   uint64_t epoch_ctr = 0, fqn = 0, dummy_ctr = 0;
   uint64_t maxq64 = 0;
-  std::unordered_map<uint64_t, std::vector<uint64_t>> cache;   // localCache (pir.go:120)
+  std::unordered_map<uint64_t, uint32_t> cache;   // localCache (pir.go:120): idx -> arena slot
 };
 
 struct Engine {
@@ -182,19 +199,24 @@ struct Engine {
   uint64_t FBN = 0, QMIP = 0, Support = 0, prepCount = 0;
   double prepTime = 0, storage = 0, commOn = 0, commOff = 0;
 
-  DevBuf db, parts_d, tag, pp, parity, ridx, rval, hist, fqn;
-  DevBuf offs, bits, subs_d, sb_d, res_d, qoffs, ans, out, dist, qvec;
-  HostBuf in_h, out_h;
+  DevBuf db, parts_d, tag, pp, parity, ridx, rval, hist, fqn, arena;
+  DevBuf offs, qoffs, ans_srv;
+  DevBuf subs_d, sb_d, bits, res_d, ans, qvec;
+  HostBuf desc_h, out_h;
   std::vector<PartHost> parts;
   uint32_t maxH = 0, maxPH = 0, maxSS = 0, maxRepl = 0;
 
   // per-step host view
   std::vector<PmSub> subs;
   std::vector<uint32_t> sb;
-  std::vector<uint64_t> sub_gid;   // global id per sub (REAL) for mapping
-  PmRes* res_h = nullptr;
-  uint64_t* out_h_words = nullptr;
-  float* dist_h = nullptr;
+  std::vector<uint64_t> sub_gid;   // global id per REAL / HOSTCACHE sub
+  PmOutHdr* hdr = nullptr;         // results of the last step (pinned)
+  uint64_t* rows = nullptr;
+  // batch_query scratch
+  std::vector<std::vector<uint64_t>> pq;
+  std::unordered_map<uint64_t, uint32_t> resp_map;
+  std::vector<uint64_t> resp_rows;
+  std::vector<float> resp_dist;
 };
 
 // NewPianoPIR parameterisation (pir.go:479-514) + NewPianoPIRClient (:130-175)
@@ -254,13 +276,15 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
     g->P = 1; g->PS = N;
   }
   g->parts.resize(g->P);
-  uint64_t off_tag = 0, off_pp = 0, off_par = 0, off_ridx = 0, off_rval = 0, off_hist = 0;
+  if (g->E > pmk::step_max_e()) return fail(PM_EINVAL, "DBEntrySize above the step kernel's LDS limit");
+  uint64_t off_tag = 0, off_pp = 0, off_par = 0, off_ridx = 0, off_rval = 0, off_hist = 0, off_ar = 0;
   for (uint64_t i = 0; i < g->P; ++i) {
     PartHost& ph = g->parts[i];
     uint64_t start = i * g->PS, end = std::min((i + 1) * g->PS, N);
     if (end <= start) return fail(PM_EINVAL, "empty partition (DBSize too small for BatchSize)");
     part_params(ph, end - start, F);
     if (ph.d.CS > 32768) return fail(PM_EINVAL, "ChunkSize > 32768 unsupported (16-bit prep offsets)");
+    if (ph.d.SS > pmk::step_max_ss()) return fail(PM_EINVAL, "SetSize above the step kernel's LDS limit");
     if ((uint64_t)ph.d.H >= (1ull << 29)) return fail(PM_EINVAL, "tag space >= 2^29 (util.go:161)");
     ph.d.row0 = start; ph.d.seed = seed; ph.d.idx = i;
     g->maxH = std::max(g->maxH, ph.d.H);
@@ -274,6 +298,8 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
     ph.d.ridx = (uint32_t*)(uintptr_t)off_ridx; off_ridx += (uint64_t)ph.d.SS * ph.d.Qpc;
     ph.d.rval = (uint64_t*)(uintptr_t)off_rval; off_rval += (uint64_t)ph.d.SS * ph.d.Qpc * g->E;
     ph.d.hist = (uint32_t*)(uintptr_t)off_hist; off_hist += ph.d.SS;
+    ph.d.arena = (uint64_t*)(uintptr_t)off_ar; off_ar += (uint64_t)ph.d.MaxQ * g->E;
+    ph.cache.reserve(ph.d.MaxQ * 2);
   }
   CHK(g->db.reserve(N * g->E * 8));
   HIPCHK(hipMemcpy(g->db.p, rawDB, N * g->E * 8, hipMemcpyHostToDevice));
@@ -284,6 +310,7 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
   CHK(g->rval.reserve(off_rval * 8));
   CHK(g->hist.reserve(off_hist * 4));
   CHK(g->fqn.reserve(g->P * 4));
+  CHK(g->arena.reserve(std::max<uint64_t>(8, off_ar * 8)));
   CHK(g->parts_d.reserve(g->P * sizeof(PmPart)));
   for (uint64_t i = 0; i < g->P; ++i) {
     PmPart& d = g->parts[i].d;
@@ -294,6 +321,7 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
     d.rval = g->rval.as<uint64_t>() + (uintptr_t)d.rval;
     d.hist = g->hist.as<uint32_t>() + (uintptr_t)d.hist;
     d.fqn = g->fqn.as<uint32_t>() + i;
+    d.arena = g->arena.as<uint64_t>() + (uintptr_t)d.arena;
   }
   HIPCHK(hipMemsetAsync(g->fqn.p, 0, g->P * 4, ctx->stream));
   HIPCHK(hipMemsetAsync(g->hist.p, 0, off_hist * 4, ctx->stream));
@@ -369,11 +397,12 @@ static int engine_prep(Engine* g, uint64_t p0, uint64_t p1) {
   return 0;
 }
 
-// One batched step: the sub-queries in g->subs (partition-major, ranges in
-// g->sb).  HOSTCACHE rows are provided in `cached` (nsub x E, only those rows
-// read).  Results land in g->res_h / g->out_h_words (/ g->dist_h if q != NULL).
-static int engine_step(Engine* g, const std::vector<std::vector<uint64_t>>& cached, const float* q,
-                       uint32_t dim) {
+// One batched step over the sub-queries in g->subs (partition-major, ranges in
+// g->sb): k_match -> k_resolve -> k_answer -> k_chain.  The descriptor is
+// read zero-copy from pinned host memory and the results (status header +
+// entry + L2 distance to q) are written by the GPU straight into pinned host
+// memory, so a step costs four launches and one stream synchronisation.
+static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
   pm_ctx* c = g->ctx;
   hipStream_t st = c->stream;
   const uint32_t nsub = (uint32_t)g->subs.size();
@@ -384,87 +413,72 @@ static int engine_step(Engine* g, const std::vector<std::vector<uint64_t>>& cach
   CHK(g->sb_d.reserve((g->P + 1) * 4));
   CHK(g->bits.reserve((uint64_t)nsub * words * 8));
   CHK(g->res_d.reserve(nsub * sizeof(PmRes)));
-  CHK(g->qoffs.reserve((uint64_t)nsub * g->maxSS * 4));
   CHK(g->ans.reserve((uint64_t)nsub * E * 8));
-  CHK(g->out.reserve((uint64_t)nsub * E * 8));
-  CHK(g->dist.reserve((uint64_t)nsub * 4));
-  // pinned staging: subs | sb | cached rows
-  const size_t in_bytes = nsub * sizeof(PmSub) + (g->P + 1) * 4 + 16;
-  bool any_cached = false;
-  for (auto& s : g->subs) any_cached |= (s.kind == SUB_HOSTCACHE);
-  const size_t cached_bytes = any_cached ? (size_t)nsub * E * 8 : 0;
-  CHK(g->in_h.reserve(in_bytes + cached_bytes));
-  char* ip = g->in_h.as<char>();
-  memcpy(ip, g->subs.data(), nsub * sizeof(PmSub));
-  memcpy(ip + nsub * sizeof(PmSub), g->sb.data(), (g->P + 1) * 4);
-  HIPCHK(hipMemcpyAsync(g->subs_d.p, ip, nsub * sizeof(PmSub), hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemcpyAsync(g->sb_d.p, ip + nsub * sizeof(PmSub), (g->P + 1) * 4, hipMemcpyHostToDevice, st));
-  if (any_cached) {
-    uint64_t* cw = (uint64_t*)(ip + in_bytes);
-    for (uint32_t s = 0; s < nsub; ++s)
-      if (g->subs[s].kind == SUB_HOSTCACHE) {
-        memcpy(cw + (uint64_t)s * E, cached[s].data(), E * 8);
-        HIPCHK(hipMemcpyAsync(g->out.as<uint64_t>() + (uint64_t)s * E, cw + (uint64_t)s * E, E * 8,
-                              hipMemcpyHostToDevice, st));
-      }
-  }
-  const PmPart* dp = g->parts_d.as<PmPart>();
-  const PmSub* ds = g->subs_d.as<PmSub>();
-  const uint32_t* dsb = g->sb_d.as<uint32_t>();
-  PmRes* dr = g->res_d.as<PmRes>();
+  const size_t dsub = nsub * sizeof(PmSub);
+  CHK(g->desc_h.reserve(dsub + (g->P + 1) * 4));
+  CHK(g->out_h.reserve(nsub * sizeof(PmOutHdr) + (size_t)nsub * E * 8));
+  char* dh = g->desc_h.as<char>();
+  memcpy(dh, g->subs.data(), dsub);
+  memcpy(dh + dsub, g->sb.data(), (g->P + 1) * 4);
+  PmStep S{};
+  S.parts = g->parts_d.as<PmPart>();
+  S.subs_h = (const PmSub*)dh;
+  S.sb_h = (const uint32_t*)(dh + dsub);
+  S.subs = g->subs_d.as<PmSub>();
+  S.sb = g->sb_d.as<uint32_t>();
+  S.bits = g->bits.as<uint64_t>();
+  S.res = g->res_d.as<PmRes>();
+  S.ans = g->ans.as<uint64_t>();
+  S.db = g->db.as<uint64_t>();
+  S.q = q_dev;
+  S.hdr_h = g->out_h.as<PmOutHdr>();
+  S.rows_h = (uint64_t*)(g->out_h.as<char>() + nsub * sizeof(PmOutHdr));
+  S.words = words; S.E = (uint32_t)E; S.dim = q_dev ? dim : 0; S.nsub = nsub; S.np = (uint32_t)g->P;
   uint32_t nreal = 0;
-  for (auto& s : g->subs) nreal += s.kind == SUB_REAL;
-  double match_aes = (double)nreal * g->maxPH;
-  c->timed("hint_match", match_aes, [&] { pmk::hint_match(st, dp, ds, nsub, g->maxPH, g->bits.as<uint64_t>(), words); });
-  c->timed("resolve", 0, [&] {
-    pmk::resolve(st, dp, (int)g->P, ds, dsb, g->bits.as<uint64_t>(), words, dr, g->qoffs.as<uint32_t>(), g->maxSS);
-  });
-  double ans_bytes = 0;
-  for (auto& s : g->subs)
-    if (s.kind == SUB_REAL || s.kind == SUB_DUMMY) {
-      const PmPart& d = g->parts[s.part].d;
-      ans_bytes += (double)d.SS * (E * 8 + 4) + E * 8;
+  for (auto& x : g->subs) nreal += x.kind == SUB_REAL;
+  c->timed("hint_match", (double)nreal * g->maxPH, [&] { pmk::step_match(st, S, g->maxPH); }, 2);
+  c->timed("resolve", 0, [&] { pmk::step_resolve(st, S); }, 2);
+  if (c->debug_sync) {   // validate every resolution record before k_answer consumes it
+    std::vector<PmRes> rr(nsub);
+    HIPCHK(hipMemcpy(rr.data(), S.res, nsub * sizeof(PmRes), hipMemcpyDeviceToHost));
+    for (uint32_t s = 0; s < nsub; ++s) {
+      const PmPart& d = g->parts[g->subs[s].part].d;
+      const PmRes& r = rr[s];
+      const bool bad = (r.status == ST_OK && (r.hit >= d.PH || r.slot >= d.MaxQ || r.chunk >= d.SS || r.ing >= d.Qpc)) ||
+                       (r.status == ST_CACHED && r.slot >= d.MaxQ) || (r.status == ST_DUP && r.slot >= nsub) ||
+                       (r.status > ST_SKIP) || (r.status > ST_ERANGE && r.status < ST_DUMMY);
+      fprintf(stderr, "[pm] res s=%u part=%u kind=%u idx=%lu -> st=%u hit=%u chunk=%u ing=%u tag=%u pp=%u slot=%u flags=%u%s\n",
+              s, g->subs[s].part, g->subs[s].kind, (unsigned long)g->subs[s].idx, r.status, r.hit, r.chunk, r.ing,
+              r.tag, r.pp, r.slot, r.flags, bad ? "  <-- BAD" : "");
     }
-  c->timed("answer", ans_bytes, [&] {
-    pmk::answer(st, dp, ds, dr, nsub, g->qoffs.as<uint32_t>(), g->maxSS, g->db.as<uint64_t>(), (uint32_t)E,
-                g->ans.as<uint64_t>());
-  });
-  c->timed("decode", 0, [&] {
-    pmk::decode(st, dp, (int)g->P, ds, dsb, dr, g->ans.as<uint64_t>(), (uint32_t)E, g->out.as<uint64_t>());
-  });
-  if (q) {
-    HIPCHK(hipMemcpyAsync(g->qvec.p, q, dim * 4, hipMemcpyHostToDevice, st));
-    c->timed("l2_rows", (double)nsub * dim * 4, [&] {
-      pmk::l2_rows(st, (const float*)g->out.p, E * 2, nsub, nullptr, g->qvec.as<float>(), dim, g->dist.as<float>());
-    });
   }
+  double ans_bytes = 0;
+  for (auto& x : g->subs)
+    if (x.kind == SUB_REAL || x.kind == SUB_DUMMY) ans_bytes += (double)g->parts[x.part].d.SS * E * 8;
+  c->timed("answer", ans_bytes, [&] { pmk::step_answer(st, S); }, 2);
+  c->timed("chain", 0, [&] { pmk::step_chain(st, S); }, 2);
   HIPCHK(hipGetLastError());
-  const size_t ob = nsub * sizeof(PmRes) + (size_t)nsub * E * 8 + (size_t)nsub * 4;
-  CHK(g->out_h.reserve(ob));
-  char* op = g->out_h.as<char>();
-  HIPCHK(hipMemcpyAsync(op, dr, nsub * sizeof(PmRes), hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(op + nsub * sizeof(PmRes), g->out.p, (size_t)nsub * E * 8, hipMemcpyDeviceToHost, st));
-  if (q)
-    HIPCHK(hipMemcpyAsync(op + nsub * sizeof(PmRes) + (size_t)nsub * E * 8, g->dist.p, nsub * 4,
-                          hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
-  g->res_h = (PmRes*)op;
-  g->out_h_words = (uint64_t*)(op + nsub * sizeof(PmRes));
-  g->dist_h = q ? (float*)(op + nsub * sizeof(PmRes) + (size_t)nsub * E * 8) : nullptr;
-  // host mirrors: FinishedQueryNum and localCache (pir.go:469-470)
+  g->hdr = S.hdr_h;
+  g->rows = S.rows_h;
+  // host mirrors: FinishedQueryNum and the localCache index (pir.go:469-470);
+  // in-step cache hits copy the earlier response
   for (uint32_t s = 0; s < nsub; ++s) {
-    if (g->res_h[s].status != ST_OK) continue;
-    PartHost& ph = g->parts[g->subs[s].part];
-    ph.fqn++;
-    const uint64_t* w = g->out_h_words + (uint64_t)s * E;
-    ph.cache[g->subs[s].idx] = std::vector<uint64_t>(w, w + E);
+    const PmOutHdr& h = g->hdr[s];
+    if (h.status == ST_OK) {
+      PartHost& ph = g->parts[g->subs[s].part];
+      ph.fqn++;
+      ph.cache[g->subs[s].idx] = h.ref;
+    } else if (h.status == ST_DUP) {
+      memcpy(g->rows + (uint64_t)s * E, g->rows + (uint64_t)h.ref * E, E * 8);
+      g->hdr[s].dist = g->hdr[h.ref].dist;
+    }
   }
   return 0;
 }
 
 // Append one sub-query of partition p to the step being built.
-static void add_sub(Engine* g, uint32_t p, bool real, uint64_t local, uint64_t gid,
-                    std::vector<std::vector<uint64_t>>& cached) {
+static void add_sub(Engine* g, uint32_t p, bool real, uint64_t local, uint64_t gid) {
   PartHost& ph = g->parts[p];
   PmSub s{p, SUB_NONE, 0};
   if (!real) {
@@ -472,11 +486,10 @@ static void add_sub(Engine* g, uint32_t p, bool real, uint64_t local, uint64_t g
   } else {
     s.kind = SUB_REAL; s.idx = local;
     auto it = ph.cache.find(local);
-    if (it != ph.cache.end()) { s.kind = SUB_HOSTCACHE; cached.resize(g->subs.size() + 1); cached.back() = it->second; }
+    if (it != ph.cache.end()) { s.kind = SUB_HOSTCACHE; s.idx = it->second; }
   }
   g->subs.push_back(s);
   g->sub_gid.push_back(gid);
-  if (cached.size() < g->subs.size()) cached.resize(g->subs.size());
 }
 static void begin_step(Engine* g) {
   g->subs.clear(); g->sub_gid.clear();
@@ -526,18 +539,12 @@ extern "C" int pm_pir_query(pm_pir* h, uint64_t idx, int real, uint64_t* out, in
   if (ph.fqn == ph.maxq64) CHK(engine_prep(g, 0, 1));
   memset(out, 0, g->E * 8);
   if (real && idx >= ph.d.N) { if (status) *status = PM_Q_ERANGE; return 0; }
-  std::vector<std::vector<uint64_t>> cached;
   begin_step(g);
-  add_sub(g, 0, real != 0, idx, idx, cached);
+  add_sub(g, 0, real != 0, idx, idx);
   close_partition(g, 0);
-  if (g->subs[0].kind == SUB_HOSTCACHE) {   // local cache hit (pir.go:381-383)
-    memcpy(out, cached[0].data(), g->E * 8);
-    if (status) *status = PM_Q_OK;
-    return 0;
-  }
-  CHK(engine_step(g, cached, nullptr, 0));
-  const uint32_t st = g->res_h[0].status;
-  if (st == ST_OK || st == ST_DUP) memcpy(out, g->out_h_words, g->E * 8);
+  CHK(engine_step(g, nullptr, 0));
+  const uint32_t st = g->hdr[0].status;
+  if (st == ST_OK || st == ST_DUP || st == ST_CACHED) memcpy(out, g->rows, g->E * 8);
   if (status) *status = status_to_api(st);
   return 0;
 }
@@ -557,15 +564,15 @@ extern "C" int pm_pir_server_answer(pm_pir* h, const uint32_t* offsets, uint64_t
   const PmPart& d = g->parts[0].d;
   if (nq == 0) return 0;
   CHK(g->qoffs.reserve(nq * d.SS * 4));
-  CHK(g->ans.reserve(nq * g->E * 8));
+  CHK(g->ans_srv.reserve(nq * g->E * 8));
   CHK(upload_parts(g));
   HIPCHK(hipMemcpyAsync(g->qoffs.p, offsets, nq * d.SS * 4, hipMemcpyHostToDevice, c->stream));
   c->timed("answer", (double)nq * (d.SS * (g->E * 8 + 4) + g->E * 8), [&] {
     pmk::server_answer(c->stream, g->parts_d.as<PmPart>(), g->qoffs.as<uint32_t>(), (uint32_t)nq, d.SS,
-                       g->db.as<uint64_t>(), (uint32_t)g->E, g->ans.as<uint64_t>());
+                       g->db.as<uint64_t>(), (uint32_t)g->E, g->ans_srv.as<uint64_t>());
   });
   HIPCHK(hipGetLastError());
-  HIPCHK(hipMemcpyAsync(out, g->ans.p, nq * g->E * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(out, g->ans_srv.p, nq * g->E * 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   return 0;
 }
@@ -640,72 +647,75 @@ extern "C" int pm_batchpir_dummy_preprocessing(pm_batchpir* h) {   // batch-pir.
 }
 
 // Query (batch-pir.go:170-248).  Partitions whose FinishedQueryNum cannot reach
-// MaxQueryNum inside this batch run as one fused step; the rest replay the
-// reference's per-sub-query re-preprocessing check (pir.go:527-530) one
-// sub-query at a time.
-static int batch_query(Engine* g, const uint64_t* idx, uint64_t n, uint64_t* out, const float* q,
+// MaxQueryNum inside this batch run as fused steps (at most
+// step_max_sub_per_part() sub-queries per partition per step); the rest replay
+// the reference's per-sub-query re-preprocessing check (pir.go:527-530) one
+// sub-query at a time.  q_dev / dist_out: optional L2 of every answer to q.
+static int batch_query(Engine* g, const uint64_t* idx, uint64_t n, uint64_t* out, const float* q_dev,
                        uint32_t dim, float* dist_out) {
   const uint64_t E = g->E, P = g->P;
   for (uint64_t i = 0; i < n; ++i)
     if (idx[i] >= g->N) return fail(PM_EINVAL, "id " + std::to_string(idx[i]) + " >= DBSize");
   const uint64_t qn = n / P;
-  std::vector<std::vector<uint64_t>> pq(P);
-  for (uint64_t i = 0; i < n; ++i) pq[idx[i] / g->PS].push_back(idx[i]);
-  for (auto& v : pq) while (v.size() < qn) v.push_back(kDefaultValue);
+  g->pq.resize(P);
+  for (auto& v : g->pq) v.clear();
+  for (uint64_t i = 0; i < n; ++i) g->pq[idx[i] / g->PS].push_back(idx[i]);
+  for (auto& v : g->pq) while (v.size() < qn) v.push_back(kDefaultValue);
   // responses[id] = last response made for it (batch-pir.go:187,213)
-  std::unordered_map<uint64_t, std::pair<std::vector<uint64_t>, float>> responses;
+  g->resp_map.clear();
+  size_t nresp = 0;
+  g->resp_rows.resize(std::max<size_t>(g->resp_rows.size(), n * E));
+  g->resp_dist.resize(std::max<size_t>(g->resp_dist.size(), n));
   auto collect = [&]() {
     for (size_t s = 0; s < g->subs.size(); ++s) {
-      const PmSub& sb = g->subs[s];
-      if (sb.kind != SUB_REAL && sb.kind != SUB_HOSTCACHE) continue;
-      const uint64_t* w = g->out_h_words + (uint64_t)s * E;
-      responses[g->sub_gid[s]] = {std::vector<uint64_t>(w, w + E), g->dist_h ? g->dist_h[s] : 0.0f};
+      const uint32_t k = g->subs[s].kind;
+      if (k != SUB_REAL && k != SUB_HOSTCACHE) continue;
+      auto ins = g->resp_map.emplace(g->sub_gid[s], (uint32_t)nresp);
+      if (ins.second) ++nresp;
+      const uint32_t slot = ins.first->second;
+      memcpy(&g->resp_rows[(size_t)slot * E], g->rows + (uint64_t)s * E, E * 8);
+      g->resp_dist[slot] = g->hdr[s].dist;
     }
   };
-  std::vector<std::vector<uint64_t>> cached;
-  // fast partitions, in rounds of at most kStepPerPart sub-queries per
-  // partition (the resolve kernel tracks that many refreshed hints per step)
-  std::vector<bool> slow(P, false);
+  std::vector<char> slow(P, 0);
   for (uint64_t p = 0; p < P; ++p) {
     uint64_t nreal = 0;
-    for (uint64_t j = 0; j < qn; ++j) nreal += pq[p][j] != kDefaultValue;
+    for (uint64_t j = 0; j < qn; ++j) nreal += g->pq[p][j] != kDefaultValue;
     const PartHost& ph = g->parts[p];
     slow[p] = qn && ph.fqn + nreal >= ph.maxq64;
   }
-  const uint64_t kStepPerPart = 256;
-  for (uint64_t j0 = 0; j0 < qn; j0 += kStepPerPart) {
-    const uint64_t j1 = std::min(qn, j0 + kStepPerPart);
-    cached.clear();
+  const uint64_t kStep = pmk::step_max_sub_per_part();
+  for (uint64_t j0 = 0; j0 < qn; j0 += kStep) {
+    const uint64_t j1 = std::min(qn, j0 + kStep);
     begin_step(g);
     for (uint64_t p = 0; p < P; ++p) {
       if (!slow[p])
         for (uint64_t j = j0; j < j1; ++j) {
-          const uint64_t id = pq[p][j];
-          add_sub(g, (uint32_t)p, id != kDefaultValue, id - p * g->PS, id, cached);
+          const uint64_t id = g->pq[p][j];
+          add_sub(g, (uint32_t)p, id != kDefaultValue, id - p * g->PS, id);
         }
       close_partition(g, (uint32_t)p);
     }
-    if (!g->subs.empty()) { CHK(engine_step(g, cached, q, dim)); collect(); }
+    if (!g->subs.empty()) { CHK(engine_step(g, q_dev, dim)); collect(); }
   }
   for (uint64_t p = 0; p < P; ++p) {
     if (!slow[p]) continue;
     for (uint64_t j = 0; j < qn; ++j) {
       PartHost& ph = g->parts[p];
       if (ph.fqn == ph.maxq64) CHK(engine_prep(g, p, p + 1));
-      cached.clear();
       begin_step(g);
-      const uint64_t id = pq[p][j];
-      add_sub(g, (uint32_t)p, id != kDefaultValue, id - p * g->PS, id, cached);
+      const uint64_t id = g->pq[p][j];
+      add_sub(g, (uint32_t)p, id != kDefaultValue, id - p * g->PS, id);
       close_partition(g, (uint32_t)p);
-      CHK(engine_step(g, cached, q, dim));
+      CHK(engine_step(g, q_dev, dim));
       collect();
     }
   }
   for (uint64_t i = 0; i < n; ++i) {
-    auto it = responses.find(idx[i]);
-    if (it != responses.end()) {
-      memcpy(out + i * E, it->second.first.data(), E * 8);
-      if (dist_out) dist_out[i] = it->second.second;
+    auto it = g->resp_map.find(idx[i]);
+    if (it != g->resp_map.end()) {
+      memcpy(out + i * E, &g->resp_rows[(size_t)it->second * E], E * 8);
+      if (dist_out) dist_out[i] = g->resp_dist[it->second];
     } else {
       memset(out + i * E, 0, E * 8);
       if (dist_out) dist_out[i] = 0;
@@ -949,7 +959,6 @@ static int get_vertex_info(pm_graph* g, const std::vector<int64_t>& ids, const f
       hipStream_t st = g->ctx->stream;
       CHK(g->dids.reserve(n * 4)); CHK(g->ddist.reserve(n * 4));
       HIPCHK(hipMemcpyAsync(g->dids.p, u.data(), n * 4, hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemcpyAsync(g->dq.p, q, g->dim * 4, hipMemcpyHostToDevice, st));
       g->ctx->timed("l2_rows", (double)n * g->dim * 4, [&] {
         pmk::l2_rows(st, g->dvec.as<float>(), g->dim, n, g->dids.as<uint32_t>(), g->dq.as<float>(), (uint32_t)g->dim, g->ddist.as<float>());
       });
@@ -961,8 +970,8 @@ static int get_vertex_info(pm_graph* g, const std::vector<int64_t>& ids, const f
   Engine* e = &g->pir->e;
   const uint64_t E = e->E;
   std::vector<uint64_t> qi(ids.begin(), ids.end()), resp(n * E);
-  if (q) CHK(e->qvec.reserve(g->dim * 4));
-  CHK(batch_query(e, qi.data(), n, resp.data(), q, (uint32_t)g->dim, q ? dist.data() : nullptr));
+  CHK(batch_query(e, qi.data(), n, resp.data(), q ? g->dq.as<float>() : nullptr, (uint32_t)g->dim,
+                  q ? dist.data() : nullptr));
   for (uint64_t i = 0; i < n; ++i) {
     const uint8_t* b = (const uint8_t*)&resp[i * E];
     nbs[i].resize(g->m);
@@ -987,11 +996,12 @@ extern "C" int pm_search_knn(pm_graph* g, const float* query, int k, int max_ste
   std::vector<VD> heap;
   hipStream_t st = g->ctx->stream;
   if (!benchmarking) {
+    // the query stays resident for every distance this search computes
+    HIPCHK(hipMemcpyAsync(g->dq.p, query, g->dim * 4, hipMemcpyHostToDevice, st));
     const uint64_t ns = g->start.size();
     std::vector<float> d(ns);
     if (ns) {
       CHK(g->ddist.reserve(ns * 4));
-      HIPCHK(hipMemcpyAsync(g->dq.p, query, g->dim * 4, hipMemcpyHostToDevice, st));
       g->ctx->timed("l2_rows", (double)ns * g->dim * 4, [&] {
         pmk::l2_rows(st, g->dvec.as<float>(), g->dim, ns, g->dstart.as<uint32_t>(), g->dq.as<float>(), (uint32_t)g->dim, g->ddist.as<float>());
       });

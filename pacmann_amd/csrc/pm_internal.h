@@ -48,6 +48,7 @@ struct PmPart {
   uint64_t* rval;    // [SS*Qpc*E] replacementVal
   uint32_t* hist;    // [SS]  QueryHistogram
   uint32_t* fqn;     // [1]   FinishedQueryNum
+  uint64_t* arena;   // [MaxQ*E] localCache rows (pir.go:120), slot = FinishedQueryNum at answer time
 };
 
 // Sub-query kinds / statuses for one batched step.
@@ -58,17 +59,36 @@ enum : uint32_t {
 };
 struct PmSub {
   uint32_t part, kind;
-  uint64_t idx;   // local index in the partition (REAL) / dummy counter (DUMMY)
+  uint64_t idx;   // REAL: local index; DUMMY: dummy counter; HOSTCACHE: arena slot
 };
-// Per-sub-query resolution record written by the resolve kernel.
+// Per-sub-query resolution record written by k_resolve.
 struct PmRes {
   uint32_t status, hit, chunk, ing;   // ing = in-group index (QueryHistogram before)
-  uint32_t ref, pad0, pad1, pad2;     // ST_DUP: earlier sub-query holding the response
+  uint32_t tag, pp;                   // hit hint's tag / program point used for the expansion
+  uint32_t slot;                      // OK: arena slot; CACHED: arena slot; DUP: earlier sub
+  uint32_t flags;                     // bit 0: hint refreshed earlier in this step (k_chain)
 };
-
-struct Launch {   // per-step scalar launch arguments
+// Per-sub-query result header, written by the GPU into pinned host memory.
+struct PmOutHdr {
+  uint32_t status, ref;
+  float dist;
+  uint32_t pad;
+};
+// Arguments of the four step kernels (pm_query.hip).
+struct PmStep {
+  const PmPart* parts;
+  const PmSub* subs_h;    // pinned host descriptor, read zero-copy by k_match
+  const uint32_t* sb_h;   // sub_begin[np+1] (pinned host)
+  PmSub* subs;            // device copies
+  uint32_t* sb;
+  uint64_t* bits;         // [nsub][words] hint-match bits
+  PmRes* res;             // [nsub]
+  uint64_t* ans;          // [nsub][E] raw answers of chained sub-queries
   const uint64_t* db;
-  uint32_t E, EX;   // words per entry, XOR width (E & ~3, xorSlices semantics)
+  const float* q;         // search query (device) or null
+  PmOutHdr* hdr_h;        // pinned host outputs
+  uint64_t* rows_h;
+  uint32_t words, E, dim, nsub, np, pad;
 };
 
 }  // namespace pm
@@ -84,17 +104,13 @@ void prep_fold(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxH, 
                const uint16_t* offs, uint64_t offs_stride, const uint64_t* db, uint32_t E);
 void prep_repl(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxRepl,
                const uint64_t* db, uint32_t E);
-void hint_match(hipStream_t st, const PmPart* dparts, const PmSub* subs, uint32_t nsub,
-                uint32_t maxPH, uint64_t* bits, uint32_t words);
-void resolve(hipStream_t st, const PmPart* dparts, int nparts, const PmSub* subs,
-             const uint32_t* sub_begin, const uint64_t* bits, uint32_t words, PmRes* res,
-             uint32_t* qoffs, uint32_t maxSS);
-void answer(hipStream_t st, const PmPart* dparts, const PmSub* subs, const PmRes* res,
-            uint32_t nsub, const uint32_t* qoffs, uint32_t maxSS, const uint64_t* db, uint32_t E,
-            uint64_t* ans);
-void decode(hipStream_t st, const PmPart* dparts, int nparts, const PmSub* subs,
-            const uint32_t* sub_begin, const PmRes* res, const uint64_t* ans, uint32_t E,
-            uint64_t* out);
+void step_match(hipStream_t st, const PmStep& S, uint32_t maxPH);
+void step_resolve(hipStream_t st, const PmStep& S);
+void step_answer(hipStream_t st, const PmStep& S);
+void step_chain(hipStream_t st, const PmStep& S);
+uint32_t step_max_sub_per_part();
+uint32_t step_max_ss();
+uint32_t step_max_e();
 void server_answer(hipStream_t st, const PmPart* dpart, const uint32_t* offs, uint32_t nq,
                    uint32_t SS, const uint64_t* db, uint32_t E, uint64_t* out);
 void l2_rows(hipStream_t st, const float* rows, uint64_t row_stride_floats, uint64_t nrows,

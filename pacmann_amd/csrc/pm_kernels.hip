@@ -5,8 +5,6 @@
 
 namespace pm {
 
-static constexpr AesTables kAesHost{};
-__device__ const AesTables g_aes = kAesHost;
 
 __device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
   return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
@@ -129,181 +127,18 @@ __global__ void __launch_bounds__(kBlock) k_prep_init(const PmPart* __restrict__
   if (i == 0) *P.fqn = 0;
 }
 
-// ---------------------------------------------------------------------------
-// Online query, one batched step over every partition's sub-queries
-// (batch-pir.go:189-216 -> pir.go:354-471).
-// ---------------------------------------------------------------------------
-constexpr int kMatchHintsPerThread = 8;
-
-// HOT LOOP C (pir.go:404-414) against the state at the start of the step, for
-// every (real sub-query, primary hint) pair: one bit per hint.
-__global__ void __launch_bounds__(kBlock) k_hint_match(const PmPart* __restrict__ parts,
-                                                       const PmSub* __restrict__ subs,
-                                                       uint64_t* __restrict__ bits, uint32_t words) {
-  __shared__ uint32_t te[kTeLdsWords];
-  const PmSub sub = subs[blockIdx.y];
-  if (sub.kind != SUB_REAL) return;
-  const PmPart& P = parts[sub.part];
-  const uint32_t base = blockIdx.x * kBlock * kMatchHintsPerThread;
-  if (base >= P.PH) return;
-  aes_lds_init(te, g_aes.te0);
-  __syncthreads();
-  const AesLane A{te, threadIdx.x & 31u};
-  const uint32_t mask = P.CS - 1, chunk = (uint32_t)(sub.idx >> P.log2CS),
-                 offset = (uint32_t)(sub.idx & mask);
-  uint64_t* out = bits + (uint64_t)blockIdx.y * words;
-#pragma unroll 1
-  for (int k = 0; k < kMatchHintsPerThread; ++k) {
-    const uint32_t h = base + k * kBlock + threadIdx.x;
-    bool m = false;
-    if (h < P.PH) {
-      const uint32_t pp = P.pp[h];
-      m = ((prf_lo32(A, P.rk, P.tag[h], chunk) & mask) == offset) &&
-          (pp == kDefaultProgramPoint || (pp >> P.log2CS) != chunk);
-    }
-    const uint64_t b = __ballot(m);
-    if ((threadIdx.x & 63) == 0 && (h - (threadIdx.x & 63)) < P.PH) out[h >> 6] = b;
-  }
-}
-
-// Sequential part of Client.Query per partition: budget checks, first
-// matching hint (stale bits + re-evaluation of hints refreshed earlier in
-// this step), set expansion (HOT LOOP D, pir.go:424-427), programmed point and
-// replacement substitution (:430-439), refresh of tag / program point /
-// counters (:460-470).  Parities are refreshed by k_decode once the server
-// answer is in.  One workgroup per partition.
-constexpr int kMaxMod = 256;
-__global__ void __launch_bounds__(kBlock) k_resolve(const PmPart* __restrict__ parts,
-                                                    const PmSub* __restrict__ subs,
-                                                    const uint32_t* __restrict__ sub_begin,
-                                                    const uint64_t* __restrict__ bits, uint32_t words,
-                                                    PmRes* __restrict__ res,
-                                                    uint32_t* __restrict__ qoffs, uint32_t maxSS) {
-  __shared__ uint32_t te[kTeLdsWords];
-  __shared__ uint32_t mod_h[kMaxMod], mod_tag[kMaxMod], mod_pp[kMaxMod];
-  __shared__ uint32_t s_nmod, s_best, s_go, s_chunk, s_off, s_tag, s_pp, s_repl;
-  const uint32_t p = blockIdx.x;
-  const PmPart& P = parts[p];
-  const uint32_t b0 = sub_begin[p], b1 = sub_begin[p + 1];
-  if (b0 == b1) return;
-  aes_lds_init(te, g_aes.te0);
-  if (threadIdx.x == 0) s_nmod = 0;
-  __syncthreads();
-  const AesLane A{te, threadIdx.x & 31u};
-  const uint32_t mask = P.CS - 1, lg = P.log2CS;
-  for (uint32_t s = b0; s < b1; ++s) {
-    const PmSub sub = subs[s];
-    uint32_t* qo = qoffs + (uint64_t)s * maxSS;
-    if (sub.kind == SUB_DUMMY) {   // pir.go:363-371
-      for (uint32_t i = threadIdx.x; i < P.SS; i += kBlock)
-        qo[i] = (uint32_t)(hash4(P.seed, DOM_DUMMY, P.idx, sub.idx, i) & mask);
-      if (threadIdx.x == 0) res[s] = PmRes{ST_DUMMY, 0, 0, 0, 0, 0, 0, 0};
-      continue;
-    }
-    if (sub.kind != SUB_REAL) {
-      if (threadIdx.x == 0) res[s] = PmRes{sub.kind == SUB_HOSTCACHE ? ST_CACHED : ST_SKIP, 0, 0, 0, 0, 0, 0, 0};
-      continue;
-    }
-    // --- checks in reference order (thread 0), result broadcast via LDS ---
-    if (threadIdx.x == 0) {
-      uint32_t st = 0xffffffffu;
-      if (sub.idx >= P.N) st = ST_ERANGE;
-      if (st == 0xffffffffu)
-        for (uint32_t t = b0; t < s; ++t)
-          if (subs[t].kind == SUB_REAL && subs[t].idx == sub.idx && res[t].status == ST_OK) {
-            res[s] = PmRes{ST_DUP, 0, 0, 0, t, 0, 0, 0};
-            st = ST_DUP;
-            break;
-          }
-      const uint32_t chunk = (uint32_t)(sub.idx >> lg);
-      if (st == 0xffffffffu && *P.fqn >= P.MaxQ) st = ST_EBUDGET;
-      if (st == 0xffffffffu && P.hist[chunk] >= P.Qpc) st = ST_ECHUNK;
-      if (st != 0xffffffffu && st != ST_DUP) res[s] = PmRes{st, 0, 0, 0, 0, 0, 0, 0};
-      s_go = (st == 0xffffffffu);
-      s_chunk = chunk;
-      s_off = (uint32_t)(sub.idx & mask);
-      s_best = 0xffffffffu;
-    }
-    __syncthreads();
-    if (!s_go) { __syncthreads(); continue; }
-    const uint32_t chunk = s_chunk, offset = s_off, nmod = s_nmod;
-    // --- first set stale bit, skipping refreshed hints ---
-    const uint64_t* bw = bits + (uint64_t)s * words;
-    const uint32_t nw = (P.PH + 63) / 64;
-    for (uint32_t w = threadIdx.x; w < nw; w += kBlock) {
-      uint64_t v = bw[w];
-      if (v) {
-        for (uint32_t k = 0; k < nmod; ++k)
-          if ((mod_h[k] >> 6) == w) v &= ~(1ull << (mod_h[k] & 63));
-        if (v) { atomicMin(&s_best, w * 64 + (uint32_t)__builtin_ctzll(v)); break; }
-      }
-    }
-    // --- refreshed hints re-evaluated with their current tag / program point ---
-    for (uint32_t k = threadIdx.x; k < nmod; k += kBlock) {
-      const uint32_t pp = mod_pp[k];
-      if ((prf_lo32(A, P.rk, mod_tag[k], chunk) & mask) == offset &&
-          (pp == kDefaultProgramPoint || (pp >> lg) != chunk))
-        atomicMin(&s_best, mod_h[k]);
-    }
-    __syncthreads();
-    const uint32_t hit = s_best;
-    if (hit == 0xffffffffu) {   // pir.go:416-419
-      if (threadIdx.x == 0) res[s] = PmRes{ST_ENOHIT, 0, 0, 0, 0, 0, 0, 0};
-      __syncthreads();
-      continue;
-    }
-    if (threadIdx.x == 0) {
-      uint32_t tag = P.tag[hit], pp = P.pp[hit];
-      for (uint32_t k = 0; k < nmod; ++k)
-        if (mod_h[k] == hit) { tag = mod_tag[k]; pp = mod_pp[k]; }
-      const uint32_t ing = P.hist[chunk];
-      s_tag = tag;
-      s_pp = pp;
-      s_repl = P.ridx[chunk * P.Qpc + ing];
-      res[s] = PmRes{ST_OK, hit, chunk, ing, 0, 0, 0, 0};
-      // refresh (pir.go:460-470); parity in k_decode
-      const uint32_t ntag = P.tag[P.PH + chunk * P.Qpc + ing];
-      P.tag[hit] = ntag;
-      P.pp[hit] = (uint32_t)sub.idx;
-      *P.fqn += 1;
-      P.hist[chunk] = ing + 1;
-      uint32_t k = 0;
-      while (k < nmod && mod_h[k] != hit) ++k;
-      if (k < kMaxMod) {
-        mod_h[k] = hit; mod_tag[k] = ntag; mod_pp[k] = (uint32_t)sub.idx;
-        if (k == nmod) s_nmod = nmod + 1;
-      }
-    }
-    __syncthreads();
-    const uint32_t tag = s_tag, pp = s_pp, repl = s_repl;
-    for (uint32_t i = threadIdx.x; i < P.SS; i += kBlock) {
-      uint32_t o = prf_lo32(A, P.rk, tag, i) & mask;
-      if (pp != kDefaultProgramPoint && i == (pp >> lg)) o = pp & mask;
-      if (i == chunk) o = repl & mask;
-      qo[i] = o;
-    }
-    __syncthreads();
-  }
-}
-
-// PianoPIRServer.PrivateQuery (pir.go:65-88) for every sub-query that sends
-// one (real after resolution, and dummies): XOR of SetSize gathered rows.
-// One workgroup per sub-query: lanes = (row slice, 16-B segment); slices are
-// XOR-combined through LDS.
+// PianoPIRServer.PrivateQuery (pir.go:65-88) for nq client-supplied offset
+// sets: XOR of SetSize gathered rows.  One workgroup per offset set: lanes =
+// (row slice, 16-B segment); slices are XOR-combined through LDS.
 template <int W>
-__global__ void __launch_bounds__(kBlock) k_answer(const PmPart* __restrict__ parts,
-                                                   const PmSub* __restrict__ subs,
-                                                   const PmRes* __restrict__ res,
-                                                   const uint32_t* __restrict__ qoffs, uint32_t maxSS,
-                                                   const uint64_t* __restrict__ db, uint32_t E,
-                                                   uint64_t* __restrict__ ans) {
+__global__ void __launch_bounds__(kBlock) k_server_answer(const PmPart* __restrict__ parts,
+                                                          const uint32_t* __restrict__ qoffs,
+                                                          uint32_t maxSS,
+                                                          const uint64_t* __restrict__ db, uint32_t E,
+                                                          uint64_t* __restrict__ ans) {
   __shared__ uint64_t red[kBlock * 2];
   const uint32_t s = blockIdx.x;
-  if (res) {
-    const uint32_t st = res[s].status;
-    if (st != ST_OK && st != ST_DUMMY) return;
-  }
-  const PmPart& P = parts[subs ? subs[s].part : 0];
+  const PmPart& P = parts[0];
   const uint32_t EX = E & ~3u, NSEG = EX / W;
   const uint32_t* qo = qoffs + (uint64_t)s * maxSS;
   const uint64_t* base = db + P.row0 * E;
@@ -343,49 +178,6 @@ __global__ void __launch_bounds__(kBlock) k_answer(const PmPart* __restrict__ pa
     __syncthreads();
   }
   for (uint32_t w = EX + threadIdx.x; w < E; w += kBlock) out[w] = 0;
-}
-
-// Decode + parity refresh, in sub-query order per partition (pir.go:450-468):
-//   response = answer ^ replVal ^ primaryParity[hit]
-//   primaryParity[hit] = backupParity[chunk][ing] ^ response
-// Lane w owns word w of every entry, so consecutive sub-queries that hit the
-// same hint need no barrier.
-__global__ void __launch_bounds__(kBlock) k_decode(const PmPart* __restrict__ parts,
-                                                   const PmSub* __restrict__ subs,
-                                                   const uint32_t* __restrict__ sub_begin,
-                                                   const PmRes* __restrict__ res,
-                                                   const uint64_t* __restrict__ ans, uint32_t E,
-                                                   uint64_t* __restrict__ out) {
-  const uint32_t p = blockIdx.x;
-  const PmPart& P = parts[p];
-  const uint32_t b0 = sub_begin[p], b1 = sub_begin[p + 1];
-  const uint32_t EX = E & ~3u;
-  for (uint32_t s = b0; s < b1; ++s) {
-    const PmRes r = res[s];
-    uint64_t* o = out + (uint64_t)s * E;
-    if (r.status == ST_OK) {
-      const uint64_t slot = (uint64_t)r.chunk * P.Qpc + r.ing;
-      const uint64_t* rv = P.rval + slot * E;
-      const uint64_t* bp = P.parity + ((uint64_t)P.PH + slot) * E;
-      uint64_t* pp = P.parity + (uint64_t)r.hit * E;
-      const uint64_t* a = ans + (uint64_t)s * E;
-      for (uint32_t w = threadIdx.x; w < E; w += kBlock) {
-        if (w < EX) {
-          const uint64_t resp = a[w] ^ rv[w] ^ pp[w];
-          pp[w] = bp[w] ^ resp;
-          o[w] = resp;
-        } else {
-          pp[w] = bp[w];
-          o[w] = 0;
-        }
-      }
-    } else if (r.status == ST_DUP) {
-      const uint64_t* src = out + (uint64_t)r.ref * E;
-      for (uint32_t w = threadIdx.x; w < E; w += kBlock) o[w] = src[w];
-    } else if (r.status != ST_CACHED) {
-      for (uint32_t w = threadIdx.x; w < E; w += kBlock) o[w] = 0;
-    }
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -529,32 +321,12 @@ void prep_repl(hipStream_t st, const PmPart* d, int np, uint32_t maxRepl, const 
   hipLaunchKernelGGL(k_prep_repl, dim3(cdiv((uint64_t)maxRepl * E, kBlock), np), dim3(kBlock), 0, st,
                      d, db, E);
 }
-void hint_match(hipStream_t st, const PmPart* d, const PmSub* subs, uint32_t nsub, uint32_t maxPH,
-                uint64_t* bits, uint32_t words) {
-  hipLaunchKernelGGL(k_hint_match, dim3(cdiv(maxPH, kBlock * kMatchHintsPerThread), nsub),
-                     dim3(kBlock), 0, st, d, subs, bits, words);
-}
-void resolve(hipStream_t st, const PmPart* d, int np, const PmSub* subs, const uint32_t* sb,
-             const uint64_t* bits, uint32_t words, PmRes* res, uint32_t* qoffs, uint32_t maxSS) {
-  hipLaunchKernelGGL(k_resolve, dim3(np), dim3(kBlock), 0, st, d, subs, sb, bits, words, res, qoffs,
-                     maxSS);
-}
-void answer(hipStream_t st, const PmPart* d, const PmSub* subs, const PmRes* res, uint32_t nsub,
-            const uint32_t* qoffs, uint32_t maxSS, const uint64_t* db, uint32_t E, uint64_t* ans) {
-  if (E % 2 == 0)
-    hipLaunchKernelGGL(k_answer<2>, dim3(nsub), dim3(kBlock), 0, st, d, subs, res, qoffs, maxSS, db, E,
-                       ans);
-  else
-    hipLaunchKernelGGL(k_answer<1>, dim3(nsub), dim3(kBlock), 0, st, d, subs, res, qoffs, maxSS, db, E,
-                       ans);
-}
-void decode(hipStream_t st, const PmPart* d, int np, const PmSub* subs, const uint32_t* sb,
-            const PmRes* res, const uint64_t* ans, uint32_t E, uint64_t* out) {
-  hipLaunchKernelGGL(k_decode, dim3(np), dim3(kBlock), 0, st, d, subs, sb, res, ans, E, out);
-}
 void server_answer(hipStream_t st, const PmPart* d, const uint32_t* offs, uint32_t nq, uint32_t SS,
                    const uint64_t* db, uint32_t E, uint64_t* out) {
-  answer(st, d, nullptr, nullptr, nq, offs, SS, db, E, out);
+  if (E % 2 == 0)
+    hipLaunchKernelGGL(k_server_answer<2>, dim3(nq), dim3(kBlock), 0, st, d, offs, SS, db, E, out);
+  else
+    hipLaunchKernelGGL(k_server_answer<1>, dim3(nq), dim3(kBlock), 0, st, d, offs, SS, db, E, out);
 }
 void l2_rows(hipStream_t st, const float* rows, uint64_t stride, uint64_t nrows, const uint32_t* ids,
              const float* q, uint32_t dim, float* out) {
