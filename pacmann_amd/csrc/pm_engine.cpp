@@ -145,6 +145,11 @@ extern "C" int pm_ctx_create(int device, pm_ctx** out) {
   HIPCHK(hipGetDeviceCount(&n));
   if (device < 0 || device >= n) return fail(PM_EINVAL, "no such HIP device " + std::to_string(device));
   HIPCHK(hipSetDevice(device));
+  // Each online step ends in one host wait; spin instead of yielding so the
+  // host resumes the beam search as soon as the GPU finishes.  Ignored if the
+  // device is already initialised with other flags.
+  (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
+  (void)hipGetLastError();
   pm_ctx* c = new pm_ctx();
   c->device = device;
   const char* dbg = getenv("PM_DEBUG_SYNC");
@@ -199,8 +204,8 @@ struct Engine {
   uint64_t FBN = 0, QMIP = 0, Support = 0, prepCount = 0;
   double prepTime = 0, storage = 0, commOn = 0, commOff = 0;
 
-  DevBuf db, parts_d, tag, pp, parity, ridx, rval, hist, fqn, arena;
-  DevBuf offs, qoffs, ans_srv;
+  DevBuf db, parts_d, tag, pp, parity, ridx, rval, hist, fqn, arena, tab;
+  DevBuf qoffs, ans_srv;
   DevBuf subs_d, sb_d, bits, res_d, ans, qvec;
   HostBuf desc_h, out_h;
   std::vector<PartHost> parts;
@@ -277,7 +282,8 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
   }
   g->parts.resize(g->P);
   if (g->E > pmk::step_max_e()) return fail(PM_EINVAL, "DBEntrySize above the step kernel's LDS limit");
-  uint64_t off_tag = 0, off_pp = 0, off_par = 0, off_ridx = 0, off_rval = 0, off_hist = 0, off_ar = 0;
+  uint64_t off_tag = 0, off_pp = 0, off_par = 0, off_ridx = 0, off_rval = 0, off_hist = 0, off_ar = 0,
+           off_tab = 0;
   for (uint64_t i = 0; i < g->P; ++i) {
     PartHost& ph = g->parts[i];
     uint64_t start = i * g->PS, end = std::min((i + 1) * g->PS, N);
@@ -299,6 +305,7 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
     ph.d.rval = (uint64_t*)(uintptr_t)off_rval; off_rval += (uint64_t)ph.d.SS * ph.d.Qpc * g->E;
     ph.d.hist = (uint32_t*)(uintptr_t)off_hist; off_hist += ph.d.SS;
     ph.d.arena = (uint64_t*)(uintptr_t)off_ar; off_ar += (uint64_t)ph.d.MaxQ * g->E;
+    ph.d.tab = (uint16_t*)(uintptr_t)off_tab; off_tab += (uint64_t)ph.d.H * ph.d.SS;
     ph.cache.reserve(ph.d.MaxQ * 2);
   }
   CHK(g->db.reserve(N * g->E * 8));
@@ -311,6 +318,7 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
   CHK(g->hist.reserve(off_hist * 4));
   CHK(g->fqn.reserve(g->P * 4));
   CHK(g->arena.reserve(std::max<uint64_t>(8, off_ar * 8)));
+  CHK(g->tab.reserve(off_tab * 2));
   CHK(g->parts_d.reserve(g->P * sizeof(PmPart)));
   for (uint64_t i = 0; i < g->P; ++i) {
     PmPart& d = g->parts[i].d;
@@ -322,6 +330,7 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
     d.hist = g->hist.as<uint32_t>() + (uintptr_t)d.hist;
     d.fqn = g->fqn.as<uint32_t>() + i;
     d.arena = g->arena.as<uint64_t>() + (uintptr_t)d.arena;
+    d.tab = g->tab.as<uint16_t>() + (uintptr_t)d.tab;
   }
   HIPCHK(hipMemsetAsync(g->fqn.p, 0, g->P * 4, ctx->stream));
   HIPCHK(hipMemsetAsync(g->hist.p, 0, off_hist * 4, ctx->stream));
@@ -356,41 +365,25 @@ static int engine_prep(Engine* g, uint64_t p0, uint64_t p1) {
   const PmPart* dp = g->parts_d.as<PmPart>() + p0;
   const int np = (int)(p1 - p0);
   c->timed("prep_init", 0, [&] { pmk::prep_init(st, dp, np, g->maxH, g->maxRepl, (uint32_t)g->E, g->skipPrep); });
+  double aes = 0, fold = 0, repl = 0;
+  for (uint64_t i = p0; i < p1; ++i) {
+    const PmPart& d = g->parts[i].d;
+    aes += (double)d.H * d.SS;
+    // algorithmic fold bytes: hpc * SS (hint, chunk) pairs of one E-word entry
+    fold += ((double)d.PH + (double)(d.SS - 1) * d.Qpc) * d.SS * (double)g->E * 8;
+    repl += (double)d.SS * d.Qpc * g->E * 8 * 2;
+  }
+  // the PRF table is built even by DummyPreprocessing: queries still evaluate the PRF
+  c->timed("prep_offsets", aes, [&] { pmk::prep_offsets(st, dp, np, g->maxH, g->maxSS); });
   if (g->skipPrep) {   // DummyPreprocessing (pir.go:520-523): zero hints
     for (uint64_t i = p0; i < p1; ++i) {
       const PmPart& d = g->parts[i].d;
       HIPCHK(hipMemsetAsync(d.parity, 0, (uint64_t)d.H * g->E * 8, st));
       HIPCHK(hipMemsetAsync(d.rval, 0, (uint64_t)d.SS * d.Qpc * g->E * 8, st));
     }
-    HIPCHK(hipStreamSynchronize(st));
-    return 0;
-  }
-  // group partitions so the 16-bit offset scratch stays within budget
-  const uint64_t per = (uint64_t)g->maxH * g->maxSS;
-  const uint64_t budget = 1ull << 30;
-  uint64_t group = std::max<uint64_t>(1, budget / (per * 2));
-  group = std::min<uint64_t>(group, (uint64_t)np);
-  CHK(g->offs.reserve(group * per * 2));
-  for (uint64_t a = p0; a < p1; a += group) {
-    const uint64_t b = std::min(p1, a + group);
-    const PmPart* dpa = g->parts_d.as<PmPart>() + a;
-    const int n = (int)(b - a);
-    double aes = 0, fold = 0, repl = 0;
-    for (uint64_t i = a; i < b; ++i) {
-      const PmPart& d = g->parts[i].d;
-      aes += (double)d.H * d.SS;
-      // algorithmic fold bytes: hpc * SS pairs of one E-word entry
-      fold += ((double)d.PH + (double)(d.SS - 1) * d.Qpc) * d.SS * (double)g->E * 8;
-      repl += (double)d.SS * d.Qpc * g->E * 8 * 2;
-    }
-    c->timed("prep_offsets", aes, [&] {
-      pmk::prep_offsets(st, dpa, n, g->maxH, g->maxSS, g->offs.as<uint16_t>(), per);
-    });
-    c->timed("prep_fold", fold, [&] {
-      pmk::prep_fold(st, dpa, n, g->maxH, g->maxSS, g->offs.as<uint16_t>(), per, g->db.as<uint64_t>(),
-                     (uint32_t)g->E);
-    });
-    c->timed("prep_repl", repl, [&] { pmk::prep_repl(st, dpa, n, g->maxRepl, g->db.as<uint64_t>(), (uint32_t)g->E); });
+  } else {
+    c->timed("prep_fold", fold, [&] { pmk::prep_fold(st, dp, np, g->maxH, g->db.as<uint64_t>(), (uint32_t)g->E); });
+    c->timed("prep_repl", repl, [&] { pmk::prep_repl(st, dp, np, g->maxRepl, g->db.as<uint64_t>(), (uint32_t)g->E); });
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(st));
@@ -677,6 +670,7 @@ static int batch_query(Engine* g, const uint64_t* idx, uint64_t n, uint64_t* out
       g->resp_dist[slot] = g->hdr[s].dist;
     }
   };
+  bool qn_done = false;
   std::vector<char> slow(P, 0);
   for (uint64_t p = 0; p < P; ++p) {
     uint64_t nreal = 0;
@@ -685,7 +679,36 @@ static int batch_query(Engine* g, const uint64_t* idx, uint64_t n, uint64_t* out
     slow[p] = qn && ph.fqn + nreal >= ph.maxq64;
   }
   const uint64_t kStep = pmk::step_max_sub_per_part();
-  for (uint64_t j0 = 0; j0 < qn; j0 += kStep) {
+  bool any_slow = false;
+  for (uint64_t p = 0; p < P; ++p) any_slow |= slow[p] != 0;
+  if (!any_slow && qn <= kStep && qn > 0) {
+    // common case: one fused step; map ids straight onto the pinned result rows
+    begin_step(g);
+    for (uint64_t p = 0; p < P; ++p) {
+      for (uint64_t j = 0; j < qn; ++j) {
+        const uint64_t id = g->pq[p][j];
+        add_sub(g, (uint32_t)p, id != kDefaultValue, id - p * g->PS, id);
+      }
+      close_partition(g, (uint32_t)p);
+    }
+    CHK(engine_step(g, q_dev, dim));
+    for (size_t s = 0; s < g->subs.size(); ++s) {
+      const uint32_t k = g->subs[s].kind;
+      if (k == SUB_REAL || k == SUB_HOSTCACHE) g->resp_map[g->sub_gid[s]] = (uint32_t)s;   // last wins
+    }
+    for (uint64_t i = 0; i < n; ++i) {
+      auto it = g->resp_map.find(idx[i]);
+      if (it != g->resp_map.end()) {
+        memcpy(out + i * E, g->rows + (uint64_t)it->second * E, E * 8);
+        if (dist_out) dist_out[i] = g->hdr[it->second].dist;
+      } else {
+        memset(out + i * E, 0, E * 8);
+        if (dist_out) dist_out[i] = 0;
+      }
+    }
+    qn_done = true;
+  }
+  for (uint64_t j0 = 0; !qn_done && j0 < qn; j0 += kStep) {
     const uint64_t j1 = std::min(qn, j0 + kStep);
     begin_step(g);
     for (uint64_t p = 0; p < P; ++p) {
@@ -711,7 +734,7 @@ static int batch_query(Engine* g, const uint64_t* idx, uint64_t n, uint64_t* out
       collect();
     }
   }
-  for (uint64_t i = 0; i < n; ++i) {
+  for (uint64_t i = 0; !qn_done && i < n; ++i) {
     auto it = g->resp_map.find(idx[i]);
     if (it != g->resp_map.end()) {
       memcpy(out + i * E, &g->resp_rows[(size_t)it->second * E], E * 8);
@@ -851,7 +874,6 @@ struct SplitMix {   // host id stream standing in for Go's global math/rand
   uint64_t intn(uint64_t n) { return next() % n; }
 };
 struct VD { float dist; int64_t id; };
-struct Known { std::vector<int64_t> nb; float dist; };
 
 struct pm_graph {
   pm_ctx* ctx = nullptr;
@@ -866,6 +888,17 @@ struct pm_graph {
   std::vector<uint64_t> start;   // StartVertices ids
   DevBuf dstart;
   uint64_t total = 0, succ = 0;
+  // SearchKNN scratch, reused across calls (no per-step allocation)
+  std::vector<int64_t> batch;
+  std::vector<uint64_t> qids, resp;
+  std::vector<float> dist, start_d;
+  std::vector<uint32_t> nb;                       // [len(batch)][m] of the last GetVertexInfo
+  std::unordered_map<int64_t, uint32_t> known;    // knownVertices: id -> slot
+  std::vector<uint32_t> known_nb;                 // [slot][m]
+  std::vector<float> known_dist;
+  std::vector<int64_t> known_id, known_reach;
+  std::vector<VD> heap, all;
+  std::vector<std::pair<VD, uint32_t>> fs;
   ~pm_graph() { delete pir; }
 };
 
@@ -943,45 +976,40 @@ static VD heap_pop(std::vector<VD>& h) {
   VD r = h.back(); h.pop_back(); return r;
 }
 
-// GetVertexInfo (private-search.go:441-506) with the L2 distance of every
-// returned vector to `q` computed on the GPU (k_l2_rows) next to the decode.
-static int get_vertex_info(pm_graph* g, const std::vector<int64_t>& ids, const float* q,
-                           std::vector<std::vector<int64_t>>& nbs, std::vector<float>& dist) {
-  g->total += ids.size();
-  const uint64_t n = ids.size();
-  nbs.assign(n, {});
-  dist.assign(n, 0.0f);
+// GetVertexInfo (private-search.go:441-506) for g->batch, with the L2 distance
+// of every returned vector to the resident query computed on the GPU next to
+// the decode (k_answer).  Fills g->nb and g->dist.
+static int get_vertex_info(pm_graph* g, bool with_q) {
+  const uint64_t n = g->batch.size(), m = g->m;
+  g->total += n;
+  g->nb.resize(n * m);
+  g->dist.assign(n, 0.0f);
   if (g->nonprivate) {
-    std::vector<uint32_t> u(ids.begin(), ids.end());
     for (uint64_t i = 0; i < n; ++i)
-      nbs[i].assign(&g->graph[(uint64_t)ids[i] * g->m], &g->graph[(uint64_t)ids[i] * g->m] + g->m);
-    if (q && n) {
+      memcpy(&g->nb[i * m], &g->graph[(uint64_t)g->batch[i] * m], m * 4);
+    if (with_q && n) {
       hipStream_t st = g->ctx->stream;
+      std::vector<uint32_t> u(g->batch.begin(), g->batch.end());
       CHK(g->dids.reserve(n * 4)); CHK(g->ddist.reserve(n * 4));
       HIPCHK(hipMemcpyAsync(g->dids.p, u.data(), n * 4, hipMemcpyHostToDevice, st));
       g->ctx->timed("l2_rows", (double)n * g->dim * 4, [&] {
         pmk::l2_rows(st, g->dvec.as<float>(), g->dim, n, g->dids.as<uint32_t>(), g->dq.as<float>(), (uint32_t)g->dim, g->ddist.as<float>());
       });
-      HIPCHK(hipMemcpyAsync(dist.data(), g->ddist.p, n * 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(g->dist.data(), g->ddist.p, n * 4, hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
     }
     return 0;
   }
   Engine* e = &g->pir->e;
   const uint64_t E = e->E;
-  std::vector<uint64_t> qi(ids.begin(), ids.end()), resp(n * E);
-  CHK(batch_query(e, qi.data(), n, resp.data(), q ? g->dq.as<float>() : nullptr, (uint32_t)g->dim,
-                  q ? dist.data() : nullptr));
-  for (uint64_t i = 0; i < n; ++i) {
-    const uint8_t* b = (const uint8_t*)&resp[i * E];
-    nbs[i].resize(g->m);
-    bool correct = true;
-    for (uint64_t j = 0; j < g->m; ++j) {
-      uint32_t t; memcpy(&t, b + (g->dim + j) * 4, 4);
-      nbs[i][j] = (int64_t)t;
-      if (t != g->graph[(uint64_t)ids[i] * g->m + j]) correct = false;
-    }
-    if (correct) g->succ++;
+  g->qids.assign(g->batch.begin(), g->batch.end());
+  g->resp.resize(n * E);
+  CHK(batch_query(e, g->qids.data(), n, g->resp.data(), with_q ? g->dq.as<float>() : nullptr,
+                  (uint32_t)g->dim, with_q ? g->dist.data() : nullptr));
+  for (uint64_t i = 0; i < n; ++i) {   // Entry2VectorAndNeighbors (private-search.go:418-439)
+    uint32_t* nbi = &g->nb[i * m];
+    memcpy(nbi, (const uint8_t*)&g->resp[i * E] + g->dim * 4, m * 4);
+    if (memcmp(nbi, &g->graph[(uint64_t)g->batch[i] * m], m * 4) == 0) g->succ++;
   }
   return 0;
 }
@@ -990,72 +1018,74 @@ static int get_vertex_info(pm_graph* g, const std::vector<int64_t>& ids, const f
 extern "C" int pm_search_knn(pm_graph* g, const float* query, int k, int max_step, int parallel,
                              int benchmarking, int64_t* ids_out, int64_t* steps_out) {
   if (!g->pir && !g->nonprivate) return fail(PM_EINVAL, "pm_graph_preprocess not called");
-  const int64_t n = (int64_t)g->n, m = (int64_t)g->m;
-  std::unordered_map<int64_t, int64_t> reach;
-  std::unordered_map<int64_t, Known> known;
-  std::vector<VD> heap;
+  const int64_t n = (int64_t)g->n;
+  const uint64_t m = g->m;
   hipStream_t st = g->ctx->stream;
+  g->known.clear();
+  g->known_nb.clear(); g->known_dist.clear(); g->known_id.clear(); g->known_reach.clear();
+  g->heap.clear();
+  auto add_known = [&](int64_t id, const uint32_t* nb, float d, int64_t reach) {
+    const uint32_t slot = (uint32_t)g->known_id.size();
+    g->known.emplace(id, slot);
+    g->known_nb.insert(g->known_nb.end(), nb, nb + m);
+    g->known_dist.push_back(d);
+    g->known_id.push_back(id);
+    g->known_reach.push_back(reach);
+  };
   if (!benchmarking) {
     // the query stays resident for every distance this search computes
     HIPCHK(hipMemcpyAsync(g->dq.p, query, g->dim * 4, hipMemcpyHostToDevice, st));
     const uint64_t ns = g->start.size();
-    std::vector<float> d(ns);
+    g->start_d.resize(ns);
     if (ns) {
       CHK(g->ddist.reserve(ns * 4));
       g->ctx->timed("l2_rows", (double)ns * g->dim * 4, [&] {
         pmk::l2_rows(st, g->dvec.as<float>(), g->dim, ns, g->dstart.as<uint32_t>(), g->dq.as<float>(), (uint32_t)g->dim, g->ddist.as<float>());
       });
-      HIPCHK(hipMemcpyAsync(d.data(), g->ddist.p, ns * 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(g->start_d.data(), g->ddist.p, ns * 4, hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
     }
-    std::vector<std::pair<VD, size_t>> fs;
-    for (size_t i = 0; i < ns; ++i) fs.push_back({{d[i], (int64_t)g->start[i]}, i});
-    std::stable_sort(fs.begin(), fs.end(), [](const auto& a, const auto& b) { return a.first.dist < b.first.dist; });
-    for (size_t i = 0; (int64_t)heap.size() < parallel && i < fs.size(); ++i) {
-      const int64_t id = fs[i].first.id;
-      if (known.count(id)) continue;
-      Known kv;
-      kv.nb.assign(&g->graph[(uint64_t)id * g->m], &g->graph[(uint64_t)id * g->m] + g->m);
-      kv.dist = fs[i].first.dist;
-      known[id] = std::move(kv);
-      heap_push(heap, fs[i].first);
-      reach[id] = 0;
+    g->fs.clear();
+    for (uint64_t i = 0; i < ns; ++i) g->fs.push_back({{g->start_d[i], (int64_t)g->start[i]}, (uint32_t)i});
+    std::stable_sort(g->fs.begin(), g->fs.end(), [](const auto& a, const auto& b) { return a.first.dist < b.first.dist; });
+    for (size_t i = 0; (int64_t)g->heap.size() < parallel && i < g->fs.size(); ++i) {
+      const int64_t id = g->fs[i].first.id;
+      if (g->known.count(id)) continue;
+      add_known(id, &g->graph[(uint64_t)id * m], g->fs[i].first.dist, 0);
+      heap_push(g->heap, g->fs[i].first);
     }
   }
-  std::vector<std::vector<int64_t>> nbs;
-  std::vector<float> dist;
   for (int step = 0; step < max_step; ++step) {
-    std::vector<int64_t> batch;
+    g->batch.clear();
     for (int r = 0; r < parallel; ++r) {
-      if (heap.empty() || benchmarking) {
-        for (int64_t i = 0; i < m; ++i) batch.push_back((int64_t)g->rng.intn((uint64_t)n));
+      if (g->heap.empty() || benchmarking) {
+        for (uint64_t i = 0; i < m; ++i) g->batch.push_back((int64_t)g->rng.intn((uint64_t)n));
       } else {
-        VD it = heap_pop(heap);
-        const Known& v = known[it.id];
-        batch.insert(batch.end(), v.nb.begin(), v.nb.end());
+        const VD it = heap_pop(g->heap);
+        const uint32_t* nb = &g->known_nb[(size_t)g->known[it.id] * m];
+        for (uint64_t i = 0; i < m; ++i) g->batch.push_back((int64_t)nb[i]);
       }
     }
-    CHK(get_vertex_info(g, batch, benchmarking ? nullptr : query, nbs, dist));
+    CHK(get_vertex_info(g, !benchmarking));
     if (benchmarking) continue;
-    for (size_t i = 0; i < batch.size(); ++i) {
-      const int64_t id = batch[i];
-      if (known.count(id)) continue;
+    for (size_t i = 0; i < g->batch.size(); ++i) {
+      const int64_t id = g->batch[i];
+      if (g->known.count(id)) continue;
+      const uint32_t* nb = &g->nb[i * m];
       bool ok = false;
-      for (auto x : nbs[i]) if (x != 0) { ok = true; break; }
+      for (uint64_t j = 0; j < m; ++j) if (nb[j] != 0) { ok = true; break; }
       if (!ok) continue;
-      reach[id] = step;
-      known[id] = Known{std::move(nbs[i]), dist[i]};
-      heap_push(heap, {dist[i], id});
+      add_known(id, nb, g->dist[i], step);
+      heap_push(g->heap, {g->dist[i], id});
     }
   }
-  std::vector<VD> all;
-  all.reserve(known.size());
-  for (auto& kv : known) all.push_back({kv.second.dist, kv.first});
-  std::sort(all.begin(), all.end(), [](const VD& a, const VD& b) {
+  g->all.clear();
+  for (size_t i = 0; i < g->known_id.size(); ++i) g->all.push_back({g->known_dist[i], g->known_id[i]});
+  std::sort(g->all.begin(), g->all.end(), [](const VD& a, const VD& b) {
     return a.dist < b.dist || (a.dist == b.dist && a.id < b.id); });
   for (int i = 0; i < k; ++i) {
-    if (i >= (int)all.size()) { ids_out[i] = -1; if (steps_out) steps_out[i] = -1; }
-    else { ids_out[i] = all[i].id; if (steps_out) steps_out[i] = reach[all[i].id]; }
+    if (i >= (int)g->all.size()) { ids_out[i] = -1; if (steps_out) steps_out[i] = -1; }
+    else { ids_out[i] = g->all[i].id; if (steps_out) steps_out[i] = g->known_reach[g->known[g->all[i].id]]; }
   }
   return 0;
 }

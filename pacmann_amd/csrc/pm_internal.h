@@ -49,6 +49,12 @@ struct PmPart {
   uint32_t* hist;    // [SS]  QueryHistogram
   uint32_t* fqn;     // [1]   FinishedQueryNum
   uint64_t* arena;   // [MaxQ*E] localCache rows (pir.go:120), slot = FinishedQueryNum at answer time
+  // PRF table: tab[c*H + t] = PRF(tag t, chunk c) & (CS-1) for every tag t in
+  // [0, H) and chunk c in [0, SS) (kSkip at a backup tag's own chunk).  Every
+  // tag a hint can carry is a hint index (primary tags start at h, a refresh
+  // hands over backup tag PH+g*Qpc+j), so this table, built once per
+  // preprocessing, holds every PRF value the online phase needs.
+  uint16_t* tab;
 };
 
 // Sub-query kinds / statuses for one batched step.
@@ -81,7 +87,7 @@ struct PmStep {
   const uint32_t* sb_h;   // sub_begin[np+1] (pinned host)
   PmSub* subs;            // device copies
   uint32_t* sb;
-  uint64_t* bits;         // [nsub][words] hint-match bits
+  uint64_t* bits;         // [nsub][words] hint-match bits (k_match -> k_resolve)
   PmRes* res;             // [nsub]
   uint64_t* ans;          // [nsub][E] raw answers of chained sub-queries
   const uint64_t* db;
@@ -98,10 +104,9 @@ namespace pmk {
 using namespace pm;
 void prep_init(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxH, uint32_t maxRepl,
                uint32_t E, bool zero_state);
-void prep_offsets(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxH, uint32_t maxSS,
-                  uint16_t* offs, uint64_t offs_stride);
-void prep_fold(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxH, uint32_t maxSS,
-               const uint16_t* offs, uint64_t offs_stride, const uint64_t* db, uint32_t E);
+void prep_offsets(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxH, uint32_t maxSS);
+void prep_fold(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxH, const uint64_t* db,
+               uint32_t E);
 void prep_repl(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxRepl,
                const uint64_t* db, uint32_t E);
 void step_match(hipStream_t st, const PmStep& S, uint32_t maxPH);

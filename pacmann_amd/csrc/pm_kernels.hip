@@ -12,18 +12,17 @@ __device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
 
 // ---------------------------------------------------------------------------
 // Client hint preprocessing (pir.go:267-352), split in two kernels:
-//   prep_offsets: off[c][h] = PRF(tag_h, c) & (CS-1) for every hint h and
+//   prep_offsets: tab[c][h] = PRF(tag_h, c) & (CS-1) for every hint h and
 //                 chunk c (HOT LOOP A/B's PRF), kSkip for a backup hint's own
-//                 chunk (pir.go:332-334).  AES-bound.
+//                 chunk (pir.go:332-334).  AES-bound.  The table stays resident
+//                 and serves every online PRF (PmPart::tab).
 //   prep_fold:    parity[h] = XOR_c chunk_c[off[c][h]]  (HOT LOOP A/B's
 //                 EntryXor), one lane per (hint, 16-B segment), parity held in
 //                 a register for the whole chunk sweep.  Gather-bound.
 // ---------------------------------------------------------------------------
 constexpr int kOffsChunksPerBlock = 16;
 
-__global__ void __launch_bounds__(kBlock) k_prep_offsets(const PmPart* __restrict__ parts,
-                                                         uint16_t* __restrict__ offs,
-                                                         uint64_t offs_stride) {
+__global__ void __launch_bounds__(kBlock) k_prep_offsets(const PmPart* __restrict__ parts) {
   __shared__ uint32_t te[kTeLdsWords];
   const PmPart& P = parts[blockIdx.z];
   const uint32_t H = P.H, SS = P.SS;
@@ -36,7 +35,7 @@ __global__ void __launch_bounds__(kBlock) k_prep_offsets(const PmPart* __restric
   if (h >= H) return;
   const uint32_t mask = P.CS - 1;
   const uint32_t own = h >= P.PH ? (h - P.PH) / P.Qpc : 0xffffffffu;
-  uint16_t* o = offs + blockIdx.z * offs_stride;
+  uint16_t* o = P.tab;
   const uint32_t c1 = min(SS, c0 + kOffsChunksPerBlock);
   for (uint32_t c = c0; c < c1; ++c) {
     uint16_t v = (uint16_t)(prf_lo32(A, P.rk, h, c) & mask);   // initial tag of hint h is h
@@ -46,8 +45,6 @@ __global__ void __launch_bounds__(kBlock) k_prep_offsets(const PmPart* __restric
 
 template <int W>   // 64-bit words per lane segment: 2 (16-B loads) or 1
 __global__ void __launch_bounds__(kBlock) k_prep_fold(const PmPart* __restrict__ parts,
-                                                      const uint16_t* __restrict__ offs,
-                                                      uint64_t offs_stride,
                                                       const uint64_t* __restrict__ db, uint32_t E) {
   const PmPart& P = parts[blockIdx.y];
   const uint32_t EX = E & ~3u, NSEG = EX / W;
@@ -59,7 +56,7 @@ __global__ void __launch_bounds__(kBlock) k_prep_fold(const PmPart* __restrict__
   }
   const uint32_t h = (uint32_t)(e / NSEG), seg = (uint32_t)(e % NSEG);
   if (h >= H) return;
-  const uint16_t* o = offs + blockIdx.y * offs_stride + h;
+  const uint16_t* o = P.tab + h;
   const uint64_t* base = db + (P.row0 * E) + (uint64_t)seg * W;
   const uint32_t CS = P.CS, SS = P.SS;
   const uint64_t N = P.N;
@@ -297,23 +294,21 @@ void prep_init(hipStream_t st, const PmPart* d, int np, uint32_t maxH, uint32_t 
   const uint32_t n = maxH > maxRepl ? maxH : maxRepl;
   hipLaunchKernelGGL(k_prep_init, dim3(cdiv(n, kBlock), np), dim3(kBlock), 0, st, d);
 }
-void prep_offsets(hipStream_t st, const PmPart* d, int np, uint32_t maxH, uint32_t maxSS,
-                  uint16_t* offs, uint64_t stride) {
+void prep_offsets(hipStream_t st, const PmPart* d, int np, uint32_t maxH, uint32_t maxSS) {
   hipLaunchKernelGGL(k_prep_offsets, dim3(cdiv(maxH, kBlock), cdiv(maxSS, kOffsChunksPerBlock), np),
-                     dim3(kBlock), 0, st, d, offs, stride);
+                     dim3(kBlock), 0, st, d);
 }
-void prep_fold(hipStream_t st, const PmPart* d, int np, uint32_t maxH, uint32_t, const uint16_t* offs,
-               uint64_t stride, const uint64_t* db, uint32_t E) {
+void prep_fold(hipStream_t st, const PmPart* d, int np, uint32_t maxH, const uint64_t* db, uint32_t E) {
   const uint32_t EX = E & ~3u;
   if (EX == 0) {
     hipLaunchKernelGGL(k_prep_fold<2>, dim3(cdiv((uint64_t)maxH * E, kBlock), np), dim3(kBlock), 0,
-                       st, d, offs, stride, db, E);
+                       st, d, db, E);
   } else if (E % 2 == 0) {
     hipLaunchKernelGGL(k_prep_fold<2>, dim3(cdiv((uint64_t)maxH * (EX / 2), kBlock), np),
-                       dim3(kBlock), 0, st, d, offs, stride, db, E);
+                       dim3(kBlock), 0, st, d, db, E);
   } else {
     hipLaunchKernelGGL(k_prep_fold<1>, dim3(cdiv((uint64_t)maxH * EX, kBlock), np), dim3(kBlock), 0,
-                       st, d, offs, stride, db, E);
+                       st, d, db, E);
   }
 }
 void prep_repl(hipStream_t st, const PmPart* d, int np, uint32_t maxRepl, const uint64_t* db,

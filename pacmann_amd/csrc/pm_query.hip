@@ -6,6 +6,10 @@
 //                           pair against the state at the start of the step:
 //                           one bit per hint.  Also stages the step descriptor
 //                           from pinned host memory into device memory.
+//
+// No AES runs here: every PRF(tag, chunk) & (CS-1) the online phase needs is a
+// lookup in the partition's resident PRF table (PmPart::tab, built by
+// k_prep_offsets), because every tag is a hint index in [0, H).
 //   k_resolve (1 WG/part.)  the sequential part of Client.Query: cache /
 //                           budget checks, first matching hint (stale bits +
 //                           re-evaluation of hints refreshed earlier in the
@@ -30,7 +34,6 @@ constexpr uint32_t kNone = 0xffffffffu;
 
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(kBlock) k_match(PmStep S) {
-  __shared__ uint32_t te[kTeLdsWords];
   __shared__ PmSub s_sub;
   const uint32_t s = blockIdx.y;
   if (threadIdx.x == 0) {
@@ -46,17 +49,14 @@ __global__ void __launch_bounds__(kBlock) k_match(PmStep S) {
   const PmPart& P = S.parts[sub.part];
   const uint32_t base = blockIdx.x * kBlock;
   if (base >= P.PH) return;
-  aes_lds_init(te, g_aes.te0);
-  __syncthreads();
-  const AesLane A{te, threadIdx.x & 31u};
   const uint32_t mask = P.CS - 1, chunk = (uint32_t)(sub.idx >> P.log2CS),
                  offset = (uint32_t)(sub.idx & mask);
+  const uint16_t* row = P.tab + (uint64_t)chunk * P.H;
   const uint32_t h = base + threadIdx.x;
   bool m = false;
-  if (h < P.PH) {
+  if (h < P.PH && sub.idx < P.N) {
     const uint32_t pp = P.pp[h];
-    m = ((prf_lo32(A, P.rk, P.tag[h], chunk) & mask) == offset) &&
-        (pp == kDefaultProgramPoint || (pp >> P.log2CS) != chunk);
+    m = row[P.tag[h]] == offset && (pp == kDefaultProgramPoint || (pp >> P.log2CS) != chunk);
   }
   const uint64_t b = __ballot(m);
   if ((threadIdx.x & 63) == 0 && (h - (threadIdx.x & 63)) < P.PH) S.bits[(uint64_t)s * S.words + (h >> 6)] = b;
@@ -89,7 +89,6 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t x) {
 constexpr int kMaxSubPerPart = 256;
 
 __global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
-  __shared__ uint32_t te[kTeLdsWords];
   __shared__ uint64_t s_idx[kMaxSubPerPart];
   __shared__ uint32_t s_kind[kMaxSubPerPart], s_chunk[kMaxSubPerPart], s_st[kMaxSubPerPart],
       s_hist0[kMaxSubPerPart], s_c1[kMaxSubPerPart], s_c2[kMaxSubPerPart], s_t1[kMaxSubPerPart],
@@ -101,7 +100,6 @@ __global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
   const uint32_t b0 = S.sb[p], n = S.sb[p + 1] - b0;
   if (n == 0) return;
   const uint32_t lg = P.log2CS, mask = P.CS - 1, nw = (P.PH + 63) / 64;
-  aes_lds_init(te, g_aes.te0);
   // --- phase 0: prefetch the partition's sub-queries and counters -----------
   for (uint32_t j = threadIdx.x; j < n; j += kBlock) {
     const PmSub sub = S.subs[b0 + j];
@@ -134,7 +132,6 @@ __global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
   volatile uint32_t* vmh = m_h;
   volatile uint32_t* vmt = m_tag;
   volatile uint32_t* vmp = m_pp;
-  const AesLane A{te, lane & 31u};
   uint32_t fqn = s_fqn, nmod = 0;
   for (uint32_t j = 0; j < n; ++j) {
     const uint32_t s = b0 + j, kind = s_kind[j];
@@ -183,7 +180,7 @@ __global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
           uint32_t cand = kNone;
           if (k < nmod) {
             const uint32_t pp = vmp[k];
-            if ((prf_lo32(A, P.rk, vmt[k], chunk) & mask) == off &&
+            if (P.tab[(uint64_t)chunk * P.H + vmt[k]] == off &&
                 (pp == kDefaultProgramPoint || (pp >> lg) != chunk))
               cand = vmh[k];
           }
@@ -258,7 +255,6 @@ enum : uint32_t { A_ZERO = 0, A_FINAL = 1, A_CHAINED = 2, A_CACHED = 3, A_DUMMY 
 
 template <int W>
 __global__ void __launch_bounds__(kAnsBlock) k_answer(PmStep S) {
-  __shared__ uint32_t te[kTeLdsWords];
   __shared__ uint32_t qo[kMaxSSLds];
   __shared__ uint64_t red[kAnsBlock * 2];
   __shared__ __attribute__((aligned(16))) RowBuf row;
@@ -274,12 +270,9 @@ __global__ void __launch_bounds__(kAnsBlock) k_answer(PmStep S) {
   const uint32_t mask = P.CS - 1, lg = P.log2CS;
   // ---- query set (pir.go:363-371 dummy; :424-444 real) -------------------
   if (mode == A_FINAL || mode == A_CHAINED) {
-    aes_lds_init(te, g_aes.te0);
-    __syncthreads();
-    const AesLane A{te, tid & 31u};
     const uint32_t pchunk = r.pp != kDefaultProgramPoint ? (r.pp >> lg) : kNone;
     for (uint32_t i = tid; i < P.SS; i += kAnsBlock) {
-      uint32_t o = prf_lo32(A, P.rk, r.tag, i) & mask;
+      uint32_t o = P.tab[(uint64_t)i * P.H + r.tag];
       if (i == pchunk) o = r.pp & mask;
       if (i == r.chunk) o = P.ridx[r.chunk * P.Qpc + r.ing] & mask;
       qo[i] = o;

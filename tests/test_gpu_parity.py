@@ -214,7 +214,8 @@ def test_batch_pir_basic(ctx, oracle):
     assert not got[2:].any()
 
 
-@pytest.mark.parametrize("N,E,B,n", [(200_000, 80, 32, 96), (50_000, 12, 8, 24), (30_000, 6, 32, 200)])
+@pytest.mark.parametrize("N,E,B,n", [(200_000, 80, 32, 96), (50_000, 12, 8, 24), (30_000, 6, 32, 200),
+                                     (30_000, 6, 4, 2000)])
 def test_batch_pir_sequence(ctx, oracle, N, E, B, n):
     """Many batches (duplicates, drops, dummies) through the batch layer's
     re-preprocessing trigger (batch-pir.go:239-245) and, for the last case,
