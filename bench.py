@@ -36,8 +36,9 @@ sys.path.insert(0, str(ROOT))
 N, DIM, M, K_TOP, STEP, PARALLEL, F = 1_000_000, 128, 32, 10, 20, 3, 8
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 METRIC = "private queries/sec + PIR-scan HBM GB/s, SIFT1M d=128 at 1/2/4/8 GPUs"
-KERNELS = ["prep_offsets", "prep_fold", "prep_repl", "hint_match", "resolve", "answer", "decode",
+KERNELS = ["prep_offsets", "prep_fold", "prep_repl", "hint_match", "resolve", "answer", "chain",
            "l2_rows"]
+HOST = ["host_search_knn", "host_batch_query", "host_step_launch", "host_step_wait", "host_step_post"]
 
 
 def make_data(rank: int):
@@ -124,6 +125,7 @@ def main():
     ctx.timing(False)
 
     ktime = {k: ctx.timing_get(k) for k in KERNELS}
+    htime = {k: ctx.timing_get(k) for k in HOST}
     if dist:
         import torch
         t = torch.tensor([elapsed], dtype=torch.float64)
@@ -168,6 +170,7 @@ def main():
         "preprocessing_s": round(stats["PreprocessingTime"], 6),
         "pir_answer": roof("answer"),
         "kernel_ms": {k: round(ktime[k][1], 3) for k in KERNELS},
+        "host_ms": {k: round(htime[k][1], 3) for k in HOST},
         "dominant_kernel": dom,
     }
     if not args.no_cpu_baseline and ws == 1:

@@ -20,6 +20,46 @@
 
 using namespace pm;
 
+// Open-addressing uint64 -> uint32 map with O(1) clear (generation stamps).
+// Replaces node-allocating std::unordered_map on the per-round host path
+// (knownVertices, the batch response map, the per-partition localCache index).
+struct FlatMap {
+  std::vector<uint64_t> key;
+  std::vector<uint32_t> val, gen;
+  uint32_t cur = 1, count = 0, mask = 0;
+  explicit FlatMap(uint32_t cap_pow2 = 256) { rehash(cap_pow2); }
+  static uint64_t mix(uint64_t x) { x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; return x; }
+  void rehash(uint32_t cap) {
+    std::vector<uint64_t> k0; std::vector<uint32_t> v0, g0;
+    k0.swap(key); v0.swap(val); g0.swap(gen);
+    key.assign(cap, 0); val.assign(cap, 0); gen.assign(cap, 0);
+    mask = cap - 1; count = 0;
+    const uint32_t old = cur; cur = 1;
+    for (size_t i = 0; i < k0.size(); ++i) if (g0[i] == old) put(k0[i], v0[i]);
+  }
+  void clear() { if (++cur == 0) { std::fill(gen.begin(), gen.end(), 0); cur = 1; } count = 0; }
+  void reserve(uint32_t n) { uint32_t c = (uint32_t)key.size(); while (c < 2 * n) c *= 2; if (c != key.size()) rehash(c); }
+  // returns pointer to the value (inserting `v` if absent) and whether it was inserted
+  uint32_t* find(uint64_t k) {
+    for (uint32_t i = (uint32_t)mix(k) & mask;; i = (i + 1) & mask) {
+      if (gen[i] != cur) return nullptr;
+      if (key[i] == k) return &val[i];
+    }
+  }
+  void put(uint64_t k, uint32_t v) {   // insert or overwrite
+    if (2 * (count + 1) > key.size()) rehash((uint32_t)key.size() * 2);
+    for (uint32_t i = (uint32_t)mix(k) & mask;; i = (i + 1) & mask) {
+      if (gen[i] != cur) { gen[i] = cur; key[i] = k; val[i] = v; ++count; return; }
+      if (key[i] == k) { val[i] = v; return; }
+    }
+  }
+  bool emplace(uint64_t k, uint32_t v) {   // insert if absent; true if inserted
+    if (find(k)) return false;
+    put(k, v);
+    return true;
+  }
+};
+
 // ---------------------------------------------------------------------------
 // errors
 // ---------------------------------------------------------------------------
@@ -110,6 +150,9 @@ struct pm_ctx {
   int timing = 0;   // 0 off, 1 preprocessing / leaf kernels, 2 also the per-step kernels
   bool debug_sync = false;   // PM_DEBUG_SYNC=1: synchronise after every launch (fault triage)
   std::string last_kernel;
+  // host-side wall-clock accumulators ("host_*" names in pm_timing_get)
+  std::unordered_map<std::string, std::pair<uint64_t, double>> host;
+  void host_add(const char* name, double ms) { auto& h = host[name]; h.first++; h.second += ms; }
   std::vector<TimedLaunch> launches;
   std::vector<hipEvent_t> pool;
   hipEvent_t ev() {
@@ -166,12 +209,21 @@ extern "C" int pm_timing_reset(pm_ctx* c) {
   HIPCHK(hipStreamSynchronize(c->stream));
   for (auto& t : c->launches) { c->pool.push_back(t.a); c->pool.push_back(t.b); }
   c->launches.clear();
+  c->host.clear();
   return 0;
 }
 extern "C" int pm_timing_get(pm_ctx* c, const char* name, uint64_t* launches, double* total_ms,
                              double* bytes) {
   HIPCHK(hipStreamSynchronize(c->stream));
   uint64_t n = 0; double ms = 0, by = 0;
+  if (strncmp(name, "host_", 5) == 0) {
+    auto it = c->host.find(name);
+    if (it != c->host.end()) { n = it->second.first; ms = it->second.second; }
+    if (launches) *launches = n;
+    if (total_ms) *total_ms = ms;
+    if (bytes) *bytes = 0;
+    return 0;
+  }
   for (auto& t : c->launches) {
     if (t.name != name) continue;
     float x = 0;
@@ -191,7 +243,7 @@ struct PartHost {
   PmPart d{};
   uint64_t epoch_ctr = 0, fqn = 0, dummy_ctr = 0;
   uint64_t maxq64 = 0;
-  std::unordered_map<uint64_t, uint32_t> cache;   // localCache (pir.go:120): idx -> arena slot
+  FlatMap cache;   // localCache (pir.go:120): idx -> arena slot
 };
 
 struct Engine {
@@ -204,7 +256,7 @@ struct Engine {
   uint64_t FBN = 0, QMIP = 0, Support = 0, prepCount = 0;
   double prepTime = 0, storage = 0, commOn = 0, commOff = 0;
 
-  DevBuf db, parts_d, tag, pp, parity, ridx, rval, hist, fqn, arena, tab;
+  DevBuf db, parts_d, tag, pp, parity, ridx, rval, hist, fqn, arena, tab, tabT, done;
   DevBuf qoffs, ans_srv;
   DevBuf subs_d, sb_d, bits, res_d, ans, qvec;
   HostBuf desc_h, out_h;
@@ -219,7 +271,7 @@ struct Engine {
   uint64_t* rows = nullptr;
   // batch_query scratch
   std::vector<std::vector<uint64_t>> pq;
-  std::unordered_map<uint64_t, uint32_t> resp_map;
+  FlatMap resp_map;
   std::vector<uint64_t> resp_rows;
   std::vector<float> resp_dist;
 };
@@ -306,7 +358,7 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
     ph.d.hist = (uint32_t*)(uintptr_t)off_hist; off_hist += ph.d.SS;
     ph.d.arena = (uint64_t*)(uintptr_t)off_ar; off_ar += (uint64_t)ph.d.MaxQ * g->E;
     ph.d.tab = (uint16_t*)(uintptr_t)off_tab; off_tab += (uint64_t)ph.d.H * ph.d.SS;
-    ph.cache.reserve(ph.d.MaxQ * 2);
+    ph.cache.reserve(ph.d.MaxQ);
   }
   CHK(g->db.reserve(N * g->E * 8));
   HIPCHK(hipMemcpy(g->db.p, rawDB, N * g->E * 8, hipMemcpyHostToDevice));
@@ -319,6 +371,8 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
   CHK(g->fqn.reserve(g->P * 4));
   CHK(g->arena.reserve(std::max<uint64_t>(8, off_ar * 8)));
   CHK(g->tab.reserve(off_tab * 2));
+  CHK(g->tabT.reserve(off_tab * 2));
+  CHK(g->done.reserve(4 * (3 + 16 * 4096)));
   CHK(g->parts_d.reserve(g->P * sizeof(PmPart)));
   for (uint64_t i = 0; i < g->P; ++i) {
     PmPart& d = g->parts[i].d;
@@ -330,6 +384,7 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
     d.hist = g->hist.as<uint32_t>() + (uintptr_t)d.hist;
     d.fqn = g->fqn.as<uint32_t>() + i;
     d.arena = g->arena.as<uint64_t>() + (uintptr_t)d.arena;
+    d.tabT = g->tabT.as<uint16_t>() + (uintptr_t)d.tab;
     d.tab = g->tab.as<uint16_t>() + (uintptr_t)d.tab;
   }
   HIPCHK(hipMemsetAsync(g->fqn.p, 0, g->P * 4, ctx->stream));
@@ -391,11 +446,17 @@ static int engine_prep(Engine* g, uint64_t p0, uint64_t p1) {
 }
 
 // One batched step over the sub-queries in g->subs (partition-major, ranges in
-// g->sb): k_match -> k_resolve -> k_answer -> k_chain.  The descriptor is
+// g->sb): k_match -> k_resolve -> k_answer.  The descriptor is
 // read zero-copy from pinned host memory and the results (status header +
 // entry + L2 distance to q) are written by the GPU straight into pinned host
-// memory, so a step costs four launches and one stream synchronisation.
+// memory, so a step costs three launches and one stream synchronisation.
+using Clock = std::chrono::steady_clock;
+static inline double ms_since(Clock::time_point t) {
+  return std::chrono::duration<double, std::milli>(Clock::now() - t).count();
+}
+
 static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
+  auto t_begin = Clock::now();
   pm_ctx* c = g->ctx;
   hipStream_t st = c->stream;
   const uint32_t nsub = (uint32_t)g->subs.size();
@@ -422,6 +483,7 @@ static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
   S.bits = g->bits.as<uint64_t>();
   S.res = g->res_d.as<PmRes>();
   S.ans = g->ans.as<uint64_t>();
+  S.done = g->done.as<uint32_t>();
   S.db = g->db.as<uint64_t>();
   S.q = q_dev;
   S.hdr_h = g->out_h.as<PmOutHdr>();
@@ -449,9 +511,12 @@ static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
   for (auto& x : g->subs)
     if (x.kind == SUB_REAL || x.kind == SUB_DUMMY) ans_bytes += (double)g->parts[x.part].d.SS * E * 8;
   c->timed("answer", ans_bytes, [&] { pmk::step_answer(st, S); }, 2);
-  c->timed("chain", 0, [&] { pmk::step_chain(st, S); }, 2);
   HIPCHK(hipGetLastError());
+  c->host_add("host_step_launch", ms_since(t_begin));
+  auto t_wait = Clock::now();
   HIPCHK(hipStreamSynchronize(st));
+  c->host_add("host_step_wait", ms_since(t_wait));
+  auto t_post = Clock::now();
   g->hdr = S.hdr_h;
   g->rows = S.rows_h;
   // host mirrors: FinishedQueryNum and the localCache index (pir.go:469-470);
@@ -461,12 +526,13 @@ static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
     if (h.status == ST_OK) {
       PartHost& ph = g->parts[g->subs[s].part];
       ph.fqn++;
-      ph.cache[g->subs[s].idx] = h.ref;
+      ph.cache.put(g->subs[s].idx, h.ref);
     } else if (h.status == ST_DUP) {
       memcpy(g->rows + (uint64_t)s * E, g->rows + (uint64_t)h.ref * E, E * 8);
       g->hdr[s].dist = g->hdr[h.ref].dist;
     }
   }
+  c->host_add("host_step_post", ms_since(t_post));
   return 0;
 }
 
@@ -478,8 +544,7 @@ static void add_sub(Engine* g, uint32_t p, bool real, uint64_t local, uint64_t g
     s.kind = SUB_DUMMY; s.idx = ph.dummy_ctr++;
   } else {
     s.kind = SUB_REAL; s.idx = local;
-    auto it = ph.cache.find(local);
-    if (it != ph.cache.end()) { s.kind = SUB_HOSTCACHE; s.idx = it->second; }
+    if (const uint32_t* slot = ph.cache.find(local)) { s.kind = SUB_HOSTCACHE; s.idx = *slot; }
   }
   g->subs.push_back(s);
   g->sub_gid.push_back(gid);
@@ -644,8 +709,17 @@ extern "C" int pm_batchpir_dummy_preprocessing(pm_batchpir* h) {   // batch-pir.
 // step_max_sub_per_part() sub-queries per partition per step); the rest replay
 // the reference's per-sub-query re-preprocessing check (pir.go:527-530) one
 // sub-query at a time.  q_dev / dist_out: optional L2 of every answer to q.
+static int batch_query_impl(Engine* g, const uint64_t* idx, uint64_t n, uint64_t* out, const float* q_dev,
+                            uint32_t dim, float* dist_out);
 static int batch_query(Engine* g, const uint64_t* idx, uint64_t n, uint64_t* out, const float* q_dev,
                        uint32_t dim, float* dist_out) {
+  auto t = Clock::now();
+  int r = batch_query_impl(g, idx, n, out, q_dev, dim, dist_out);
+  g->ctx->host_add("host_batch_query", ms_since(t));
+  return r;
+}
+static int batch_query_impl(Engine* g, const uint64_t* idx, uint64_t n, uint64_t* out, const float* q_dev,
+                            uint32_t dim, float* dist_out) {
   const uint64_t E = g->E, P = g->P;
   for (uint64_t i = 0; i < n; ++i)
     if (idx[i] >= g->N) return fail(PM_EINVAL, "id " + std::to_string(idx[i]) + " >= DBSize");
@@ -663,9 +737,8 @@ static int batch_query(Engine* g, const uint64_t* idx, uint64_t n, uint64_t* out
     for (size_t s = 0; s < g->subs.size(); ++s) {
       const uint32_t k = g->subs[s].kind;
       if (k != SUB_REAL && k != SUB_HOSTCACHE) continue;
-      auto ins = g->resp_map.emplace(g->sub_gid[s], (uint32_t)nresp);
-      if (ins.second) ++nresp;
-      const uint32_t slot = ins.first->second;
+      if (g->resp_map.emplace(g->sub_gid[s], (uint32_t)nresp)) ++nresp;
+      const uint32_t slot = *g->resp_map.find(g->sub_gid[s]);
       memcpy(&g->resp_rows[(size_t)slot * E], g->rows + (uint64_t)s * E, E * 8);
       g->resp_dist[slot] = g->hdr[s].dist;
     }
@@ -694,13 +767,12 @@ static int batch_query(Engine* g, const uint64_t* idx, uint64_t n, uint64_t* out
     CHK(engine_step(g, q_dev, dim));
     for (size_t s = 0; s < g->subs.size(); ++s) {
       const uint32_t k = g->subs[s].kind;
-      if (k == SUB_REAL || k == SUB_HOSTCACHE) g->resp_map[g->sub_gid[s]] = (uint32_t)s;   // last wins
+      if (k == SUB_REAL || k == SUB_HOSTCACHE) g->resp_map.put(g->sub_gid[s], (uint32_t)s);   // last wins
     }
     for (uint64_t i = 0; i < n; ++i) {
-      auto it = g->resp_map.find(idx[i]);
-      if (it != g->resp_map.end()) {
-        memcpy(out + i * E, g->rows + (uint64_t)it->second * E, E * 8);
-        if (dist_out) dist_out[i] = g->hdr[it->second].dist;
+      if (const uint32_t* sp = g->resp_map.find(idx[i])) {
+        memcpy(out + i * E, g->rows + (uint64_t)*sp * E, E * 8);
+        if (dist_out) dist_out[i] = g->hdr[*sp].dist;
       } else {
         memset(out + i * E, 0, E * 8);
         if (dist_out) dist_out[i] = 0;
@@ -735,10 +807,9 @@ static int batch_query(Engine* g, const uint64_t* idx, uint64_t n, uint64_t* out
     }
   }
   for (uint64_t i = 0; !qn_done && i < n; ++i) {
-    auto it = g->resp_map.find(idx[i]);
-    if (it != g->resp_map.end()) {
-      memcpy(out + i * E, &g->resp_rows[(size_t)it->second * E], E * 8);
-      if (dist_out) dist_out[i] = g->resp_dist[it->second];
+    if (const uint32_t* sp = g->resp_map.find(idx[i])) {
+      memcpy(out + i * E, &g->resp_rows[(size_t)*sp * E], E * 8);
+      if (dist_out) dist_out[i] = g->resp_dist[*sp];
     } else {
       memset(out + i * E, 0, E * 8);
       if (dist_out) dist_out[i] = 0;
@@ -893,7 +964,7 @@ struct pm_graph {
   std::vector<uint64_t> qids, resp;
   std::vector<float> dist, start_d;
   std::vector<uint32_t> nb;                       // [len(batch)][m] of the last GetVertexInfo
-  std::unordered_map<int64_t, uint32_t> known;    // knownVertices: id -> slot
+  FlatMap known;                                  // knownVertices: id -> slot
   std::vector<uint32_t> known_nb;                 // [slot][m]
   std::vector<float> known_dist;
   std::vector<int64_t> known_id, known_reach;
@@ -1015,8 +1086,17 @@ static int get_vertex_info(pm_graph* g, bool with_q) {
 }
 
 // SearchKNN (graphann/search.go:114-234).  Same tie rules as oracle/pm_oracle.cpp.
+static int search_knn_impl(pm_graph* g, const float* query, int k, int max_step, int parallel,
+                           int benchmarking, int64_t* ids_out, int64_t* steps_out);
 extern "C" int pm_search_knn(pm_graph* g, const float* query, int k, int max_step, int parallel,
                              int benchmarking, int64_t* ids_out, int64_t* steps_out) {
+  auto t = Clock::now();
+  int r = search_knn_impl(g, query, k, max_step, parallel, benchmarking, ids_out, steps_out);
+  g->ctx->host_add("host_search_knn", ms_since(t));
+  return r;
+}
+static int search_knn_impl(pm_graph* g, const float* query, int k, int max_step, int parallel,
+                           int benchmarking, int64_t* ids_out, int64_t* steps_out) {
   if (!g->pir && !g->nonprivate) return fail(PM_EINVAL, "pm_graph_preprocess not called");
   const int64_t n = (int64_t)g->n;
   const uint64_t m = g->m;
@@ -1026,7 +1106,7 @@ extern "C" int pm_search_knn(pm_graph* g, const float* query, int k, int max_ste
   g->heap.clear();
   auto add_known = [&](int64_t id, const uint32_t* nb, float d, int64_t reach) {
     const uint32_t slot = (uint32_t)g->known_id.size();
-    g->known.emplace(id, slot);
+    g->known.put((uint64_t)id, slot);
     g->known_nb.insert(g->known_nb.end(), nb, nb + m);
     g->known_dist.push_back(d);
     g->known_id.push_back(id);
@@ -1050,7 +1130,7 @@ extern "C" int pm_search_knn(pm_graph* g, const float* query, int k, int max_ste
     std::stable_sort(g->fs.begin(), g->fs.end(), [](const auto& a, const auto& b) { return a.first.dist < b.first.dist; });
     for (size_t i = 0; (int64_t)g->heap.size() < parallel && i < g->fs.size(); ++i) {
       const int64_t id = g->fs[i].first.id;
-      if (g->known.count(id)) continue;
+      if (g->known.find((uint64_t)id)) continue;
       add_known(id, &g->graph[(uint64_t)id * m], g->fs[i].first.dist, 0);
       heap_push(g->heap, g->fs[i].first);
     }
@@ -1062,7 +1142,7 @@ extern "C" int pm_search_knn(pm_graph* g, const float* query, int k, int max_ste
         for (uint64_t i = 0; i < m; ++i) g->batch.push_back((int64_t)g->rng.intn((uint64_t)n));
       } else {
         const VD it = heap_pop(g->heap);
-        const uint32_t* nb = &g->known_nb[(size_t)g->known[it.id] * m];
+        const uint32_t* nb = &g->known_nb[(size_t)*g->known.find((uint64_t)it.id) * m];
         for (uint64_t i = 0; i < m; ++i) g->batch.push_back((int64_t)nb[i]);
       }
     }
@@ -1070,7 +1150,7 @@ extern "C" int pm_search_knn(pm_graph* g, const float* query, int k, int max_ste
     if (benchmarking) continue;
     for (size_t i = 0; i < g->batch.size(); ++i) {
       const int64_t id = g->batch[i];
-      if (g->known.count(id)) continue;
+      if (g->known.find((uint64_t)id)) continue;
       const uint32_t* nb = &g->nb[i * m];
       bool ok = false;
       for (uint64_t j = 0; j < m; ++j) if (nb[j] != 0) { ok = true; break; }
@@ -1085,7 +1165,7 @@ extern "C" int pm_search_knn(pm_graph* g, const float* query, int k, int max_ste
     return a.dist < b.dist || (a.dist == b.dist && a.id < b.id); });
   for (int i = 0; i < k; ++i) {
     if (i >= (int)g->all.size()) { ids_out[i] = -1; if (steps_out) steps_out[i] = -1; }
-    else { ids_out[i] = g->all[i].id; if (steps_out) steps_out[i] = g->known_reach[g->known[g->all[i].id]]; }
+    else { ids_out[i] = g->all[i].id; if (steps_out) steps_out[i] = g->known_reach[*g->known.find((uint64_t)g->all[i].id)]; }
   }
   return 0;
 }

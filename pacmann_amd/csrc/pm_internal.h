@@ -55,6 +55,7 @@ struct PmPart {
   // hands over backup tag PH+g*Qpc+j), so this table, built once per
   // preprocessing, holds every PRF value the online phase needs.
   uint16_t* tab;
+  uint16_t* tabT;    // the same table hint-major: tabT[t*SS + c] (set expansion reads one row)
 };
 
 // Sub-query kinds / statuses for one batched step.
@@ -72,7 +73,8 @@ struct PmRes {
   uint32_t status, hit, chunk, ing;   // ing = in-group index (QueryHistogram before)
   uint32_t tag, pp;                   // hit hint's tag / program point used for the expansion
   uint32_t slot;                      // OK: arena slot; CACHED: arena slot; DUP: earlier sub
-  uint32_t flags;                     // bit 0: hint refreshed earlier in this step (k_chain)
+  uint32_t flags;                     // bit 0: hint refreshed earlier in this step (chained);
+                                      // bit 1: a later sub-query in this step re-hits this hint
 };
 // Per-sub-query result header, written by the GPU into pinned host memory.
 struct PmOutHdr {
@@ -90,6 +92,9 @@ struct PmStep {
   uint64_t* bits;         // [nsub][words] hint-match bits (k_match -> k_resolve)
   PmRes* res;             // [nsub]
   uint64_t* ans;          // [nsub][E] raw answers of chained sub-queries
+  uint32_t* done;         // [0] k_answer arrival counter of chain workgroups,
+                          // [1] chained sub-queries, [2] workgroups involved in chains,
+                          // [3..] chained sub-query list (zeroed by k_match, filled by k_resolve)
   const uint64_t* db;
   const float* q;         // search query (device) or null
   PmOutHdr* hdr_h;        // pinned host outputs
@@ -112,7 +117,6 @@ void prep_repl(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxRep
 void step_match(hipStream_t st, const PmStep& S, uint32_t maxPH);
 void step_resolve(hipStream_t st, const PmStep& S);
 void step_answer(hipStream_t st, const PmStep& S);
-void step_chain(hipStream_t st, const PmStep& S);
 uint32_t step_max_sub_per_part();
 uint32_t step_max_ss();
 uint32_t step_max_e();

@@ -36,10 +36,13 @@ __global__ void __launch_bounds__(kBlock) k_prep_offsets(const PmPart* __restric
   const uint32_t mask = P.CS - 1;
   const uint32_t own = h >= P.PH ? (h - P.PH) / P.Qpc : 0xffffffffu;
   uint16_t* o = P.tab;
+  uint16_t* oT = P.tabT + (uint64_t)h * SS;
   const uint32_t c1 = min(SS, c0 + kOffsChunksPerBlock);
   for (uint32_t c = c0; c < c1; ++c) {
     uint16_t v = (uint16_t)(prf_lo32(A, P.rk, h, c) & mask);   // initial tag of hint h is h
-    o[(uint64_t)c * H + h] = (c == own) ? kSkip : v;
+    v = (c == own) ? kSkip : v;
+    o[(uint64_t)c * H + h] = v;   // chunk-major: hint search
+    oT[c] = v;                    // hint-major: set expansion
   }
 }
 

@@ -22,8 +22,10 @@
 //                           parity refresh (pir.go:450-468), the L2 distance of
 //                           the decoded vector to the search query, and the
 //                           write of the result straight into host-mapped memory.
-//   k_chain   (1 WG/part.)  decode of sub-queries whose hint was already
-//                           refreshed earlier in the same step (rare), in order.
+//                           The last workgroup to finish (arrival counter,
+//                           agent-scope release/acquire) then decodes, in
+//                           order, the rare sub-queries whose hint was already
+//                           refreshed earlier in the same step.
 #include "pm_aes.h"
 #include "pm_internal.h"
 
@@ -41,8 +43,10 @@ __global__ void __launch_bounds__(kBlock) k_match(PmStep S) {
     s_sub = sub;
     if (blockIdx.x == 0) S.subs[s] = sub;
   }
-  if (blockIdx.x == 0 && s == 0)
+  if (blockIdx.x == 0 && s == 0) {
     for (uint32_t i = threadIdx.x; i <= S.np; i += kBlock) S.sb[i] = S.sb_h[i];
+    if (threadIdx.x < 3) S.done[threadIdx.x] = 0;
+  }
   __syncthreads();
   const PmSub sub = s_sub;
   if (sub.kind != SUB_REAL) return;
@@ -93,7 +97,8 @@ __global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
   __shared__ uint32_t s_kind[kMaxSubPerPart], s_chunk[kMaxSubPerPart], s_st[kMaxSubPerPart],
       s_hist0[kMaxSubPerPart], s_c1[kMaxSubPerPart], s_c2[kMaxSubPerPart], s_t1[kMaxSubPerPart],
       s_p1[kMaxSubPerPart], s_t2[kMaxSubPerPart], s_p2[kMaxSubPerPart];
-  __shared__ uint32_t m_h[kMaxSubPerPart], m_tag[kMaxSubPerPart], m_pp[kMaxSubPerPart];
+  __shared__ uint32_t m_h[kMaxSubPerPart], m_tag[kMaxSubPerPart], m_pp[kMaxSubPerPart],
+      m_sub[kMaxSubPerPart];
   __shared__ uint32_t s_fqn;
   const uint32_t p = blockIdx.x;
   const PmPart& P = S.parts[p];
@@ -132,6 +137,7 @@ __global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
   volatile uint32_t* vmh = m_h;
   volatile uint32_t* vmt = m_tag;
   volatile uint32_t* vmp = m_pp;
+  volatile uint32_t* vms = m_sub;
   uint32_t fqn = s_fqn, nmod = 0;
   for (uint32_t j = 0; j < n; ++j) {
     const uint32_t s = b0 + j, kind = s_kind[j];
@@ -208,8 +214,20 @@ __global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
             P.tag[hit] = ntag;
             P.pp[hit] = (uint32_t)idx;
             P.hist[chunk] = hist + 1;
-            if (chained) { vmt[bk] = ntag; vmp[bk] = (uint32_t)idx; }
-            else { vmh[nmod] = hit; vmt[nmod] = ntag; vmp[nmod] = (uint32_t)idx; }
+            if (chained) {
+              // the previous holder of this hint must publish its parity refresh
+              const uint32_t prev = vms[bk];
+              const uint32_t pf = S.res[prev].flags;
+              // this chained sub-query counts itself; the chain head is counted once
+              const uint32_t add = 1u + ((!(pf & 1u) && !(pf & 4u)) ? 1u : 0u);
+              S.res[prev].flags = pf | 2u | 4u;
+              const uint32_t pos = atomicAdd(&S.done[1], 1u);
+              S.done[3 + pos] = s;
+              atomicAdd(&S.done[2], add);
+              vmt[bk] = ntag; vmp[bk] = (uint32_t)idx; vms[bk] = s;
+            } else {
+              vmh[nmod] = hit; vmt[nmod] = ntag; vmp[nmod] = (uint32_t)idx; vms[nmod] = s;
+            }
           }
           if (!chained) ++nmod;
           ++fqn;
@@ -253,11 +271,46 @@ union RowBuf {   // one decoded entry; the L2 reads its leading floats
 // What a k_answer workgroup does for its sub-query.
 enum : uint32_t { A_ZERO = 0, A_FINAL = 1, A_CHAINED = 2, A_CACHED = 3, A_DUMMY = 4 };
 
+// Decode one chained sub-query (its hint was refreshed earlier in this step)
+// once every earlier refresh is visible; the whole workgroup participates.
+__device__ void decode_chained(const PmStep& S, uint32_t s, RowBuf& row) {
+  const PmSub sub = S.subs[s];
+  const PmRes r = S.res[s];
+  const PmPart& P = S.parts[sub.part];
+  const uint32_t E = S.E, EX = E & ~3u, tid = threadIdx.x;
+  const uint64_t slot = (uint64_t)r.chunk * P.Qpc + r.ing;
+  const uint64_t* rv = P.rval + slot * E;
+  const uint64_t* bp = P.parity + ((uint64_t)P.PH + slot) * E;
+  uint64_t* pp = P.parity + (uint64_t)r.hit * E;
+  const uint64_t* a = S.ans + (uint64_t)s * E;
+  for (uint32_t w = tid; w < E; w += blockDim.x) {
+    uint64_t v = 0;
+    if (w < EX) {
+      v = a[w] ^ rv[w] ^ pp[w];
+      pp[w] = bp[w] ^ v;
+    } else {
+      pp[w] = bp[w];
+    }
+    row.w[w] = v;
+  }
+  __syncthreads();
+  uint64_t* orow = S.rows_h + (uint64_t)s * E;
+  uint64_t* ar = P.arena + (uint64_t)r.slot * E;
+  for (uint32_t w = tid; w < E; w += blockDim.x) { orow[w] = row.w[w]; ar[w] = row.w[w]; }
+  if (tid < 64) {
+    float d = 0.0f;
+    if (S.q && tid < 8) d = l2_lds(row.f, S.q, S.dim);
+    if (tid == 0) S.hdr_h[s] = PmOutHdr{r.status, r.slot, d, 0};
+  }
+  __syncthreads();
+}
+
 template <int W>
 __global__ void __launch_bounds__(kAnsBlock) k_answer(PmStep S) {
   __shared__ uint32_t qo[kMaxSSLds];
   __shared__ uint64_t red[kAnsBlock * 2];
   __shared__ __attribute__((aligned(16))) RowBuf row;
+  __shared__ uint32_t s_last;
   const uint32_t s = blockIdx.x, tid = threadIdx.x;
   const uint32_t E = S.E, EX = E & ~3u, NSEG = EX / W;
   const PmSub sub = S.subs[s];
@@ -268,11 +321,19 @@ __global__ void __launch_bounds__(kAnsBlock) k_answer(PmStep S) {
                       : r.status == ST_CACHED ? A_CACHED
                       : r.status == ST_DUMMY ? A_DUMMY : A_ZERO;
   const uint32_t mask = P.CS - 1, lg = P.log2CS;
+  // decode operands: independent of the gather, issued first (pir.go:450-468)
+  const uint64_t dslot = (uint64_t)r.chunk * P.Qpc + r.ing;
+  const uint64_t* rv = P.rval + dslot * E;
+  const uint64_t* bp = P.parity + ((uint64_t)P.PH + dslot) * E;
+  uint64_t* pp = P.parity + (uint64_t)r.hit * E;
+  uint64_t e_rv = 0, e_bp = 0, e_pp = 0;
+  if (mode == A_FINAL && tid < E) { e_rv = rv[tid]; e_bp = bp[tid]; e_pp = pp[tid]; }
   // ---- query set (pir.go:363-371 dummy; :424-444 real) -------------------
   if (mode == A_FINAL || mode == A_CHAINED) {
     const uint32_t pchunk = r.pp != kDefaultProgramPoint ? (r.pp >> lg) : kNone;
+    const uint16_t* trow = P.tabT + (uint64_t)r.tag * P.SS;
     for (uint32_t i = tid; i < P.SS; i += kAnsBlock) {
-      uint32_t o = P.tab[(uint64_t)i * P.H + r.tag];
+      uint32_t o = trow[i];
       if (i == pchunk) o = r.pp & mask;
       if (i == r.chunk) o = P.ridx[r.chunk * P.Qpc + r.ing] & mask;
       qo[i] = o;
@@ -321,19 +382,17 @@ __global__ void __launch_bounds__(kAnsBlock) k_answer(PmStep S) {
       __syncthreads();
     }
   }
-  // ---- decode + refresh (pir.go:450-468), or the cached row ----------------
+  // ---- decode + refresh, or the cached row -----------------------------
   if (mode == A_FINAL) {
-    const uint64_t slot = (uint64_t)r.chunk * P.Qpc + r.ing;
-    const uint64_t* rv = P.rval + slot * E;
-    const uint64_t* bp = P.parity + ((uint64_t)P.PH + slot) * E;
-    uint64_t* pp = P.parity + (uint64_t)r.hit * E;
     for (uint32_t w = tid; w < E; w += kAnsBlock) {
+      const uint64_t rvw = w < kAnsBlock ? e_rv : rv[w], bpw = w < kAnsBlock ? e_bp : bp[w],
+                     ppw = w < kAnsBlock ? e_pp : pp[w];
       uint64_t v = 0;
       if (w < EX) {
-        v = row.w[w] ^ rv[w] ^ pp[w];
-        pp[w] = bp[w] ^ v;
+        v = row.w[w] ^ rvw ^ ppw;
+        pp[w] = bpw ^ v;
       } else {
-        pp[w] = bp[w];
+        pp[w] = bpw;
       }
       row.w[w] = v;
     }
@@ -345,64 +404,40 @@ __global__ void __launch_bounds__(kAnsBlock) k_answer(PmStep S) {
   }
   __syncthreads();
   // ---- results: row + header into pinned host memory, arena copy -----------
-  if (mode == A_CHAINED) return;   // k_chain finishes it
-  const bool has_row = (mode == A_FINAL || mode == A_CACHED);
-  for (uint32_t w = tid; w < E; w += kAnsBlock) orow[w] = has_row ? row.w[w] : 0;
-  if (mode == A_FINAL) {
-    uint64_t* ar = P.arena + (uint64_t)r.slot * E;
-    for (uint32_t w = tid; w < E; w += kAnsBlock) ar[w] = row.w[w];
-  }
-  if (tid < 64) {
-    float d = 0.0f;
-    if (has_row && S.q && tid < 8) d = l2_lds(row.f, S.q, S.dim);
-    if (tid == 0) S.hdr_h[s] = PmOutHdr{r.status, r.slot, d, 0};
-  }
-}
-
-// Sub-queries whose hint was refreshed earlier in the same step: decode in
-// order once the earlier parity refreshes are visible (kernel boundary).
-__global__ void __launch_bounds__(kBlock) k_chain(PmStep S) {
-  __shared__ __attribute__((aligned(16))) RowBuf row;
-  __shared__ uint32_t s_any;
-  const uint32_t p = blockIdx.x;
-  const PmPart& P = S.parts[p];
-  const uint32_t b0 = S.sb[p], b1 = S.sb[p + 1];
-  if (threadIdx.x == 0) s_any = 0;
-  __syncthreads();
-  for (uint32_t s = b0 + threadIdx.x; s < b1; s += kBlock)
-    if (S.res[s].status == ST_OK && (S.res[s].flags & 1u)) s_any = 1;
-  __syncthreads();
-  if (!s_any) return;
-  const uint32_t E = S.E, EX = E & ~3u, tid = threadIdx.x;
-  for (uint32_t s = b0; s < b1; ++s) {
-    const PmRes r = S.res[s];
-    if (!(r.status == ST_OK && (r.flags & 1u))) continue;
-    const uint64_t slot = (uint64_t)r.chunk * P.Qpc + r.ing;
-    const uint64_t* rv = P.rval + slot * E;
-    const uint64_t* bp = P.parity + ((uint64_t)P.PH + slot) * E;
-    uint64_t* pp = P.parity + (uint64_t)r.hit * E;
-    const uint64_t* a = S.ans + (uint64_t)s * E;
-    for (uint32_t w = tid; w < E; w += kBlock) {
-      if (w < EX) {
-        const uint64_t v = a[w] ^ rv[w] ^ pp[w];
-        pp[w] = bp[w] ^ v;
-        row.w[w] = v;
-      } else {
-        pp[w] = bp[w];
-        row.w[w] = 0;
-      }
+  if (mode != A_CHAINED) {
+    const bool has_row = (mode == A_FINAL || mode == A_CACHED);
+    for (uint32_t w = tid; w < E; w += kAnsBlock) orow[w] = has_row ? row.w[w] : 0;
+    if (mode == A_FINAL) {
+      uint64_t* ar = P.arena + (uint64_t)r.slot * E;
+      for (uint32_t w = tid; w < E; w += kAnsBlock) ar[w] = row.w[w];
     }
-    __syncthreads();
-    uint64_t* orow = S.rows_h + (uint64_t)s * E;
-    uint64_t* ar = P.arena + (uint64_t)r.slot * E;
-    for (uint32_t w = tid; w < E; w += kBlock) { orow[w] = row.w[w]; ar[w] = row.w[w]; }
     if (tid < 64) {
       float d = 0.0f;
-      if (S.q && tid < 8) d = l2_lds(row.f, S.q, S.dim);
+      if (has_row && S.q && tid < 8) d = l2_lds(row.f, S.q, S.dim);
       if (tid == 0) S.hdr_h[s] = PmOutHdr{r.status, r.slot, d, 0};
     }
-    __syncthreads();
   }
+  // ---- arrival: workgroups of refresh chains count in; the last one decodes
+  // the chained sub-queries in order.  Producer side: drain this wave's stores,
+  // barrier, one lane releases at agent scope and counts (MI355X_MICROARCH.md
+  // § visibility).  Workgroups outside every chain skip all of this.
+  if (!(r.status == ST_OK && (r.flags & 3u))) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t prev = __hip_atomic_fetch_add(&S.done[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (prev + 1 == S.done[2]);
+    if (s_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!s_last) return;
+  const uint32_t nchain = S.done[1];
+  for (uint32_t k = 0; k < nchain; ++k) decode_chained(S, S.done[3 + k], row);
 }
 
 }  // namespace pm
@@ -420,9 +455,6 @@ void step_answer(hipStream_t st, const PmStep& S) {
     hipLaunchKernelGGL(k_answer<2>, dim3(S.nsub), dim3(kAnsBlock), 0, st, S);
   else
     hipLaunchKernelGGL(k_answer<1>, dim3(S.nsub), dim3(kAnsBlock), 0, st, S);
-}
-void step_chain(hipStream_t st, const PmStep& S) {
-  hipLaunchKernelGGL(k_chain, dim3(S.np), dim3(kBlock), 0, st, S);
 }
 uint32_t step_max_sub_per_part() { return kMaxSubPerPart; }
 uint32_t step_max_ss() { return kMaxSSLds; }
