@@ -24,7 +24,10 @@ __all__ = [
     "QueryError",
 ]
 
-LIB_PATH = Path(__file__).resolve().parent / "libpacmann.so"
+import os as _os
+
+# PM_LIB selects a diagnostic build (e.g. the PM_STAMPS variant); default is the product .so
+LIB_PATH = Path(_os.environ.get("PM_LIB") or (Path(__file__).resolve().parent / "libpacmann.so"))
 _lib = None
 
 u8p = C.POINTER(C.c_uint8)

@@ -16,6 +16,7 @@
 
 #include "../../include/pacmann.h"
 #include "pm_aes.h"
+#define PM_HOST_TU 1
 #include "pm_internal.h"
 
 using namespace pm;
@@ -258,7 +259,9 @@ struct Engine {
 
   DevBuf db, parts_d, tag, pp, parity, ridx, rval, hist, fqn, arena, tab, tabT, done;
   DevBuf qoffs, ans_srv;
-  DevBuf subs_d, sb_d, bits, res_d, ans, qvec;
+  DevBuf subs_d, sb_d, bits, res_d, ans, qvec, stamps;
+  std::vector<double> stamp_sum;   // PM_STAMPS builds: accumulated phase deltas
+  uint64_t stamp_n = 0;
   HostBuf desc_h, out_h;
   std::vector<PartHost> parts;
   uint32_t maxH = 0, maxPH = 0, maxSS = 0, maxRepl = 0;
@@ -484,15 +487,28 @@ static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
   S.res = g->res_d.as<PmRes>();
   S.ans = g->ans.as<uint64_t>();
   S.done = g->done.as<uint32_t>();
+#ifdef PM_STAMPS
+  CHK(g->stamps.reserve(g->P * 64 * 8));
+  HIPCHK(hipMemsetAsync(g->stamps.p, 0, g->P * 64 * 8, st));
+  S.stamps = g->stamps.as<uint64_t>();
+#endif
   S.db = g->db.as<uint64_t>();
   S.q = q_dev;
   S.hdr_h = g->out_h.as<PmOutHdr>();
   S.rows_h = (uint64_t*)(g->out_h.as<char>() + nsub * sizeof(PmOutHdr));
   S.words = words; S.E = (uint32_t)E; S.dim = q_dev ? dim : 0; S.nsub = nsub; S.np = (uint32_t)g->P;
+  S.args_valid = (nsub <= kArgSubs && g->P <= kArgParts) ? 1u : 0u;
+  if (S.args_valid) {
+    memcpy(S.subs_a, g->subs.data(), dsub);
+    memcpy(S.sb_a, g->sb.data(), (g->P + 1) * 4);
+  }
   uint32_t nreal = 0;
   for (auto& x : g->subs) nreal += x.kind == SUB_REAL;
   c->timed("hint_match", (double)nreal * g->maxPH, [&] { pmk::step_match(st, S, g->maxPH); }, 2);
-  c->timed("resolve", 0, [&] { pmk::step_resolve(st, S); }, 2);
+  uint32_t max_per_part = 0;
+  for (uint64_t p = 0; p < g->P; ++p) max_per_part = std::max(max_per_part, g->sb[p + 1] - g->sb[p]);
+  const bool lds = pmk::step_resolve_lds_ok(g->maxPH, max_per_part);
+  c->timed("resolve", 0, [&] { pmk::step_resolve(st, S, lds); }, 2);
   if (c->debug_sync) {   // validate every resolution record before k_answer consumes it
     std::vector<PmRes> rr(nsub);
     HIPCHK(hipMemcpy(rr.data(), S.res, nsub * sizeof(PmRes), hipMemcpyDeviceToHost));
@@ -533,6 +549,16 @@ static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
     }
   }
   c->host_add("host_step_post", ms_since(t_post));
+#ifdef PM_STAMPS
+  {   // partition 0's phase deltas in shader clocks, accumulated; printed at exit
+    std::vector<uint64_t> t(64);
+    HIPCHK(hipMemcpy(t.data(), g->stamps.p, 64 * 8, hipMemcpyDeviceToHost));
+    g->stamp_sum.resize(64, 0.0);
+    for (int i = 1; i < 64; ++i)
+      if (t[i] && t[0]) g->stamp_sum[i] += (double)(t[i] - t[0]);
+    g->stamp_n++;
+  }
+#endif
   return 0;
 }
 
@@ -560,8 +586,19 @@ static void close_partition(Engine* g, uint32_t p) {   // sub_begin[p+1] = curre
 // ---------------------------------------------------------------------------
 // PianoPIR C ABI
 // ---------------------------------------------------------------------------
-struct pm_pir { Engine e; };
-struct pm_batchpir { Engine e; };
+static void print_stamps(const Engine& e) {
+#ifdef PM_STAMPS
+  if (!e.stamp_n) return;
+  fprintf(stderr, "[pm-stamps] k_resolve partition 0, mean shader clocks since start over %lu steps:", (unsigned long)e.stamp_n);
+  for (size_t i = 1; i < e.stamp_sum.size(); ++i)
+    if (e.stamp_sum[i] > 0) fprintf(stderr, " %zu:%.0f", i, e.stamp_sum[i] / e.stamp_n);
+  fprintf(stderr, "\n");
+#else
+  (void)e;
+#endif
+}
+struct pm_pir { Engine e; ~pm_pir() { print_stamps(e); } };
+struct pm_batchpir { Engine e; ~pm_batchpir() { print_stamps(e); } };
 
 extern "C" int pm_pir_create(pm_ctx* ctx, uint64_t DBSize, uint64_t DBEntryByteNum, const uint64_t* rawDB,
                              uint64_t F, uint64_t seed, pm_pir** out) {

@@ -5,6 +5,18 @@
 
 #include <string>
 
+// Device code sees the state pointers of PmPart / PmStep in the global address
+// space, so their accesses lower to global_* instead of flat_* instructions
+// (a flat access counts on lgkmcnt too: every later LDS wait would also wait
+// for the outstanding global stores of the resolve chain).  Same layout on
+// host and device (64-bit pointers).  Host-only translation units (the engine)
+// define PM_HOST_TU so their device pass sees the plain host types.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(PM_HOST_TU)
+#define PM_G __attribute__((address_space(1)))
+#else
+#define PM_G
+#endif
+
 namespace pm {
 
 constexpr uint32_t kDefaultProgramPoint = 0x7fffffffu;   // pir.go:15
@@ -41,21 +53,21 @@ struct PmPart {
   uint32_t CS, log2CS, SS, PH, Qpc, H, MaxQ, pad;
   uint32_t rk[44];   // expanded AES-128 key (expandKeyAsm layout)
   // client state, device-resident
-  uint32_t* tag;     // [H]   short tags (primary tags mutate on refresh)
-  uint32_t* pp;      // [PH]  primaryProgramPoint
-  uint64_t* parity;  // [H*E] primary parities then backup parities
-  uint32_t* ridx;    // [SS*Qpc] replacementIdx
-  uint64_t* rval;    // [SS*Qpc*E] replacementVal
-  uint32_t* hist;    // [SS]  QueryHistogram
-  uint32_t* fqn;     // [1]   FinishedQueryNum
-  uint64_t* arena;   // [MaxQ*E] localCache rows (pir.go:120), slot = FinishedQueryNum at answer time
+  PM_G uint32_t* tag;     // [H]   short tags (primary tags mutate on refresh)
+  PM_G uint32_t* pp;      // [PH]  primaryProgramPoint
+  PM_G uint64_t* parity;  // [H*E] primary parities then backup parities
+  PM_G uint32_t* ridx;    // [SS*Qpc] replacementIdx
+  PM_G uint64_t* rval;    // [SS*Qpc*E] replacementVal
+  PM_G uint32_t* hist;    // [SS]  QueryHistogram
+  PM_G uint32_t* fqn;     // [1]   FinishedQueryNum
+  PM_G uint64_t* arena;   // [MaxQ*E] localCache rows (pir.go:120), slot = FinishedQueryNum at answer time
   // PRF table: tab[c*H + t] = PRF(tag t, chunk c) & (CS-1) for every tag t in
   // [0, H) and chunk c in [0, SS) (kSkip at a backup tag's own chunk).  Every
   // tag a hint can carry is a hint index (primary tags start at h, a refresh
   // hands over backup tag PH+g*Qpc+j), so this table, built once per
   // preprocessing, holds every PRF value the online phase needs.
-  uint16_t* tab;
-  uint16_t* tabT;    // the same table hint-major: tabT[t*SS + c] (set expansion reads one row)
+  PM_G uint16_t* tab;
+  PM_G uint16_t* tabT;    // the same table hint-major: tabT[t*SS + c] (set expansion reads one row)
 };
 
 // Sub-query kinds / statuses for one batched step.
@@ -82,24 +94,31 @@ struct PmOutHdr {
   float dist;
   uint32_t pad;
 };
-// Arguments of the four step kernels (pm_query.hip).
+// Arguments of the step kernels (pm_query.hip).
+constexpr uint32_t kArgSubs = 112, kArgParts = 32;
 struct PmStep {
-  const PmPart* parts;
-  const PmSub* subs_h;    // pinned host descriptor, read zero-copy by k_match
-  const uint32_t* sb_h;   // sub_begin[np+1] (pinned host)
-  PmSub* subs;            // device copies
-  uint32_t* sb;
-  uint64_t* bits;         // [nsub][words] hint-match bits (k_match -> k_resolve)
-  PmRes* res;             // [nsub]
-  uint64_t* ans;          // [nsub][E] raw answers of chained sub-queries
-  uint32_t* done;         // [0] k_answer arrival counter of chain workgroups,
+  const PM_G PmPart* parts;
+  const PM_G PmSub* subs_h;    // pinned host descriptor, read zero-copy by k_match
+  const PM_G uint32_t* sb_h;   // sub_begin[np+1] (pinned host)
+  PM_G PmSub* subs;            // device copies
+  PM_G uint32_t* sb;
+  PM_G uint64_t* bits;         // [nsub][words] hint-match bits (k_match -> k_resolve)
+  PM_G PmRes* res;             // [nsub]
+  PM_G uint64_t* ans;          // [nsub][E] raw answers of chained sub-queries
+  PM_G uint32_t* done;         // [0] k_answer arrival counter of chain workgroups,
                           // [1] chained sub-queries, [2] workgroups involved in chains,
                           // [3..] chained sub-query list (zeroed by k_match, filled by k_resolve)
-  const uint64_t* db;
-  const float* q;         // search query (device) or null
-  PmOutHdr* hdr_h;        // pinned host outputs
-  uint64_t* rows_h;
-  uint32_t words, E, dim, nsub, np, pad;
+  const PM_G uint64_t* db;
+  const PM_G float* q;         // search query (device) or null
+  PM_G PmOutHdr* hdr_h;        // pinned host outputs
+  PM_G uint64_t* rows_h;
+  PM_G uint64_t* stamps;       // PM_STAMPS diagnostic builds only: s_memtime per phase
+  uint32_t words, E, dim, nsub, np;
+  // Small steps ship the descriptor inside the kernel arguments (no PCIe
+  // round trip); larger ones use subs_h / sb_h.
+  uint32_t args_valid;
+  uint32_t sb_a[kArgParts + 1];
+  PmSub subs_a[kArgSubs];
 };
 
 }  // namespace pm
@@ -115,7 +134,8 @@ void prep_fold(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxH, 
 void prep_repl(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxRepl,
                const uint64_t* db, uint32_t E);
 void step_match(hipStream_t st, const PmStep& S, uint32_t maxPH);
-void step_resolve(hipStream_t st, const PmStep& S);
+void step_resolve(hipStream_t st, const PmStep& S, bool lds);
+bool step_resolve_lds_ok(uint32_t maxPH, uint32_t max_sub_per_part);
 void step_answer(hipStream_t st, const PmStep& S);
 uint32_t step_max_sub_per_part();
 uint32_t step_max_ss();

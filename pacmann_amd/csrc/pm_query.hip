@@ -36,26 +36,30 @@ constexpr uint32_t kNone = 0xffffffffu;
 
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(kBlock) k_match(PmStep S) {
-  __shared__ PmSub s_sub;
   const uint32_t s = blockIdx.y;
-  if (threadIdx.x == 0) {
-    const PmSub sub = S.subs_h[s];   // zero-copy read of the host descriptor
-    s_sub = sub;
-    if (blockIdx.x == 0) S.subs[s] = sub;
+  PmSub sub;
+  if (S.args_valid) {
+    sub = S.subs_a[s];
+    __builtin_amdgcn_sched_barrier(0);
+  } else {   // zero-copy read of the host descriptor; staged for the later kernels
+    __shared__ PmSub s_sub;
+    if (threadIdx.x == 0) {
+      s_sub = S.subs_h[s];
+      if (blockIdx.x == 0) S.subs[s] = s_sub;
+    }
+    if (blockIdx.x == 0 && s == 0)
+      for (uint32_t i = threadIdx.x; i <= S.np; i += kBlock) S.sb[i] = S.sb_h[i];
+    __syncthreads();
+    sub = s_sub;
   }
-  if (blockIdx.x == 0 && s == 0) {
-    for (uint32_t i = threadIdx.x; i <= S.np; i += kBlock) S.sb[i] = S.sb_h[i];
-    if (threadIdx.x < 3) S.done[threadIdx.x] = 0;
-  }
-  __syncthreads();
-  const PmSub sub = s_sub;
+  if (blockIdx.x == 0 && s == 0 && threadIdx.x < 3) S.done[threadIdx.x] = 0;
   if (sub.kind != SUB_REAL) return;
   const PmPart& P = S.parts[sub.part];
   const uint32_t base = blockIdx.x * kBlock;
   if (base >= P.PH) return;
   const uint32_t mask = P.CS - 1, chunk = (uint32_t)(sub.idx >> P.log2CS),
                  offset = (uint32_t)(sub.idx & mask);
-  const uint16_t* row = P.tab + (uint64_t)chunk * P.H;
+  const PM_G uint16_t* row = P.tab + (uint64_t)chunk * P.H;
   const uint32_t h = base + threadIdx.x;
   bool m = false;
   if (h < P.PH && sub.idx < P.N) {
@@ -64,6 +68,19 @@ __global__ void __launch_bounds__(kBlock) k_match(PmStep S) {
   }
   const uint64_t b = __ballot(m);
   if ((threadIdx.x & 63) == 0 && (h - (threadIdx.x & 63)) < P.PH) S.bits[(uint64_t)s * S.words + (h >> 6)] = b;
+}
+
+// Descriptor accessors: kernel arguments when they carry it, else the device copies.
+// (Two explicit branches: a select of the two addresses would merge them into
+// one generic pointer and a flat load.)
+__device__ __forceinline__ PmSub step_sub(const PmStep& S, uint32_t s) {
+  if (S.args_valid) return S.subs_a[s];
+  PmSub v = S.subs[s];
+  __builtin_amdgcn_sched_barrier(0);
+  return v;
+}
+__device__ __forceinline__ uint32_t step_sb(const PmStep& S, uint32_t p) {
+  return S.args_valid ? S.sb_a[p] : S.sb[p];
 }
 
 // First set bit at position >= start in a sub-query's match bitmask (one wave).
@@ -90,55 +107,289 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t x) {
   return x;
 }
 
-constexpr int kMaxSubPerPart = 256;
+#ifdef PM_STAMPS
+#define STAMP(i)                                                                 \
+  do {                                                                           \
+    if (threadIdx.x == 0 && S.stamps) {                                          \
+      uint64_t t_;                                                               \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+      S.stamps[blockIdx.x * 64 + (i)] = t_;                                      \
+    }                                                                            \
+  } while (0)
+#else
+#define STAMP(i) do {} while (0)
+#endif
 
+constexpr int kMaxSubPerPart = 256;
+// LDS staging limits of the fast resolve path (SIFT1M / MS-MARCO shapes);
+// larger configurations take the global-memory path of the same kernel.
+constexpr uint32_t kLdsPH = 8192, kLdsBitWords = 2048, kSpecSubs = 64;   // staging: 8 items per thread
+
+template <bool LDS>
 __global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
   __shared__ uint64_t s_idx[kMaxSubPerPart];
   __shared__ uint32_t s_kind[kMaxSubPerPart], s_chunk[kMaxSubPerPart], s_st[kMaxSubPerPart],
       s_hist0[kMaxSubPerPart], s_c1[kMaxSubPerPart], s_c2[kMaxSubPerPart], s_t1[kMaxSubPerPart],
-      s_p1[kMaxSubPerPart], s_t2[kMaxSubPerPart], s_p2[kMaxSubPerPart];
+      s_p1[kMaxSubPerPart], s_t2[kMaxSubPerPart], s_p2[kMaxSubPerPart], s_sing[kMaxSubPerPart];
   __shared__ uint32_t m_h[kMaxSubPerPart], m_tag[kMaxSubPerPart], m_pp[kMaxSubPerPart],
       m_sub[kMaxSubPerPart];
-  __shared__ uint32_t s_fqn;
+  __shared__ uint32_t s_fqn, s_chain[kMaxSubPerPart];
+  __shared__ PmRes s_res[kMaxSubPerPart];
+  // fast path staging: match bits, tags / program points, speculative re-evaluation values
+  __shared__ uint64_t bits_l[LDS ? kLdsBitWords : 1];
+  __shared__ uint32_t tag_l[LDS ? kLdsPH : 1], pp_l[LDS ? kLdsPH : 1];
+  __shared__ uint16_t spec_v[LDS ? kSpecSubs * kSpecSubs : 1];
   const uint32_t p = blockIdx.x;
-  const PmPart& P = S.parts[p];
-  const uint32_t b0 = S.sb[p], n = S.sb[p + 1] - b0;
+  const PmPart P = S.parts[p];   // a copy: the chain loop's memory clobbers must not reload it
+  const uint32_t b0 = step_sb(S, p), n = step_sb(S, p + 1) - b0;
   if (n == 0) return;
-  const uint32_t lg = P.log2CS, mask = P.CS - 1, nw = (P.PH + 63) / 64;
-  // --- phase 0: prefetch the partition's sub-queries and counters -----------
-  for (uint32_t j = threadIdx.x; j < n; j += kBlock) {
-    const PmSub sub = S.subs[b0 + j];
-    s_kind[j] = sub.kind;
-    s_idx[j] = sub.idx;
-    const uint32_t c = (uint32_t)(sub.idx >> lg);
-    s_chunk[j] = c;
-    s_hist0[j] = (sub.kind == SUB_REAL && sub.idx < P.N) ? P.hist[c] : 0;
-    s_st[j] = kNone;
+  const uint32_t lg = P.log2CS, mask = P.CS - 1, nw = (P.PH + 63) / 64, H = P.H;
+  const uint32_t tid = threadIdx.x;
+  STAMP(0);
+  // --- phase 0: prefetch sub-queries, counters, match bits, tags ------------
+  // Every global load of the staging is issued before the first LDS store:
+  // the kernel is latency-bound, so one round trip instead of one per item.
+  {
+    constexpr int U = 8;
+    PmSub sv[2];
+    uint32_t hv[2];
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));   // (uint4 is a union: no SROA)
+    uint64_t bv[U];
+    u32x4 tv[U], pv[U];
+    const uint32_t nb = LDS ? n * nw : 0, ph4 = LDS ? P.PH / 4 : 0;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const uint32_t j = tid + u * kBlock;
+      if (j < n) sv[u] = step_sub(S, b0 + j);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = tid + u * kBlock;
+      if (i < nb) bv[u] = S.bits[(uint64_t)(b0 + i / nw) * S.words + (i % nw)];
+      if (i < ph4) {
+        tv[u] = reinterpret_cast<const PM_G u32x4*>(P.tag)[i];
+        pv[u] = reinterpret_cast<const PM_G u32x4*>(P.pp)[i];
+      }
+    }
+    const uint32_t fq = tid == 0 ? *P.fqn : 0;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const uint32_t j = tid + u * kBlock;
+      hv[u] = (j < n && sv[u].kind == SUB_REAL && sv[u].idx < P.N) ? P.hist[(uint32_t)(sv[u].idx >> lg)] : 0;
+    }
+    for (uint32_t j = tid + 2 * kBlock; j < n; j += kBlock) {   // n > 512: rare
+      const PmSub sub = step_sub(S, b0 + j);
+      s_kind[j] = sub.kind; s_idx[j] = sub.idx; s_chunk[j] = (uint32_t)(sub.idx >> lg); s_st[j] = kNone;
+      s_hist0[j] = (sub.kind == SUB_REAL && sub.idx < P.N) ? P.hist[(uint32_t)(sub.idx >> lg)] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const uint32_t j = tid + u * kBlock;
+      if (j < n) {
+        s_kind[j] = sv[u].kind; s_idx[j] = sv[u].idx; s_chunk[j] = (uint32_t)(sv[u].idx >> lg);
+        s_hist0[j] = hv[u]; s_st[j] = kNone;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = tid + u * kBlock;
+      if (i < nb) bits_l[i] = bv[u];
+      if (i < ph4) {
+        reinterpret_cast<u32x4*>(tag_l)[i] = tv[u];
+        reinterpret_cast<u32x4*>(pp_l)[i] = pv[u];
+      }
+    }
+    if (tid == 0) s_fqn = fq;
   }
-  if (threadIdx.x == 0) s_fqn = *P.fqn;
   __syncthreads();
-  // --- phase 1: first two stale candidates per real sub-query + their state --
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  STAMP(1);
+  auto bits_of = [&](uint32_t j) -> const uint64_t* {
+    return LDS ? bits_l + (uint64_t)j * nw : S.bits + (uint64_t)(b0 + j) * S.words;
+  };
+  auto tag_of = [&](uint32_t h) -> uint32_t { return LDS ? tag_l[h] : P.tag[h]; };
+  auto pp_of = [&](uint32_t h) -> uint32_t { return LDS ? pp_l[h] : P.pp[h]; };
+  // --- phase 1: first two stale candidates per real sub-query + their state;
+  //     speculative in-group index of every sub-query (all earlier succeed)
+  const uint32_t wave = tid >> 6, lane = tid & 63;
   for (uint32_t j = wave; j < n; j += kBlock / 64) {
     if (s_kind[j] != SUB_REAL) continue;
-    const uint64_t* bw = S.bits + (uint64_t)(b0 + j) * S.words;
+    const uint64_t* bw = bits_of(j);
     const uint32_t c1 = find_next(bw, nw, 0);
     const uint32_t c2 = c1 == kNone ? kNone : find_next(bw, nw, c1 + 1);
     if (lane == 0) {
       s_c1[j] = c1; s_c2[j] = c2;
-      s_t1[j] = c1 == kNone ? 0 : P.tag[c1]; s_p1[j] = c1 == kNone ? 0 : P.pp[c1];
-      s_t2[j] = c2 == kNone ? 0 : P.tag[c2]; s_p2[j] = c2 == kNone ? 0 : P.pp[c2];
+      s_t1[j] = c1 == kNone ? 0 : tag_of(c1); s_p1[j] = c1 == kNone ? 0 : pp_of(c1);
+      s_t2[j] = c2 == kNone ? 0 : tag_of(c2); s_p2[j] = c2 == kNone ? 0 : pp_of(c2);
+    }
+  }
+  if (LDS && n <= kSpecSubs && wave == kBlock / 64 - 1) {
+    // The last wave (the one with the least candidate work above) predicts, in
+    // registers, the in-chunk index each sub-query would get if every earlier
+    // one succeeds, and issues the table loads of the values the re-evaluation
+    // in phase 2 would then need:
+    //   spec_v[k][j] = PRF(tag the refresh of sub k would hand out, chunk of j)
+    const uint32_t k = lane;
+    const bool real = k < n && s_kind[k] == SUB_REAL;
+    const uint64_t idx = k < n ? s_idx[k] : ~0ull;
+    const uint32_t ch = k < n ? s_chunk[k] : kNone;
+    bool first = real;                 // not a repeat of an earlier real sub-query
+    for (uint32_t t = 0; t + 1 < n; ++t) {
+      const uint64_t it = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(idx >> 32), t) << 32) |
+                          __builtin_amdgcn_readlane((uint32_t)idx, t);
+      const bool rt = __builtin_amdgcn_readlane(real ? 1u : 0u, t) != 0;
+      if (k > t && rt && it == idx) first = false;
+    }
+    uint32_t ing = k < n ? s_hist0[k] : 0;
+    for (uint32_t q = 0; q + 1 < n; ++q) {
+      const bool fq = __builtin_amdgcn_readlane(first ? 1u : 0u, q) != 0;
+      const uint32_t cq = __builtin_amdgcn_readlane(ch, q);
+      if (k > q && fq && cq == ch) ++ing;
+    }
+    if (k < n) s_sing[k] = ing;
+    for (uint32_t e0 = 0; e0 < n * n; e0 += 64) {   // uniform: every lane joins the shuffles
+      const uint32_t e = e0 + lane, kk = (e / n) & 63, j = e % n;
+      const uint32_t sk = __shfl(ing, kk), ck = __shfl(ch, kk), cj = __shfl(ch, j);
+      const bool rk = __shfl(real ? 1u : 0u, kk) != 0, rj = __shfl(real ? 1u : 0u, j) != 0;
+      if (e < n * n && kk < j && rk && rj && ck < P.SS && cj < P.SS && sk < P.Qpc)
+        spec_v[kk * kSpecSubs + j] = P.tab[(uint64_t)cj * H + P.PH + ck * P.Qpc + sk];
     }
   }
   __syncthreads();
+  STAMP(2);
+  STAMP(3);
   if (wave != 0) return;
-  // --- phase 2: the sequential chain of Client.Query calls, on wave 0 --------
-  volatile uint32_t* vst = s_st;
-  volatile uint32_t* vmh = m_h;
-  volatile uint32_t* vmt = m_tag;
-  volatile uint32_t* vmp = m_pp;
-  volatile uint32_t* vms = m_sub;
-  uint32_t fqn = s_fqn, nmod = 0;
+  if (n <= 64) {
+    // --- phase 2 (n <= 64): the chain in wave-0 registers -------------------
+    // Lane k holds sub-query k (request, stale candidates, result) and entry k
+    // of the list of hints refreshed so far in this step; each iteration reads
+    // the current sub-query with v_readlane and decides with ballots, so the
+    // only memory access per iteration is the re-evaluation value of each
+    // refreshed hint (LDS when predicted, else the PRF table).
+    const uint32_t k = lane;
+    const bool in = k < n;
+    const uint32_t kd = in ? s_kind[k] : SUB_NONE;
+    const uint64_t ix = in ? s_idx[k] : 0;
+    const uint32_t ch = in ? s_chunk[k] : kNone, h0 = in ? s_hist0[k] : 0;
+    const bool real = in && kd == SUB_REAL;
+    const uint32_t c1 = real ? s_c1[k] : kNone, c2 = real ? s_c2[k] : kNone;
+    const uint32_t t1 = real ? s_t1[k] : 0, p1 = real ? s_p1[k] : 0;
+    const uint32_t t2 = real ? s_t2[k] : 0, p2 = real ? s_p2[k] : 0;
+    const bool spec = LDS && n <= kSpecSubs;
+    const uint32_t sg = (spec && real) ? s_sing[k] : kNone;
+    // tag sub k's refresh would hand out if every earlier sub-query succeeds
+    const uint32_t pred = (sg < P.Qpc && ch < P.SS) ? P.PH + ch * P.Qpc + sg : kNone;
+    // per sub-query result
+    uint32_t st = kNone, rhit = 0, ring = 0, rtag = 0, rpp = 0, rslot = 0, rfl = 0;
+    // per refreshed-hint entry: hint, current tag / program point, last holder, its predicted tag
+    uint32_t mh = kNone, mt = 0, mp = 0, ms = 0, mpt = kNone;
+    uint32_t cl = 0;   // chain list entry
+    uint32_t fqn = s_fqn, nmod = 0, nchain = 0, cadd = 0;
+    auto rl = [](uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane(v, l); };
+    for (uint32_t j = 0; j < n; ++j) {
+      const uint32_t kind = rl(kd, j), chunk = rl(ch, j);
+      const uint64_t idx = ((uint64_t)rl((uint32_t)(ix >> 32), j) << 32) | rl((uint32_t)ix, j);
+      uint32_t status = kNone, hit = 0, hist = 0, tag = 0, pp = 0, slot = 0, fl = 0;
+      if (kind == SUB_DUMMY) status = ST_DUMMY;
+      else if (kind == SUB_HOSTCACHE) { status = ST_CACHED; slot = (uint32_t)idx; }
+      else if (kind != SUB_REAL) status = ST_SKIP;
+      else if (idx >= P.N) status = ST_ERANGE;
+      else {
+        const uint32_t off = (uint32_t)(idx & mask);
+        // local cache hit inside this step (pir.go:381-383)
+        const uint64_t dup = __ballot(k < j && real && ix == idx && st == ST_OK);
+        if (dup) { status = ST_DUP; slot = b0 + (uint32_t)__builtin_ctzll(dup); }
+        else if (fqn >= P.MaxQ) status = ST_EBUDGET;                        // pir.go:386-391
+        else {
+          hist = rl(h0, j) + (uint32_t)__builtin_popcountll(__ballot(k < j && st == ST_OK && ch == chunk));
+          if (hist >= P.Qpc) status = ST_ECHUNK;                            // pir.go:396-400
+        }
+        if (status == kNone) {
+          // first stale match not refreshed earlier in this step
+          uint32_t c = rl(c1, j), which = 1;
+          while (c != kNone && __ballot(k < nmod && mh == c)) {
+            if (which == 1) { c = rl(c2, j); which = 2; }
+            else { c = find_next(bits_of(j), nw, c + 1); which = 3; }
+          }
+          // hints refreshed earlier in this step, with their current tag / program point
+          uint32_t cand = kNone;
+          if (k < nmod) {
+            const uint32_t o = mt == mpt ? (uint32_t)spec_v[ms * kSpecSubs + j]
+                                         : (uint32_t)P.tab[(uint64_t)chunk * H + mt];
+            if (o == off && (mp == kDefaultProgramPoint || (mp >> lg) != chunk)) cand = mh;
+          }
+          uint32_t bm = kNone, bk = 0;
+          for (uint64_t cm = __ballot(cand != kNone); cm; cm &= cm - 1) {   // usually 0 or 1 bits
+            const uint32_t b = (uint32_t)__builtin_ctzll(cm), v = rl(cand, b);
+            if (v < bm) { bm = v; bk = b; }
+          }
+          hit = min(c, bm);
+          if (hit == kNone) {
+            status = ST_ENOHIT;                                              // pir.go:416-419
+          } else {
+            const bool chained = hit == bm;
+            if (chained) { tag = rl(mt, bk); pp = rl(mp, bk); }
+            else if (which == 1) { tag = rl(t1, j); pp = rl(p1, j); }
+            else if (which == 2) { tag = rl(t2, j); pp = rl(p2, j); }
+            else { tag = tag_of(hit); pp = pp_of(hit); }
+            status = ST_OK; slot = fqn; fl = chained ? 1u : 0u;
+            // refresh (pir.go:460-470): backup hint (chunk, hist) has tag PH + chunk*Qpc + hist
+            const uint32_t ntag = P.PH + chunk * P.Qpc + hist, npred = rl(pred, j);
+            if (chained) {
+              // the previous holder must publish its parity refresh; this chained
+              // sub-query counts itself, the chain head is counted once
+              const uint32_t prev = rl(ms, bk), pf = rl(rfl, prev);
+              cadd += 1u + ((!(pf & 1u) && !(pf & 4u)) ? 1u : 0u);
+              if (k == prev) rfl = pf | 2u | 4u;
+              if (k == nchain) cl = b0 + j;
+              if (k == bk) { mt = ntag; mp = (uint32_t)idx; ms = j; mpt = npred; }
+              ++nchain;
+            } else {
+              if (k == nmod) { mh = hit; mt = ntag; mp = (uint32_t)idx; ms = j; mpt = npred; }
+              ++nmod;
+            }
+            ++fqn;
+          }
+        }
+      }
+      if (k == j) { st = status; rhit = hit; ring = hist; rtag = tag; rpp = pp; rslot = slot; rfl = fl; }
+      if (j < 32) STAMP(4 + j);
+    }
+    // --- flush (one writer per result / hint / chunk) -----------------------
+    if (in) {
+      const bool ok = st == ST_OK;
+      S.res[b0 + k] = PmRes{st, ok ? rhit : 0u, ok ? ch : 0u, ok ? ring : 0u, ok ? rtag : 0u,
+                            ok ? rpp : 0u, (ok || st == ST_DUP || st == ST_CACHED) ? rslot : 0u, ok ? rfl : 0u};
+    }
+    if (k < nmod) { P.tag[mh] = mt; P.pp[mh] = mp; }
+    bool last = in && st == ST_OK;   // QueryHistogram: the last success per chunk writes
+    for (uint32_t t = 0; t < n; ++t)
+      if (t > k && rl(st, t) == ST_OK && rl(ch, t) == ch) last = false;
+    if (last) P.hist[ch] = ring + 1;
+    if (nchain) {   // this partition's chained sub-queries, contiguous and in order
+      uint32_t pos = 0;
+      if (k == 0) {
+        pos = atomicAdd(&S.done[1], nchain);
+        atomicAdd(&S.done[2], cadd);
+      }
+      pos = __builtin_amdgcn_readfirstlane(pos);
+      if (k < nchain) S.done[3 + pos + k] = cl;
+    }
+    if (k == 0) *P.fqn = fqn;
+    STAMP(40);
+    return;
+  }
+  // --- phase 2 (n > 64): the sequential chain of Client.Query calls, on wave 0
+  // The chain state lives in plain LDS arrays: lane 0 writes, every lane of the
+  // same wave reads in a later iteration (LDS instructions of one wave complete
+  // in order); an empty asm memory clobber at the end of each iteration keeps
+  // the compiler from reusing values across it.  (volatile pointers here would
+  // compile to flat accesses that also wait for the outstanding global stores.)
+  // Nothing is written to global memory inside the loop (on CDNA vmcnt counts
+  // stores too, so any load wait there would also wait for them): results,
+  // refreshed tags / program points, counters and the chain list are kept in
+  // LDS and flushed by the whole wave afterwards.
+  const bool spec = LDS && n <= kSpecSubs;
+  uint32_t fqn = s_fqn, nmod = 0, nchain = 0, cadd = 0;
   for (uint32_t j = 0; j < n; ++j) {
     const uint32_t s = b0 + j, kind = s_kind[j];
     PmRes r{kNone, 0, 0, 0, 0, 0, 0, 0};
@@ -152,7 +403,7 @@ __global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
       if (r.status == kNone) {   // local cache hit inside this step (pir.go:381-383)
         for (uint32_t k0 = 0; k0 < j; k0 += 64) {
           const uint32_t k = k0 + lane;
-          const bool d = k < j && s_kind[k] == SUB_REAL && s_idx[k] == idx && vst[k] == ST_OK;
+          const bool d = k < j && s_kind[k] == SUB_REAL && s_idx[k] == idx && s_st[k] == ST_OK;
           const uint64_t m = __ballot(d);
           if (m) { r.status = ST_DUP; r.slot = b0 + k0 + (uint32_t)__builtin_ctzll(m); break; }
         }
@@ -163,7 +414,7 @@ __global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
         for (uint32_t k0 = 0; k0 < j; k0 += 64) {
           const uint32_t k = k0 + lane;
           hist += (uint32_t)__builtin_popcountll(
-              __ballot(k < j && vst[k] == ST_OK && s_chunk[k] == chunk));
+              __ballot(k < j && s_st[k] == ST_OK && s_chunk[k] == chunk));
         }
         if (hist >= P.Qpc) r.status = ST_ECHUNK;                          // pir.go:396-400
       }
@@ -174,10 +425,10 @@ __global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
           if (c == kNone) break;
           bool mod = false;
           for (uint32_t k0 = 0; k0 < nmod; k0 += 64)
-            mod |= __ballot(k0 + lane < nmod && vmh[k0 + lane] == c) != 0;
+            mod |= __ballot(k0 + lane < nmod && m_h[k0 + lane] == c) != 0;
           if (!mod) break;
           if (which == 1) { c = s_c2[j]; which = 2; }
-          else { c = find_next(S.bits + (uint64_t)s * S.words, nw, c + 1); which = 3; }
+          else { c = find_next(bits_of(j), nw, c + 1); which = 3; }
         }
         // hints refreshed earlier in this step, with their current tag / program point
         uint32_t bm = kNone, bk = kNone;
@@ -185,10 +436,12 @@ __global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
           const uint32_t k = k0 + lane;
           uint32_t cand = kNone;
           if (k < nmod) {
-            const uint32_t pp = vmp[k];
-            if (P.tab[(uint64_t)chunk * P.H + vmt[k]] == off &&
-                (pp == kDefaultProgramPoint || (pp >> lg) != chunk))
-              cand = vmh[k];
+            const uint32_t pp = m_pp[k], tg = m_tag[k], ks = m_sub[k];
+            // the speculative value holds when sub ks received its predicted tag
+            const uint32_t o = (spec && s_sing[ks] < P.Qpc && tg == P.PH + s_chunk[ks] * P.Qpc + s_sing[ks])
+                                   ? (uint32_t)spec_v[ks * kSpecSubs + j]
+                                   : (uint32_t)P.tab[(uint64_t)chunk * H + tg];
+            if (o == off && (pp == kDefaultProgramPoint || (pp >> lg) != chunk)) cand = m_h[k];
           }
           const uint32_t mn = wave_min(cand);
           if (mn < bm) {
@@ -203,41 +456,62 @@ __global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
         } else {
           const bool chained = hit == bm;
           uint32_t tag, pp;
-          if (chained) { tag = vmt[bk]; pp = vmp[bk]; }
+          if (chained) { tag = m_tag[bk]; pp = m_pp[bk]; }
           else if (which == 1) { tag = s_t1[j]; pp = s_p1[j]; }
           else if (which == 2) { tag = s_t2[j]; pp = s_p2[j]; }
-          else { tag = P.tag[hit]; pp = P.pp[hit]; }
+          else { tag = tag_of(hit); pp = pp_of(hit); }
           r = PmRes{ST_OK, hit, chunk, hist, tag, pp, fqn, chained ? 1u : 0u};
           // refresh (pir.go:460-470): backup hint (chunk, hist) has tag PH + chunk*Qpc + hist
           const uint32_t ntag = P.PH + chunk * P.Qpc + hist;
-          if (lane == 0) {
-            P.tag[hit] = ntag;
-            P.pp[hit] = (uint32_t)idx;
-            P.hist[chunk] = hist + 1;
-            if (chained) {
-              // the previous holder of this hint must publish its parity refresh
-              const uint32_t prev = vms[bk];
-              const uint32_t pf = S.res[prev].flags;
-              // this chained sub-query counts itself; the chain head is counted once
-              const uint32_t add = 1u + ((!(pf & 1u) && !(pf & 4u)) ? 1u : 0u);
-              S.res[prev].flags = pf | 2u | 4u;
-              const uint32_t pos = atomicAdd(&S.done[1], 1u);
-              S.done[3 + pos] = s;
-              atomicAdd(&S.done[2], add);
-              vmt[bk] = ntag; vmp[bk] = (uint32_t)idx; vms[bk] = s;
-            } else {
-              vmh[nmod] = hit; vmt[nmod] = ntag; vmp[nmod] = (uint32_t)idx; vms[nmod] = s;
+          if (chained) {
+            // the previous holder of this hint must publish its parity refresh;
+            // this chained sub-query counts itself, the chain head is counted once
+            const uint32_t prev = m_sub[bk];
+            const uint32_t pf = s_res[prev].flags;
+            cadd += 1u + ((!(pf & 1u) && !(pf & 4u)) ? 1u : 0u);
+            if (lane == 0) {
+              s_res[prev].flags = pf | 2u | 4u;
+              s_chain[nchain] = s;
+              m_tag[bk] = ntag; m_pp[bk] = (uint32_t)idx; m_sub[bk] = j;
             }
+            ++nchain;
+          } else {
+            if (lane == 0) { m_h[nmod] = hit; m_tag[nmod] = ntag; m_pp[nmod] = (uint32_t)idx; m_sub[nmod] = j; }
+            ++nmod;
           }
-          if (!chained) ++nmod;
           ++fqn;
         }
       }
     }
-    if (lane == 0) { vst[j] = r.status; S.res[s] = r; }
+    if (lane == 0) { s_st[j] = r.status; s_res[j] = r; }
     __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    if (j < 32) STAMP(4 + j);
+  }
+  // --- flush (pir.go:460-470 refresh; one writer per hint / chunk) ----------
+  for (uint32_t k = lane; k < n; k += 64) S.res[b0 + k] = s_res[k];
+  for (uint32_t k = lane; k < nmod; k += 64) {
+    P.tag[m_h[k]] = m_tag[k];
+    P.pp[m_h[k]] = m_pp[k];
+  }
+  for (uint32_t k = lane; k < n; k += 64) {   // QueryHistogram: the last success per chunk writes
+    if (s_st[k] != ST_OK) continue;
+    const uint32_t c = s_chunk[k];
+    bool last = true;
+    for (uint32_t t = k + 1; t < n; ++t) last &= !(s_st[t] == ST_OK && s_chunk[t] == c);
+    if (last) P.hist[c] = s_res[k].ing + 1;
+  }
+  if (nchain) {   // this partition's chained sub-queries, contiguous and in order
+    uint32_t pos = 0;
+    if (lane == 0) {
+      pos = atomicAdd(&S.done[1], nchain);
+      atomicAdd(&S.done[2], cadd);
+    }
+    pos = __builtin_amdgcn_readfirstlane(pos);
+    for (uint32_t k = lane; k < nchain; k += 64) S.done[3 + pos + k] = s_chain[k];
   }
   if (lane == 0) *P.fqn = fqn;
+  STAMP(40);
 }
 
 // L2Dist of the first `dim` floats of an LDS row against q (device), one
@@ -274,7 +548,7 @@ enum : uint32_t { A_ZERO = 0, A_FINAL = 1, A_CHAINED = 2, A_CACHED = 3, A_DUMMY 
 // Decode one chained sub-query (its hint was refreshed earlier in this step)
 // once every earlier refresh is visible; the whole workgroup participates.
 __device__ void decode_chained(const PmStep& S, uint32_t s, RowBuf& row) {
-  const PmSub sub = S.subs[s];
+  const PmSub sub = step_sub(S, s);
   const PmRes r = S.res[s];
   const PmPart& P = S.parts[sub.part];
   const uint32_t E = S.E, EX = E & ~3u, tid = threadIdx.x;
@@ -313,7 +587,7 @@ __global__ void __launch_bounds__(kAnsBlock) k_answer(PmStep S) {
   __shared__ uint32_t s_last;
   const uint32_t s = blockIdx.x, tid = threadIdx.x;
   const uint32_t E = S.E, EX = E & ~3u, NSEG = EX / W;
-  const PmSub sub = S.subs[s];
+  const PmSub sub = step_sub(S, s);
   const PmRes r = S.res[s];
   const PmPart& P = S.parts[sub.part];
   uint64_t* const orow = S.rows_h + (uint64_t)s * E;
@@ -447,8 +721,14 @@ static inline unsigned cdiv(uint64_t a, uint64_t b) { return (unsigned)((a + b -
 void step_match(hipStream_t st, const PmStep& S, uint32_t maxPH) {
   hipLaunchKernelGGL(k_match, dim3(cdiv(maxPH, kBlock), S.nsub), dim3(kBlock), 0, st, S);
 }
-void step_resolve(hipStream_t st, const PmStep& S) {
-  hipLaunchKernelGGL(k_resolve, dim3(S.np), dim3(kBlock), 0, st, S);
+void step_resolve(hipStream_t st, const PmStep& S, bool lds) {
+  if (lds)
+    hipLaunchKernelGGL(k_resolve<true>, dim3(S.np), dim3(kBlock), 0, st, S);
+  else
+    hipLaunchKernelGGL(k_resolve<false>, dim3(S.np), dim3(kBlock), 0, st, S);
+}
+bool step_resolve_lds_ok(uint32_t maxPH, uint32_t max_sub_per_part) {
+  return maxPH <= kLdsPH && max_sub_per_part * ((maxPH + 63) / 64) <= kLdsBitWords;
 }
 void step_answer(hipStream_t st, const PmStep& S) {
   if (S.E % 2 == 0)
