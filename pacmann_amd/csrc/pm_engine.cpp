@@ -277,6 +277,7 @@ struct Engine {
   FlatMap resp_map;
   std::vector<uint64_t> resp_rows;
   std::vector<float> resp_dist;
+  std::vector<uint64_t> zero_row;   // response of dropped / failed ids (batch-pir.go:229-236)
 };
 
 // NewPianoPIR parameterisation (pir.go:479-514) + NewPianoPIRClient (:130-175)
@@ -746,18 +747,23 @@ extern "C" int pm_batchpir_dummy_preprocessing(pm_batchpir* h) {   // batch-pir.
 // step_max_sub_per_part() sub-queries per partition per step); the rest replay
 // the reference's per-sub-query re-preprocessing check (pir.go:527-530) one
 // sub-query at a time.  q_dev / dist_out: optional L2 of every answer to q.
+// Query (batch-pir.go:170-248).  Responses go to out[n][E], or, when rows_out
+// is given, rows_out[i] points at response i (pinned result rows of the step,
+// the collected rows of a multi-step query, or a zero row); valid until the
+// next query on this engine.
 static int batch_query_impl(Engine* g, const uint64_t* idx, uint64_t n, uint64_t* out, const float* q_dev,
-                            uint32_t dim, float* dist_out);
+                            uint32_t dim, float* dist_out, const uint64_t** rows_out);
 static int batch_query(Engine* g, const uint64_t* idx, uint64_t n, uint64_t* out, const float* q_dev,
-                       uint32_t dim, float* dist_out) {
+                       uint32_t dim, float* dist_out, const uint64_t** rows_out = nullptr) {
   auto t = Clock::now();
-  int r = batch_query_impl(g, idx, n, out, q_dev, dim, dist_out);
+  int r = batch_query_impl(g, idx, n, out, q_dev, dim, dist_out, rows_out);
   g->ctx->host_add("host_batch_query", ms_since(t));
   return r;
 }
 static int batch_query_impl(Engine* g, const uint64_t* idx, uint64_t n, uint64_t* out, const float* q_dev,
-                            uint32_t dim, float* dist_out) {
+                            uint32_t dim, float* dist_out, const uint64_t** rows_out) {
   const uint64_t E = g->E, P = g->P;
+  if (g->zero_row.size() != E) g->zero_row.assign(E, 0);
   for (uint64_t i = 0; i < n; ++i)
     if (idx[i] >= g->N) return fail(PM_EINVAL, "id " + std::to_string(idx[i]) + " >= DBSize");
   const uint64_t qn = n / P;
@@ -807,13 +813,11 @@ static int batch_query_impl(Engine* g, const uint64_t* idx, uint64_t n, uint64_t
       if (k == SUB_REAL || k == SUB_HOSTCACHE) g->resp_map.put(g->sub_gid[s], (uint32_t)s);   // last wins
     }
     for (uint64_t i = 0; i < n; ++i) {
-      if (const uint32_t* sp = g->resp_map.find(idx[i])) {
-        memcpy(out + i * E, g->rows + (uint64_t)*sp * E, E * 8);
-        if (dist_out) dist_out[i] = g->hdr[*sp].dist;
-      } else {
-        memset(out + i * E, 0, E * 8);
-        if (dist_out) dist_out[i] = 0;
-      }
+      const uint32_t* sp = g->resp_map.find(idx[i]);
+      const uint64_t* row = sp ? g->rows + (uint64_t)*sp * E : g->zero_row.data();
+      if (rows_out) rows_out[i] = row;
+      else memcpy(out + i * E, row, E * 8);
+      if (dist_out) dist_out[i] = sp ? g->hdr[*sp].dist : 0.0f;
     }
     qn_done = true;
   }
@@ -844,13 +848,11 @@ static int batch_query_impl(Engine* g, const uint64_t* idx, uint64_t n, uint64_t
     }
   }
   for (uint64_t i = 0; !qn_done && i < n; ++i) {
-    if (const uint32_t* sp = g->resp_map.find(idx[i])) {
-      memcpy(out + i * E, &g->resp_rows[(size_t)*sp * E], E * 8);
-      if (dist_out) dist_out[i] = g->resp_dist[*sp];
-    } else {
-      memset(out + i * E, 0, E * 8);
-      if (dist_out) dist_out[i] = 0;
-    }
+    const uint32_t* sp = g->resp_map.find(idx[i]);
+    const uint64_t* row = sp ? &g->resp_rows[(size_t)*sp * E] : g->zero_row.data();
+    if (rows_out) rows_out[i] = row;
+    else memcpy(out + i * E, row, E * 8);
+    if (dist_out) dist_out[i] = sp ? g->resp_dist[*sp] : 0.0f;
   }
   if (g->QMIP >= g->parts[0].maxq64 - 2) {
     CHK(batch_prep(g));
@@ -992,13 +994,15 @@ struct pm_graph {
   std::vector<float> vectors;
   std::vector<uint32_t> graph;
   DevBuf dvec, dq, dids, ddist;
+  HostBuf stage_h;                                // pinned: query and start-vertex distances
   pm_batchpir* pir = nullptr;
   std::vector<uint64_t> start;   // StartVertices ids
   DevBuf dstart;
   uint64_t total = 0, succ = 0;
   // SearchKNN scratch, reused across calls (no per-step allocation)
   std::vector<int64_t> batch;
-  std::vector<uint64_t> qids, resp;
+  std::vector<uint64_t> qids;
+  std::vector<const uint64_t*> rowp;              // response rows of the last GetVertexInfo
   std::vector<float> dist, start_d;
   std::vector<uint32_t> nb;                       // [len(batch)][m] of the last GetVertexInfo
   FlatMap known;                                  // knownVertices: id -> slot
@@ -1109,14 +1113,25 @@ static int get_vertex_info(pm_graph* g, bool with_q) {
     return 0;
   }
   Engine* e = &g->pir->e;
-  const uint64_t E = e->E;
+  // the ground-truth rows of the success check (private-search.go:483-497) are
+  // pulled into the cache while the GPU answers
+  for (uint64_t i = 0; i < n; ++i) {
+    const char* gr = (const char*)&g->graph[(uint64_t)g->batch[i] * m];
+    for (uint64_t b = 0; b < m * 4; b += 64) __builtin_prefetch(gr + b);
+    __builtin_prefetch(gr + m * 4 - 1);
+  }
   g->qids.assign(g->batch.begin(), g->batch.end());
-  g->resp.resize(n * E);
-  CHK(batch_query(e, g->qids.data(), n, g->resp.data(), with_q ? g->dq.as<float>() : nullptr,
-                  (uint32_t)g->dim, with_q ? g->dist.data() : nullptr));
-  for (uint64_t i = 0; i < n; ++i) {   // Entry2VectorAndNeighbors (private-search.go:418-439)
+  g->rowp.resize(n);
+  CHK(batch_query(e, g->qids.data(), n, nullptr, with_q ? g->dq.as<float>() : nullptr,
+                  (uint32_t)g->dim, with_q ? g->dist.data() : nullptr, g->rowp.data()));
+  const uint64_t nb_off = g->dim * 4;   // Entry2VectorAndNeighbors (private-search.go:418-439)
+  for (uint64_t i = 0; i < n; ++i) {
+    const char* r = (const char*)g->rowp[i] + nb_off;
+    for (uint64_t b = 0; b < m * 4; b += 64) __builtin_prefetch(r + b);
+  }
+  for (uint64_t i = 0; i < n; ++i) {
     uint32_t* nbi = &g->nb[i * m];
-    memcpy(nbi, (const uint8_t*)&g->resp[i * E] + g->dim * 4, m * 4);
+    memcpy(nbi, (const char*)g->rowp[i] + nb_off, m * 4);
     if (memcmp(nbi, &g->graph[(uint64_t)g->batch[i] * m], m * 4) == 0) g->succ++;
   }
   return 0;
@@ -1150,21 +1165,32 @@ static int search_knn_impl(pm_graph* g, const float* query, int k, int max_step,
     g->known_reach.push_back(reach);
   };
   if (!benchmarking) {
-    // the query stays resident for every distance this search computes
-    HIPCHK(hipMemcpyAsync(g->dq.p, query, g->dim * 4, hipMemcpyHostToDevice, st));
+    auto t_init = Clock::now();
+    // the query stays resident for every distance this search computes; it and
+    // the start-vertex distances move through pinned staging (async, no bounce)
     const uint64_t ns = g->start.size();
-    g->start_d.resize(ns);
+    CHK(g->stage_h.reserve(g->dim * 4 + ns * 4));
+    float* qh = g->stage_h.as<float>();
+    float* sdh = qh + g->dim;
+    memcpy(qh, query, g->dim * 4);
+    HIPCHK(hipMemcpyAsync(g->dq.p, qh, g->dim * 4, hipMemcpyHostToDevice, st));
     if (ns) {
       CHK(g->ddist.reserve(ns * 4));
       g->ctx->timed("l2_rows", (double)ns * g->dim * 4, [&] {
         pmk::l2_rows(st, g->dvec.as<float>(), g->dim, ns, g->dstart.as<uint32_t>(), g->dq.as<float>(), (uint32_t)g->dim, g->ddist.as<float>());
       });
-      HIPCHK(hipMemcpyAsync(g->start_d.data(), g->ddist.p, ns * 4, hipMemcpyDeviceToHost, st));
-      HIPCHK(hipStreamSynchronize(st));
+      HIPCHK(hipMemcpyAsync(sdh, g->ddist.p, ns * 4, hipMemcpyDeviceToHost, st));
     }
+    HIPCHK(hipStreamSynchronize(st));
+    // the first `parallel` start vertices in stable distance order (search.go:130-146):
+    // a partial sort on (dist, position) selects exactly those
     g->fs.clear();
-    for (uint64_t i = 0; i < ns; ++i) g->fs.push_back({{g->start_d[i], (int64_t)g->start[i]}, (uint32_t)i});
-    std::stable_sort(g->fs.begin(), g->fs.end(), [](const auto& a, const auto& b) { return a.first.dist < b.first.dist; });
+    for (uint64_t i = 0; i < ns; ++i) g->fs.push_back({{sdh[i], (int64_t)g->start[i]}, (uint32_t)i});
+    const size_t take = std::min<size_t>(g->fs.size(), (size_t)std::max(parallel, 0));
+    std::partial_sort(g->fs.begin(), g->fs.begin() + take, g->fs.end(), [](const auto& a, const auto& b) {
+      return a.first.dist < b.first.dist || (a.first.dist == b.first.dist && a.second < b.second); });
+    g->fs.resize(take);   // start ids are distinct: none of the first `parallel` is skipped as known
+    g->ctx->host_add("host_knn_init", ms_since(t_init));
     for (size_t i = 0; (int64_t)g->heap.size() < parallel && i < g->fs.size(); ++i) {
       const int64_t id = g->fs[i].first.id;
       if (g->known.find((uint64_t)id)) continue;
@@ -1196,14 +1222,18 @@ static int search_knn_impl(pm_graph* g, const float* query, int k, int max_step,
       heap_push(g->heap, {g->dist[i], id});
     }
   }
+  auto t_fin = Clock::now();
   g->all.clear();
   for (size_t i = 0; i < g->known_id.size(); ++i) g->all.push_back({g->known_dist[i], g->known_id[i]});
-  std::sort(g->all.begin(), g->all.end(), [](const VD& a, const VD& b) {
+  // top k in (dist, id) order (search.go:222-233); ids are unique, so a partial sort is exact
+  std::partial_sort(g->all.begin(), g->all.begin() + std::min<size_t>(g->all.size(), (size_t)std::max(k, 0)),
+                    g->all.end(), [](const VD& a, const VD& b) {
     return a.dist < b.dist || (a.dist == b.dist && a.id < b.id); });
   for (int i = 0; i < k; ++i) {
     if (i >= (int)g->all.size()) { ids_out[i] = -1; if (steps_out) steps_out[i] = -1; }
     else { ids_out[i] = g->all[i].id; if (steps_out) steps_out[i] = g->known_reach[*g->known.find((uint64_t)g->all[i].id)]; }
   }
+  g->ctx->host_add("host_knn_final", ms_since(t_fin));
   return 0;
 }
 
