@@ -556,7 +556,10 @@ static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
     HIPCHK(hipMemcpy(t.data(), g->stamps.p, 64 * 8, hipMemcpyDeviceToHost));
     g->stamp_sum.resize(64, 0.0);
     for (int i = 1; i < 64; ++i)
-      if (t[i] && t[0]) g->stamp_sum[i] += (double)(t[i] - t[0]);
+    {   // each kernel's stamps relative to its own first one
+      const uint64_t base = i >= 48 ? t[48] : i >= 41 ? t[41] : t[0];
+      if (t[i] && base && i != 41 && i != 48) g->stamp_sum[i] += (double)(t[i] - base);
+    }
     g->stamp_n++;
   }
 #endif
@@ -590,7 +593,7 @@ static void close_partition(Engine* g, uint32_t p) {   // sub_begin[p+1] = curre
 static void print_stamps(const Engine& e) {
 #ifdef PM_STAMPS
   if (!e.stamp_n) return;
-  fprintf(stderr, "[pm-stamps] k_resolve partition 0, mean shader clocks since start over %lu steps:", (unsigned long)e.stamp_n);
+  fprintf(stderr, "[pm-stamps] mean shader clocks since kernel start over %lu steps (1-40 k_resolve part 0, 42-47 k_match, 49-63 k_answer):", (unsigned long)e.stamp_n);
   for (size_t i = 1; i < e.stamp_sum.size(); ++i)
     if (e.stamp_sum[i] > 0) fprintf(stderr, " %zu:%.0f", i, e.stamp_sum[i] / e.stamp_n);
   fprintf(stderr, "\n");

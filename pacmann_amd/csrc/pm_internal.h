@@ -95,7 +95,10 @@ struct PmOutHdr {
   uint32_t pad;
 };
 // Arguments of the step kernels (pm_query.hip).
-constexpr uint32_t kArgSubs = 112, kArgParts = 32;
+#ifndef PM_KARG_SUBS
+#define PM_KARG_SUBS 112
+#endif
+constexpr uint32_t kArgSubs = PM_KARG_SUBS, kArgParts = PM_KARG_SUBS > 1 ? 32 : 1;
 struct PmStep {
   const PM_G PmPart* parts;
   const PM_G PmSub* subs_h;    // pinned host descriptor, read zero-copy by k_match

@@ -34,6 +34,30 @@ namespace pm {
 constexpr int kAnsBlock = 512;
 constexpr uint32_t kNone = 0xffffffffu;
 
+#ifdef PM_STAMPS
+#define STAMP(i)                                                                 \
+  do {                                                                           \
+    if (threadIdx.x == 0 && S.stamps) {                                          \
+      uint64_t t_;                                                               \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+      S.stamps[blockIdx.x * 64 + (i)] = t_;                                      \
+    }                                                                            \
+  } while (0)
+// stamps of one workgroup of the other step kernels at fixed slots
+#define STAMP_AT(cond, slot)                                                     \
+  do {                                                                           \
+    if ((cond) && threadIdx.x == 0 && S.stamps) {                                \
+      uint64_t t_;                                                               \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+      S.stamps[slot] = t_;                                                       \
+    }                                                                            \
+  } while (0)
+#else
+#define STAMP(i) do {} while (0)
+#define STAMP_AT(cond, slot) do { (void)(cond); } while (0)
+#endif
+// slots: k_resolve partition 0: 0..40; k_match block (0,0): 41..47; k_answer block 0: 48..63
+
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(kBlock) k_match(PmStep S) {
   const uint32_t s = blockIdx.y;
@@ -53,10 +77,13 @@ __global__ void __launch_bounds__(kBlock) k_match(PmStep S) {
     sub = s_sub;
   }
   if (blockIdx.x == 0 && s == 0 && threadIdx.x < 3) S.done[threadIdx.x] = 0;
+  const bool stamp_wg = blockIdx.x == 0 && s == 0;
+  STAMP_AT(stamp_wg, 41);
   if (sub.kind != SUB_REAL) return;
   const PmPart& P = S.parts[sub.part];
   const uint32_t base = blockIdx.x * kBlock;
   if (base >= P.PH) return;
+  STAMP_AT(stamp_wg, 42);
   const uint32_t mask = P.CS - 1, chunk = (uint32_t)(sub.idx >> P.log2CS),
                  offset = (uint32_t)(sub.idx & mask);
   const PM_G uint16_t* row = P.tab + (uint64_t)chunk * P.H;
@@ -67,6 +94,7 @@ __global__ void __launch_bounds__(kBlock) k_match(PmStep S) {
     m = row[P.tag[h]] == offset && (pp == kDefaultProgramPoint || (pp >> P.log2CS) != chunk);
   }
   const uint64_t b = __ballot(m);
+  STAMP_AT(stamp_wg, 43);
   if ((threadIdx.x & 63) == 0 && (h - (threadIdx.x & 63)) < P.PH) S.bits[(uint64_t)s * S.words + (h >> 6)] = b;
 }
 
@@ -107,18 +135,6 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t x) {
   return x;
 }
 
-#ifdef PM_STAMPS
-#define STAMP(i)                                                                 \
-  do {                                                                           \
-    if (threadIdx.x == 0 && S.stamps) {                                          \
-      uint64_t t_;                                                               \
-      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
-      S.stamps[blockIdx.x * 64 + (i)] = t_;                                      \
-    }                                                                            \
-  } while (0)
-#else
-#define STAMP(i) do {} while (0)
-#endif
 
 constexpr int kMaxSubPerPart = 256;
 // LDS staging limits of the fast resolve path (SIFT1M / MS-MARCO shapes);
@@ -591,6 +607,8 @@ __global__ void __launch_bounds__(kAnsBlock) k_answer(PmStep S) {
   const PmRes r = S.res[s];
   const PmPart& P = S.parts[sub.part];
   uint64_t* const orow = S.rows_h + (uint64_t)s * E;
+  const bool stamp_wg = blockIdx.x == 0;
+  STAMP_AT(stamp_wg, 48);
   const uint32_t mode = r.status == ST_OK ? ((r.flags & 1u) ? A_CHAINED : A_FINAL)
                       : r.status == ST_CACHED ? A_CACHED
                       : r.status == ST_DUMMY ? A_DUMMY : A_ZERO;
@@ -616,29 +634,41 @@ __global__ void __launch_bounds__(kAnsBlock) k_answer(PmStep S) {
     for (uint32_t i = tid; i < P.SS; i += kAnsBlock)
       qo[i] = (uint32_t)(hash4(P.seed, DOM_DUMMY, P.idx, sub.idx, i) & mask);
   }
+  STAMP_AT(stamp_wg && mode == A_FINAL, 49);
   __syncthreads();
+  STAMP_AT(stamp_wg, 50);
   // ---- server XOR gather (HOT LOOP E) into row.w[0..EX) --------------------
   if (mode == A_FINAL || mode == A_CHAINED || mode == A_DUMMY) {
-    const uint64_t* base = S.db + P.row0 * E;
+    const PM_G uint64_t* base = S.db + P.row0 * E;
     for (uint32_t seg0 = 0; seg0 < NSEG; seg0 += kAnsBlock) {
       const uint32_t nseg = min(NSEG - seg0, (uint32_t)kAnsBlock);
       const uint32_t nsl = kAnsBlock / nseg;
       const uint32_t sl = tid / nseg, seg = seg0 + tid % nseg;
       uint64_t a0 = 0, a1 = 0;
       if (sl < nsl) {
-#pragma unroll 4
-        for (uint32_t i = sl; i < P.SS; i += nsl) {
-          const uint64_t rr = (uint64_t)i * P.CS + qo[i];
-          if (rr < P.N) {
-            const uint64_t* q = base + rr * E + (uint64_t)seg * W;
-            if (W == 2) {
-              const uint4 x = *reinterpret_cast<const uint4*>(q);
-              a0 ^= ((uint64_t)x.y << 32) | x.x;
-              a1 ^= ((uint64_t)x.w << 32) | x.z;
-            } else {
-              a0 ^= *q;
+        // every row load of a batch is issued before the first is consumed: the
+        // gather is one HBM round trip per kG rows a thread reads, not one per 4
+        constexpr int kG = 16;
+        typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+        for (uint32_t i0 = sl; i0 < P.SS; i0 += kG * nsl) {
+          uint64_t rr[kG];
+#pragma unroll
+          for (int u = 0; u < kG; ++u) {
+            const uint32_t i = i0 + u * nsl;
+            rr[u] = i < P.SS ? (uint64_t)i * P.CS + qo[i] : P.N;
+          }
+          u64x2 x[kG];
+#pragma unroll
+          for (int u = 0; u < kG; ++u) {
+            x[u] = u64x2{0, 0};
+            if (rr[u] < P.N) {
+              const PM_G uint64_t* q = base + rr[u] * E + (uint64_t)seg * W;
+              if (W == 2) x[u] = *reinterpret_cast<const PM_G u64x2*>(q);
+              else x[u].x = *q;
             }
           }
+#pragma unroll
+          for (int u = 0; u < kG; ++u) { a0 ^= x[u].x; a1 ^= x[u].y; }
         }
       }
       red[tid * 2] = a0;
@@ -656,6 +686,7 @@ __global__ void __launch_bounds__(kAnsBlock) k_answer(PmStep S) {
       __syncthreads();
     }
   }
+  STAMP_AT(stamp_wg, 51);
   // ---- decode + refresh, or the cached row -----------------------------
   if (mode == A_FINAL) {
     for (uint32_t w = tid; w < E; w += kAnsBlock) {
@@ -677,6 +708,7 @@ __global__ void __launch_bounds__(kAnsBlock) k_answer(PmStep S) {
     for (uint32_t w = tid; w < E; w += kAnsBlock) row.w[w] = a[w];
   }
   __syncthreads();
+  STAMP_AT(stamp_wg, 52);
   // ---- results: row + header into pinned host memory, arena copy -----------
   if (mode != A_CHAINED) {
     const bool has_row = (mode == A_FINAL || mode == A_CACHED);
@@ -691,6 +723,7 @@ __global__ void __launch_bounds__(kAnsBlock) k_answer(PmStep S) {
       if (tid == 0) S.hdr_h[s] = PmOutHdr{r.status, r.slot, d, 0};
     }
   }
+  STAMP_AT(stamp_wg, 53);
   // ---- arrival: workgroups of refresh chains count in; the last one decodes
   // the chained sub-queries in order.  Producer side: drain this wave's stores,
   // barrier, one lane releases at agent scope and counts (MI355X_MICROARCH.md
