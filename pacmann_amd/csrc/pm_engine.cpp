@@ -257,14 +257,14 @@ struct Engine {
   uint64_t FBN = 0, QMIP = 0, Support = 0, prepCount = 0;
   double prepTime = 0, storage = 0, commOn = 0, commOff = 0;
 
-  DevBuf db, parts_d, tag, pp, parity, ridx, rval, hist, fqn, arena, tab, tabT, done;
+  DevBuf db, zero16, parts_d, tag, pp, parity, ridx, rval, hist, fqn, arena, tab, tabT, done;
   DevBuf qoffs, ans_srv;
   DevBuf subs_d, sb_d, bits, res_d, ans, qvec, stamps;
   std::vector<double> stamp_sum;   // PM_STAMPS builds: accumulated phase deltas
   uint64_t stamp_n = 0;
   HostBuf desc_h, out_h;
   std::vector<PartHost> parts;
-  uint32_t maxH = 0, maxPH = 0, maxSS = 0, maxRepl = 0;
+  uint32_t maxH = 0, maxPH = 0, maxSS = 0, maxRepl = 0, maxCS = 0, minCS = ~0u;
 
   // per-step host view
   std::vector<PmSub> subs;
@@ -350,6 +350,8 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
     if ((uint64_t)ph.d.H >= (1ull << 29)) return fail(PM_EINVAL, "tag space >= 2^29 (util.go:161)");
     ph.d.row0 = start; ph.d.seed = seed; ph.d.idx = i;
     g->maxH = std::max(g->maxH, ph.d.H);
+    g->maxCS = std::max(g->maxCS, ph.d.CS);
+    g->minCS = std::min(g->minCS, ph.d.CS);
     g->maxPH = std::max(g->maxPH, ph.d.PH);
     g->maxSS = std::max(g->maxSS, ph.d.SS);
     g->maxRepl = std::max(g->maxRepl, ph.d.SS * ph.d.Qpc);
@@ -365,6 +367,8 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
     ph.cache.reserve(ph.d.MaxQ);
   }
   CHK(g->db.reserve(N * g->E * 8));
+  CHK(g->zero16.reserve(64));
+  HIPCHK(hipMemset(g->zero16.p, 0, 64));
   HIPCHK(hipMemcpy(g->db.p, rawDB, N * g->E * 8, hipMemcpyHostToDevice));
   CHK(g->tag.reserve(off_tag * 4));
   CHK(g->pp.reserve(off_pp * 4));
@@ -441,7 +445,8 @@ static int engine_prep(Engine* g, uint64_t p0, uint64_t p1) {
       HIPCHK(hipMemsetAsync(d.rval, 0, (uint64_t)d.SS * d.Qpc * g->E * 8, st));
     }
   } else {
-    c->timed("prep_fold", fold, [&] { pmk::prep_fold(st, dp, np, g->maxH, g->db.as<uint64_t>(), (uint32_t)g->E); });
+    c->timed("prep_fold", fold, [&] { pmk::prep_fold(st, dp, np, g->maxH, g->db.as<uint64_t>(), (uint32_t)g->E, g->minCS, g->maxCS,
+                                               g->zero16.as<uint64_t>()); });
     c->timed("prep_repl", repl, [&] { pmk::prep_repl(st, dp, np, g->maxRepl, g->db.as<uint64_t>(), (uint32_t)g->E); });
   }
   HIPCHK(hipGetLastError());

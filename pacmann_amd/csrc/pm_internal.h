@@ -133,7 +133,7 @@ void prep_init(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxH, 
                uint32_t E, bool zero_state);
 void prep_offsets(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxH, uint32_t maxSS);
 void prep_fold(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxH, const uint64_t* db,
-               uint32_t E);
+               uint32_t E, uint32_t minCS, uint32_t maxCS, const uint64_t* zero16);
 void prep_repl(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxRepl,
                const uint64_t* db, uint32_t E);
 void step_match(hipStream_t st, const PmStep& S, uint32_t maxPH);

@@ -100,6 +100,217 @@ __global__ void __launch_bounds__(kBlock) k_prep_fold(const PmPart* __restrict__
     for (uint32_t w = EX; w < E; ++w) P.parity[(uint64_t)h * E + w] = 0;
 }
 
+// Cache-blocked fold (same result as k_prep_fold): a workgroup owns one
+// partition, one SW-word column slice of every entry and one group of hints.
+// For each chunk it stages the slice of all CS entries of the chunk into LDS
+// with direct global->LDS loads (double-buffered, one barrier per chunk) and
+// XORs the entry each of its hints selects into parity accumulators held in
+// registers, so a DB byte is read from HBM once per hint group instead of once
+// per hint that selects it.  Entry CS of a staged chunk is a zero row (kSkip
+// selects it); rows past N are staged from a 16-byte zero source.
+constexpr int kFoldThreads = 1024, kFoldHPT = 4;
+constexpr uint32_t kFoldMaxItems = 4;   // 16-B staging items per thread per chunk
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void g_cvoid_t;
+
+template <int SW>   // 64-bit words per column slice: 8, 4 or 2
+__global__ void __launch_bounds__(kFoldThreads) k_prep_fold_blk(const PmPart* __restrict__ parts,
+                                                                const uint64_t* __restrict__ db,
+                                                                const uint64_t* __restrict__ zero16,
+                                                                uint32_t E, uint32_t w0) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t fold_lds[];   // [2][(CS+1)*SW]
+  typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+  constexpr uint32_t IPE = SW / 2;   // 16-B items per entry slice
+  const PmPart& P = parts[blockIdx.z];
+  const uint32_t H = P.H, CS = P.CS, SS = P.SS, tid = threadIdx.x;
+  const uint32_t ng = (H + kFoldThreads * kFoldHPT - 1) / (kFoldThreads * kFoldHPT);
+  if (blockIdx.x >= ng) return;   // block-uniform
+  const uint32_t hb = (H + ng - 1) / ng, h0 = blockIdx.x * hb, h1 = min(H, h0 + hb);
+  const uint32_t w = w0 + blockIdx.y * SW;
+  const uint64_t N = P.N;
+  const PM_G uint64_t* base = (const PM_G uint64_t*)db + P.row0 * E + w;
+  const PM_G uint16_t* tab = P.tab;
+  const uint32_t rowWords = (CS + 1) * SW, items = CS * IPE;
+  const uint32_t wave_item0 = tid & ~63u;
+  uint32_t hk[kFoldHPT];
+  uint64_t acc[kFoldHPT][SW];
+#pragma unroll
+  for (int k = 0; k < kFoldHPT; ++k) {
+    hk[k] = h0 + tid + k * kFoldThreads;
+#pragma unroll
+    for (int x = 0; x < SW; ++x) acc[k][x] = 0;
+  }
+  uint32_t v[kFoldHPT], nv[kFoldHPT];
+  // item it of chunk c: entry it / IPE, 16-B piece it % IPE, LDS byte offset it * 16
+  auto stage = [&](uint32_t c, uint32_t buf) {
+    uint64_t* L = fold_lds + buf * rowWords;
+#pragma unroll
+    for (uint32_t i = 0; i < kFoldMaxItems; ++i) {
+      const uint32_t it = tid + i * kFoldThreads;
+      if (i * kFoldThreads + wave_item0 < items && it < items) {
+        const uint64_t r = (uint64_t)c * CS + it / IPE;
+        const PM_G uint64_t* src = r < N ? base + r * E + (it % IPE) * 2 : (const PM_G uint64_t*)zero16;
+        __builtin_amdgcn_global_load_lds((g_cvoid_t*)src, (lds_void_t*)(L + (i * kFoldThreads + wave_item0) * 2),
+                                         16, 0, 0);
+      }
+    }
+  };
+  auto load_tab = [&](uint32_t c, uint32_t* out) {
+#pragma unroll
+    for (int k = 0; k < kFoldHPT; ++k) out[k] = hk[k] < h1 ? tab[(uint64_t)c * H + hk[k]] : kSkip;
+  };
+  stage(0, 0);
+  load_tab(0, v);
+  for (uint32_t x = tid; x < 2 * SW; x += kFoldThreads) fold_lds[(x / SW) * rowWords + CS * SW + x % SW] = 0;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (uint32_t c = 0; c < SS; ++c) {
+    const bool more = c + 1 < SS;
+    if (more) { stage(c + 1, (c + 1) & 1); load_tab(c + 1, nv); }
+    const uint64_t* L = fold_lds + (c & 1) * rowWords;
+#pragma unroll
+    for (int k = 0; k < kFoldHPT; ++k) {
+      const uint32_t o = v[k] == kSkip ? CS : v[k];
+      const uint64_t* row = L + o * SW;
+#pragma unroll
+      for (int x = 0; x < SW; x += 2) {
+        const u64x2 y = *reinterpret_cast<const u64x2*>(row + x);
+        acc[k][x] ^= y.x;
+        acc[k][x + 1] ^= y.y;
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kFoldHPT; ++k) v[k] = nv[k];
+  }
+#pragma unroll
+  for (int k = 0; k < kFoldHPT; ++k) {
+    if (hk[k] >= h1) continue;
+    PM_G uint64_t* dst = P.parity + (uint64_t)hk[k] * E + w;
+#pragma unroll
+    for (int x = 0; x < SW; x += 2) *reinterpret_cast<PM_G u64x2*>(dst + x) = u64x2{acc[k][x], acc[k][x + 1]};
+    if (w == 0)   // xorSlices leaves the words past len&~3 zero
+      for (uint32_t t = E & ~3u; t < E; ++t) P.parity[(uint64_t)hk[k] * E + t] = 0;
+  }
+}
+
+// Pipelined form of k_prep_fold_blk for CS * SW == 2048 * G (every
+// partition): three LDS buffers, two chunks in flight, and the PRF-table row
+// of the chunk staged through LDS too, so every load of the loop is a direct
+// global->LDS load and the waits are counted per wave (G or G+1 loads per
+// chunk), never vmcnt(0).  One extern __shared__ array; raw s_barrier.
+constexpr uint32_t kPipeTabWords = 1024;   // 8 KB table row (<= 4096 hints per group)
+
+// s_waitcnt vmcnt(n) for a runtime n, n <= 15.  n must be wave-uniform, and is
+// made visibly so: s_waitcnt is a scalar instruction, and in a switch lowered
+// as divergent (exec-masked) branches every case's wait would execute.
+__device__ __forceinline__ void wait_vmcnt(uint32_t n) {
+  switch (__builtin_amdgcn_readfirstlane(n)) {
+#define PM_VMC(i) case i: asm volatile("s_waitcnt vmcnt(" #i ")" ::: "memory"); break;
+    PM_VMC(1) PM_VMC(2) PM_VMC(3) PM_VMC(4) PM_VMC(5) PM_VMC(6) PM_VMC(7) PM_VMC(8)
+    PM_VMC(9) PM_VMC(10) PM_VMC(11) PM_VMC(12) PM_VMC(13) PM_VMC(14) PM_VMC(15)
+#undef PM_VMC
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
+template <int SW, int G, int NB>   // G = 16-B staging loads per thread per chunk; NB LDS buffers
+__global__ void __launch_bounds__(kFoldThreads) k_prep_fold_pipe(const PmPart* __restrict__ parts,
+                                                                 const uint64_t* __restrict__ db,
+                                                                 const uint64_t* __restrict__ zero16,
+                                                                 uint32_t E, uint32_t ngmax, uint32_t nsl,
+                                                                 uint32_t units) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t fold_lds[];   // [NB][(CS+1)*SW + 1024]
+  typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+  constexpr uint32_t IPE = SW / 2, CS = G * kFoldThreads / IPE;
+  // XCD-aware order: workgroups b and b + 8 share an XCD (MI355X_MICROARCH.md
+  // § Workgroup dispatch), so the nsl column slices of one (partition, hint
+  // group) unit are dealt to one XCD back to back and the 128-B lines they
+  // split are fetched into that XCD's L2 once.
+  const uint32_t xcd = blockIdx.x % 8, k = blockIdx.x / 8;
+  const uint32_t unit = xcd + 8 * (k / nsl), slice = k % nsl;
+  if (unit >= units) return;   // block-uniform
+  const PmPart& P = parts[unit / ngmax];
+  const uint32_t H = P.H, SS = P.SS, tid = threadIdx.x;
+  const uint32_t ng = (H + kFoldThreads * kFoldHPT - 1) / (kFoldThreads * kFoldHPT);
+  const uint32_t grp = unit % ngmax;
+  if (grp >= ng) return;   // block-uniform
+  const uint32_t hb = (((H + ng - 1) / ng) + 7) & ~7u, h0 = grp * hb, h1 = min(H, h0 + hb);
+  const uint32_t w = slice * SW;
+  const uint64_t N = P.N;
+  const PM_G uint64_t* base = (const PM_G uint64_t*)db + P.row0 * E + w;
+  const PM_G uint16_t* tab = P.tab;
+  constexpr uint32_t TABW = (CS + 1) * SW, BUFW = TABW + kPipeTabWords;
+  const uint32_t wave_item0 = tid & ~63u;
+  const bool tab_wave = tid < 512;   // waves 0-7 stage the table row: 3 loads per chunk, others 2
+  uint32_t hk[kFoldHPT];
+  uint64_t acc[kFoldHPT][SW];
+#pragma unroll
+  for (int k = 0; k < kFoldHPT; ++k) {
+    hk[k] = h0 + tid + k * kFoldThreads;
+#pragma unroll
+    for (int x = 0; x < SW; ++x) acc[k][x] = 0;
+  }
+  auto stage = [&](uint32_t c, uint32_t buf) {
+    uint64_t* L = fold_lds + buf * BUFW;
+#pragma unroll
+    for (uint32_t i = 0; i < (uint32_t)G; ++i) {
+      const uint32_t it = tid + i * kFoldThreads;
+      const uint64_t r = (uint64_t)c * CS + it / IPE;
+      const PM_G uint64_t* src = r < N ? base + r * E + (it % IPE) * 2 : (const PM_G uint64_t*)zero16;
+      __builtin_amdgcn_global_load_lds((g_cvoid_t*)src, (lds_void_t*)(L + (i * kFoldThreads + wave_item0) * 2),
+                                       16, 0, 0);
+    }
+    if (tab_wave) {   // 8 table entries (16 B) per lane; h0 and H are multiples of 8
+      const uint32_t hh = h0 + tid * 8;
+      const PM_G uint64_t* src = hh < h1 ? (const PM_G uint64_t*)(tab + (uint64_t)c * H + hh)
+                                         : (const PM_G uint64_t*)zero16;
+      __builtin_amdgcn_global_load_lds((g_cvoid_t*)src, (lds_void_t*)(L + TABW + wave_item0 * 2), 16, 0, 0);
+    }
+  };
+  for (uint32_t x = tid; x < NB * SW; x += kFoldThreads) fold_lds[(x / SW) * BUFW + CS * SW + x % SW] = 0;
+  // chunks 0 .. NB-2 in flight; chunk c + NB - 1 is issued while chunk c is folded
+  for (uint32_t c = 0; c + 1 < (uint32_t)NB && c < SS; ++c) stage(c, c);
+  const uint32_t ops = G + (tab_wave ? 1 : 0);   // loads per chunk of this wave
+  auto wait_chunk = [&](uint32_t next) {   // chunk `next` landed; later ones may stay in flight
+    const uint32_t issued = min(SS, next + NB - 1);   // chunks issued so far
+    wait_vmcnt(issued > next + 1 ? (issued - next - 1) * ops : 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+  wait_chunk(0);
+#ifndef PM_FOLD_ABL
+#define PM_FOLD_ABL 0   // diagnostic builds: 1 = no LDS compute, 2 = no staging in the loop
+#endif
+  for (uint32_t c = 0; c < SS; ++c) {
+    if (PM_FOLD_ABL != 2 && c + NB - 1 < SS) stage(c + NB - 1, (c + NB - 1) % NB);
+    const uint64_t* L = fold_lds + (c % NB) * BUFW;
+    const uint16_t* T = reinterpret_cast<const uint16_t*>(L + TABW);
+#pragma unroll
+    for (int k = 0; k < (PM_FOLD_ABL == 1 ? 0 : kFoldHPT); ++k) {
+      const uint32_t t = hk[k] < h1 ? T[hk[k] - h0] : kSkip;
+      const uint64_t* row = L + (t == kSkip ? CS : t) * SW;
+#pragma unroll
+      for (int x = 0; x < SW; x += 2) {
+        const u64x2 y = *reinterpret_cast<const u64x2*>(row + x);
+        acc[k][x] ^= y.x;
+        acc[k][x + 1] ^= y.y;
+      }
+    }
+    if (c + 1 < SS) wait_chunk(c + 1);
+  }
+#pragma unroll
+  for (int k = 0; k < kFoldHPT; ++k) {
+    if (hk[k] >= h1) continue;
+    PM_G uint64_t* dst = P.parity + (uint64_t)hk[k] * E + w;
+#pragma unroll
+    for (int x = 0; x < SW; x += 2) *reinterpret_cast<PM_G u64x2*>(dst + x) = u64x2{acc[k][x], acc[k][x + 1]};
+    if (w == 0)   // xorSlices leaves the words past len&~3 zero
+      for (uint32_t t = E & ~3u; t < E; ++t) P.parity[(uint64_t)hk[k] * E + t] = 0;
+  }
+}
+
 // Replacement rows (pir.go:345-350): Qpc random offsets per chunk, idx + copy.
 __global__ void __launch_bounds__(kBlock) k_prep_repl(const PmPart* __restrict__ parts,
                                                       const uint64_t* __restrict__ db, uint32_t E) {
@@ -301,18 +512,60 @@ void prep_offsets(hipStream_t st, const PmPart* d, int np, uint32_t maxH, uint32
   hipLaunchKernelGGL(k_prep_offsets, dim3(cdiv(maxH, kBlock), cdiv(maxSS, kOffsChunksPerBlock), np),
                      dim3(kBlock), 0, st, d);
 }
-void prep_fold(hipStream_t st, const PmPart* d, int np, uint32_t maxH, const uint64_t* db, uint32_t E) {
+void prep_fold(hipStream_t st, const PmPart* d, int np, uint32_t maxH, const uint64_t* db, uint32_t E,
+               uint32_t minCS, uint32_t maxCS, const uint64_t* zero16) {
   const uint32_t EX = E & ~3u;
   if (EX == 0) {
     hipLaunchKernelGGL(k_prep_fold<2>, dim3(cdiv((uint64_t)maxH * E, kBlock), np), dim3(kBlock), 0,
                        st, d, db, E);
-  } else if (E % 2 == 0) {
-    hipLaunchKernelGGL(k_prep_fold<2>, dim3(cdiv((uint64_t)maxH * (EX / 2), kBlock), np),
-                       dim3(kBlock), 0, st, d, db, E);
-  } else {
-    hipLaunchKernelGGL(k_prep_fold<1>, dim3(cdiv((uint64_t)maxH * EX, kBlock), np), dim3(kBlock), 0,
-                       st, d, db, E);
+    return;
   }
+  // column-slice width: the widest whose double-buffered chunk fits in LDS and
+  // whose staging fits kFoldMaxItems 16-B items per thread
+  const uint32_t ng = cdiv(maxH, (uint64_t)kFoldThreads * kFoldHPT);
+  auto fits = [&](uint32_t sw) {
+    return 2ull * (maxCS + 1) * sw * 8 <= 150u * 1024 &&
+           (uint64_t)maxCS * (sw / 2) <= (uint64_t)kFoldMaxItems * kFoldThreads;
+  };
+  auto launch = [&](uint32_t sw, uint32_t w0, uint32_t nsl) {
+    const size_t lds = 2ull * (maxCS + 1) * sw * 8;
+    const dim3 grid(ng, nsl, np), blk(kFoldThreads);
+    if (sw == 8) hipLaunchKernelGGL(k_prep_fold_blk<8>, grid, blk, lds, st, d, db, zero16, E, w0);
+    else if (sw == 4) hipLaunchKernelGGL(k_prep_fold_blk<4>, grid, blk, lds, st, d, db, zero16, E, w0);
+    else hipLaunchKernelGGL(k_prep_fold_blk<2>, grid, blk, lds, st, d, db, zero16, E, w0);
+  };
+  if (minCS == maxCS && (maxCS == 512 || maxCS == 1024 || maxCS == 2048) && E % 2 == 0) {
+    // (SW, G): CS 512 -> (4, 1), 1024 -> (4, 2), 2048 -> (2, 2); EX % SW == 0
+    const uint32_t psw = maxCS == 2048 ? 2 : 4, nsl = EX / psw, units = np * ng;
+#ifndef PM_FOLD_NB512
+#define PM_FOLD_NB512 4
+#endif
+    const uint32_t nb = maxCS == 512 ? PM_FOLD_NB512 : 3;   // LDS buffers: <= 150 KB
+    const size_t lds = (size_t)nb * ((maxCS + 1) * psw + kPipeTabWords) * 8;
+    const dim3 grid(cdiv(units, 8) * 8 * nsl), blk(kFoldThreads);
+    if (maxCS == 512)
+      hipLaunchKernelGGL((k_prep_fold_pipe<4, 1, PM_FOLD_NB512>), grid, blk, lds, st, d, db, zero16, E, ng, nsl,
+                         units);
+    else if (maxCS == 1024)
+      hipLaunchKernelGGL((k_prep_fold_pipe<4, 2, 3>), grid, blk, lds, st, d, db, zero16, E, ng, nsl, units);
+    else
+      hipLaunchKernelGGL((k_prep_fold_pipe<2, 2, 3>), grid, blk, lds, st, d, db, zero16, E, ng, nsl, units);
+    return;
+  }
+  uint32_t sw = 8;
+  while (sw > 2 && !fits(sw)) sw /= 2;
+  if (!fits(sw) || E % 2) {   // very wide chunks or odd entries: the unblocked gather
+    if (E % 2 == 0)
+      hipLaunchKernelGGL(k_prep_fold<2>, dim3(cdiv((uint64_t)maxH * (EX / 2), kBlock), np),
+                         dim3(kBlock), 0, st, d, db, E);
+    else
+      hipLaunchKernelGGL(k_prep_fold<1>, dim3(cdiv((uint64_t)maxH * EX, kBlock), np), dim3(kBlock), 0,
+                         st, d, db, E);
+    return;
+  }
+  const uint32_t nfull = EX / sw, rem = EX % sw;   // EX is a multiple of 4
+  if (nfull) launch(sw, 0, nfull);
+  if (rem) launch(rem, nfull * sw, 1);
 }
 void prep_repl(hipStream_t st, const PmPart* d, int np, uint32_t maxRepl, const uint64_t* db,
                uint32_t E) {

@@ -109,8 +109,10 @@ def assert_state_equal(a, b):
         assert np.array_equal(a[k], b[k]), k
 
 
+# chunk sizes 512 (pipelined fold, SW 4), 1024 (SW 4, 2 loads per thread),
+# 2048 (SW 2), 256 (double-buffered fold), odd E (unblocked fold), E < 4 (zero)
 @pytest.mark.parametrize("N,E,F", [(18750, 4, 40), (5000, 6, 8), (3000, 5, 8), (2000, 2, 8),
-                                   (62500, 80, 8)])
+                                   (62500, 80, 8), (262144, 8, 8), (1_000_000, 4, 8)])
 def test_pir_preprocessing_state(ctx, oracle, N, E, F):
     import pacmann_amd as pm
     db = rand_db(N, E, seed=N)
