@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <chrono>
@@ -137,6 +138,7 @@ struct HostBuf {
     if (p) { (void)hipHostFree(p); p = nullptr; n = 0; }
     hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocCoherent | hipHostMallocMapped);
     if (e != hipSuccess) return fail(PM_ENOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+    memset(p, 0, bytes);   // no stale step token (PmOutHdr::token is never 0)
     n = bytes;
     return 0;
   }
@@ -262,6 +264,7 @@ struct Engine {
   DevBuf subs_d, sb_d, bits, res_d, ans, qvec, stamps;
   std::vector<double> stamp_sum;   // PM_STAMPS builds: accumulated phase deltas
   uint64_t stamp_n = 0;
+  uint32_t step_token = 0;         // PmStep::token of the last step
   HostBuf desc_h, out_h;
   std::vector<PartHost> parts;
   uint32_t maxH = 0, maxPH = 0, maxSS = 0, maxRepl = 0, maxCS = 0, minCS = ~0u;
@@ -464,6 +467,34 @@ static inline double ms_since(Clock::time_point t) {
   return std::chrono::duration<double, std::milli>(Clock::now() - t).count();
 }
 
+// Completion of a step: every result header in pinned memory carries this
+// step's token (k_answer writes it after the row has drained), so the host
+// polls the headers instead of waiting for the kernel's completion signal.
+// Timing / debug runs, and a step not published within 5 s (a fault, or a
+// bug), fall back to the stream synchronisation, which reports errors.
+static int wait_step(pm_ctx* c, const PmOutHdr* hdr, uint32_t nsub, uint32_t token) {
+  if (c->timing >= 2 || c->debug_sync) {
+    HIPCHK(hipStreamSynchronize(c->stream));
+  } else {
+    const volatile uint32_t* tok = &hdr[0].token;
+    const size_t stride = sizeof(PmOutHdr) / sizeof(uint32_t);
+    auto t0 = Clock::now();
+    uint32_t s = 0;
+    for (uint64_t spin = 0; s < nsub; ++spin) {
+      if (tok[s * stride] == token) { ++s; continue; }
+      if ((spin & 0xffff) == 0xffff && ms_since(t0) > 5000.0) {
+        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(hipGetLastError());
+        break;
+      }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+  }
+  for (uint32_t s = 0; s < nsub; ++s)
+    if (hdr[s].token != token) return fail(PM_EHIP, "step results not published (sub-query " + std::to_string(s) + ")");
+  return 0;
+}
+
 static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
   auto t_begin = Clock::now();
   pm_ctx* c = g->ctx;
@@ -504,6 +535,8 @@ static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
   S.rows_h = (uint64_t*)(g->out_h.as<char>() + nsub * sizeof(PmOutHdr));
   S.words = words; S.E = (uint32_t)E; S.dim = q_dev ? dim : 0; S.nsub = nsub; S.np = (uint32_t)g->P;
   S.args_valid = (nsub <= kArgSubs && g->P <= kArgParts) ? 1u : 0u;
+  if (++g->step_token == 0) ++g->step_token;   // 0 never marks a published header
+  S.token = g->step_token;
   if (S.args_valid) {
     memcpy(S.subs_a, g->subs.data(), dsub);
     memcpy(S.sb_a, g->sb.data(), (g->P + 1) * 4);
@@ -536,7 +569,7 @@ static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
   HIPCHK(hipGetLastError());
   c->host_add("host_step_launch", ms_since(t_begin));
   auto t_wait = Clock::now();
-  HIPCHK(hipStreamSynchronize(st));
+  CHK(wait_step(c, S.hdr_h, nsub, S.token));
   c->host_add("host_step_wait", ms_since(t_wait));
   auto t_post = Clock::now();
   g->hdr = S.hdr_h;

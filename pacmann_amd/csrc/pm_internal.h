@@ -89,10 +89,12 @@ struct PmRes {
                                       // bit 1: a later sub-query in this step re-hits this hint
 };
 // Per-sub-query result header, written by the GPU into pinned host memory.
-struct PmOutHdr {
+// One 16-byte store: the step token is written together with the rest, after
+// the row of the sub-query has drained; the host polls it (no stream sync).
+struct alignas(16) PmOutHdr {
   uint32_t status, ref;
   float dist;
-  uint32_t pad;
+  uint32_t token;
 };
 // Arguments of the step kernels (pm_query.hip).
 #ifndef PM_KARG_SUBS
@@ -120,6 +122,7 @@ struct PmStep {
   // Small steps ship the descriptor inside the kernel arguments (no PCIe
   // round trip); larger ones use subs_h / sb_h.
   uint32_t args_valid;
+  uint32_t token;              // written into every PmOutHdr of this step
   uint32_t sb_a[kArgParts + 1];
   PmSub subs_a[kArgSubs];
 };

@@ -558,6 +558,15 @@ union RowBuf {   // one decoded entry; the L2 reads its leading floats
   float f[2 * kMaxELds];
 };
 
+// Result header of sub-query s, once every thread's row stores have drained
+// (the host reads the row as soon as it sees the token).  Lane 0 holds `d`.
+__device__ __forceinline__ void publish_hdr(const PmStep& S, uint32_t s, uint32_t status, uint32_t ref,
+                                            float d) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) S.hdr_h[s] = PmOutHdr{status, ref, d, S.token};
+}
+
 // What a k_answer workgroup does for its sub-query.
 enum : uint32_t { A_ZERO = 0, A_FINAL = 1, A_CHAINED = 2, A_CACHED = 3, A_DUMMY = 4 };
 
@@ -587,11 +596,9 @@ __device__ void decode_chained(const PmStep& S, uint32_t s, RowBuf& row) {
   uint64_t* orow = S.rows_h + (uint64_t)s * E;
   uint64_t* ar = P.arena + (uint64_t)r.slot * E;
   for (uint32_t w = tid; w < E; w += blockDim.x) { orow[w] = row.w[w]; ar[w] = row.w[w]; }
-  if (tid < 64) {
-    float d = 0.0f;
-    if (S.q && tid < 8) d = l2_lds(row.f, S.q, S.dim);
-    if (tid == 0) S.hdr_h[s] = PmOutHdr{r.status, r.slot, d, 0};
-  }
+  float d = 0.0f;
+  if (S.q && tid < 8) d = l2_lds(row.f, S.q, S.dim);
+  publish_hdr(S, s, r.status, r.slot, d);
   __syncthreads();
 }
 
@@ -717,11 +724,9 @@ __global__ void __launch_bounds__(kAnsBlock) k_answer(PmStep S) {
       uint64_t* ar = P.arena + (uint64_t)r.slot * E;
       for (uint32_t w = tid; w < E; w += kAnsBlock) ar[w] = row.w[w];
     }
-    if (tid < 64) {
-      float d = 0.0f;
-      if (has_row && S.q && tid < 8) d = l2_lds(row.f, S.q, S.dim);
-      if (tid == 0) S.hdr_h[s] = PmOutHdr{r.status, r.slot, d, 0};
-    }
+    float d = 0.0f;
+    if (has_row && S.q && tid < 8) d = l2_lds(row.f, S.q, S.dim);
+    publish_hdr(S, s, r.status, r.slot, d);
   }
   STAMP_AT(stamp_wg, 53);
   // ---- arrival: workgroups of refresh chains count in; the last one decodes
