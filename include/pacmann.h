@@ -116,12 +116,29 @@ typedef struct {
 int  pm_batchpir_create(pm_ctx* ctx, uint64_t DBSize, uint64_t DBEntryByteNum, uint64_t BatchSize,
                         const uint64_t* rawDB, uint64_t FailureProbLog2, uint64_t seed,
                         pm_batchpir** out);
+/* One shard of the same batch PIR for multi-GPU use: this
+ * handle keeps the DB slice, keys and hint state of the partitions p with
+ * p % nshards == shard only (rawDB is still the whole DB; only those rows are
+ * uploaded).  Bucketing, dummies, drops, counters and the re-preprocessing
+ * trigger are the global ones, so every shard, fed the same batches, makes the
+ * same decisions; pm_batchpir_query(_ok) fills the entries of its own
+ * partitions and leaves the others zero (ok = 0).  Summing the entries (and
+ * OR-ing ok) over all shards gives the unsharded answer bit for bit (keys
+ * derive from the global partition index). */
+int  pm_batchpir_create_shard(pm_ctx* ctx, uint64_t DBSize, uint64_t DBEntryByteNum, uint64_t BatchSize,
+                              const uint64_t* rawDB, uint64_t FailureProbLog2, uint64_t seed,
+                              uint32_t shard, uint32_t nshards, pm_batchpir** out);
 void pm_batchpir_destroy(pm_batchpir* h);
 int  pm_batchpir_preprocessing(pm_batchpir* h);         /* batch-pir.go:119-155 */
 int  pm_batchpir_dummy_preprocessing(pm_batchpir* h);   /* batch-pir.go:157-166 */
 /* Query (batch-pir.go:170-248): out = n x DBEntrySize words; dropped or failed
  * ids get an all-zero entry exactly like the reference. */
 int  pm_batchpir_query(pm_batchpir* h, const uint64_t* ids, uint64_t n, uint64_t* out);
+/* The same query with a per-id success mask: ok[i] = 1 when entry i is the
+ * answer of a successful sub-query (or its local-cache copy), 0 when the id
+ * was dropped by the bucketing (batch-pir.go:195-200) or its sub-query failed
+ * (the error batch-pir.go:205 swallows); those entries are zero. */
+int  pm_batchpir_query_ok(pm_batchpir* h, const uint64_t* ids, uint64_t n, uint64_t* out, uint8_t* ok);
 int  pm_batchpir_stats_get(pm_batchpir* h, pm_batchpir_stats* s);
 int  pm_batchpir_subconfig(pm_batchpir* h, uint64_t partition, pm_pir_config* cfg);
 

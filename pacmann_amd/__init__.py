@@ -87,6 +87,8 @@ SIGNATURES = {
     "pm_batchpir_preprocessing": (C.c_int, [vp]),
     "pm_batchpir_dummy_preprocessing": (C.c_int, [vp]),
     "pm_batchpir_query": (C.c_int, [vp, u64p, u64, u64p]),
+    "pm_batchpir_query_ok": (C.c_int, [vp, u64p, u64, u64p, C.POINTER(C.c_uint8)]),
+    "pm_batchpir_create_shard": (C.c_int, [vp, u64, u64, u64, u64p, u64, u64, C.c_uint32, C.c_uint32, C.POINTER(vp)]),
     "pm_batchpir_stats_get": (C.c_int, [vp, C.POINTER(BatchStats)]),
     "pm_batchpir_subconfig": (C.c_int, [vp, u64, C.POINTER(PirConfig)]),
     "pm_pir_export": (C.c_int, [vp, u32p, u64p, u64p, u64p, u64p, u64p, u64p, u64p, u64p]),
@@ -324,9 +326,13 @@ class SimpleBatchPianoPIR:
     """pianopir.SimpleBatchPianoPIR (batch-pir.go:40-276) on the GPU."""
 
     def __init__(self, DBSize: int, DBEntryByteNum: int, BatchSize: int, rawDB,
-                 FailureProbLog2: int, seed: int = 1, ctx: Context | None = None, _handle=None):
+                 FailureProbLog2: int, seed: int = 1, ctx: Context | None = None, _handle=None,
+                 shard: int = 0, nshards: int = 1):
+        """shard / nshards: hold only partitions p % nshards == shard
+        (pm_batchpir_create_shard); see ShardedBatchPIR for the combine."""
         self.ctx = ctx or default_context()
         self.E = DBEntryByteNum // 8
+        self.shard, self.nshards = shard, nshards
         self._owned = _handle is None
         if _handle is not None:
             self.h = _handle
@@ -335,8 +341,8 @@ class SimpleBatchPianoPIR:
         if db.size != DBSize * self.E:   # batch-pir.go:57-59 log.Fatalf
             raise ValueError(f"BatchPIR: len(rawDB) = {db.size}; want {DBSize * self.E}")
         h = vp()
-        _check(lib().pm_batchpir_create(self.ctx.h, DBSize, DBEntryByteNum, BatchSize, _p(db, u64p),
-                                        FailureProbLog2, seed, C.byref(h)))
+        _check(lib().pm_batchpir_create_shard(self.ctx.h, DBSize, DBEntryByteNum, BatchSize, _p(db, u64p),
+                                              FailureProbLog2, seed, shard, nshards, C.byref(h)))
         self.h = h
 
     def __del__(self):
@@ -356,6 +362,17 @@ class SimpleBatchPianoPIR:
         out = np.zeros((len(ids), self.E), dtype=np.uint64)
         _check(lib().pm_batchpir_query(self.h, _p(ids, u64p), len(ids), _p(out, u64p)))
         return out, None
+
+    def QueryWithMask(self, idx):
+        """Query plus the per-id success mask of pm_batchpir_query_ok: True where
+        the entry answers a successful sub-query, False where the id was dropped
+        or its sub-query failed (entry all zero)."""
+        ids = _u64(idx).ravel()
+        out = np.zeros((len(ids), self.E), dtype=np.uint64)
+        ok = np.zeros(len(ids), dtype=np.uint8)
+        _check(lib().pm_batchpir_query_ok(self.h, _p(ids, u64p), len(ids), _p(out, u64p),
+                                          ok.ctypes.data_as(C.POINTER(C.c_uint8))))
+        return out, ok.astype(bool)
 
     def stats(self) -> dict:
         s = BatchStats()

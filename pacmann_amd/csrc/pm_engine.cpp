@@ -244,6 +244,7 @@ extern "C" int pm_timing_get(pm_ctx* c, const char* name, uint64_t* launches, do
 // ---------------------------------------------------------------------------
 struct PartHost {
   PmPart d{};
+  bool owned = true;   // sharded engines hold the state of their own partitions only
   uint64_t epoch_ctr = 0, fqn = 0, dummy_ctr = 0;
   uint64_t maxq64 = 0;
   FlatMap cache;   // localCache (pir.go:120): idx -> arena slot
@@ -254,12 +255,14 @@ struct Engine {
   bool is_batch = false;
   uint64_t N = 0, E = 0, Ebytes = 0, F = 0, seed = 0;
   uint64_t B = 0, P = 1, PS = 0;
+  uint32_t shard = 0, nshards = 1;   // partition p is owned when p % nshards == shard
   bool skipPrep = false;
   // SimpleBatchPianoPIR stats (batch-pir.go:46-52)
   uint64_t FBN = 0, QMIP = 0, Support = 0, prepCount = 0;
   double prepTime = 0, storage = 0, commOn = 0, commOff = 0;
 
-  DevBuf db, zero16, parts_d, tag, pp, parity, ridx, rval, hist, fqn, arena, tab, tabT, done;
+  DevBuf db, zero16, parts_d, owned_d, tag, pp, parity, ridx, rval, hist, fqn, arena, tab, tabT, done;
+  std::vector<uint32_t> owned_list;   // owned partitions in order (owned_d holds their PmPart)
   DevBuf qoffs, ans_srv;
   DevBuf subs_d, sb_d, bits, res_d, ans, qvec, stamps;
   std::vector<double> stamp_sum;   // PM_STAMPS builds: accumulated phase deltas
@@ -280,6 +283,7 @@ struct Engine {
   FlatMap resp_map;
   std::vector<uint64_t> resp_rows;
   std::vector<float> resp_dist;
+  std::vector<uint8_t> resp_ok;
   std::vector<uint64_t> zero_row;   // response of dropped / failed ids (batch-pir.go:229-236)
 };
 
@@ -323,7 +327,9 @@ static double part_storage(const PartHost& p, uint64_t Ebytes) {   // LocalStora
 static double part_comm(const PartHost& p, uint64_t E) { return (double)((uint64_t)p.d.SS * 4 + E * 8); }
 
 static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, uint64_t B,
-                         const uint64_t* rawDB, uint64_t F, uint64_t seed, bool batch) {
+                         const uint64_t* rawDB, uint64_t F, uint64_t seed, bool batch,
+                         uint32_t shard = 0, uint32_t nshards = 1) {
+  if (nshards == 0 || shard >= nshards) return fail(PM_EINVAL, "shard must be < nshards");
   if (!ctx) return fail(PM_EINVAL, "ctx is NULL");
   if (!rawDB && N) return fail(PM_EINVAL, "rawDB is NULL");
   if (N == 0) return fail(PM_EINVAL, "DBSize must be > 0");
@@ -341,17 +347,25 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
   }
   g->parts.resize(g->P);
   if (g->E > pmk::step_max_e()) return fail(PM_EINVAL, "DBEntrySize above the step kernel's LDS limit");
+  g->shard = shard; g->nshards = nshards;
   uint64_t off_tag = 0, off_pp = 0, off_par = 0, off_ridx = 0, off_rval = 0, off_hist = 0, off_ar = 0,
-           off_tab = 0;
+           off_tab = 0, off_db = 0;
   for (uint64_t i = 0; i < g->P; ++i) {
     PartHost& ph = g->parts[i];
     uint64_t start = i * g->PS, end = std::min((i + 1) * g->PS, N);
     if (end <= start) return fail(PM_EINVAL, "empty partition (DBSize too small for BatchSize)");
     part_params(ph, end - start, F);
+    ph.owned = i % nshards == shard;
+    if (!ph.owned) {   // parameters only (bucketing and accounting are global)
+      ph.d.seed = seed; ph.d.idx = i;
+      continue;
+    }
+    g->owned_list.push_back((uint32_t)i);
     if (ph.d.CS > 32768) return fail(PM_EINVAL, "ChunkSize > 32768 unsupported (16-bit prep offsets)");
     if (ph.d.SS > pmk::step_max_ss()) return fail(PM_EINVAL, "SetSize above the step kernel's LDS limit");
     if ((uint64_t)ph.d.H >= (1ull << 29)) return fail(PM_EINVAL, "tag space >= 2^29 (util.go:161)");
-    ph.d.row0 = start; ph.d.seed = seed; ph.d.idx = i;
+    ph.d.row0 = off_db; off_db += end - start;   // rows of owned partitions, packed
+    ph.d.seed = seed; ph.d.idx = i;
     g->maxH = std::max(g->maxH, ph.d.H);
     g->maxCS = std::max(g->maxCS, ph.d.CS);
     g->minCS = std::min(g->minCS, ph.d.CS);
@@ -369,10 +383,14 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
     ph.d.tab = (uint16_t*)(uintptr_t)off_tab; off_tab += (uint64_t)ph.d.H * ph.d.SS;
     ph.cache.reserve(ph.d.MaxQ);
   }
-  CHK(g->db.reserve(N * g->E * 8));
+  CHK(g->db.reserve(std::max<uint64_t>(8, off_db * g->E * 8)));
   CHK(g->zero16.reserve(64));
   HIPCHK(hipMemset(g->zero16.p, 0, 64));
-  HIPCHK(hipMemcpy(g->db.p, rawDB, N * g->E * 8, hipMemcpyHostToDevice));
+  for (uint32_t i : g->owned_list) {
+    const uint64_t start = (uint64_t)i * g->PS, rows = g->parts[i].d.N;
+    HIPCHK(hipMemcpy(g->db.as<uint64_t>() + g->parts[i].d.row0 * g->E, rawDB + start * g->E, rows * g->E * 8,
+                     hipMemcpyHostToDevice));
+  }
   CHK(g->tag.reserve(off_tag * 4));
   CHK(g->pp.reserve(off_pp * 4));
   CHK(g->parity.reserve(off_par * 8));
@@ -385,8 +403,10 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
   CHK(g->tabT.reserve(off_tab * 2));
   CHK(g->done.reserve(4 * (3 + 16 * 4096)));
   CHK(g->parts_d.reserve(g->P * sizeof(PmPart)));
+  CHK(g->owned_d.reserve(std::max<size_t>(1, g->owned_list.size()) * sizeof(PmPart)));
   for (uint64_t i = 0; i < g->P; ++i) {
     PmPart& d = g->parts[i].d;
+    if (!g->parts[i].owned) continue;
     d.tag = g->tag.as<uint32_t>() + (uintptr_t)d.tag;
     d.pp = g->pp.as<uint32_t>() + (uintptr_t)d.pp;
     d.parity = g->parity.as<uint64_t>() + (uintptr_t)d.parity;
@@ -405,11 +425,15 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
 }
 
 static int upload_parts(Engine* g) {
-  std::vector<PmPart> v(g->P);
+  std::vector<PmPart> v(g->P), w;
   for (uint64_t i = 0; i < g->P; ++i) v[i] = g->parts[i].d;
+  for (uint32_t i : g->owned_list) w.push_back(g->parts[i].d);
   HIPCHK(hipMemcpyAsync(g->parts_d.p, v.data(), g->P * sizeof(PmPart), hipMemcpyHostToDevice,
                         g->ctx->stream));
-  HIPCHK(hipStreamSynchronize(g->ctx->stream));   // v goes out of scope
+  if (!w.empty())
+    HIPCHK(hipMemcpyAsync(g->owned_d.p, w.data(), w.size() * sizeof(PmPart), hipMemcpyHostToDevice,
+                          g->ctx->stream));
+  HIPCHK(hipStreamSynchronize(g->ctx->stream));   // v, w go out of scope
   return 0;
 }
 
@@ -418,7 +442,13 @@ static int upload_parts(Engine* g) {
 static int engine_prep(Engine* g, uint64_t p0, uint64_t p1) {
   pm_ctx* c = g->ctx;
   hipStream_t st = c->stream;
-  for (uint64_t i = p0; i < p1; ++i) {
+  // the owned partitions in [p0, p1): all of them (owned_d) or a single one
+  if (p1 - p0 > 1 && !(p0 == 0 && p1 == g->P)) return fail(PM_EINVAL, "engine_prep: unsupported range");
+  std::vector<uint64_t> todo;
+  for (uint64_t i = p0; i < p1; ++i)
+    if (g->parts[i].owned) todo.push_back(i);
+  if (todo.empty()) return 0;
+  for (uint64_t i : todo) {
     PartHost& ph = g->parts[i];
     uint8_t key[16];
     derive_key(g->seed, i, ph.epoch_ctr, key);
@@ -428,11 +458,11 @@ static int engine_prep(Engine* g, uint64_t p0, uint64_t p1) {
     ph.cache.clear();
   }
   CHK(upload_parts(g));
-  const PmPart* dp = g->parts_d.as<PmPart>() + p0;
-  const int np = (int)(p1 - p0);
+  const PmPart* dp = p1 - p0 == 1 ? g->parts_d.as<PmPart>() + p0 : g->owned_d.as<PmPart>();
+  const int np = (int)todo.size();
   c->timed("prep_init", 0, [&] { pmk::prep_init(st, dp, np, g->maxH, g->maxRepl, (uint32_t)g->E, g->skipPrep); });
   double aes = 0, fold = 0, repl = 0;
-  for (uint64_t i = p0; i < p1; ++i) {
+  for (uint64_t i : todo) {
     const PmPart& d = g->parts[i].d;
     aes += (double)d.H * d.SS;
     // algorithmic fold bytes: hpc * SS (hint, chunk) pairs of one E-word entry
@@ -442,7 +472,7 @@ static int engine_prep(Engine* g, uint64_t p0, uint64_t p1) {
   // the PRF table is built even by DummyPreprocessing: queries still evaluate the PRF
   c->timed("prep_offsets", aes, [&] { pmk::prep_offsets(st, dp, np, g->maxH, g->maxSS); });
   if (g->skipPrep) {   // DummyPreprocessing (pir.go:520-523): zero hints
-    for (uint64_t i = p0; i < p1; ++i) {
+    for (uint64_t i : todo) {
       const PmPart& d = g->parts[i].d;
       HIPCHK(hipMemsetAsync(d.parity, 0, (uint64_t)d.H * g->E * 8, st));
       HIPCHK(hipMemsetAsync(d.rval, 0, (uint64_t)d.SS * d.Qpc * g->E * 8, st));
@@ -607,6 +637,7 @@ static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
 // Append one sub-query of partition p to the step being built.
 static void add_sub(Engine* g, uint32_t p, bool real, uint64_t local, uint64_t gid) {
   PartHost& ph = g->parts[p];
+  if (!ph.owned) return;   // another shard answers this partition
   PmSub s{p, SUB_NONE, 0};
   if (!real) {
     s.kind = SUB_DUMMY; s.idx = ph.dummy_ctr++;
@@ -758,9 +789,14 @@ static void record_stats(Engine* g, double t) {   // RecordStats batch-pir.go:11
 }
 extern "C" int pm_batchpir_create(pm_ctx* ctx, uint64_t DBSize, uint64_t DBEntryByteNum, uint64_t BatchSize,
                                   const uint64_t* rawDB, uint64_t F, uint64_t seed, pm_batchpir** out) {
+  return pm_batchpir_create_shard(ctx, DBSize, DBEntryByteNum, BatchSize, rawDB, F, seed, 0, 1, out);
+}
+extern "C" int pm_batchpir_create_shard(pm_ctx* ctx, uint64_t DBSize, uint64_t DBEntryByteNum,
+                                        uint64_t BatchSize, const uint64_t* rawDB, uint64_t F, uint64_t seed,
+                                        uint32_t shard, uint32_t nshards, pm_batchpir** out) {
   if (!out) return fail(PM_EINVAL, "out is NULL");
   pm_batchpir* h = new pm_batchpir();
-  int r = engine_create(ctx, &h->e, DBSize, DBEntryByteNum, BatchSize, rawDB, F, seed, true);
+  int r = engine_create(ctx, &h->e, DBSize, DBEntryByteNum, BatchSize, rawDB, F, seed, true, shard, nshards);
   if (r) { delete h; return r; }
   *out = h;
   return 0;
@@ -793,16 +829,18 @@ extern "C" int pm_batchpir_dummy_preprocessing(pm_batchpir* h) {   // batch-pir.
 // the collected rows of a multi-step query, or a zero row); valid until the
 // next query on this engine.
 static int batch_query_impl(Engine* g, const uint64_t* idx, uint64_t n, uint64_t* out, const float* q_dev,
-                            uint32_t dim, float* dist_out, const uint64_t** rows_out);
+                            uint32_t dim, float* dist_out, const uint64_t** rows_out, uint8_t* ok);
 static int batch_query(Engine* g, const uint64_t* idx, uint64_t n, uint64_t* out, const float* q_dev,
-                       uint32_t dim, float* dist_out, const uint64_t** rows_out = nullptr) {
+                       uint32_t dim, float* dist_out, const uint64_t** rows_out = nullptr,
+                       uint8_t* ok = nullptr) {
   auto t = Clock::now();
-  int r = batch_query_impl(g, idx, n, out, q_dev, dim, dist_out, rows_out);
+  int r = batch_query_impl(g, idx, n, out, q_dev, dim, dist_out, rows_out, ok);
   g->ctx->host_add("host_batch_query", ms_since(t));
   return r;
 }
+static inline bool status_ok(uint32_t st) { return st == ST_OK || st == ST_CACHED || st == ST_DUP; }
 static int batch_query_impl(Engine* g, const uint64_t* idx, uint64_t n, uint64_t* out, const float* q_dev,
-                            uint32_t dim, float* dist_out, const uint64_t** rows_out) {
+                            uint32_t dim, float* dist_out, const uint64_t** rows_out, uint8_t* ok) {
   const uint64_t E = g->E, P = g->P;
   if (g->zero_row.size() != E) g->zero_row.assign(E, 0);
   for (uint64_t i = 0; i < n; ++i)
@@ -817,6 +855,7 @@ static int batch_query_impl(Engine* g, const uint64_t* idx, uint64_t n, uint64_t
   size_t nresp = 0;
   g->resp_rows.resize(std::max<size_t>(g->resp_rows.size(), n * E));
   g->resp_dist.resize(std::max<size_t>(g->resp_dist.size(), n));
+  g->resp_ok.resize(std::max<size_t>(g->resp_ok.size(), n));
   auto collect = [&]() {
     for (size_t s = 0; s < g->subs.size(); ++s) {
       const uint32_t k = g->subs[s].kind;
@@ -825,6 +864,7 @@ static int batch_query_impl(Engine* g, const uint64_t* idx, uint64_t n, uint64_t
       const uint32_t slot = *g->resp_map.find(g->sub_gid[s]);
       memcpy(&g->resp_rows[(size_t)slot * E], g->rows + (uint64_t)s * E, E * 8);
       g->resp_dist[slot] = g->hdr[s].dist;
+      g->resp_ok[slot] = status_ok(g->hdr[s].status);
     }
   };
   bool qn_done = false;
@@ -859,6 +899,7 @@ static int batch_query_impl(Engine* g, const uint64_t* idx, uint64_t n, uint64_t
       if (rows_out) rows_out[i] = row;
       else memcpy(out + i * E, row, E * 8);
       if (dist_out) dist_out[i] = sp ? g->hdr[*sp].dist : 0.0f;
+      if (ok) ok[i] = sp && status_ok(g->hdr[*sp].status);
     }
     qn_done = true;
   }
@@ -894,6 +935,7 @@ static int batch_query_impl(Engine* g, const uint64_t* idx, uint64_t n, uint64_t
     if (rows_out) rows_out[i] = row;
     else memcpy(out + i * E, row, E * 8);
     if (dist_out) dist_out[i] = sp ? g->resp_dist[*sp] : 0.0f;
+    if (ok) ok[i] = sp && g->resp_ok[*sp];
   }
   if (g->QMIP >= g->parts[0].maxq64 - 2) {
     CHK(batch_prep(g));
@@ -905,6 +947,10 @@ static int batch_query_impl(Engine* g, const uint64_t* idx, uint64_t n, uint64_t
 }
 extern "C" int pm_batchpir_query(pm_batchpir* h, const uint64_t* ids, uint64_t n, uint64_t* out) {
   return batch_query(&h->e, ids, n, out, nullptr, 0, nullptr);
+}
+extern "C" int pm_batchpir_query_ok(pm_batchpir* h, const uint64_t* ids, uint64_t n, uint64_t* out,
+                                    uint8_t* ok) {
+  return batch_query(&h->e, ids, n, out, nullptr, 0, nullptr, nullptr, ok);
 }
 extern "C" int pm_batchpir_stats_get(pm_batchpir* h, pm_batchpir_stats* s) {
   const Engine& g = h->e;
@@ -927,6 +973,7 @@ extern "C" int pm_batchpir_subconfig(pm_batchpir* h, uint64_t p, pm_pir_config* 
 extern "C" int pm_batchpir_export(pm_batchpir* h, uint64_t p, uint32_t* rk, uint64_t* pt, uint64_t* par,
                                   uint64_t* pp, uint64_t* bt, uint64_t* bpar, uint64_t* ri, uint64_t* rv,
                                   uint64_t* hist) {
+  if (p >= h->e.P || !h->e.parts[p].owned) return fail(PM_EINVAL, "partition not held by this shard");
   return engine_export(&h->e, p, rk, pt, par, pp, bt, bpar, ri, rv, hist);
 }
 

@@ -284,3 +284,69 @@ def test_search_loop_with_maintenance(ctx, oracle):
     assert np.array_equal(ga, oa)
     assert g.PIR.stats()["PrepCount"] == o.pir().stats()["PrepCount"] > 1
     assert g.counts() == o.counts()
+
+
+@pytest.mark.gpu
+def test_batch_query_mask(ctx, oracle):
+    """pm_batchpir_query_ok: ok => the entry is rawDB[id]; not ok => the id was
+    dropped by the bucketing (batch-pir.go:195-200) or failed, entry zero;
+    rows identical to the oracle's, across batches with drops and repeats."""
+    import pacmann_amd as pm
+    N, E, B = 40_000, 8, 16
+    db = rand_db(N, E, 99)
+    g = pm.SimpleBatchPianoPIR(N, E * 8, B, db, 8, seed=SEED, ctx=ctx)
+    o = oracle.SimpleBatchPianoPIR(N, E * 8, B, db, 8, seed=SEED)
+    g.Preprocessing()
+    o.Preprocessing()
+    P = g.Config()["PartitionNum"]
+    PS = g.Config()["PartitionSize"]
+    rng = np.random.default_rng(5)
+    dropped = 0
+    for b in range(30):
+        q = rng.integers(0, N, size=2 * P, dtype=np.uint64)
+        q[:6] = rng.integers(0, PS, size=6)          # crowd partition 0: drops
+        q[9] = q[10]                                  # a repeat
+        got, ok = g.QueryWithMask(q)
+        want, _ = o.Query(q)
+        assert np.array_equal(got, want), b
+        rows = db.reshape(N, E)[q.astype(np.int64)]
+        assert np.array_equal(got[ok], rows[ok]), b
+        assert not got[~ok].any(), b
+        dropped += int((~ok).sum())
+    assert dropped > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nshards", [2, 3])
+def test_batch_pir_shards(ctx, oracle, nshards):
+    """pm_batchpir_create_shard: shards fed the same batches; their entries
+    summed (and masks OR-ed) equal the unsharded oracle bit for bit, through
+    the batch layer's re-preprocessing trigger; each shard's partitions carry
+    the oracle's state; a foreign partition is refused."""
+    import pacmann_amd as pm
+    N, E, B = 30_000, 6, 8
+    db = rand_db(N, E, 77)
+    shards = [pm.SimpleBatchPianoPIR(N, E * 8, B, db, 8, seed=SEED, ctx=ctx, shard=r, nshards=nshards)
+              for r in range(nshards)]
+    o = oracle.SimpleBatchPianoPIR(N, E * 8, B, db, 8, seed=SEED)
+    for s in shards:
+        s.Preprocessing()
+    o.Preprocessing()
+    P = shards[0].Config()["PartitionNum"]
+    rng = np.random.default_rng(11)
+    maxq = shards[0].SubConfig(0)["MaxQueryNum"]
+    for b in range(int(maxq // 3) + 6):
+        q = rng.integers(0, N, size=3 * B, dtype=np.uint64)
+        q[4] = q[1]
+        parts = [s.QueryWithMask(q) for s in shards]
+        got = sum(p[0] for p in parts)
+        ok = np.logical_or.reduce([p[1] for p in parts])
+        want, _ = o.Query(q)
+        assert np.array_equal(got, want), b
+        assert not got[~ok].any(), b
+    for k in ("FinishedBatchNum", "QueriesMadeInPartition", "SupportBatchNum", "PrepCount"):
+        assert all(s.stats()[k] == o.stats()[k] for s in shards), k
+    for p in range(P):
+        assert_state_equal(shards[p % nshards].export_state(p), o.sub(p).export_state())
+    with pytest.raises(Exception):
+        shards[0].export_state(1)
