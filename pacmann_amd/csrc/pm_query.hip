@@ -148,7 +148,7 @@ __global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
       s_hist0[kMaxSubPerPart], s_c1[kMaxSubPerPart], s_c2[kMaxSubPerPart], s_t1[kMaxSubPerPart],
       s_p1[kMaxSubPerPart], s_t2[kMaxSubPerPart], s_p2[kMaxSubPerPart], s_sing[kMaxSubPerPart];
   __shared__ uint32_t m_h[kMaxSubPerPart], m_tag[kMaxSubPerPart], m_pp[kMaxSubPerPart],
-      m_sub[kMaxSubPerPart];
+      m_sub[kMaxSubPerPart], m_pt[kMaxSubPerPart];
   __shared__ uint32_t s_fqn, s_chain[kMaxSubPerPart];
   __shared__ PmRes s_res[kMaxSubPerPart];
   // fast path staging: match bits, tags / program points, speculative re-evaluation values
@@ -162,112 +162,195 @@ __global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
   const uint32_t lg = P.log2CS, mask = P.CS - 1, nw = (P.PH + 63) / 64, H = P.H;
   const uint32_t tid = threadIdx.x;
   STAMP(0);
-  // --- phase 0: prefetch sub-queries, counters, match bits, tags ------------
-  // Every global load of the staging is issued before the first LDS store:
-  // the kernel is latency-bound, so one round trip instead of one per item.
-  {
-    constexpr int U = 8;
-    PmSub sv[2];
-    uint32_t hv[2];
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));   // (uint4 is a union: no SROA)
-    uint64_t bv[U];
-    u32x4 tv[U], pv[U];
-    const uint32_t nb = LDS ? n * nw : 0, ph4 = LDS ? P.PH / 4 : 0;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const uint32_t j = tid + u * kBlock;
-      if (j < n) sv[u] = step_sub(S, b0 + j);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t i = tid + u * kBlock;
-      if (i < nb) bv[u] = S.bits[(uint64_t)(b0 + i / nw) * S.words + (i % nw)];
-      if (i < ph4) {
-        tv[u] = reinterpret_cast<const PM_G u32x4*>(P.tag)[i];
-        pv[u] = reinterpret_cast<const PM_G u32x4*>(P.pp)[i];
-      }
-    }
-    const uint32_t fq = tid == 0 ? *P.fqn : 0;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const uint32_t j = tid + u * kBlock;
-      hv[u] = (j < n && sv[u].kind == SUB_REAL && sv[u].idx < P.N) ? P.hist[(uint32_t)(sv[u].idx >> lg)] : 0;
-    }
-    for (uint32_t j = tid + 2 * kBlock; j < n; j += kBlock) {   // n > 512: rare
-      const PmSub sub = step_sub(S, b0 + j);
-      s_kind[j] = sub.kind; s_idx[j] = sub.idx; s_chunk[j] = (uint32_t)(sub.idx >> lg); s_st[j] = kNone;
-      s_hist0[j] = (sub.kind == SUB_REAL && sub.idx < P.N) ? P.hist[(uint32_t)(sub.idx >> lg)] : 0;
-    }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const uint32_t j = tid + u * kBlock;
-      if (j < n) {
-        s_kind[j] = sv[u].kind; s_idx[j] = sv[u].idx; s_chunk[j] = (uint32_t)(sv[u].idx >> lg);
-        s_hist0[j] = hv[u]; s_st[j] = kNone;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t i = tid + u * kBlock;
-      if (i < nb) bits_l[i] = bv[u];
-      if (i < ph4) {
-        reinterpret_cast<u32x4*>(tag_l)[i] = tv[u];
-        reinterpret_cast<u32x4*>(pp_l)[i] = pv[u];
-      }
-    }
-    if (tid == 0) s_fqn = fq;
-  }
-  __syncthreads();
-  STAMP(1);
-  auto bits_of = [&](uint32_t j) -> const uint64_t* {
-    return LDS ? bits_l + (uint64_t)j * nw : S.bits + (uint64_t)(b0 + j) * S.words;
-  };
-  auto tag_of = [&](uint32_t h) -> uint32_t { return LDS ? tag_l[h] : P.tag[h]; };
-  auto pp_of = [&](uint32_t h) -> uint32_t { return LDS ? pp_l[h] : P.pp[h]; };
-  // --- phase 1: first two stale candidates per real sub-query + their state;
-  //     speculative in-group index of every sub-query (all earlier succeed)
   const uint32_t wave = tid >> 6, lane = tid & 63;
-  for (uint32_t j = wave; j < n; j += kBlock / 64) {
-    if (s_kind[j] != SUB_REAL) continue;
-    const uint64_t* bw = bits_of(j);
-    const uint32_t c1 = find_next(bw, nw, 0);
-    const uint32_t c2 = c1 == kNone ? kNone : find_next(bw, nw, c1 + 1);
-    if (lane == 0) {
-      s_c1[j] = c1; s_c2[j] = c2;
-      s_t1[j] = c1 == kNone ? 0 : tag_of(c1); s_p1[j] = c1 == kNone ? 0 : pp_of(c1);
-      s_t2[j] = c2 == kNone ? 0 : tag_of(c2); s_p2[j] = c2 == kNone ? 0 : pp_of(c2);
+  // fast prologue (n <= 64 sub-queries, the usual shape): no staging of tags,
+  // program points or match bits; two independent chains of two round trips
+  const bool fast = LDS && n <= kSpecSubs && nw <= 128;
+  // match bits, tags and program points: LDS-staged by the staged prologue,
+  // read from global memory on the (rare) paths of the fast one that need them
+  const bool staged = LDS && !fast;
+  auto bits_of = [&](uint32_t j) -> const uint64_t* {
+    return staged ? bits_l + (uint64_t)j * nw : (const uint64_t*)(S.bits + (uint64_t)(b0 + j) * S.words);
+  };
+  auto tag_of = [&](uint32_t h) -> uint32_t { return staged ? tag_l[h] : P.tag[h]; };
+  auto pp_of = [&](uint32_t h) -> uint32_t { return staged ? pp_l[h] : P.pp[h]; };
+  if (fast) {
+    constexpr uint32_t NFW = kBlock / 64 - 1;   // candidate waves; the last wave predicts
+    if (wave < NFW) {
+      // first two stale candidates of each real sub-query straight from its match
+      // bits (a lane holds words lane and lane + 64), then their tag / program point
+      for (uint32_t j = wave; j < n; j += NFW) {
+        const PmSub sub = step_sub(S, b0 + j);
+        uint32_t c1 = kNone, c2 = kNone;
+        if (sub.kind == SUB_REAL && sub.idx < P.N) {
+          const PM_G uint64_t* bw = S.bits + (uint64_t)(b0 + j) * S.words;
+          uint64_t v0 = lane < nw ? bw[lane] : 0, v1 = lane + 64 < nw ? bw[lane + 64] : 0;
+          auto lowest = [&]() -> uint32_t {   // lowest set bit over words 0..nw-1
+            const uint64_t m0 = __ballot(v0 != 0);
+            if (m0) {
+              const uint32_t w = (uint32_t)__builtin_ctzll(m0);
+              return w * 64 + (uint32_t)__builtin_ctzll(__shfl(v0, w));
+            }
+            const uint64_t m1 = __ballot(v1 != 0);
+            if (m1) {
+              const uint32_t w = (uint32_t)__builtin_ctzll(m1);
+              return (64 + w) * 64 + (uint32_t)__builtin_ctzll(__shfl(v1, w));
+            }
+            return kNone;
+          };
+          c1 = lowest();
+          if (c1 != kNone) {
+            if ((c1 >> 6) == lane) v0 &= ~(1ull << (c1 & 63));
+            if ((c1 >> 6) == lane + 64) v1 &= ~(1ull << (c1 & 63));
+            c2 = lowest();
+          }
+        }
+        if (lane == 0) {
+          const uint32_t t1 = c1 == kNone ? 0 : P.tag[c1], p1 = c1 == kNone ? 0 : P.pp[c1];
+          const uint32_t t2 = c2 == kNone ? 0 : P.tag[c2], p2 = c2 == kNone ? 0 : P.pp[c2];
+          s_c1[j] = c1; s_c2[j] = c2; s_t1[j] = t1; s_p1[j] = p1; s_t2[j] = t2; s_p2[j] = p2;
+        }
+      }
+    } else {
+      // The last wave: the request of every sub-query and its chunk's
+      // QueryHistogram, then, in registers, the in-chunk index each would get if
+      // every earlier one succeeds, and the table loads of the values the
+      // re-evaluation in the chain would then need:
+      //   spec_v[k][j] = PRF(tag the refresh of sub k would hand out, chunk of j)
+      const uint32_t k = lane;
+      const uint32_t fq = lane == 0 ? *P.fqn : 0;
+      PmSub sub{0, SUB_NONE, 0};
+      if (k < n) sub = step_sub(S, b0 + k);
+      const bool real = k < n && sub.kind == SUB_REAL;
+      const uint64_t idx = k < n ? sub.idx : ~0ull;
+      const uint32_t ch = k < n ? (uint32_t)(sub.idx >> lg) : kNone;
+      const uint32_t h0 = (real && sub.idx < P.N) ? P.hist[ch] : 0;
+      if (k < n) { s_kind[k] = sub.kind; s_idx[k] = sub.idx; s_chunk[k] = ch; s_st[k] = kNone; s_hist0[k] = h0; }
+      if (lane == 0) s_fqn = fq;
+      bool first = real;                 // not a repeat of an earlier real sub-query
+      for (uint32_t t = 0; t + 1 < n; ++t) {
+        const uint64_t it = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(idx >> 32), t) << 32) |
+                            __builtin_amdgcn_readlane((uint32_t)idx, t);
+        const bool rt = __builtin_amdgcn_readlane(real ? 1u : 0u, t) != 0;
+        if (k > t && rt && it == idx) first = false;
+      }
+      uint32_t ing = h0;
+      for (uint32_t q = 0; q + 1 < n; ++q) {
+        const bool fqq = __builtin_amdgcn_readlane(first ? 1u : 0u, q) != 0;
+        const uint32_t cq = __builtin_amdgcn_readlane(ch, q);
+        if (k > q && fqq && cq == ch) ++ing;
+      }
+      if (k < n) s_sing[k] = ing;
+      for (uint32_t e0 = 0; e0 < n * n; e0 += 64) {   // uniform: every lane joins the shuffles
+        const uint32_t e = e0 + lane, kk = (e / n) & 63, j = e % n;
+        const uint32_t sk = __shfl(ing, kk), ck = __shfl(ch, kk), cj = __shfl(ch, j);
+        const bool rk = __shfl(real ? 1u : 0u, kk) != 0, rj = __shfl(real ? 1u : 0u, j) != 0;
+        if (e < n * n && kk < j && rk && rj && ck < P.SS && cj < P.SS && sk < P.Qpc)
+          spec_v[kk * kSpecSubs + j] = P.tab[(uint64_t)cj * H + P.PH + ck * P.Qpc + sk];
+      }
     }
-  }
-  if (LDS && n <= kSpecSubs && wave == kBlock / 64 - 1) {
-    // The last wave (the one with the least candidate work above) predicts, in
-    // registers, the in-chunk index each sub-query would get if every earlier
-    // one succeeds, and issues the table loads of the values the re-evaluation
-    // in phase 2 would then need:
-    //   spec_v[k][j] = PRF(tag the refresh of sub k would hand out, chunk of j)
-    const uint32_t k = lane;
-    const bool real = k < n && s_kind[k] == SUB_REAL;
-    const uint64_t idx = k < n ? s_idx[k] : ~0ull;
-    const uint32_t ch = k < n ? s_chunk[k] : kNone;
-    bool first = real;                 // not a repeat of an earlier real sub-query
-    for (uint32_t t = 0; t + 1 < n; ++t) {
-      const uint64_t it = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(idx >> 32), t) << 32) |
-                          __builtin_amdgcn_readlane((uint32_t)idx, t);
-      const bool rt = __builtin_amdgcn_readlane(real ? 1u : 0u, t) != 0;
-      if (k > t && rt && it == idx) first = false;
+  } else {
+    // --- phase 0: prefetch sub-queries, counters, match bits, tags ------------
+    // Every global load of the staging is issued before the first LDS store:
+    // the kernel is latency-bound, so one round trip instead of one per item.
+    {
+      constexpr int U = 8;
+      PmSub sv[2];
+      uint32_t hv[2];
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));   // (uint4 is a union: no SROA)
+      uint64_t bv[U];
+      u32x4 tv[U], pv[U];
+      const uint32_t nb = LDS ? n * nw : 0, ph4 = LDS ? P.PH / 4 : 0;
+  #pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const uint32_t j = tid + u * kBlock;
+        if (j < n) sv[u] = step_sub(S, b0 + j);
+      }
+  #pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t i = tid + u * kBlock;
+        if (i < nb) bv[u] = S.bits[(uint64_t)(b0 + i / nw) * S.words + (i % nw)];
+        if (i < ph4) {
+          tv[u] = reinterpret_cast<const PM_G u32x4*>(P.tag)[i];
+          pv[u] = reinterpret_cast<const PM_G u32x4*>(P.pp)[i];
+        }
+      }
+      const uint32_t fq = tid == 0 ? *P.fqn : 0;
+  #pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const uint32_t j = tid + u * kBlock;
+        hv[u] = (j < n && sv[u].kind == SUB_REAL && sv[u].idx < P.N) ? P.hist[(uint32_t)(sv[u].idx >> lg)] : 0;
+      }
+      for (uint32_t j = tid + 2 * kBlock; j < n; j += kBlock) {   // n > 512: rare
+        const PmSub sub = step_sub(S, b0 + j);
+        s_kind[j] = sub.kind; s_idx[j] = sub.idx; s_chunk[j] = (uint32_t)(sub.idx >> lg); s_st[j] = kNone;
+        s_hist0[j] = (sub.kind == SUB_REAL && sub.idx < P.N) ? P.hist[(uint32_t)(sub.idx >> lg)] : 0;
+      }
+  #pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const uint32_t j = tid + u * kBlock;
+        if (j < n) {
+          s_kind[j] = sv[u].kind; s_idx[j] = sv[u].idx; s_chunk[j] = (uint32_t)(sv[u].idx >> lg);
+          s_hist0[j] = hv[u]; s_st[j] = kNone;
+        }
+      }
+  #pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t i = tid + u * kBlock;
+        if (i < nb) bits_l[i] = bv[u];
+        if (i < ph4) {
+          reinterpret_cast<u32x4*>(tag_l)[i] = tv[u];
+          reinterpret_cast<u32x4*>(pp_l)[i] = pv[u];
+        }
+      }
+      if (tid == 0) s_fqn = fq;
     }
-    uint32_t ing = k < n ? s_hist0[k] : 0;
-    for (uint32_t q = 0; q + 1 < n; ++q) {
-      const bool fq = __builtin_amdgcn_readlane(first ? 1u : 0u, q) != 0;
-      const uint32_t cq = __builtin_amdgcn_readlane(ch, q);
-      if (k > q && fq && cq == ch) ++ing;
+    __syncthreads();
+    STAMP(1);
+    // --- phase 1: first two stale candidates per real sub-query + their state;
+    //     speculative in-group index of every sub-query (all earlier succeed)
+    for (uint32_t j = wave; j < n; j += kBlock / 64) {
+      if (s_kind[j] != SUB_REAL) continue;
+      const uint64_t* bw = bits_of(j);
+      const uint32_t c1 = find_next(bw, nw, 0);
+      const uint32_t c2 = c1 == kNone ? kNone : find_next(bw, nw, c1 + 1);
+      if (lane == 0) {
+        s_c1[j] = c1; s_c2[j] = c2;
+        s_t1[j] = c1 == kNone ? 0 : tag_of(c1); s_p1[j] = c1 == kNone ? 0 : pp_of(c1);
+        s_t2[j] = c2 == kNone ? 0 : tag_of(c2); s_p2[j] = c2 == kNone ? 0 : pp_of(c2);
+      }
     }
-    if (k < n) s_sing[k] = ing;
-    for (uint32_t e0 = 0; e0 < n * n; e0 += 64) {   // uniform: every lane joins the shuffles
-      const uint32_t e = e0 + lane, kk = (e / n) & 63, j = e % n;
-      const uint32_t sk = __shfl(ing, kk), ck = __shfl(ch, kk), cj = __shfl(ch, j);
-      const bool rk = __shfl(real ? 1u : 0u, kk) != 0, rj = __shfl(real ? 1u : 0u, j) != 0;
-      if (e < n * n && kk < j && rk && rj && ck < P.SS && cj < P.SS && sk < P.Qpc)
-        spec_v[kk * kSpecSubs + j] = P.tab[(uint64_t)cj * H + P.PH + ck * P.Qpc + sk];
+    if (LDS && n <= kSpecSubs && wave == kBlock / 64 - 1) {
+      // The last wave (the one with the least candidate work above) predicts, in
+      // registers, the in-chunk index each sub-query would get if every earlier
+      // one succeeds, and issues the table loads of the values the re-evaluation
+      // in phase 2 would then need:
+      //   spec_v[k][j] = PRF(tag the refresh of sub k would hand out, chunk of j)
+      const uint32_t k = lane;
+      const bool real = k < n && s_kind[k] == SUB_REAL;
+      const uint64_t idx = k < n ? s_idx[k] : ~0ull;
+      const uint32_t ch = k < n ? s_chunk[k] : kNone;
+      bool first = real;                 // not a repeat of an earlier real sub-query
+      for (uint32_t t = 0; t + 1 < n; ++t) {
+        const uint64_t it = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(idx >> 32), t) << 32) |
+                            __builtin_amdgcn_readlane((uint32_t)idx, t);
+        const bool rt = __builtin_amdgcn_readlane(real ? 1u : 0u, t) != 0;
+        if (k > t && rt && it == idx) first = false;
+      }
+      uint32_t ing = k < n ? s_hist0[k] : 0;
+      for (uint32_t q = 0; q + 1 < n; ++q) {
+        const bool fq = __builtin_amdgcn_readlane(first ? 1u : 0u, q) != 0;
+        const uint32_t cq = __builtin_amdgcn_readlane(ch, q);
+        if (k > q && fq && cq == ch) ++ing;
+      }
+      if (k < n) s_sing[k] = ing;
+      for (uint32_t e0 = 0; e0 < n * n; e0 += 64) {   // uniform: every lane joins the shuffles
+        const uint32_t e = e0 + lane, kk = (e / n) & 63, j = e % n;
+        const uint32_t sk = __shfl(ing, kk), ck = __shfl(ch, kk), cj = __shfl(ch, j);
+        const bool rk = __shfl(real ? 1u : 0u, kk) != 0, rj = __shfl(real ? 1u : 0u, j) != 0;
+        if (e < n * n && kk < j && rk && rj && ck < P.SS && cj < P.SS && sk < P.Qpc)
+          spec_v[kk * kSpecSubs + j] = P.tab[(uint64_t)cj * H + P.PH + ck * P.Qpc + sk];
+      }
     }
   }
   __syncthreads();
@@ -301,7 +384,67 @@ __global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
     uint32_t cl = 0;   // chain list entry
     uint32_t fqn = s_fqn, nmod = 0, nchain = 0, cadd = 0;
     auto rl = [](uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane(v, l); };
-    for (uint32_t j = 0; j < n; ++j) {
+    // --- parallel prefix ---------------------------------------------------
+    // A sub-query's outcome depends on the earlier ones only through (a) a
+    // local-cache hit (an earlier success with the same index), (b) the budget
+    // and per-chunk counters, (c) whether its first stale candidate was
+    // refreshed earlier, and (d) whether a hint refreshed earlier now matches
+    // it below that candidate.  Assuming every earlier valid first occurrence
+    // succeeds on its first candidate, (a)-(d) are decided for all lanes at
+    // once ((d) with the predicted table values).  The first valid first
+    // occurrence that would not succeed that plainly ends the prefix; the chain
+    // below resumes there, from the state the prefix leaves.
+    uint32_t jf = n;
+    {
+      const uint32_t off = (uint32_t)(ix & mask);
+      bool firstocc = real;
+      uint32_t src = k;   // first real sub-query with this index
+      for (uint32_t t = 0; t + 1 < n; ++t) {
+        const uint64_t it = ((uint64_t)rl((uint32_t)(ix >> 32), t) << 32) | rl((uint32_t)ix, t);
+        if (firstocc && t < k && rl(kd, t) == SUB_REAL && it == ix) { firstocc = false; src = t; }
+      }
+      const bool cand = real && ix < P.N && firstocc;
+      const uint64_t okm = __ballot(cand), below = (1ull << k) - 1;   // k < 64
+      uint32_t hist = h0;
+      for (uint32_t t = 0; t + 1 < n; ++t)
+        if (t < k && ((okm >> t) & 1) && rl(ch, t) == ch) ++hist;
+      const uint32_t fk = fqn + (uint32_t)__builtin_popcountll(okm & below);
+      const uint32_t ntag = P.PH + ch * P.Qpc + hist;   // the refresh this sub-query makes
+      bool simple = cand && hist < P.Qpc && fk < P.MaxQ && c1 != kNone;
+      for (uint32_t t = 0; t + 1 < n; ++t) {
+        if (!((okm >> t) & 1)) continue;
+        const uint32_t c1t = rl(c1, t), cht = rl(ch, t), ntt = rl(ntag, t), prt = rl(pred, t);
+        if (t < k) {
+          if (c1t == c1) simple = false;                      // (c)
+          if (cht != ch && c1t < c1 &&                          // (d): unpredicted, or a match
+              (ntt != prt || (uint32_t)spec_v[t * kSpecSubs + k] == off))
+            simple = false;
+        }
+      }
+      const uint64_t hard = __ballot(cand && !simple);
+      jf = hard ? (uint32_t)__builtin_ctzll(hard) : n;
+      if (in && k < jf) {
+        if (kd == SUB_DUMMY) st = ST_DUMMY;
+        else if (kd == SUB_HOSTCACHE) { st = ST_CACHED; rslot = (uint32_t)ix; }
+        else if (kd != SUB_REAL) st = ST_SKIP;
+        else if (ix >= P.N) st = ST_ERANGE;
+        else if (!firstocc) { st = ST_DUP; rslot = b0 + src; }
+        else { st = ST_OK; rhit = c1; ring = hist; rtag = t1; rpp = p1; rslot = fk; }
+      }
+      // the prefix's refreshed hints become the first entries, in order
+      const uint64_t okp = okm & (jf >= 64 ? ~0ull : ((1ull << jf) - 1));
+      if ((okp >> k) & 1) {
+        const uint32_t e = (uint32_t)__builtin_popcountll(okp & below);
+        m_h[e] = c1; m_tag[e] = ntag; m_pp[e] = (uint32_t)ix; m_sub[e] = k; m_pt[e] = pred;
+      }
+      nmod = (uint32_t)__builtin_popcountll(okp);
+      fqn += nmod;
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+      if (k < nmod) { mh = m_h[k]; mt = m_tag[k]; mp = m_pp[k]; ms = m_sub[k]; mpt = m_pt[k]; }
+    }
+    STAMP(38);
+    for (uint32_t j = jf; j < n; ++j) {
       const uint32_t kind = rl(kd, j), chunk = rl(ch, j);
       const uint64_t idx = ((uint64_t)rl((uint32_t)(ix >> 32), j) << 32) | rl((uint32_t)ix, j);
       uint32_t status = kNone, hit = 0, hist = 0, tag = 0, pp = 0, slot = 0, fl = 0;
@@ -370,6 +513,7 @@ __global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
       if (k == j) { st = status; rhit = hit; ring = hist; rtag = tag; rpp = pp; rslot = slot; rfl = fl; }
       if (j < 32) STAMP(4 + j);
     }
+    STAMP(39);
     // --- flush (one writer per result / hint / chunk) -----------------------
     if (in) {
       const bool ok = st == ST_OK;
