@@ -38,8 +38,8 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 METRIC = "private queries/sec + PIR-scan HBM GB/s, SIFT1M d=128 at 1/2/4/8 GPUs"
 KERNELS = ["prep_offsets", "prep_fold", "prep_repl", "hint_match", "resolve", "answer", "chain",
            "l2_rows"]
-HOST = ["host_search_knn", "host_knn_init", "host_knn_final", "host_batch_query", "host_step_launch",
-        "host_step_wait", "host_step_post"]
+HOST = ["host_search_knn", "host_knn_init", "host_knn_final", "host_knn_batch", "host_knn_update",
+        "host_gvi_parse", "host_batch_query", "host_step_launch", "host_step_wait", "host_step_post"]
 
 
 def make_data(rank: int):

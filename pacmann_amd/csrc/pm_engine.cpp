@@ -145,6 +145,10 @@ struct HostBuf {
   template <class T> T* as() const { return (T*)p; }
 };
 
+// Host wall-clock accumulators, read back as "host_*" through pm_timing_get.
+enum HostTimer : int { HT_STEP_LAUNCH, HT_STEP_WAIT, HT_STEP_POST, HT_BATCH_QUERY, HT_GVI_PARSE, HT_SEARCH_KNN, HT_KNN_INIT, HT_KNN_BATCH, HT_KNN_UPDATE, HT_KNN_FINAL, HT_COUNT };
+static const char* const kHostTimerName[HT_COUNT] = {"host_step_launch", "host_step_wait", "host_step_post", "host_batch_query", "host_gvi_parse", "host_search_knn", "host_knn_init", "host_knn_batch", "host_knn_update", "host_knn_final"};
+
 struct TimedLaunch { std::string name; hipEvent_t a, b; double bytes; };
 
 struct pm_ctx {
@@ -154,8 +158,9 @@ struct pm_ctx {
   bool debug_sync = false;   // PM_DEBUG_SYNC=1: synchronise after every launch (fault triage)
   std::string last_kernel;
   // host-side wall-clock accumulators ("host_*" names in pm_timing_get)
-  std::unordered_map<std::string, std::pair<uint64_t, double>> host;
-  void host_add(const char* name, double ms) { auto& h = host[name]; h.first++; h.second += ms; }
+  uint64_t host_n[HT_COUNT] = {};
+  double host_ms[HT_COUNT] = {};
+  void host_add(HostTimer t, double ms) { host_n[t]++; host_ms[t] += ms; }
   std::vector<TimedLaunch> launches;
   std::vector<hipEvent_t> pool;
   hipEvent_t ev() {
@@ -212,7 +217,7 @@ extern "C" int pm_timing_reset(pm_ctx* c) {
   HIPCHK(hipStreamSynchronize(c->stream));
   for (auto& t : c->launches) { c->pool.push_back(t.a); c->pool.push_back(t.b); }
   c->launches.clear();
-  c->host.clear();
+  for (int i = 0; i < HT_COUNT; ++i) { c->host_n[i] = 0; c->host_ms[i] = 0; }
   return 0;
 }
 extern "C" int pm_timing_get(pm_ctx* c, const char* name, uint64_t* launches, double* total_ms,
@@ -220,8 +225,8 @@ extern "C" int pm_timing_get(pm_ctx* c, const char* name, uint64_t* launches, do
   HIPCHK(hipStreamSynchronize(c->stream));
   uint64_t n = 0; double ms = 0, by = 0;
   if (strncmp(name, "host_", 5) == 0) {
-    auto it = c->host.find(name);
-    if (it != c->host.end()) { n = it->second.first; ms = it->second.second; }
+    for (int i = 0; i < HT_COUNT; ++i)
+      if (strcmp(name, kHostTimerName[i]) == 0) { n = c->host_n[i]; ms = c->host_ms[i]; }
     if (launches) *launches = n;
     if (total_ms) *total_ms = ms;
     if (bytes) *bytes = 0;
@@ -268,6 +273,7 @@ struct Engine {
   std::vector<double> stamp_sum;   // PM_STAMPS builds: accumulated phase deltas
   uint64_t stamp_n = 0;
   uint32_t step_token = 0;         // PmStep::token of the last step
+  size_t pf_off = 0, pf_len = ~size_t(0);   // bytes of each result row the caller reads next
   HostBuf desc_h, out_h;
   std::vector<PartHost> parts;
   uint32_t maxH = 0, maxPH = 0, maxSS = 0, maxRepl = 0, maxCS = 0, minCS = ~0u;
@@ -502,7 +508,10 @@ static inline double ms_since(Clock::time_point t) {
 // polls the headers instead of waiting for the kernel's completion signal.
 // Timing / debug runs, and a step not published within 5 s (a fault, or a
 // bug), fall back to the stream synchronisation, which reports errors.
-static int wait_step(pm_ctx* c, const PmOutHdr* hdr, uint32_t nsub, uint32_t token) {
+// While polling, the bytes [pf_off, pf_off + pf_len) of each published row are
+// prefetched, so the caller's reads of the results hit the cache.
+static int wait_step(pm_ctx* c, const PmOutHdr* hdr, uint32_t nsub, uint32_t token, const char* rows,
+                     size_t row_bytes, size_t pf_off, size_t pf_len) {
   if (c->timing >= 2 || c->debug_sync) {
     HIPCHK(hipStreamSynchronize(c->stream));
   } else {
@@ -511,7 +520,12 @@ static int wait_step(pm_ctx* c, const PmOutHdr* hdr, uint32_t nsub, uint32_t tok
     auto t0 = Clock::now();
     uint32_t s = 0;
     for (uint64_t spin = 0; s < nsub; ++spin) {
-      if (tok[s * stride] == token) { ++s; continue; }
+      if (tok[s * stride] == token) {
+        const char* r = rows + s * row_bytes + pf_off;
+        for (size_t b = 0; b < pf_len; b += 64) __builtin_prefetch(r + b);
+        ++s;
+        continue;
+      }
       if ((spin & 0xffff) == 0xffff && ms_since(t0) > 5000.0) {
         HIPCHK(hipStreamSynchronize(c->stream));
         HIPCHK(hipGetLastError());
@@ -597,10 +611,11 @@ static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
     if (x.kind == SUB_REAL || x.kind == SUB_DUMMY) ans_bytes += (double)g->parts[x.part].d.SS * E * 8;
   c->timed("answer", ans_bytes, [&] { pmk::step_answer(st, S); }, 2);
   HIPCHK(hipGetLastError());
-  c->host_add("host_step_launch", ms_since(t_begin));
+  c->host_add(HT_STEP_LAUNCH, ms_since(t_begin));
   auto t_wait = Clock::now();
-  CHK(wait_step(c, S.hdr_h, nsub, S.token));
-  c->host_add("host_step_wait", ms_since(t_wait));
+  CHK(wait_step(c, S.hdr_h, nsub, S.token, (const char*)S.rows_h, E * 8, g->pf_off,
+                std::min<size_t>(g->pf_len, E * 8 - std::min<size_t>(g->pf_off, E * 8))));
+  c->host_add(HT_STEP_WAIT, ms_since(t_wait));
   auto t_post = Clock::now();
   g->hdr = S.hdr_h;
   g->rows = S.rows_h;
@@ -617,7 +632,7 @@ static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
       g->hdr[s].dist = g->hdr[h.ref].dist;
     }
   }
-  c->host_add("host_step_post", ms_since(t_post));
+  c->host_add(HT_STEP_POST, ms_since(t_post));
 #ifdef PM_STAMPS
   {   // partition 0's phase deltas in shader clocks, accumulated; printed at exit
     std::vector<uint64_t> t(64);
@@ -835,7 +850,7 @@ static int batch_query(Engine* g, const uint64_t* idx, uint64_t n, uint64_t* out
                        uint8_t* ok = nullptr) {
   auto t = Clock::now();
   int r = batch_query_impl(g, idx, n, out, q_dev, dim, dist_out, rows_out, ok);
-  g->ctx->host_add("host_batch_query", ms_since(t));
+  g->ctx->host_add(HT_BATCH_QUERY, ms_since(t));
   return r;
 }
 static inline bool status_ok(uint32_t st) { return st == ST_OK || st == ST_CACHED || st == ST_DUP; }
@@ -1138,6 +1153,8 @@ extern "C" int pm_graph_preprocess(pm_graph* g) {
     }
     delete g->pir; g->pir = nullptr;
     CHK(pm_batchpir_create(g->ctx, g->n, ebytes, g->m, raw.data(), 8, g->pir_seed, &g->pir));
+    g->pir->e.pf_off = g->dim * 4;   // the search reads the neighbour lists of the rows
+    g->pir->e.pf_len = g->m * 4;
     if (g->skipPrep) CHK(pm_batchpir_dummy_preprocessing(g->pir));
     else CHK(pm_batchpir_preprocessing(g->pir));
   }
@@ -1212,6 +1229,7 @@ static int get_vertex_info(pm_graph* g, bool with_q) {
   g->rowp.resize(n);
   CHK(batch_query(e, g->qids.data(), n, nullptr, with_q ? g->dq.as<float>() : nullptr,
                   (uint32_t)g->dim, with_q ? g->dist.data() : nullptr, g->rowp.data()));
+  auto t_parse = Clock::now();
   const uint64_t nb_off = g->dim * 4;   // Entry2VectorAndNeighbors (private-search.go:418-439)
   for (uint64_t i = 0; i < n; ++i) {
     const char* r = (const char*)g->rowp[i] + nb_off;
@@ -1222,6 +1240,7 @@ static int get_vertex_info(pm_graph* g, bool with_q) {
     memcpy(nbi, (const char*)g->rowp[i] + nb_off, m * 4);
     if (memcmp(nbi, &g->graph[(uint64_t)g->batch[i] * m], m * 4) == 0) g->succ++;
   }
+  g->ctx->host_add(HT_GVI_PARSE, ms_since(t_parse));
   return 0;
 }
 
@@ -1232,7 +1251,7 @@ extern "C" int pm_search_knn(pm_graph* g, const float* query, int k, int max_ste
                              int benchmarking, int64_t* ids_out, int64_t* steps_out) {
   auto t = Clock::now();
   int r = search_knn_impl(g, query, k, max_step, parallel, benchmarking, ids_out, steps_out);
-  g->ctx->host_add("host_search_knn", ms_since(t));
+  g->ctx->host_add(HT_SEARCH_KNN, ms_since(t));
   return r;
 }
 static int search_knn_impl(pm_graph* g, const float* query, int k, int max_step, int parallel,
@@ -1278,7 +1297,7 @@ static int search_knn_impl(pm_graph* g, const float* query, int k, int max_step,
     std::partial_sort(g->fs.begin(), g->fs.begin() + take, g->fs.end(), [](const auto& a, const auto& b) {
       return a.first.dist < b.first.dist || (a.first.dist == b.first.dist && a.second < b.second); });
     g->fs.resize(take);   // start ids are distinct: none of the first `parallel` is skipped as known
-    g->ctx->host_add("host_knn_init", ms_since(t_init));
+    g->ctx->host_add(HT_KNN_INIT, ms_since(t_init));
     for (size_t i = 0; (int64_t)g->heap.size() < parallel && i < g->fs.size(); ++i) {
       const int64_t id = g->fs[i].first.id;
       if (g->known.find((uint64_t)id)) continue;
@@ -1287,6 +1306,7 @@ static int search_knn_impl(pm_graph* g, const float* query, int k, int max_step,
     }
   }
   for (int step = 0; step < max_step; ++step) {
+    auto t_batch = Clock::now();
     g->batch.clear();
     for (int r = 0; r < parallel; ++r) {
       if (g->heap.empty() || benchmarking) {
@@ -1297,8 +1317,10 @@ static int search_knn_impl(pm_graph* g, const float* query, int k, int max_step,
         for (uint64_t i = 0; i < m; ++i) g->batch.push_back((int64_t)nb[i]);
       }
     }
+    g->ctx->host_add(HT_KNN_BATCH, ms_since(t_batch));
     CHK(get_vertex_info(g, !benchmarking));
     if (benchmarking) continue;
+    auto t_round = Clock::now();
     for (size_t i = 0; i < g->batch.size(); ++i) {
       const int64_t id = g->batch[i];
       if (g->known.find((uint64_t)id)) continue;
@@ -1309,6 +1331,7 @@ static int search_knn_impl(pm_graph* g, const float* query, int k, int max_step,
       add_known(id, nb, g->dist[i], step);
       heap_push(g->heap, {g->dist[i], id});
     }
+    g->ctx->host_add(HT_KNN_UPDATE, ms_since(t_round));
   }
   auto t_fin = Clock::now();
   g->all.clear();
@@ -1321,7 +1344,7 @@ static int search_knn_impl(pm_graph* g, const float* query, int k, int max_step,
     if (i >= (int)g->all.size()) { ids_out[i] = -1; if (steps_out) steps_out[i] = -1; }
     else { ids_out[i] = g->all[i].id; if (steps_out) steps_out[i] = g->known_reach[*g->known.find((uint64_t)g->all[i].id)]; }
   }
-  g->ctx->host_add("host_knn_final", ms_since(t_fin));
+  g->ctx->host_add(HT_KNN_FINAL, ms_since(t_fin));
   return 0;
 }
 
