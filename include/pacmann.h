@@ -52,10 +52,16 @@ int         pm_ctx_create(int device, pm_ctx** out);
 void        pm_ctx_destroy(pm_ctx* ctx);
 const char* pm_last_error(void);
 int         pm_ctx_sync(pm_ctx* ctx);
-/* Per-kernel timing with HIP events recorded on the stream each kernel runs
- * on.  Names: "prep_offsets", "prep_fold", "prep_repl", "hint_match",
- * "resolve", "answer", "decode", "l2_rows", "ip_scan", "prf". */
-int pm_timing_enable(pm_ctx* ctx, int on);
+/* Per-kernel timing.  Level 1: HIP events around the preprocessing and leaf
+ * kernels on the stream they run on ("prep_offsets", "prep_fold",
+ * "prep_repl", "l2_rows", "ip_scan", "prf", server "answer").  Level 2 also
+ * times the three kernels of every online step ("hint_match", "resolve",
+ * "answer") with events carried in their own dispatch packets
+ * (hipExtLaunchKernelGGL), and synchronises each step.  Host wall-clock
+ * accumulators are always on: "host_step_launch", "host_step_wait",
+ * "host_step_post", "host_batch_query", "host_gvi_parse", "host_search_knn",
+ * "host_knn_init", "host_knn_batch", "host_knn_update", "host_knn_final". */
+int pm_timing_enable(pm_ctx* ctx, int level);
 int pm_timing_reset(pm_ctx* ctx);
 int pm_timing_get(pm_ctx* ctx, const char* kernel, uint64_t* launches, double* total_ms,
                   double* alg_bytes);

@@ -183,6 +183,16 @@ struct pm_ctx {
     (void)hipEventRecord(t.b, stream);
     launches.push_back(t);
   }
+  // The same for launchers that attach the events to the kernel's own dispatch
+  // packet (hipExtLaunchKernelGGL): no marker latency around short kernels.
+  template <class F> void timed_ext(const char* name, double bytes, F&& f, int level) {
+    last_kernel = name;
+    if (debug_sync) { timed(name, bytes, [&] { f(pmk::PmEvents{}); }, level); return; }
+    if (timing < level) { f(pmk::PmEvents{}); return; }
+    TimedLaunch t{name, ev(), ev(), bytes};
+    f(pmk::PmEvents{t.a, t.b});
+    launches.push_back(t);
+  }
   ~pm_ctx() {
     for (auto& t : launches) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
     for (auto e : pool) (void)hipEventDestroy(e);
@@ -587,11 +597,12 @@ static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
   }
   uint32_t nreal = 0;
   for (auto& x : g->subs) nreal += x.kind == SUB_REAL;
-  c->timed("hint_match", (double)nreal * g->maxPH, [&] { pmk::step_match(st, S, g->maxPH); }, 2);
+  // timing level 2: the step kernels carry their events in their own dispatch packets
+  c->timed_ext("hint_match", (double)nreal * g->maxPH, [&](pmk::PmEvents ev) { pmk::step_match(st, S, g->maxPH, ev); }, 2);
   uint32_t max_per_part = 0;
   for (uint64_t p = 0; p < g->P; ++p) max_per_part = std::max(max_per_part, g->sb[p + 1] - g->sb[p]);
   const bool lds = pmk::step_resolve_lds_ok(g->maxPH, max_per_part);
-  c->timed("resolve", 0, [&] { pmk::step_resolve(st, S, lds); }, 2);
+  c->timed_ext("resolve", 0, [&](pmk::PmEvents ev) { pmk::step_resolve(st, S, lds, ev); }, 2);
   if (c->debug_sync) {   // validate every resolution record before k_answer consumes it
     std::vector<PmRes> rr(nsub);
     HIPCHK(hipMemcpy(rr.data(), S.res, nsub * sizeof(PmRes), hipMemcpyDeviceToHost));
@@ -608,14 +619,18 @@ static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
   }
   double ans_bytes = 0;
   for (auto& x : g->subs)
-    if (x.kind == SUB_REAL || x.kind == SUB_DUMMY) ans_bytes += (double)g->parts[x.part].d.SS * E * 8;
-  c->timed("answer", ans_bytes, [&] { pmk::step_answer(st, S); }, 2);
+    if (x.kind == SUB_REAL || x.kind == SUB_DUMMY) {   // rows*E*8 + 4*SS + 8*E
+      const double ss = g->parts[x.part].d.SS;
+      ans_bytes += ss * E * 8 + 4 * ss + 8.0 * E;
+    }
+  c->timed_ext("answer", ans_bytes, [&](pmk::PmEvents ev) { pmk::step_answer(st, S, ev); }, 2);
   HIPCHK(hipGetLastError());
   c->host_add(HT_STEP_LAUNCH, ms_since(t_begin));
   auto t_wait = Clock::now();
   CHK(wait_step(c, S.hdr_h, nsub, S.token, (const char*)S.rows_h, E * 8, g->pf_off,
                 std::min<size_t>(g->pf_len, E * 8 - std::min<size_t>(g->pf_off, E * 8))));
   c->host_add(HT_STEP_WAIT, ms_since(t_wait));
+
   auto t_post = Clock::now();
   g->hdr = S.hdr_h;
   g->rows = S.rows_h;

@@ -139,10 +139,13 @@ void prep_fold(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxH, 
                uint32_t E, uint32_t minCS, uint32_t maxCS, const uint64_t* zero16);
 void prep_repl(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxRepl,
                const uint64_t* db, uint32_t E);
-void step_match(hipStream_t st, const PmStep& S, uint32_t maxPH);
-void step_resolve(hipStream_t st, const PmStep& S, bool lds);
+// Timing events carried by a launch's own dispatch packet (null: untimed)
+struct PmEvents { hipEvent_t a = nullptr, b = nullptr; };
+void step_match(hipStream_t st, const PmStep& S, uint32_t maxPH, PmEvents ev = {});
+uint32_t step_match_blocks(uint32_t maxPH);   // k_match workgroups per sub-query
+void step_resolve(hipStream_t st, const PmStep& S, bool lds, PmEvents ev = {});
 bool step_resolve_lds_ok(uint32_t maxPH, uint32_t max_sub_per_part);
-void step_answer(hipStream_t st, const PmStep& S);
+void step_answer(hipStream_t st, const PmStep& S, PmEvents ev = {});
 uint32_t step_max_sub_per_part();
 uint32_t step_max_ss();
 uint32_t step_max_e();

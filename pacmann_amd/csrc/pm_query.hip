@@ -26,6 +26,8 @@
 //                           agent-scope release/acquire) then decodes, in
 //                           order, the rare sub-queries whose hint was already
 //                           refreshed earlier in the same step.
+#include <hip/hip_ext.h>
+
 #include "pm_aes.h"
 #include "pm_internal.h"
 
@@ -58,7 +60,13 @@ constexpr uint32_t kNone = 0xffffffffu;
 #endif
 // slots: k_resolve partition 0: 0..40; k_match block (0,0): 41..47; k_answer block 0: 48..63
 
+
 // ---------------------------------------------------------------------------
+#ifndef PM_MATCH_HPT
+#define PM_MATCH_HPT 4
+#endif
+constexpr int kMatchHPT = PM_MATCH_HPT;   // hints per thread of k_match
+
 __global__ void __launch_bounds__(kBlock) k_match(PmStep S) {
   const uint32_t s = blockIdx.y;
   PmSub sub;
@@ -81,21 +89,33 @@ __global__ void __launch_bounds__(kBlock) k_match(PmStep S) {
   STAMP_AT(stamp_wg, 41);
   if (sub.kind != SUB_REAL) return;
   const PmPart& P = S.parts[sub.part];
-  const uint32_t base = blockIdx.x * kBlock;
+  const uint32_t base = blockIdx.x * kBlock * kMatchHPT;
   if (base >= P.PH) return;
   STAMP_AT(stamp_wg, 42);
   const uint32_t mask = P.CS - 1, chunk = (uint32_t)(sub.idx >> P.log2CS),
                  offset = (uint32_t)(sub.idx & mask);
   const PM_G uint16_t* row = P.tab + (uint64_t)chunk * P.H;
-  const uint32_t h = base + threadIdx.x;
-  bool m = false;
-  if (h < P.PH && sub.idx < P.N) {
-    const uint32_t pp = P.pp[h];
-    m = row[P.tag[h]] == offset && (pp == kDefaultProgramPoint || (pp >> P.log2CS) != chunk);
+  // kMatchHPT hints per thread, all loads of a kind issued together
+  uint32_t tg[kMatchHPT], pv[kMatchHPT];
+  uint16_t rv[kMatchHPT];
+  const bool live = sub.idx < P.N;
+#pragma unroll
+  for (int u = 0; u < kMatchHPT; ++u) {
+    const uint32_t h = base + u * kBlock + threadIdx.x;
+    tg[u] = 0; pv[u] = kDefaultProgramPoint;
+    if (live && h < P.PH) { tg[u] = P.tag[h]; pv[u] = P.pp[h]; }
   }
-  const uint64_t b = __ballot(m);
+#pragma unroll
+  for (int u = 0; u < kMatchHPT; ++u) rv[u] = row[tg[u]];
+#pragma unroll
+  for (int u = 0; u < kMatchHPT; ++u) {
+    const uint32_t h = base + u * kBlock + threadIdx.x;
+    const bool m = live && h < P.PH && rv[u] == offset &&
+                   (pv[u] == kDefaultProgramPoint || (pv[u] >> P.log2CS) != chunk);
+    const uint64_t b = __ballot(m);
+    if ((threadIdx.x & 63) == 0 && (h - (threadIdx.x & 63)) < P.PH) S.bits[(uint64_t)s * S.words + (h >> 6)] = b;
+  }
   STAMP_AT(stamp_wg, 43);
-  if ((threadIdx.x & 63) == 0 && (h - (threadIdx.x & 63)) < P.PH) S.bits[(uint64_t)s * S.words + (h >> 6)] = b;
 }
 
 // Descriptor accessors: kernel arguments when they carry it, else the device copies.
@@ -900,23 +920,27 @@ __global__ void __launch_bounds__(kAnsBlock) k_answer(PmStep S) {
 
 namespace pmk {
 static inline unsigned cdiv(uint64_t a, uint64_t b) { return (unsigned)((a + b - 1) / b); }
-void step_match(hipStream_t st, const PmStep& S, uint32_t maxPH) {
-  hipLaunchKernelGGL(k_match, dim3(cdiv(maxPH, kBlock), S.nsub), dim3(kBlock), 0, st, S);
+uint32_t step_match_blocks(uint32_t maxPH) { return cdiv(maxPH, kBlock * kMatchHPT); }
+// With events, the launch carries them in its own dispatch packet
+// (hipExtLaunchKernelGGL): the kernel's execution time as the profiler sees it.
+#define PM_LAUNCH(ev, kern, grid, blk, st, ...)                                              \
+  do {                                                                                       \
+    if ((ev).a) hipExtLaunchKernelGGL(kern, grid, blk, 0, st, (ev).a, (ev).b, 0, __VA_ARGS__); \
+    else hipLaunchKernelGGL(kern, grid, blk, 0, st, __VA_ARGS__);                             \
+  } while (0)
+void step_match(hipStream_t st, const PmStep& S, uint32_t maxPH, PmEvents ev) {
+  PM_LAUNCH(ev, k_match, dim3(step_match_blocks(maxPH), S.nsub), dim3(kBlock), st, S);
 }
-void step_resolve(hipStream_t st, const PmStep& S, bool lds) {
-  if (lds)
-    hipLaunchKernelGGL(k_resolve<true>, dim3(S.np), dim3(kBlock), 0, st, S);
-  else
-    hipLaunchKernelGGL(k_resolve<false>, dim3(S.np), dim3(kBlock), 0, st, S);
+void step_resolve(hipStream_t st, const PmStep& S, bool lds, PmEvents ev) {
+  if (lds) PM_LAUNCH(ev, k_resolve<true>, dim3(S.np), dim3(kBlock), st, S);
+  else PM_LAUNCH(ev, k_resolve<false>, dim3(S.np), dim3(kBlock), st, S);
 }
 bool step_resolve_lds_ok(uint32_t maxPH, uint32_t max_sub_per_part) {
   return maxPH <= kLdsPH && max_sub_per_part * ((maxPH + 63) / 64) <= kLdsBitWords;
 }
-void step_answer(hipStream_t st, const PmStep& S) {
-  if (S.E % 2 == 0)
-    hipLaunchKernelGGL(k_answer<2>, dim3(S.nsub), dim3(kAnsBlock), 0, st, S);
-  else
-    hipLaunchKernelGGL(k_answer<1>, dim3(S.nsub), dim3(kAnsBlock), 0, st, S);
+void step_answer(hipStream_t st, const PmStep& S, PmEvents ev) {
+  if (S.E % 2 == 0) PM_LAUNCH(ev, k_answer<2>, dim3(S.nsub), dim3(kAnsBlock), st, S);
+  else PM_LAUNCH(ev, k_answer<1>, dim3(S.nsub), dim3(kAnsBlock), st, S);
 }
 uint32_t step_max_sub_per_part() { return kMaxSubPerPart; }
 uint32_t step_max_ss() { return kMaxSSLds; }
