@@ -279,7 +279,7 @@ struct Engine {
   DevBuf db, zero16, parts_d, owned_d, tag, pp, parity, ridx, rval, hist, fqn, arena, tab, tabT, done;
   std::vector<uint32_t> owned_list;   // owned partitions in order (owned_d holds their PmPart)
   DevBuf qoffs, ans_srv;
-  DevBuf subs_d, sb_d, bits, res_d, ans, qvec, stamps;
+  DevBuf subs_d, sb_d, bits, cand, meta, spec, res_d, ans, qvec, stamps;
   std::vector<double> stamp_sum;   // PM_STAMPS builds: accumulated phase deltas
   uint64_t stamp_n = 0;
   uint32_t step_token = 0;         // PmStep::token of the last step
@@ -560,6 +560,10 @@ static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
   CHK(g->subs_d.reserve(nsub * sizeof(PmSub)));
   CHK(g->sb_d.reserve((g->P + 1) * 4));
   CHK(g->bits.reserve((uint64_t)nsub * words * 8));
+  const uint32_t cblk = pmk::step_match_blocks(g->maxPH);
+  CHK(g->cand.reserve((uint64_t)nsub * cblk * 6 * 4));
+  CHK(g->meta.reserve((uint64_t)nsub * 2 * 4));
+  CHK(g->spec.reserve((uint64_t)nsub * 64 * 2));
   CHK(g->res_d.reserve(nsub * sizeof(PmRes)));
   CHK(g->ans.reserve((uint64_t)nsub * E * 8));
   const size_t dsub = nsub * sizeof(PmSub);
@@ -575,6 +579,10 @@ static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
   S.subs = g->subs_d.as<PmSub>();
   S.sb = g->sb_d.as<uint32_t>();
   S.bits = g->bits.as<uint64_t>();
+  S.cand = g->cand.as<uint32_t>();
+  S.meta = g->meta.as<uint32_t>();
+  S.spec = g->spec.as<uint16_t>();
+  S.cblk = cblk;
   S.res = g->res_d.as<PmRes>();
   S.ans = g->ans.as<uint64_t>();
   S.done = g->done.as<uint32_t>();

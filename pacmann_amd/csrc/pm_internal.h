@@ -108,6 +108,8 @@ struct PmStep {
   PM_G PmSub* subs;            // device copies
   PM_G uint32_t* sb;
   PM_G uint64_t* bits;         // [nsub][words] hint-match bits (k_match -> k_resolve)
+  PM_G uint32_t* cand;         // [nsub][cblk][6]: per k_match block its first two matches
+                               // {hint, tag, program point} x 2 (hint kNone: none)
   PM_G PmRes* res;             // [nsub]
   PM_G uint64_t* ans;          // [nsub][E] raw answers of chained sub-queries
   PM_G uint32_t* done;         // [0] k_answer arrival counter of chain workgroups,
@@ -118,7 +120,9 @@ struct PmStep {
   PM_G PmOutHdr* hdr_h;        // pinned host outputs
   PM_G uint64_t* rows_h;
   PM_G uint64_t* stamps;       // PM_STAMPS diagnostic builds only: s_memtime per phase
-  uint32_t words, E, dim, nsub, np;
+  PM_G uint32_t* meta;         // [nsub][2]: chunk QueryHistogram, predicted in-chunk index
+  PM_G uint16_t* spec;         // [nsub][64]: predicted re-evaluation values (k_match -> k_resolve)
+  uint32_t words, E, dim, nsub, np, cblk;
   // Small steps ship the descriptor inside the kernel arguments (no PCIe
   // round trip); larger ones use subs_h / sb_h.
   uint32_t args_valid;

@@ -62,6 +62,38 @@ constexpr uint32_t kNone = 0xffffffffu;
 
 
 // ---------------------------------------------------------------------------
+// LDS staging limits of the fast resolve path (SIFT1M / MS-MARCO shapes);
+// larger configurations take the global-memory path of the same kernel.
+constexpr uint32_t kLdsPH = 8192, kLdsBitWords = 2048, kSpecSubs = 64;   // staging: 8 items per thread
+
+// Descriptor accessors: kernel arguments when they carry it, else the device copies.
+// (Two explicit branches: a select of the two addresses would merge them into
+// one generic pointer and a flat load.)
+__device__ __forceinline__ PmSub step_sub(const PmStep& S, uint32_t s) {
+  if (S.args_valid) return S.subs_a[s];
+  PmSub v = S.subs[s];
+  __builtin_amdgcn_sched_barrier(0);
+  return v;
+}
+__device__ __forceinline__ uint32_t step_sb(const PmStep& S, uint32_t p) {
+  return S.args_valid ? S.sb_a[p] : S.sb[p];
+}
+
+// The descriptor as k_match sees it: kernel arguments, else the pinned host
+// copy (the device copy is being written by this very kernel).
+__device__ __forceinline__ PmSub desc_sub(const PmStep& S, uint32_t i) {
+  if (S.args_valid) return S.subs_a[i];
+  PmSub v = S.subs_h[i];
+  __builtin_amdgcn_sched_barrier(0);
+  return v;
+}
+__device__ __forceinline__ uint32_t desc_sb(const PmStep& S, uint32_t p) {
+  if (S.args_valid) return S.sb_a[p];
+  uint32_t v = S.sb_h[p];
+  __builtin_amdgcn_sched_barrier(0);
+  return v;
+}
+
 #ifndef PM_MATCH_HPT
 #define PM_MATCH_HPT 4
 #endif
@@ -87,18 +119,28 @@ __global__ void __launch_bounds__(kBlock) k_match(PmStep S) {
   if (blockIdx.x == 0 && s == 0 && threadIdx.x < 3) S.done[threadIdx.x] = 0;
   const bool stamp_wg = blockIdx.x == 0 && s == 0;
   STAMP_AT(stamp_wg, 41);
+  // the descriptor is workgroup-uniform; say so, so the partition header is
+  // fetched once with scalar loads
+  sub.part = __builtin_amdgcn_readfirstlane(sub.part);
+  sub.kind = __builtin_amdgcn_readfirstlane(sub.kind);
+  sub.idx = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(sub.idx >> 32)) << 32) |
+            __builtin_amdgcn_readfirstlane((uint32_t)sub.idx);
   if (sub.kind != SUB_REAL) return;
-  const PmPart& P = S.parts[sub.part];
+  const PmPart P = S.parts[sub.part];
   const uint32_t base = blockIdx.x * kBlock * kMatchHPT;
   if (base >= P.PH) return;
   STAMP_AT(stamp_wg, 42);
   const uint32_t mask = P.CS - 1, chunk = (uint32_t)(sub.idx >> P.log2CS),
                  offset = (uint32_t)(sub.idx & mask);
   const PM_G uint16_t* row = P.tab + (uint64_t)chunk * P.H;
+  const bool live = sub.idx < P.N;
+  // Block 0 of a sub-query also prepares k_resolve's prediction: its chunk's
+  // QueryHistogram now, the rest below (loads overlap the match loads).
+  const bool meta_wg = blockIdx.x == 0;
+  const uint32_t h0k = (meta_wg && live) ? P.hist[chunk] : 0;
   // kMatchHPT hints per thread, all loads of a kind issued together
   uint32_t tg[kMatchHPT], pv[kMatchHPT];
   uint16_t rv[kMatchHPT];
-  const bool live = sub.idx < P.N;
 #pragma unroll
   for (int u = 0; u < kMatchHPT; ++u) {
     const uint32_t h = base + u * kBlock + threadIdx.x;
@@ -107,28 +149,83 @@ __global__ void __launch_bounds__(kBlock) k_match(PmStep S) {
   }
 #pragma unroll
   for (int u = 0; u < kMatchHPT; ++u) rv[u] = row[tg[u]];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (meta_wg && wave == 0) {
+    // In-chunk index this sub-query gets if every earlier one of its partition
+    // succeeds (QueryHistogram + earlier valid first occurrences in the same
+    // chunk), and the PRF values at the later sub-queries' chunks of the tag
+    // that refresh would hand out: spec[s][j] (k_resolve's re-evaluation).
+    const uint32_t pb0 = desc_sb(S, sub.part), pn = desc_sb(S, sub.part + 1) - pb0, k = s - pb0;
+    if (pn <= kSpecSubs) {
+      PmSub st{0, SUB_NONE, ~0ull};
+      if (lane < pn) st = desc_sub(S, pb0 + lane);
+      const bool validt = lane < pn && st.kind == SUB_REAL && st.idx < P.N;
+      const uint32_t cht = (uint32_t)(st.idx >> P.log2CS);
+      bool first = validt;
+      for (uint32_t t = 0; t + 1 < pn; ++t) {
+        const uint64_t it = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(st.idx >> 32), t) << 32) |
+                            __builtin_amdgcn_readlane((uint32_t)st.idx, t);
+        const bool rt = __builtin_amdgcn_readlane(st.kind == SUB_REAL ? 1u : 0u, t) != 0;
+        if (t < lane && rt && it == st.idx) first = false;
+      }
+      const uint64_t mk = __ballot(lane < k && validt && first && cht == chunk);
+      const uint32_t sing = h0k + (uint32_t)__builtin_popcountll(mk);
+      const uint32_t pred = (live && sing < P.Qpc && chunk < P.SS) ? P.PH + chunk * P.Qpc + sing : kNone;
+      uint32_t v = kSkip;
+      if (lane < pn && lane > k && validt && cht < P.SS && pred != kNone) v = P.tab[(uint64_t)cht * P.H + pred];
+      if (lane < pn) S.spec[(uint64_t)s * kSpecSubs + lane] = (uint16_t)v;
+      if (lane == 0) { S.meta[2 * (uint64_t)s] = h0k; S.meta[2 * (uint64_t)s + 1] = sing; }
+    }
+  }
+  // match bits, and the block's first two matches with the tag / program
+  // point this thread already holds (k_resolve's usual candidates)
+  __shared__ uint32_t s_cand[kBlock / 64][6];
+  uint32_t h0 = kNone, t0 = 0, p0 = 0, h1 = kNone, t1 = 0, p1 = 0;   // wave-uniform
 #pragma unroll
   for (int u = 0; u < kMatchHPT; ++u) {
     const uint32_t h = base + u * kBlock + threadIdx.x;
     const bool m = live && h < P.PH && rv[u] == offset &&
                    (pv[u] == kDefaultProgramPoint || (pv[u] >> P.log2CS) != chunk);
-    const uint64_t b = __ballot(m);
-    if ((threadIdx.x & 63) == 0 && (h - (threadIdx.x & 63)) < P.PH) S.bits[(uint64_t)s * S.words + (h >> 6)] = b;
+    uint64_t b = __ballot(m);
+    if (lane == 0 && (h - lane) < P.PH) S.bits[(uint64_t)s * S.words + (h >> 6)] = b;
+    if (b && h1 == kNone) {   // in hint order within this wave
+      const uint32_t l = (uint32_t)__builtin_ctzll(b), hl = h - lane + l;
+      const uint32_t tl = __builtin_amdgcn_readlane(tg[u], l), pl = __builtin_amdgcn_readlane(pv[u], l);
+      if (h0 == kNone) {
+        h0 = hl; t0 = tl; p0 = pl;
+        b &= b - 1;
+        if (b) {
+          const uint32_t l2 = (uint32_t)__builtin_ctzll(b);
+          h1 = h - lane + l2;
+          t1 = __builtin_amdgcn_readlane(tg[u], l2);
+          p1 = __builtin_amdgcn_readlane(pv[u], l2);
+        }
+      } else {
+        h1 = hl; t1 = tl; p1 = pl;
+      }
+    }
+  }
+  if (lane == 0) {
+    s_cand[wave][0] = h0; s_cand[wave][1] = t0; s_cand[wave][2] = p0;
+    s_cand[wave][3] = h1; s_cand[wave][4] = t1; s_cand[wave][5] = p1;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {   // merge the waves' pairs by hint index
+    uint32_t o[6] = {kNone, 0, 0, kNone, 0, 0};
+    for (uint32_t w = 0; w < kBlock / 64; ++w)
+      for (int k = 0; k < 2; ++k) {
+        const uint32_t h = s_cand[w][3 * k];
+        if (h < o[0]) {
+          o[3] = o[0]; o[4] = o[1]; o[5] = o[2];
+          o[0] = h; o[1] = s_cand[w][3 * k + 1]; o[2] = s_cand[w][3 * k + 2];
+        } else if (h < o[3]) {
+          o[3] = h; o[4] = s_cand[w][3 * k + 1]; o[5] = s_cand[w][3 * k + 2];
+        }
+      }
+    PM_G uint32_t* dst = S.cand + ((uint64_t)s * S.cblk + blockIdx.x) * 6;
+    for (int i = 0; i < 6; ++i) dst[i] = o[i];
   }
   STAMP_AT(stamp_wg, 43);
-}
-
-// Descriptor accessors: kernel arguments when they carry it, else the device copies.
-// (Two explicit branches: a select of the two addresses would merge them into
-// one generic pointer and a flat load.)
-__device__ __forceinline__ PmSub step_sub(const PmStep& S, uint32_t s) {
-  if (S.args_valid) return S.subs_a[s];
-  PmSub v = S.subs[s];
-  __builtin_amdgcn_sched_barrier(0);
-  return v;
-}
-__device__ __forceinline__ uint32_t step_sb(const PmStep& S, uint32_t p) {
-  return S.args_valid ? S.sb_a[p] : S.sb[p];
 }
 
 // First set bit at position >= start in a sub-query's match bitmask (one wave).
@@ -157,9 +254,6 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t x) {
 
 
 constexpr int kMaxSubPerPart = 256;
-// LDS staging limits of the fast resolve path (SIFT1M / MS-MARCO shapes);
-// larger configurations take the global-memory path of the same kernel.
-constexpr uint32_t kLdsPH = 8192, kLdsBitWords = 2048, kSpecSubs = 64;   // staging: 8 items per thread
 
 template <bool LDS>
 __global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
@@ -197,77 +291,44 @@ __global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
   if (fast) {
     constexpr uint32_t NFW = kBlock / 64 - 1;   // candidate waves; the last wave predicts
     if (wave < NFW) {
-      // first two stale candidates of each real sub-query straight from its match
-      // bits (a lane holds words lane and lane + 64), then their tag / program point
+      // first two stale candidates of each real sub-query, with their tag and
+      // program point: the per-block records k_match wrote (blocks in hint order)
+      const uint32_t nblk = (P.PH + kBlock * kMatchHPT - 1) / (kBlock * kMatchHPT);
       for (uint32_t j = wave; j < n; j += NFW) {
         const PmSub sub = step_sub(S, b0 + j);
-        uint32_t c1 = kNone, c2 = kNone;
+        uint32_t c1 = kNone, c2 = kNone, t1 = 0, p1 = 0, t2 = 0, p2 = 0;
         if (sub.kind == SUB_REAL && sub.idx < P.N) {
-          const PM_G uint64_t* bw = S.bits + (uint64_t)(b0 + j) * S.words;
-          uint64_t v0 = lane < nw ? bw[lane] : 0, v1 = lane + 64 < nw ? bw[lane + 64] : 0;
-          auto lowest = [&]() -> uint32_t {   // lowest set bit over words 0..nw-1
-            const uint64_t m0 = __ballot(v0 != 0);
-            if (m0) {
-              const uint32_t w = (uint32_t)__builtin_ctzll(m0);
-              return w * 64 + (uint32_t)__builtin_ctzll(__shfl(v0, w));
-            }
-            const uint64_t m1 = __ballot(v1 != 0);
-            if (m1) {
-              const uint32_t w = (uint32_t)__builtin_ctzll(m1);
-              return (64 + w) * 64 + (uint32_t)__builtin_ctzll(__shfl(v1, w));
-            }
-            return kNone;
-          };
-          c1 = lowest();
-          if (c1 != kNone) {
-            if ((c1 >> 6) == lane) v0 &= ~(1ull << (c1 & 63));
-            if ((c1 >> 6) == lane + 64) v1 &= ~(1ull << (c1 & 63));
-            c2 = lowest();
+          const PM_G uint32_t* cr = S.cand + (uint64_t)(b0 + j) * S.cblk * 6;
+          const uint32_t v = lane < nblk * 6 ? cr[lane] : kNone;
+          for (uint32_t k = 0; k < 2 * nblk && c2 == kNone; ++k) {   // uniform
+            const uint32_t h = __builtin_amdgcn_readlane(v, 3 * k);
+            if (h == kNone) { k |= 1; continue; }                    // rest of this block is empty
+            const uint32_t t = __builtin_amdgcn_readlane(v, 3 * k + 1), pp = __builtin_amdgcn_readlane(v, 3 * k + 2);
+            if (c1 == kNone) { c1 = h; t1 = t; p1 = pp; } else { c2 = h; t2 = t; p2 = pp; }
           }
         }
-        if (lane == 0) {
-          const uint32_t t1 = c1 == kNone ? 0 : P.tag[c1], p1 = c1 == kNone ? 0 : P.pp[c1];
-          const uint32_t t2 = c2 == kNone ? 0 : P.tag[c2], p2 = c2 == kNone ? 0 : P.pp[c2];
-          s_c1[j] = c1; s_c2[j] = c2; s_t1[j] = t1; s_p1[j] = p1; s_t2[j] = t2; s_p2[j] = p2;
-        }
+        if (lane == 0) { s_c1[j] = c1; s_c2[j] = c2; s_t1[j] = t1; s_p1[j] = p1; s_t2[j] = t2; s_p2[j] = p2; }
       }
     } else {
-      // The last wave: the request of every sub-query and its chunk's
-      // QueryHistogram, then, in registers, the in-chunk index each would get if
-      // every earlier one succeeds, and the table loads of the values the
-      // re-evaluation in the chain would then need:
-      //   spec_v[k][j] = PRF(tag the refresh of sub k would hand out, chunk of j)
+      // The last wave: the request of every sub-query, its chunk's
+      // QueryHistogram and predicted in-chunk index, and the predicted
+      // re-evaluation values (k_match's records; all loads independent)
       const uint32_t k = lane;
       const uint32_t fq = lane == 0 ? *P.fqn : 0;
       PmSub sub{0, SUB_NONE, 0};
       if (k < n) sub = step_sub(S, b0 + k);
-      const bool real = k < n && sub.kind == SUB_REAL;
-      const uint64_t idx = k < n ? sub.idx : ~0ull;
-      const uint32_t ch = k < n ? (uint32_t)(sub.idx >> lg) : kNone;
-      const uint32_t h0 = (real && sub.idx < P.N) ? P.hist[ch] : 0;
-      if (k < n) { s_kind[k] = sub.kind; s_idx[k] = sub.idx; s_chunk[k] = ch; s_st[k] = kNone; s_hist0[k] = h0; }
+      const bool valid = k < n && sub.kind == SUB_REAL && sub.idx < P.N;
+      const uint32_t h0 = valid ? S.meta[2 * (uint64_t)(b0 + k)] : 0;
+      const uint32_t sg = valid ? S.meta[2 * (uint64_t)(b0 + k) + 1] : kNone;
+      for (uint32_t e0 = 0; e0 < n * n; e0 += 64) {   // spec_v[kk][j], kk < j
+        const uint32_t e = e0 + lane, kk = e / n, j = e % n;
+        if (e < n * n && kk < j) spec_v[kk * kSpecSubs + j] = S.spec[(uint64_t)(b0 + kk) * kSpecSubs + j];
+      }
+      if (k < n) {
+        s_kind[k] = sub.kind; s_idx[k] = sub.idx; s_chunk[k] = (uint32_t)(sub.idx >> lg); s_st[k] = kNone;
+        s_hist0[k] = h0; s_sing[k] = sg;
+      }
       if (lane == 0) s_fqn = fq;
-      bool first = real;                 // not a repeat of an earlier real sub-query
-      for (uint32_t t = 0; t + 1 < n; ++t) {
-        const uint64_t it = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(idx >> 32), t) << 32) |
-                            __builtin_amdgcn_readlane((uint32_t)idx, t);
-        const bool rt = __builtin_amdgcn_readlane(real ? 1u : 0u, t) != 0;
-        if (k > t && rt && it == idx) first = false;
-      }
-      uint32_t ing = h0;
-      for (uint32_t q = 0; q + 1 < n; ++q) {
-        const bool fqq = __builtin_amdgcn_readlane(first ? 1u : 0u, q) != 0;
-        const uint32_t cq = __builtin_amdgcn_readlane(ch, q);
-        if (k > q && fqq && cq == ch) ++ing;
-      }
-      if (k < n) s_sing[k] = ing;
-      for (uint32_t e0 = 0; e0 < n * n; e0 += 64) {   // uniform: every lane joins the shuffles
-        const uint32_t e = e0 + lane, kk = (e / n) & 63, j = e % n;
-        const uint32_t sk = __shfl(ing, kk), ck = __shfl(ch, kk), cj = __shfl(ch, j);
-        const bool rk = __shfl(real ? 1u : 0u, kk) != 0, rj = __shfl(real ? 1u : 0u, j) != 0;
-        if (e < n * n && kk < j && rk && rj && ck < P.SS && cj < P.SS && sk < P.Qpc)
-          spec_v[kk * kSpecSubs + j] = P.tab[(uint64_t)cj * H + P.PH + ck * P.Qpc + sk];
-      }
     }
   } else {
     // --- phase 0: prefetch sub-queries, counters, match bits, tags ------------
