@@ -37,12 +37,12 @@ N, DIM, M, K_TOP, STEP, PARALLEL, F = 1_000_000, 128, 32, 10, 20, 3, 8
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 METRIC = "private queries/sec + PIR-scan HBM GB/s, SIFT1M d=128 at 1/2/4/8 GPUs"
 PREP_KERNELS = ["prep_offsets", "prep_fold", "prep_repl", "l2_rows"]   # timed in the measured region
-STEP_KERNELS = ["hint_match", "resolve", "answer"]                  # timed in the profile window
+STEP_KERNELS = ["step", "hint_match", "resolve", "answer"]          # timed in the profile window
 KERNELS = PREP_KERNELS + STEP_KERNELS
 PROFILE_QUERIES = 8
 SYMBOLS = {"prep_fold": "void pm::k_prep_fold_pipe<4, 1, 4>(pm::PmPart const*, unsigned long const*, "
                         "unsigned long const*, unsigned int, unsigned int, unsigned int, unsigned int)",
-           "answer": "void pm::k_answer<2>(pm::PmStep)", "resolve": "void pm::k_resolve<true>(pm::PmStep)",
+           "answer": "void pm::k_answer<2>(pm::PmStep)", "step": "void pm::k_step<2>(pm::PmStep)", "resolve": "void pm::k_resolve<true>(pm::PmStep)",
            "hint_match": "pm::k_match(pm::PmStep)", "prep_offsets": "pm::k_prep_offsets(pm::PmPart const*)"}
 HOST = ["host_search_knn", "host_knn_init", "host_knn_final", "host_knn_batch", "host_knn_update",
         "host_gvi_parse", "host_batch_query", "host_step_launch", "host_step_wait", "host_step_post"]
@@ -188,10 +188,13 @@ def main():
         fold["note"] = ("fold bytes (hint x chunk entry reads, SURVEY.md §8d) exceed HBM peak because the "
                         "kernel serves them from LDS; 'compulsory' is the DB read once plus the parity writes")
     note = None
-    if dom not in ("answer", "prep_fold"):
+    if dom == "step":
+        note = ("k_step runs hint match, resolution and answer of a batch-PIR step in one launch; "
+                "bytes are the answer's (SURVEY.md §8d: SS*E*8 + 4*SS + 8*E per real/dummy sub-query)")
+    elif dom not in ("answer", "prep_fold"):
         note = (f"dominant kernel by device time is {dom}, a latency-bound sequential chain with no "
                 f"§8(d) byte figure; the roofline shown is the PIR answer kernel's")
-    main_roof = roof(dom) if dom in ("answer", "prep_fold") else roof("answer", note)
+    main_roof = roof(dom, note) if dom in ("answer", "prep_fold", "step") else roof("answer", note)
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "queries/s", "n_gpus": ws,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),

@@ -155,6 +155,7 @@ struct pm_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   int timing = 0;   // 0 off, 1 preprocessing / leaf kernels, 2 also the per-step kernels
+  bool no_fuse = false;      // PM_NO_FUSE=1: the three step kernels even when k_step fits
   bool debug_sync = false;   // PM_DEBUG_SYNC=1: synchronise after every launch (fault triage)
   std::string last_kernel;
   // host-side wall-clock accumulators ("host_*" names in pm_timing_get)
@@ -215,6 +216,8 @@ extern "C" int pm_ctx_create(int device, pm_ctx** out) {
   c->device = device;
   const char* dbg = getenv("PM_DEBUG_SYNC");
   c->debug_sync = dbg && dbg[0] == '1';
+  const char* nf = getenv("PM_NO_FUSE");
+  c->no_fuse = nf && nf[0] == '1';
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e != hipSuccess) { delete c; return fail(PM_EHIP, hipGetErrorString(e)); }
   *out = c;
@@ -276,7 +279,7 @@ struct Engine {
   uint64_t FBN = 0, QMIP = 0, Support = 0, prepCount = 0;
   double prepTime = 0, storage = 0, commOn = 0, commOff = 0;
 
-  DevBuf db, zero16, parts_d, owned_d, tag, pp, parity, ridx, rval, hist, fqn, arena, tab, tabT, done;
+  DevBuf db, zero16, parts_d, owned_d, tag, pp, parity, ridx, rval, hist, fqn, arena, tab, tabT, done, hand;
   std::vector<uint32_t> owned_list;   // owned partitions in order (owned_d holds their PmPart)
   DevBuf qoffs, ans_srv;
   DevBuf subs_d, sb_d, bits, cand, meta, spec, res_d, ans, qvec, stamps;
@@ -418,6 +421,10 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
   CHK(g->tab.reserve(off_tab * 2));
   CHK(g->tabT.reserve(off_tab * 2));
   CHK(g->done.reserve(4 * (3 + 16 * 4096)));
+  HIPCHK(hipMemset(g->done.p, 0, 4 * 3));        // the chain counters start (and end each step) at 0
+  // k_step hand-off counters and flags, one per line: cnt[P], ready[P], mflag[kArgSubs]
+  CHK(g->hand.reserve((2 * g->P + kArgSubs) * 4 * kHandStride));
+  HIPCHK(hipMemset(g->hand.p, 0, (2 * g->P + kArgSubs) * 4 * kHandStride));
   CHK(g->parts_d.reserve(g->P * sizeof(PmPart)));
   CHK(g->owned_d.reserve(std::max<size_t>(1, g->owned_list.size()) * sizeof(PmPart)));
   for (uint64_t i = 0; i < g->P; ++i) {
@@ -549,91 +556,11 @@ static int wait_step(pm_ctx* c, const PmOutHdr* hdr, uint32_t nsub, uint32_t tok
   return 0;
 }
 
-static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
-  auto t_begin = Clock::now();
+// Wait for a step's results (tokens in pinned memory) and update the host
+// mirrors.
+static int wait_and_post(Engine* g, const PmStep& S, uint32_t nsub, Clock::time_point) {
   pm_ctx* c = g->ctx;
-  hipStream_t st = c->stream;
-  const uint32_t nsub = (uint32_t)g->subs.size();
-  if (nsub == 0) return 0;
   const uint64_t E = g->E;
-  const uint32_t words = (g->maxPH + 63) / 64;
-  CHK(g->subs_d.reserve(nsub * sizeof(PmSub)));
-  CHK(g->sb_d.reserve((g->P + 1) * 4));
-  CHK(g->bits.reserve((uint64_t)nsub * words * 8));
-  const uint32_t cblk = pmk::step_match_blocks(g->maxPH);
-  CHK(g->cand.reserve((uint64_t)nsub * cblk * 6 * 4));
-  CHK(g->meta.reserve((uint64_t)nsub * 2 * 4));
-  CHK(g->spec.reserve((uint64_t)nsub * 64 * 2));
-  CHK(g->res_d.reserve(nsub * sizeof(PmRes)));
-  CHK(g->ans.reserve((uint64_t)nsub * E * 8));
-  const size_t dsub = nsub * sizeof(PmSub);
-  CHK(g->desc_h.reserve(dsub + (g->P + 1) * 4));
-  CHK(g->out_h.reserve(nsub * sizeof(PmOutHdr) + (size_t)nsub * E * 8));
-  char* dh = g->desc_h.as<char>();
-  memcpy(dh, g->subs.data(), dsub);
-  memcpy(dh + dsub, g->sb.data(), (g->P + 1) * 4);
-  PmStep S{};
-  S.parts = g->parts_d.as<PmPart>();
-  S.subs_h = (const PmSub*)dh;
-  S.sb_h = (const uint32_t*)(dh + dsub);
-  S.subs = g->subs_d.as<PmSub>();
-  S.sb = g->sb_d.as<uint32_t>();
-  S.bits = g->bits.as<uint64_t>();
-  S.cand = g->cand.as<uint32_t>();
-  S.meta = g->meta.as<uint32_t>();
-  S.spec = g->spec.as<uint16_t>();
-  S.cblk = cblk;
-  S.res = g->res_d.as<PmRes>();
-  S.ans = g->ans.as<uint64_t>();
-  S.done = g->done.as<uint32_t>();
-#ifdef PM_STAMPS
-  CHK(g->stamps.reserve(g->P * 64 * 8));
-  HIPCHK(hipMemsetAsync(g->stamps.p, 0, g->P * 64 * 8, st));
-  S.stamps = g->stamps.as<uint64_t>();
-#endif
-  S.db = g->db.as<uint64_t>();
-  S.q = q_dev;
-  S.hdr_h = g->out_h.as<PmOutHdr>();
-  S.rows_h = (uint64_t*)(g->out_h.as<char>() + nsub * sizeof(PmOutHdr));
-  S.words = words; S.E = (uint32_t)E; S.dim = q_dev ? dim : 0; S.nsub = nsub; S.np = (uint32_t)g->P;
-  S.args_valid = (nsub <= kArgSubs && g->P <= kArgParts) ? 1u : 0u;
-  if (++g->step_token == 0) ++g->step_token;   // 0 never marks a published header
-  S.token = g->step_token;
-  if (S.args_valid) {
-    memcpy(S.subs_a, g->subs.data(), dsub);
-    memcpy(S.sb_a, g->sb.data(), (g->P + 1) * 4);
-  }
-  uint32_t nreal = 0;
-  for (auto& x : g->subs) nreal += x.kind == SUB_REAL;
-  // timing level 2: the step kernels carry their events in their own dispatch packets
-  c->timed_ext("hint_match", (double)nreal * g->maxPH, [&](pmk::PmEvents ev) { pmk::step_match(st, S, g->maxPH, ev); }, 2);
-  uint32_t max_per_part = 0;
-  for (uint64_t p = 0; p < g->P; ++p) max_per_part = std::max(max_per_part, g->sb[p + 1] - g->sb[p]);
-  const bool lds = pmk::step_resolve_lds_ok(g->maxPH, max_per_part);
-  c->timed_ext("resolve", 0, [&](pmk::PmEvents ev) { pmk::step_resolve(st, S, lds, ev); }, 2);
-  if (c->debug_sync) {   // validate every resolution record before k_answer consumes it
-    std::vector<PmRes> rr(nsub);
-    HIPCHK(hipMemcpy(rr.data(), S.res, nsub * sizeof(PmRes), hipMemcpyDeviceToHost));
-    for (uint32_t s = 0; s < nsub; ++s) {
-      const PmPart& d = g->parts[g->subs[s].part].d;
-      const PmRes& r = rr[s];
-      const bool bad = (r.status == ST_OK && (r.hit >= d.PH || r.slot >= d.MaxQ || r.chunk >= d.SS || r.ing >= d.Qpc)) ||
-                       (r.status == ST_CACHED && r.slot >= d.MaxQ) || (r.status == ST_DUP && r.slot >= nsub) ||
-                       (r.status > ST_SKIP) || (r.status > ST_ERANGE && r.status < ST_DUMMY);
-      fprintf(stderr, "[pm] res s=%u part=%u kind=%u idx=%lu -> st=%u hit=%u chunk=%u ing=%u tag=%u pp=%u slot=%u flags=%u%s\n",
-              s, g->subs[s].part, g->subs[s].kind, (unsigned long)g->subs[s].idx, r.status, r.hit, r.chunk, r.ing,
-              r.tag, r.pp, r.slot, r.flags, bad ? "  <-- BAD" : "");
-    }
-  }
-  double ans_bytes = 0;
-  for (auto& x : g->subs)
-    if (x.kind == SUB_REAL || x.kind == SUB_DUMMY) {   // SURVEY.md §8(d): rows*E*8 + 4*SS + 8*E
-      const double ss = g->parts[x.part].d.SS;
-      ans_bytes += ss * E * 8 + 4 * ss + 8.0 * E;
-    }
-  c->timed_ext("answer", ans_bytes, [&](pmk::PmEvents ev) { pmk::step_answer(st, S, ev); }, 2);
-  HIPCHK(hipGetLastError());
-  c->host_add(HT_STEP_LAUNCH, ms_since(t_begin));
   auto t_wait = Clock::now();
   CHK(wait_step(c, S.hdr_h, nsub, S.token, (const char*)S.rows_h, E * 8, g->pf_off,
                 std::min<size_t>(g->pf_len, E * 8 - std::min<size_t>(g->pf_off, E * 8))));
@@ -670,6 +597,130 @@ static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
   }
 #endif
   return 0;
+}
+
+static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
+  auto t_begin = Clock::now();
+  pm_ctx* c = g->ctx;
+  hipStream_t st = c->stream;
+  const uint32_t nsub = (uint32_t)g->subs.size();
+  if (nsub == 0) return 0;
+  const uint64_t E = g->E;
+  const uint32_t words = (g->maxPH + 63) / 64;
+  CHK(g->subs_d.reserve(nsub * sizeof(PmSub)));
+  CHK(g->sb_d.reserve((g->P + 1) * 4));
+  CHK(g->bits.reserve((uint64_t)nsub * words * 8));
+  const uint32_t cblk = pmk::step_match_blocks(g->maxPH);
+  CHK(g->cand.reserve((uint64_t)nsub * cblk * 6 * 4));
+  CHK(g->meta.reserve((uint64_t)nsub * 2 * 4));
+  CHK(g->spec.reserve((uint64_t)nsub * 64 * 4));
+  CHK(g->res_d.reserve(nsub * sizeof(PmRes)));
+  CHK(g->ans.reserve((uint64_t)nsub * E * 8));
+  const size_t dsub = nsub * sizeof(PmSub);
+  CHK(g->desc_h.reserve(dsub + (g->P + 1) * 4));
+  CHK(g->out_h.reserve(nsub * sizeof(PmOutHdr) + (size_t)nsub * E * 8));
+  char* dh = g->desc_h.as<char>();
+  memcpy(dh, g->subs.data(), dsub);
+  memcpy(dh + dsub, g->sb.data(), (g->P + 1) * 4);
+  PmStep S{};
+  S.parts = g->parts_d.as<PmPart>();
+  S.subs_h = (const PmSub*)dh;
+  S.sb_h = (const uint32_t*)(dh + dsub);
+  S.subs = g->subs_d.as<PmSub>();
+  S.sb = g->sb_d.as<uint32_t>();
+  S.bits = g->bits.as<uint64_t>();
+  S.cand = g->cand.as<uint32_t>();
+  S.meta = g->meta.as<uint32_t>();
+  S.spec = g->spec.as<uint32_t>();
+  S.cnt = g->hand.as<uint32_t>();
+  S.ready = g->hand.as<uint32_t>() + g->P * kHandStride;
+  S.mflag = g->hand.as<uint32_t>() + 2 * g->P * kHandStride;
+  S.cblk = cblk;
+  S.res = g->res_d.as<PmRes>();
+  S.ans = g->ans.as<uint64_t>();
+  S.done = g->done.as<uint32_t>();
+#ifdef PM_STAMPS
+  CHK(g->stamps.reserve(g->P * 64 * 8));
+  HIPCHK(hipMemsetAsync(g->stamps.p, 0, g->P * 64 * 8, st));
+  S.stamps = g->stamps.as<uint64_t>();
+#endif
+  S.db = g->db.as<uint64_t>();
+  S.q = q_dev;
+  S.hdr_h = g->out_h.as<PmOutHdr>();
+  S.rows_h = (uint64_t*)(g->out_h.as<char>() + nsub * sizeof(PmOutHdr));
+  S.words = words; S.E = (uint32_t)E; S.dim = q_dev ? dim : 0; S.nsub = nsub; S.np = (uint32_t)g->P;
+  S.args_valid = (nsub <= kArgSubs && g->P <= kArgParts) ? 1u : 0u;
+  if (++g->step_token == 0) ++g->step_token;   // 0 never marks a published header
+  S.token = g->step_token;
+  if (S.args_valid) {
+    memcpy(S.subs_a, g->subs.data(), dsub);
+    memcpy(S.sb_a, g->sb.data(), (g->P + 1) * 4);
+  }
+  uint32_t nreal = 0;
+  for (auto& x : g->subs) nreal += x.kind == SUB_REAL;
+  uint32_t max_per_part = 0;
+  S.np_live = 0;
+  for (uint64_t p = 0; p < g->P; ++p) {
+    const uint32_t n = g->sb[p + 1] - g->sb[p];
+    max_per_part = std::max(max_per_part, n);
+    S.np_live += n > 0;
+  }
+  double ans_bytes = 0;
+  for (auto& x : g->subs)
+    if (x.kind == SUB_REAL || x.kind == SUB_DUMMY) {   // SURVEY.md §8(d): rows*E*8 + 4*SS + 8*E
+      const double ss = g->parts[x.part].d.SS;
+      ans_bytes += ss * E * 8 + 4 * ss + 8.0 * E;
+    }
+  // One launch (k_step) when the step fits it, else the three kernels.
+  // Timing level 2: the kernels carry their events in their own dispatch packets.
+  if (!c->no_fuse && !c->debug_sync && pmk::step_fused_ok(S, g->maxPH, max_per_part)) {
+    S.cblk = 1;   // one match workgroup per sub-query
+#ifdef PM_STEP_STAMPS
+    const uint32_t grid = 2 * nsub + (uint32_t)g->P;
+    CHK(g->stamps.reserve((uint64_t)grid * 4 * 8));
+    HIPCHK(hipMemsetAsync(g->stamps.p, 0, (uint64_t)grid * 4 * 8, st));
+    S.stamps = g->stamps.as<uint64_t>();
+#endif
+    c->timed_ext("step", ans_bytes, [&](pmk::PmEvents ev) { pmk::step_fused(st, S, ev); }, 2);
+    HIPCHK(hipGetLastError());
+    c->host_add(HT_STEP_LAUNCH, ms_since(t_begin));
+    CHK(wait_and_post(g, S, nsub, t_begin));
+#ifdef PM_STEP_STAMPS
+    if (const char* fn = getenv("PM_STAMP_FILE")) {   // append {grid, nsub, cblk, np} + grid x 4 stamps
+      HIPCHK(hipStreamSynchronize(st));
+      std::vector<uint64_t> t((uint64_t)grid * 4);
+      HIPCHK(hipMemcpy(t.data(), g->stamps.p, t.size() * 8, hipMemcpyDeviceToHost));
+      if (FILE* f = fopen(fn, "ab")) {
+        const uint32_t h[4] = {grid, nsub, cblk, (uint32_t)g->P};
+        fwrite(h, 4, 4, f);
+        fwrite(t.data(), 8, t.size(), f);
+        fclose(f);
+      }
+    }
+#endif
+    return 0;
+  }
+  c->timed_ext("hint_match", (double)nreal * g->maxPH, [&](pmk::PmEvents ev) { pmk::step_match(st, S, g->maxPH, ev); }, 2);
+  const bool lds = pmk::step_resolve_lds_ok(g->maxPH, max_per_part);
+  c->timed_ext("resolve", 0, [&](pmk::PmEvents ev) { pmk::step_resolve(st, S, lds, ev); }, 2);
+  if (c->debug_sync) {   // validate every resolution record before k_answer consumes it
+    std::vector<PmRes> rr(nsub);
+    HIPCHK(hipMemcpy(rr.data(), S.res, nsub * sizeof(PmRes), hipMemcpyDeviceToHost));
+    for (uint32_t s = 0; s < nsub; ++s) {
+      const PmPart& d = g->parts[g->subs[s].part].d;
+      const PmRes& r = rr[s];
+      const bool bad = (r.status == ST_OK && (r.hit >= d.PH || r.slot >= d.MaxQ || r.chunk >= d.SS || r.ing >= d.Qpc)) ||
+                       (r.status == ST_CACHED && r.slot >= d.MaxQ) || (r.status == ST_DUP && r.slot >= nsub) ||
+                       (r.status > ST_SKIP) || (r.status > ST_ERANGE && r.status < ST_DUMMY);
+      fprintf(stderr, "[pm] res s=%u part=%u kind=%u idx=%lu -> st=%u hit=%u chunk=%u ing=%u tag=%u pp=%u slot=%u flags=%u%s\n",
+              s, g->subs[s].part, g->subs[s].kind, (unsigned long)g->subs[s].idx, r.status, r.hit, r.chunk, r.ing,
+              r.tag, r.pp, r.slot, r.flags, bad ? "  <-- BAD" : "");
+    }
+  }
+  c->timed_ext("answer", ans_bytes, [&](pmk::PmEvents ev) { pmk::step_answer(st, S, ev); }, 2);
+  HIPCHK(hipGetLastError());
+  c->host_add(HT_STEP_LAUNCH, ms_since(t_begin));
+  return wait_and_post(g, S, nsub, t_begin);
 }
 
 // Append one sub-query of partition p to the step being built.

@@ -100,6 +100,7 @@ struct alignas(16) PmOutHdr {
 #ifndef PM_KARG_SUBS
 #define PM_KARG_SUBS 112
 #endif
+constexpr uint32_t kHandStride = 64;   // u32 words between k_step counters / flags
 constexpr uint32_t kArgSubs = PM_KARG_SUBS, kArgParts = PM_KARG_SUBS > 1 ? 32 : 1;
 struct PmStep {
   const PM_G PmPart* parts;
@@ -112,17 +113,22 @@ struct PmStep {
                                // {hint, tag, program point} x 2 (hint kNone: none)
   PM_G PmRes* res;             // [nsub]
   PM_G uint64_t* ans;          // [nsub][E] raw answers of chained sub-queries
-  PM_G uint32_t* done;         // [0] k_answer arrival counter of chain workgroups,
-                          // [1] chained sub-queries, [2] workgroups involved in chains,
-                          // [3..] chained sub-query list (zeroed by k_match, filled by k_resolve)
+  PM_G uint32_t* done;         // [0] unified chain counter (resolver_count, pm_query.hip),
+                               // [1] chained sub-queries, [3..] their list (filled by the
+                               // resolvers; re-armed by each step's finisher; zero at creation)
   const PM_G uint64_t* db;
   const PM_G float* q;         // search query (device) or null
   PM_G PmOutHdr* hdr_h;        // pinned host outputs
   PM_G uint64_t* rows_h;
   PM_G uint64_t* stamps;       // PM_STAMPS diagnostic builds only: s_memtime per phase
   PM_G uint32_t* meta;         // [nsub][2]: chunk QueryHistogram, predicted in-chunk index
-  PM_G uint16_t* spec;         // [nsub][64]: predicted re-evaluation values (k_match -> k_resolve)
+  PM_G uint32_t* spec;         // [nsub][64]: predicted re-evaluation values (k_match -> k_resolve)
+  PM_G uint32_t* cnt;          // [np][kHandStride] k_step: match workgroups done per partition
+                               // (re-armed by its resolver), one per 256-B line
+  PM_G uint32_t* ready;
+  PM_G uint32_t* mflag;        // [kArgSubs][kHandStride] k_step: token of the step whose match record is out        // [np] k_step: token of the step whose results the resolver published
   uint32_t words, E, dim, nsub, np, cblk;
+  uint32_t np_live;            // partitions with at least one sub-query in this step
   // Small steps ship the descriptor inside the kernel arguments (no PCIe
   // round trip); larger ones use subs_h / sb_h.
   uint32_t args_valid;
@@ -148,6 +154,10 @@ struct PmEvents { hipEvent_t a = nullptr, b = nullptr; };
 void step_match(hipStream_t st, const PmStep& S, uint32_t maxPH, PmEvents ev = {});
 uint32_t step_match_blocks(uint32_t maxPH);   // k_match workgroups per sub-query
 void step_resolve(hipStream_t st, const PmStep& S, bool lds, PmEvents ev = {});
+// k_step: match, resolve and answer in one launch (descriptor in the kernel
+// arguments, <= 64 sub-queries and <= 8192 hints per partition, <= 256 workgroups)
+bool step_fused_ok(const PmStep& S, uint32_t maxPH, uint32_t max_sub_per_part);
+void step_fused(hipStream_t st, const PmStep& S, PmEvents ev = {});
 bool step_resolve_lds_ok(uint32_t maxPH, uint32_t max_sub_per_part);
 void step_answer(hipStream_t st, const PmStep& S, PmEvents ev = {});
 uint32_t step_max_sub_per_part();

@@ -58,6 +58,27 @@ constexpr uint32_t kNone = 0xffffffffu;
 #define STAMP(i) do {} while (0)
 #define STAMP_AT(cond, slot) do { (void)(cond); } while (0)
 #endif
+// PM_STEP_STAMPS diagnostic builds: per k_step workgroup, s_memrealtime
+// (100 MHz, one clock for every XCD) at slots 0 start, 1 after its wait,
+// 2 end, 3 (match: after the counter add)
+#ifdef PM_STEP_STAMPS
+#define TS(i)                                                                     \
+  do {                                                                            \
+    if (threadIdx.x == 0 && S.stamps)                                             \
+      S.stamps[(uint64_t)blockIdx.x * 4 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+// slot 3: where the workgroup ran, XCC_ID << 32 | HW_ID
+#define TS_HWID()                                                                  \
+  do {                                                                             \
+    if (threadIdx.x == 0 && S.stamps)                                              \
+      S.stamps[(uint64_t)blockIdx.x * 4 + 3] =                                     \
+          ((uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |           \
+          (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);                      \
+  } while (0)
+#else
+#define TS(i) do {} while (0)
+#define TS_HWID() do {} while (0)
+#endif
 // slots: k_resolve partition 0: 0..40; k_match block (0,0): 41..47; k_answer block 0: 48..63
 
 
@@ -94,40 +115,51 @@ __device__ __forceinline__ uint32_t desc_sb(const PmStep& S, uint32_t p) {
   return v;
 }
 
-#ifndef PM_MATCH_HPT
-#define PM_MATCH_HPT 4
-#endif
-constexpr int kMatchHPT = PM_MATCH_HPT;   // hints per thread of k_match
+// Stores / loads of data handed between the roles of one fused launch
+// (k_step): write-through sc1 stores drained before a flag or counter, and
+// sc1 loads after the poll (MI355X_MICROARCH.md § inter-workgroup visibility,
+// first row of the sc1 table).  Plain accesses in the separate kernels.
+template <bool SC1> __device__ __forceinline__ void st32(PM_G uint32_t* p, uint32_t v) {
+  if (SC1) __hip_atomic_store((uint32_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+template <bool SC1> __device__ __forceinline__ void st64(PM_G uint64_t* p, uint64_t v) {
+  if (SC1) __hip_atomic_store((uint64_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+template <bool SC1> __device__ __forceinline__ uint32_t ld32(const PM_G uint32_t* p) {
+  if (SC1) return __hip_atomic_load((uint32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return *p;
+}
+template <bool SC1> __device__ __forceinline__ uint64_t ld64(const PM_G uint64_t* p) {
+  if (SC1) return __hip_atomic_load((uint64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return *p;
+}
+template <bool SC1> __device__ __forceinline__ void st_res(PM_G PmRes* p, const PmRes& r) {
+  const uint64_t* w = reinterpret_cast<const uint64_t*>(&r);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) st64<SC1>(reinterpret_cast<PM_G uint64_t*>(p) + i, w[i]);
+}
+template <bool SC1> __device__ __forceinline__ PmRes ld_res(const PM_G PmRes* p) {
+  PmRes r;
+  uint64_t* w = reinterpret_cast<uint64_t*>(&r);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = ld64<SC1>(reinterpret_cast<const PM_G uint64_t*>(p) + i);
+  return r;
+}
 
-__global__ void __launch_bounds__(kBlock) k_match(PmStep S) {
-  const uint32_t s = blockIdx.y;
-  PmSub sub;
-  if (S.args_valid) {
-    sub = S.subs_a[s];
-    __builtin_amdgcn_sched_barrier(0);
-  } else {   // zero-copy read of the host descriptor; staged for the later kernels
-    __shared__ PmSub s_sub;
-    if (threadIdx.x == 0) {
-      s_sub = S.subs_h[s];
-      if (blockIdx.x == 0) S.subs[s] = s_sub;
-    }
-    if (blockIdx.x == 0 && s == 0)
-      for (uint32_t i = threadIdx.x; i <= S.np; i += kBlock) S.sb[i] = S.sb_h[i];
-    __syncthreads();
-    sub = s_sub;
-  }
-  if (blockIdx.x == 0 && s == 0 && threadIdx.x < 3) S.done[threadIdx.x] = 0;
-  const bool stamp_wg = blockIdx.x == 0 && s == 0;
+constexpr uint32_t kMatchHints = 1024;   // hints per match workgroup (any block size)
+
+// One match workgroup (HOT LOOP C): hints [blk*kMatchHints, +kMatchHints) of
+// sub-query s against the state at the start of the step; `sub` is uniform.
+template <int NT, int kMatchHPT, bool SC1>
+__device__ __forceinline__ void match_role(const PmStep& S, uint32_t s, uint32_t blk, PmSub sub,
+                                           uint32_t (&s_cand)[NT / 64][6]) {
+  const bool stamp_wg = blk == 0 && s == 0;
   STAMP_AT(stamp_wg, 41);
-  // the descriptor is workgroup-uniform; say so, so the partition header is
-  // fetched once with scalar loads
-  sub.part = __builtin_amdgcn_readfirstlane(sub.part);
-  sub.kind = __builtin_amdgcn_readfirstlane(sub.kind);
-  sub.idx = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(sub.idx >> 32)) << 32) |
-            __builtin_amdgcn_readfirstlane((uint32_t)sub.idx);
   if (sub.kind != SUB_REAL) return;
   const PmPart P = S.parts[sub.part];
-  const uint32_t base = blockIdx.x * kBlock * kMatchHPT;
+  const uint32_t base = blk * NT * kMatchHPT;
   if (base >= P.PH) return;
   STAMP_AT(stamp_wg, 42);
   const uint32_t mask = P.CS - 1, chunk = (uint32_t)(sub.idx >> P.log2CS),
@@ -136,14 +168,14 @@ __global__ void __launch_bounds__(kBlock) k_match(PmStep S) {
   const bool live = sub.idx < P.N;
   // Block 0 of a sub-query also prepares k_resolve's prediction: its chunk's
   // QueryHistogram now, the rest below (loads overlap the match loads).
-  const bool meta_wg = blockIdx.x == 0;
+  const bool meta_wg = blk == 0;
   const uint32_t h0k = (meta_wg && live) ? P.hist[chunk] : 0;
   // kMatchHPT hints per thread, all loads of a kind issued together
   uint32_t tg[kMatchHPT], pv[kMatchHPT];
   uint16_t rv[kMatchHPT];
 #pragma unroll
   for (int u = 0; u < kMatchHPT; ++u) {
-    const uint32_t h = base + u * kBlock + threadIdx.x;
+    const uint32_t h = base + u * NT + threadIdx.x;
     tg[u] = 0; pv[u] = kDefaultProgramPoint;
     if (live && h < P.PH) { tg[u] = P.tag[h]; pv[u] = P.pp[h]; }
   }
@@ -173,21 +205,21 @@ __global__ void __launch_bounds__(kBlock) k_match(PmStep S) {
       const uint32_t pred = (live && sing < P.Qpc && chunk < P.SS) ? P.PH + chunk * P.Qpc + sing : kNone;
       uint32_t v = kSkip;
       if (lane < pn && lane > k && validt && cht < P.SS && pred != kNone) v = P.tab[(uint64_t)cht * P.H + pred];
-      if (lane < pn) S.spec[(uint64_t)s * kSpecSubs + lane] = (uint16_t)v;
-      if (lane == 0) { S.meta[2 * (uint64_t)s] = h0k; S.meta[2 * (uint64_t)s + 1] = sing; }
+      if (lane < pn) st32<SC1>(S.spec + (uint64_t)s * kSpecSubs + lane, v);
+      if (lane == 0) { st32<SC1>(S.meta + 2 * (uint64_t)s, h0k); st32<SC1>(S.meta + 2 * (uint64_t)s + 1, sing); }
     }
   }
   // match bits, and the block's first two matches with the tag / program
   // point this thread already holds (k_resolve's usual candidates)
-  __shared__ uint32_t s_cand[kBlock / 64][6];
   uint32_t h0 = kNone, t0 = 0, p0 = 0, h1 = kNone, t1 = 0, p1 = 0;   // wave-uniform
 #pragma unroll
   for (int u = 0; u < kMatchHPT; ++u) {
-    const uint32_t h = base + u * kBlock + threadIdx.x;
+    if (base + u * NT >= P.PH) break;
+    const uint32_t h = base + u * NT + threadIdx.x;
     const bool m = live && h < P.PH && rv[u] == offset &&
                    (pv[u] == kDefaultProgramPoint || (pv[u] >> P.log2CS) != chunk);
     uint64_t b = __ballot(m);
-    if (lane == 0 && (h - lane) < P.PH) S.bits[(uint64_t)s * S.words + (h >> 6)] = b;
+    if (lane == 0 && (h - lane) < P.PH) st64<SC1>(S.bits + (uint64_t)s * S.words + (h >> 6), b);
     if (b && h1 == kNone) {   // in hint order within this wave
       const uint32_t l = (uint32_t)__builtin_ctzll(b), hl = h - lane + l;
       const uint32_t tl = __builtin_amdgcn_readlane(tg[u], l), pl = __builtin_amdgcn_readlane(pv[u], l);
@@ -212,7 +244,7 @@ __global__ void __launch_bounds__(kBlock) k_match(PmStep S) {
   __syncthreads();
   if (threadIdx.x == 0) {   // merge the waves' pairs by hint index
     uint32_t o[6] = {kNone, 0, 0, kNone, 0, 0};
-    for (uint32_t w = 0; w < kBlock / 64; ++w)
+    for (uint32_t w = 0; w < NT / 64; ++w)
       for (int k = 0; k < 2; ++k) {
         const uint32_t h = s_cand[w][3 * k];
         if (h < o[0]) {
@@ -222,10 +254,37 @@ __global__ void __launch_bounds__(kBlock) k_match(PmStep S) {
           o[3] = h; o[4] = s_cand[w][3 * k + 1]; o[5] = s_cand[w][3 * k + 2];
         }
       }
-    PM_G uint32_t* dst = S.cand + ((uint64_t)s * S.cblk + blockIdx.x) * 6;
-    for (int i = 0; i < 6; ++i) dst[i] = o[i];
+    PM_G uint32_t* dst = S.cand + ((uint64_t)s * S.cblk + blk) * 6;
+    for (int i = 0; i < 6; ++i) st32<SC1>(dst + i, o[i]);
   }
   STAMP_AT(stamp_wg, 43);
+}
+
+__global__ void __launch_bounds__(kBlock) k_match(PmStep S) {
+  __shared__ uint32_t s_cand[kBlock / 64][6];
+  const uint32_t s = blockIdx.y;
+  PmSub sub;
+  if (S.args_valid) {
+    sub = S.subs_a[s];
+    __builtin_amdgcn_sched_barrier(0);
+  } else {   // zero-copy read of the host descriptor; staged for the later kernels
+    __shared__ PmSub s_sub;
+    if (threadIdx.x == 0) {
+      s_sub = S.subs_h[s];
+      if (blockIdx.x == 0) S.subs[s] = s_sub;
+    }
+    if (blockIdx.x == 0 && s == 0)
+      for (uint32_t i = threadIdx.x; i <= S.np; i += kBlock) S.sb[i] = S.sb_h[i];
+    __syncthreads();
+    sub = s_sub;
+  }
+  // the descriptor is workgroup-uniform; say so, so the partition header is
+  // fetched once with scalar loads
+  sub.part = __builtin_amdgcn_readfirstlane(sub.part);
+  sub.kind = __builtin_amdgcn_readfirstlane(sub.kind);
+  sub.idx = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(sub.idx >> 32)) << 32) |
+            __builtin_amdgcn_readfirstlane((uint32_t)sub.idx);
+  match_role<kBlock, kMatchHints / kBlock, false>(S, s, blockIdx.x, sub, s_cand);
 }
 
 // First set bit at position >= start in a sub-query's match bitmask (one wave).
@@ -234,6 +293,24 @@ __device__ __forceinline__ uint32_t find_next(const uint64_t* __restrict__ bw, u
   for (uint32_t w0 = start >> 6; w0 < nw; w0 += 64) {
     const uint32_t w = w0 + lane;
     uint64_t v = w < nw ? bw[w] : 0;
+    if (w == (start >> 6)) v &= ~0ull << (start & 63);
+    const uint64_t m = __ballot(v != 0);
+    if (m) {
+      const uint32_t fl = (uint32_t)__builtin_ctzll(m);
+      const uint64_t vf = __shfl(v, fl);
+      return (w0 + fl) * 64 + (uint32_t)__builtin_ctzll(vf);
+    }
+  }
+  return kNone;
+}
+
+// The same over a global bitmask (sc1 loads when handed over inside k_step).
+template <bool SC1>
+__device__ __forceinline__ uint32_t find_next_g(const PM_G uint64_t* bw, uint32_t nw, uint32_t start) {
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t w0 = start >> 6; w0 < nw; w0 += 64) {
+    const uint32_t w = w0 + lane;
+    uint64_t v = w < nw ? ld64<SC1>(bw + w) : 0;
     if (w == (start >> 6)) v &= ~0ull << (start & 63);
     const uint64_t m = __ballot(v != 0);
     if (m) {
@@ -255,21 +332,57 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t x) {
 
 constexpr int kMaxSubPerPart = 256;
 
-template <bool LDS>
-__global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
-  __shared__ uint64_t s_idx[kMaxSubPerPart];
-  __shared__ uint32_t s_kind[kMaxSubPerPart], s_chunk[kMaxSubPerPart], s_st[kMaxSubPerPart],
-      s_hist0[kMaxSubPerPart], s_c1[kMaxSubPerPart], s_c2[kMaxSubPerPart], s_t1[kMaxSubPerPart],
-      s_p1[kMaxSubPerPart], s_t2[kMaxSubPerPart], s_p2[kMaxSubPerPart], s_sing[kMaxSubPerPart];
-  __shared__ uint32_t m_h[kMaxSubPerPart], m_tag[kMaxSubPerPart], m_pp[kMaxSubPerPart],
-      m_sub[kMaxSubPerPart], m_pt[kMaxSubPerPart];
-  __shared__ uint32_t s_fqn, s_chain[kMaxSubPerPart];
-  __shared__ PmRes s_res[kMaxSubPerPart];
-  // fast path staging: match bits, tags / program points, speculative re-evaluation values
-  __shared__ uint64_t bits_l[LDS ? kLdsBitWords : 1];
-  __shared__ uint32_t tag_l[LDS ? kLdsPH : 1], pp_l[LDS ? kLdsPH : 1];
-  __shared__ uint16_t spec_v[LDS ? kSpecSubs * kSpecSubs : 1];
-  const uint32_t p = blockIdx.x;
+// Resolver LDS.  MODE 0: state read from global memory (large partitions);
+// 1: the fast prologue (match records) or, where that does not fit, the
+// staged one; 2: the fast prologue only (k_step: n <= kSpecSubs sub-queries,
+// nw <= 128 match words, one match record per sub-query).
+template <int MODE>
+struct ResolveLds {
+  static constexpr int NS = MODE == 2 ? kSpecSubs : kMaxSubPerPart;
+  static constexpr bool STG = MODE == 1;
+  static constexpr uint32_t NB = kLdsBitWords;
+  uint64_t s_idx[NS];
+  uint32_t s_kind[NS], s_chunk[NS], s_st[NS], s_hist0[NS], s_c1[NS], s_c2[NS], s_t1[NS],
+      s_p1[NS], s_t2[NS], s_p2[NS], s_sing[NS];
+  uint32_t m_h[NS], m_tag[NS], m_pp[NS], m_sub[NS], m_pt[NS];
+  uint32_t s_fqn, fin, s_chain[NS];
+  PmRes s_res[NS];
+  // staging: match bits, tags / program points; speculative re-evaluation values
+  uint64_t bits_l[STG ? NB : 1];
+  uint32_t tag_l[STG ? kLdsPH : 1], pp_l[STG ? kLdsPH : 1];
+  uint16_t spec_v[MODE != 0 ? kSpecSubs * kSpecSubs : 1];
+};
+
+// Unified chain counter done[0]: each live partition's resolver adds
+// 1 - (its workgroups involved in refresh chains), each involved answer
+// workgroup adds 1 once its refresh is released.  Every answer arrival
+// follows its own resolver's add, so the running sum reaches np_live exactly
+// at the last add of the step, whichever role makes it: that one decodes the
+// chain list and re-arms the counters.  Called by wave 0 of a resolver.
+template <class LdsT>
+__device__ __forceinline__ void resolver_count(const PmStep& S, LdsT& L, uint32_t nchain, uint32_t cadd) {
+  if ((threadIdx.x & 63) != 0) return;
+  if (nchain) {   // chain list and results must be visible to the finisher
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  }
+  const uint32_t d = 1u - cadd;
+  const uint32_t prev = __hip_atomic_fetch_add(&S.done[0], d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  L.fin = (prev + d == S.np_live) ? 1u : 0u;
+}
+
+// One partition's share of Client.Query for every sub-query of the step, in
+// order (wave 0 runs the chain; the other waves only help the prologue and
+// return early).  L.fin: this workgroup made the step's last chain-count add.
+template <int MODE, int NT, bool SC1>
+__device__ __forceinline__ void resolve_role(const PmStep& S, uint32_t p, ResolveLds<MODE>& L) {
+  constexpr bool LDS = MODE != 0;
+  auto& s_idx = L.s_idx; auto& s_kind = L.s_kind; auto& s_chunk = L.s_chunk; auto& s_st = L.s_st;
+  auto& s_hist0 = L.s_hist0; auto& s_c1 = L.s_c1; auto& s_c2 = L.s_c2; auto& s_t1 = L.s_t1;
+  auto& s_p1 = L.s_p1; auto& s_t2 = L.s_t2; auto& s_p2 = L.s_p2; auto& s_sing = L.s_sing;
+  auto& m_h = L.m_h; auto& m_tag = L.m_tag; auto& m_pp = L.m_pp; auto& m_sub = L.m_sub; auto& m_pt = L.m_pt;
+  auto& s_fqn = L.s_fqn; auto& s_chain = L.s_chain; auto& s_res = L.s_res;
+  auto& bits_l = L.bits_l; auto& tag_l = L.tag_l; auto& pp_l = L.pp_l; auto& spec_v = L.spec_v;
   const PmPart P = S.parts[p];   // a copy: the chain loop's memory clobbers must not reload it
   const uint32_t b0 = step_sb(S, p), n = step_sb(S, p + 1) - b0;
   if (n == 0) return;
@@ -279,27 +392,28 @@ __global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
   const uint32_t wave = tid >> 6, lane = tid & 63;
   // fast prologue (n <= 64 sub-queries, the usual shape): no staging of tags,
   // program points or match bits; two independent chains of two round trips
-  const bool fast = LDS && n <= kSpecSubs && nw <= 128;
+  const bool fast = MODE == 2 || (MODE == 1 && n <= kSpecSubs && nw <= 128);
   // match bits, tags and program points: LDS-staged by the staged prologue,
   // read from global memory on the (rare) paths of the fast one that need them
-  const bool staged = LDS && !fast;
-  auto bits_of = [&](uint32_t j) -> const uint64_t* {
-    return staged ? bits_l + (uint64_t)j * nw : (const uint64_t*)(S.bits + (uint64_t)(b0 + j) * S.words);
+  const bool staged = MODE == 1 && !fast;
+  auto find_bits = [&](uint32_t j, uint32_t start) -> uint32_t {
+    if (staged) return find_next(bits_l + (uint64_t)j * nw, nw, start);
+    return find_next_g<SC1>(S.bits + (uint64_t)(b0 + j) * S.words, nw, start);
   };
   auto tag_of = [&](uint32_t h) -> uint32_t { return staged ? tag_l[h] : P.tag[h]; };
   auto pp_of = [&](uint32_t h) -> uint32_t { return staged ? pp_l[h] : P.pp[h]; };
   if (fast) {
-    constexpr uint32_t NFW = kBlock / 64 - 1;   // candidate waves; the last wave predicts
+    constexpr uint32_t NFW = NT / 64 - 1;   // candidate waves; the last wave predicts
     if (wave < NFW) {
       // first two stale candidates of each real sub-query, with their tag and
       // program point: the per-block records k_match wrote (blocks in hint order)
-      const uint32_t nblk = (P.PH + kBlock * kMatchHPT - 1) / (kBlock * kMatchHPT);
+      const uint32_t nblk = MODE == 2 ? 1u : (P.PH + kMatchHints - 1) / kMatchHints;
       for (uint32_t j = wave; j < n; j += NFW) {
         const PmSub sub = step_sub(S, b0 + j);
         uint32_t c1 = kNone, c2 = kNone, t1 = 0, p1 = 0, t2 = 0, p2 = 0;
         if (sub.kind == SUB_REAL && sub.idx < P.N) {
           const PM_G uint32_t* cr = S.cand + (uint64_t)(b0 + j) * S.cblk * 6;
-          const uint32_t v = lane < nblk * 6 ? cr[lane] : kNone;
+          const uint32_t v = lane < nblk * 6 ? ld32<SC1>(cr + lane) : kNone;
           for (uint32_t k = 0; k < 2 * nblk && c2 == kNone; ++k) {   // uniform
             const uint32_t h = __builtin_amdgcn_readlane(v, 3 * k);
             if (h == kNone) { k |= 1; continue; }                    // rest of this block is empty
@@ -318,11 +432,11 @@ __global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
       PmSub sub{0, SUB_NONE, 0};
       if (k < n) sub = step_sub(S, b0 + k);
       const bool valid = k < n && sub.kind == SUB_REAL && sub.idx < P.N;
-      const uint32_t h0 = valid ? S.meta[2 * (uint64_t)(b0 + k)] : 0;
-      const uint32_t sg = valid ? S.meta[2 * (uint64_t)(b0 + k) + 1] : kNone;
+      const uint32_t h0 = valid ? ld32<SC1>(S.meta + 2 * (uint64_t)(b0 + k)) : 0;
+      const uint32_t sg = valid ? ld32<SC1>(S.meta + 2 * (uint64_t)(b0 + k) + 1) : kNone;
       for (uint32_t e0 = 0; e0 < n * n; e0 += 64) {   // spec_v[kk][j], kk < j
         const uint32_t e = e0 + lane, kk = e / n, j = e % n;
-        if (e < n * n && kk < j) spec_v[kk * kSpecSubs + j] = S.spec[(uint64_t)(b0 + kk) * kSpecSubs + j];
+        if (e < n * n && kk < j) spec_v[kk * kSpecSubs + j] = (uint16_t)ld32<SC1>(S.spec + (uint64_t)(b0 + kk) * kSpecSubs + j);
       }
       if (k < n) {
         s_kind[k] = sub.kind; s_idx[k] = sub.idx; s_chunk[k] = (uint32_t)(sub.idx >> lg); s_st[k] = kNone;
@@ -330,7 +444,7 @@ __global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
       }
       if (lane == 0) s_fqn = fq;
     }
-  } else {
+  } else if constexpr (MODE != 2) {
     // --- phase 0: prefetch sub-queries, counters, match bits, tags ------------
     // Every global load of the staging is issued before the first LDS store:
     // the kernel is latency-bound, so one round trip instead of one per item.
@@ -344,13 +458,13 @@ __global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
       const uint32_t nb = LDS ? n * nw : 0, ph4 = LDS ? P.PH / 4 : 0;
   #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        const uint32_t j = tid + u * kBlock;
+        const uint32_t j = tid + u * NT;
         if (j < n) sv[u] = step_sub(S, b0 + j);
       }
   #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const uint32_t i = tid + u * kBlock;
-        if (i < nb) bv[u] = S.bits[(uint64_t)(b0 + i / nw) * S.words + (i % nw)];
+        const uint32_t i = tid + u * NT;
+        if (i < nb) bv[u] = ld64<SC1>(S.bits + (uint64_t)(b0 + i / nw) * S.words + (i % nw));
         if (i < ph4) {
           tv[u] = reinterpret_cast<const PM_G u32x4*>(P.tag)[i];
           pv[u] = reinterpret_cast<const PM_G u32x4*>(P.pp)[i];
@@ -359,17 +473,17 @@ __global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
       const uint32_t fq = tid == 0 ? *P.fqn : 0;
   #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        const uint32_t j = tid + u * kBlock;
+        const uint32_t j = tid + u * NT;
         hv[u] = (j < n && sv[u].kind == SUB_REAL && sv[u].idx < P.N) ? P.hist[(uint32_t)(sv[u].idx >> lg)] : 0;
       }
-      for (uint32_t j = tid + 2 * kBlock; j < n; j += kBlock) {   // n > 512: rare
+      for (uint32_t j = tid + 2 * NT; j < n; j += NT) {   // n > 512: rare
         const PmSub sub = step_sub(S, b0 + j);
         s_kind[j] = sub.kind; s_idx[j] = sub.idx; s_chunk[j] = (uint32_t)(sub.idx >> lg); s_st[j] = kNone;
         s_hist0[j] = (sub.kind == SUB_REAL && sub.idx < P.N) ? P.hist[(uint32_t)(sub.idx >> lg)] : 0;
       }
   #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        const uint32_t j = tid + u * kBlock;
+        const uint32_t j = tid + u * NT;
         if (j < n) {
           s_kind[j] = sv[u].kind; s_idx[j] = sv[u].idx; s_chunk[j] = (uint32_t)(sv[u].idx >> lg);
           s_hist0[j] = hv[u]; s_st[j] = kNone;
@@ -377,7 +491,7 @@ __global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
       }
   #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const uint32_t i = tid + u * kBlock;
+        const uint32_t i = tid + u * NT;
         if (i < nb) bits_l[i] = bv[u];
         if (i < ph4) {
           reinterpret_cast<u32x4*>(tag_l)[i] = tv[u];
@@ -390,18 +504,17 @@ __global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
     STAMP(1);
     // --- phase 1: first two stale candidates per real sub-query + their state;
     //     speculative in-group index of every sub-query (all earlier succeed)
-    for (uint32_t j = wave; j < n; j += kBlock / 64) {
+    for (uint32_t j = wave; j < n; j += NT / 64) {
       if (s_kind[j] != SUB_REAL) continue;
-      const uint64_t* bw = bits_of(j);
-      const uint32_t c1 = find_next(bw, nw, 0);
-      const uint32_t c2 = c1 == kNone ? kNone : find_next(bw, nw, c1 + 1);
+      const uint32_t c1 = find_bits(j, 0);
+      const uint32_t c2 = c1 == kNone ? kNone : find_bits(j, c1 + 1);
       if (lane == 0) {
         s_c1[j] = c1; s_c2[j] = c2;
         s_t1[j] = c1 == kNone ? 0 : tag_of(c1); s_p1[j] = c1 == kNone ? 0 : pp_of(c1);
         s_t2[j] = c2 == kNone ? 0 : tag_of(c2); s_p2[j] = c2 == kNone ? 0 : pp_of(c2);
       }
     }
-    if (LDS && n <= kSpecSubs && wave == kBlock / 64 - 1) {
+    if (LDS && n <= kSpecSubs && wave == NT / 64 - 1) {
       // The last wave (the one with the least candidate work above) predicts, in
       // registers, the in-chunk index each sub-query would get if every earlier
       // one succeeds, and issues the table loads of the values the re-evaluation
@@ -548,7 +661,7 @@ __global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
           uint32_t c = rl(c1, j), which = 1;
           while (c != kNone && __ballot(k < nmod && mh == c)) {
             if (which == 1) { c = rl(c2, j); which = 2; }
-            else { c = find_next(bits_of(j), nw, c + 1); which = 3; }
+            else { c = find_bits(j, c + 1); which = 3; }
           }
           // hints refreshed earlier in this step, with their current tag / program point
           uint32_t cand = kNone;
@@ -598,8 +711,8 @@ __global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
     // --- flush (one writer per result / hint / chunk) -----------------------
     if (in) {
       const bool ok = st == ST_OK;
-      S.res[b0 + k] = PmRes{st, ok ? rhit : 0u, ok ? ch : 0u, ok ? ring : 0u, ok ? rtag : 0u,
-                            ok ? rpp : 0u, (ok || st == ST_DUP || st == ST_CACHED) ? rslot : 0u, ok ? rfl : 0u};
+      st_res<SC1>(S.res + b0 + k, PmRes{st, ok ? rhit : 0u, ok ? ch : 0u, ok ? ring : 0u, ok ? rtag : 0u,
+                            ok ? rpp : 0u, (ok || st == ST_DUP || st == ST_CACHED) ? rslot : 0u, ok ? rfl : 0u});
     }
     if (k < nmod) { P.tag[mh] = mt; P.pp[mh] = mp; }
     bool last = in && st == ST_OK;   // QueryHistogram: the last success per chunk writes
@@ -608,17 +721,16 @@ __global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
     if (last) P.hist[ch] = ring + 1;
     if (nchain) {   // this partition's chained sub-queries, contiguous and in order
       uint32_t pos = 0;
-      if (k == 0) {
-        pos = atomicAdd(&S.done[1], nchain);
-        atomicAdd(&S.done[2], cadd);
-      }
+      if (k == 0) pos = atomicAdd(&S.done[1], nchain);
       pos = __builtin_amdgcn_readfirstlane(pos);
       if (k < nchain) S.done[3 + pos + k] = cl;
     }
     if (k == 0) *P.fqn = fqn;
+    resolver_count(S, L, nchain, cadd);
     STAMP(40);
     return;
   }
+  if constexpr (MODE != 2) {
   // --- phase 2 (n > 64): the sequential chain of Client.Query calls, on wave 0
   // The chain state lives in plain LDS arrays: lane 0 writes, every lane of the
   // same wave reads in a later iteration (LDS instructions of one wave complete
@@ -669,7 +781,7 @@ __global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
             mod |= __ballot(k0 + lane < nmod && m_h[k0 + lane] == c) != 0;
           if (!mod) break;
           if (which == 1) { c = s_c2[j]; which = 2; }
-          else { c = find_next(bits_of(j), nw, c + 1); which = 3; }
+          else { c = find_bits(j, c + 1); which = 3; }
         }
         // hints refreshed earlier in this step, with their current tag / program point
         uint32_t bm = kNone, bk = kNone;
@@ -730,7 +842,7 @@ __global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
     if (j < 32) STAMP(4 + j);
   }
   // --- flush (pir.go:460-470 refresh; one writer per hint / chunk) ----------
-  for (uint32_t k = lane; k < n; k += 64) S.res[b0 + k] = s_res[k];
+  for (uint32_t k = lane; k < n; k += 64) st_res<SC1>(S.res + b0 + k, s_res[k]);
   for (uint32_t k = lane; k < nmod; k += 64) {
     P.tag[m_h[k]] = m_tag[k];
     P.pp[m_h[k]] = m_pp[k];
@@ -744,15 +856,25 @@ __global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
   }
   if (nchain) {   // this partition's chained sub-queries, contiguous and in order
     uint32_t pos = 0;
-    if (lane == 0) {
-      pos = atomicAdd(&S.done[1], nchain);
-      atomicAdd(&S.done[2], cadd);
-    }
+    if (lane == 0) pos = atomicAdd(&S.done[1], nchain);
     pos = __builtin_amdgcn_readfirstlane(pos);
     for (uint32_t k = lane; k < nchain; k += 64) S.done[3 + pos + k] = s_chain[k];
   }
   if (lane == 0) *P.fqn = fqn;
+  resolver_count(S, L, nchain, cadd);
   STAMP(40);
+  }
+}
+
+template <bool LDS>
+__global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
+  __shared__ ResolveLds<LDS ? 1 : 0> L;
+  const uint32_t p = blockIdx.x;
+  if (step_sb(S, p + 1) == step_sb(S, p)) return;
+  resolve_role<LDS ? 1 : 0, kBlock, false>(S, p, L);
+  __syncthreads();
+  // last add here: no answer workgroup is involved in a chain, nothing to decode
+  if (L.fin && threadIdx.x == 0) { S.done[0] = 0; S.done[1] = 0; }
 }
 
 // L2Dist of the first `dim` floats of an LDS row against q (device), one
@@ -827,103 +949,183 @@ __device__ void decode_chained(const PmStep& S, uint32_t s, RowBuf& row) {
   __syncthreads();
 }
 
-template <int W>
-__global__ void __launch_bounds__(kAnsBlock) k_answer(PmStep S) {
-  __shared__ uint32_t qo[kMaxSSLds];
-  __shared__ uint64_t red[kAnsBlock * 2];
-  __shared__ __attribute__((aligned(16))) RowBuf row;
-  __shared__ uint32_t s_last;
-  const uint32_t s = blockIdx.x, tid = threadIdx.x;
+// The finisher of a step (see resolver_count), after its acquire: decodes the
+// chained sub-queries in list order and re-arms the counters.  Whole workgroup.
+__device__ void finish_step(const PmStep& S, RowBuf& row) {
+  const uint32_t nchain = S.done[1];
+  for (uint32_t k = 0; k < nchain; ++k) decode_chained(S, S.done[3 + k], row);
+  if (threadIdx.x == 0) { S.done[0] = 0; S.done[1] = 0; }
+}
+
+template <int NT>
+struct AnswerLds {
+  uint32_t qo[kMaxSSLds];
+  uint64_t red[NT * 2];
+  __attribute__((aligned(16))) RowBuf row;
+  uint32_t s_last;
+};
+
+// What the answer of sub-query s needs from its resolution: query set,
+// gathered row, decode operands.
+__device__ __forceinline__ uint32_t answer_mode(const PmRes& r) {
+  return r.status == ST_OK ? ((r.flags & 1u) ? A_CHAINED : A_FINAL)
+       : r.status == ST_CACHED ? A_CACHED
+       : r.status == ST_DUMMY ? A_DUMMY : A_ZERO;
+}
+
+// One sub-query's answer (HOT LOOPs D + E, decode, outputs).  SC1: inside
+// k_step.  There the answer starts before its partition's resolver is done:
+// a dummy sub-query's set does not depend on the resolution at all, and a
+// real one's usually is the one its first stale candidate gives (hint c1 with
+// its tag / program point, the in-chunk index predicted from the chunk's
+// QueryHistogram — its match workgroup's record).  The set is expanded, the
+// rows gathered and the decode operands loaded for that guess while the
+// resolver runs; its result then either equals the guess in every field the
+// answer reads (kept) or the work is redone for the actual result.
+template <int W, bool SC1, int NT>
+__device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, AnswerLds<NT>& L) {
+  uint32_t* const qo = L.qo;
+  uint64_t* const red = L.red;
+  RowBuf& row = L.row;
+  const uint32_t tid = threadIdx.x;
   const uint32_t E = S.E, EX = E & ~3u, NSEG = EX / W;
   const PmSub sub = step_sub(S, s);
-  const PmRes r = S.res[s];
   const PmPart& P = S.parts[sub.part];
   uint64_t* const orow = S.rows_h + (uint64_t)s * E;
-  const bool stamp_wg = blockIdx.x == 0;
+  const bool stamp_wg = s == 0;
   STAMP_AT(stamp_wg, 48);
-  const uint32_t mode = r.status == ST_OK ? ((r.flags & 1u) ? A_CHAINED : A_FINAL)
-                      : r.status == ST_CACHED ? A_CACHED
-                      : r.status == ST_DUMMY ? A_DUMMY : A_ZERO;
   const uint32_t mask = P.CS - 1, lg = P.log2CS;
-  // decode operands: independent of the gather, issued first (pir.go:450-468)
+  uint64_t e_rv = 0, e_bp = 0, e_pp = 0;
+  // set expansion + gather into row.w[0..EX) and the decode operands for (r, mode)
+  auto gather = [&](const PmRes& r, uint32_t mode) {
+    // decode operands: independent of the gather, issued first (pir.go:450-468)
+    const uint64_t dslot = (uint64_t)r.chunk * P.Qpc + r.ing;
+    if (mode == A_FINAL && tid < E) {
+      e_rv = P.rval[dslot * E + tid];
+      e_bp = P.parity[((uint64_t)P.PH + dslot) * E + tid];
+      e_pp = P.parity[(uint64_t)r.hit * E + tid];
+    }
+    // ---- query set (pir.go:363-371 dummy; :424-444 real) -------------------
+    if (mode == A_FINAL || mode == A_CHAINED) {
+      const uint32_t pchunk = r.pp != kDefaultProgramPoint ? (r.pp >> lg) : kNone;
+      const uint16_t* trow = P.tabT + (uint64_t)r.tag * P.SS;
+      for (uint32_t i = tid; i < P.SS; i += NT) {
+        uint32_t o = trow[i];
+        if (i == pchunk) o = r.pp & mask;
+        if (i == r.chunk) o = P.ridx[r.chunk * P.Qpc + r.ing] & mask;
+        qo[i] = o;
+      }
+    } else if (mode == A_DUMMY) {
+      for (uint32_t i = tid; i < P.SS; i += NT)
+        qo[i] = (uint32_t)(hash4(P.seed, DOM_DUMMY, P.idx, sub.idx, i) & mask);
+    }
+    STAMP_AT(stamp_wg && mode == A_FINAL, 49);
+    __syncthreads();
+    STAMP_AT(stamp_wg, 50);
+    // ---- server XOR gather (HOT LOOP E) into row.w[0..EX) ------------------
+    if (mode == A_FINAL || mode == A_CHAINED || mode == A_DUMMY) {
+      const PM_G uint64_t* base = S.db + P.row0 * E;
+      for (uint32_t seg0 = 0; seg0 < NSEG; seg0 += NT) {
+        const uint32_t nseg = min(NSEG - seg0, (uint32_t)NT);
+        const uint32_t nsl = NT / nseg;
+        const uint32_t sl = tid / nseg, seg = seg0 + tid % nseg;
+        uint64_t a0 = 0, a1 = 0;
+        if (sl < nsl) {
+          // every row load of a batch is issued before the first is consumed: the
+          // gather is one HBM round trip per kG rows a thread reads, not one per 4
+          constexpr int kG = 16;
+          typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+          for (uint32_t i0 = sl; i0 < P.SS; i0 += kG * nsl) {
+            uint64_t rr[kG];
+#pragma unroll
+            for (int u = 0; u < kG; ++u) {
+              const uint32_t i = i0 + u * nsl;
+              rr[u] = i < P.SS ? (uint64_t)i * P.CS + qo[i] : P.N;
+            }
+            u64x2 x[kG];
+#pragma unroll
+            for (int u = 0; u < kG; ++u) {
+              x[u] = u64x2{0, 0};
+              if (rr[u] < P.N) {
+                const PM_G uint64_t* q = base + rr[u] * E + (uint64_t)seg * W;
+                if (W == 2) x[u] = *reinterpret_cast<const PM_G u64x2*>(q);
+                else x[u].x = *q;
+              }
+            }
+#pragma unroll
+            for (int u = 0; u < kG; ++u) { a0 ^= x[u].x; a1 ^= x[u].y; }
+          }
+        }
+        red[tid * 2] = a0;
+        red[tid * 2 + 1] = a1;
+        __syncthreads();
+        if (tid < nseg) {
+          uint64_t x0 = 0, x1 = 0;
+          for (uint32_t k = 0; k < nsl; ++k) {
+            x0 ^= red[(k * nseg + tid) * 2];
+            x1 ^= red[(k * nseg + tid) * 2 + 1];
+          }
+          row.w[seg * W] = x0;
+          if (W == 2) row.w[seg * W + 1] = x1;
+        }
+        __syncthreads();
+      }
+    }
+  };
+  PmRes r;
+  uint32_t mode;
+  if (SC1) {
+    // ---- the guess (see above), from this sub-query's match record ---------
+    PmRes g{kNone, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t gmode = kNone;
+    if (sub.kind == SUB_DUMMY) {
+      g.status = ST_DUMMY;
+      gmode = A_DUMMY;
+    } else if (sub.kind == SUB_REAL && sub.idx < P.N) {
+      if (tid == 0)
+        while (ld32<true>(S.mflag + s * kHandStride) != S.token) __builtin_amdgcn_s_sleep(1);
+      __syncthreads();
+      const PM_G uint32_t* cr = S.cand + (uint64_t)s * 6;   // one record per sub-query (cblk 1)
+      const uint32_t c1 = __builtin_amdgcn_readfirstlane(ld32<true>(cr));
+      const uint32_t t1 = __builtin_amdgcn_readfirstlane(ld32<true>(cr + 1));
+      const uint32_t p1 = __builtin_amdgcn_readfirstlane(ld32<true>(cr + 2));
+      const uint32_t sg = __builtin_amdgcn_readfirstlane(ld32<true>(S.meta + 2 * (uint64_t)s + 1));
+      const uint32_t ch = (uint32_t)(sub.idx >> lg);
+      if (c1 != kNone && sg < P.Qpc && ch < P.SS) {
+        g = PmRes{ST_OK, c1, ch, sg, t1, p1, 0, 0};
+        gmode = A_FINAL;
+      }
+    }
+    if (gmode != kNone) gather(g, gmode);
+    TS(1);
+    // ---- the resolver's results of this step (sc1 poll, then sc1 loads) ----
+    if (tid == 0)
+      while (ld32<true>(S.ready + sub.part * kHandStride) != S.token) __builtin_amdgcn_s_sleep(1);
+    __syncthreads();
+    r = ld_res<true>(S.res + s);
+    mode = answer_mode(r);
+    const bool kept = mode == gmode &&
+                      (mode == A_DUMMY || (r.hit == g.hit && r.chunk == g.chunk && r.ing == g.ing &&
+                                           r.tag == g.tag && r.pp == g.pp));
+    if (!kept) {
+      e_rv = e_bp = e_pp = 0;
+      gather(r, mode);
+    }
+  } else {
+    r = ld_res<false>(S.res + s);
+    mode = answer_mode(r);
+    gather(r, mode);
+  }
   const uint64_t dslot = (uint64_t)r.chunk * P.Qpc + r.ing;
   const uint64_t* rv = P.rval + dslot * E;
   const uint64_t* bp = P.parity + ((uint64_t)P.PH + dslot) * E;
   uint64_t* pp = P.parity + (uint64_t)r.hit * E;
-  uint64_t e_rv = 0, e_bp = 0, e_pp = 0;
-  if (mode == A_FINAL && tid < E) { e_rv = rv[tid]; e_bp = bp[tid]; e_pp = pp[tid]; }
-  // ---- query set (pir.go:363-371 dummy; :424-444 real) -------------------
-  if (mode == A_FINAL || mode == A_CHAINED) {
-    const uint32_t pchunk = r.pp != kDefaultProgramPoint ? (r.pp >> lg) : kNone;
-    const uint16_t* trow = P.tabT + (uint64_t)r.tag * P.SS;
-    for (uint32_t i = tid; i < P.SS; i += kAnsBlock) {
-      uint32_t o = trow[i];
-      if (i == pchunk) o = r.pp & mask;
-      if (i == r.chunk) o = P.ridx[r.chunk * P.Qpc + r.ing] & mask;
-      qo[i] = o;
-    }
-  } else if (mode == A_DUMMY) {
-    for (uint32_t i = tid; i < P.SS; i += kAnsBlock)
-      qo[i] = (uint32_t)(hash4(P.seed, DOM_DUMMY, P.idx, sub.idx, i) & mask);
-  }
-  STAMP_AT(stamp_wg && mode == A_FINAL, 49);
-  __syncthreads();
-  STAMP_AT(stamp_wg, 50);
-  // ---- server XOR gather (HOT LOOP E) into row.w[0..EX) --------------------
-  if (mode == A_FINAL || mode == A_CHAINED || mode == A_DUMMY) {
-    const PM_G uint64_t* base = S.db + P.row0 * E;
-    for (uint32_t seg0 = 0; seg0 < NSEG; seg0 += kAnsBlock) {
-      const uint32_t nseg = min(NSEG - seg0, (uint32_t)kAnsBlock);
-      const uint32_t nsl = kAnsBlock / nseg;
-      const uint32_t sl = tid / nseg, seg = seg0 + tid % nseg;
-      uint64_t a0 = 0, a1 = 0;
-      if (sl < nsl) {
-        // every row load of a batch is issued before the first is consumed: the
-        // gather is one HBM round trip per kG rows a thread reads, not one per 4
-        constexpr int kG = 16;
-        typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-        for (uint32_t i0 = sl; i0 < P.SS; i0 += kG * nsl) {
-          uint64_t rr[kG];
-#pragma unroll
-          for (int u = 0; u < kG; ++u) {
-            const uint32_t i = i0 + u * nsl;
-            rr[u] = i < P.SS ? (uint64_t)i * P.CS + qo[i] : P.N;
-          }
-          u64x2 x[kG];
-#pragma unroll
-          for (int u = 0; u < kG; ++u) {
-            x[u] = u64x2{0, 0};
-            if (rr[u] < P.N) {
-              const PM_G uint64_t* q = base + rr[u] * E + (uint64_t)seg * W;
-              if (W == 2) x[u] = *reinterpret_cast<const PM_G u64x2*>(q);
-              else x[u].x = *q;
-            }
-          }
-#pragma unroll
-          for (int u = 0; u < kG; ++u) { a0 ^= x[u].x; a1 ^= x[u].y; }
-        }
-      }
-      red[tid * 2] = a0;
-      red[tid * 2 + 1] = a1;
-      __syncthreads();
-      if (tid < nseg) {
-        uint64_t x0 = 0, x1 = 0;
-        for (uint32_t k = 0; k < nsl; ++k) {
-          x0 ^= red[(k * nseg + tid) * 2];
-          x1 ^= red[(k * nseg + tid) * 2 + 1];
-        }
-        row.w[seg * W] = x0;
-        if (W == 2) row.w[seg * W + 1] = x1;
-      }
-      __syncthreads();
-    }
-  }
   STAMP_AT(stamp_wg, 51);
   // ---- decode + refresh, or the cached row -----------------------------
   if (mode == A_FINAL) {
-    for (uint32_t w = tid; w < E; w += kAnsBlock) {
-      const uint64_t rvw = w < kAnsBlock ? e_rv : rv[w], bpw = w < kAnsBlock ? e_bp : bp[w],
-                     ppw = w < kAnsBlock ? e_pp : pp[w];
+    for (uint32_t w = tid; w < E; w += NT) {
+      const uint64_t rvw = w < NT ? e_rv : rv[w], bpw = w < NT ? e_bp : bp[w],
+                     ppw = w < NT ? e_pp : pp[w];
       uint64_t v = 0;
       if (w < EX) {
         v = row.w[w] ^ rvw ^ ppw;
@@ -934,20 +1136,20 @@ __global__ void __launch_bounds__(kAnsBlock) k_answer(PmStep S) {
       row.w[w] = v;
     }
   } else if (mode == A_CHAINED) {
-    for (uint32_t w = tid; w < E; w += kAnsBlock) S.ans[(uint64_t)s * E + w] = w < EX ? row.w[w] : 0;
+    for (uint32_t w = tid; w < E; w += NT) S.ans[(uint64_t)s * E + w] = w < EX ? row.w[w] : 0;
   } else if (mode == A_CACHED) {
     const uint64_t* a = P.arena + (uint64_t)r.slot * E;
-    for (uint32_t w = tid; w < E; w += kAnsBlock) row.w[w] = a[w];
+    for (uint32_t w = tid; w < E; w += NT) row.w[w] = a[w];
   }
   __syncthreads();
   STAMP_AT(stamp_wg, 52);
   // ---- results: row + header into pinned host memory, arena copy -----------
   if (mode != A_CHAINED) {
     const bool has_row = (mode == A_FINAL || mode == A_CACHED);
-    for (uint32_t w = tid; w < E; w += kAnsBlock) orow[w] = has_row ? row.w[w] : 0;
+    for (uint32_t w = tid; w < E; w += NT) orow[w] = has_row ? row.w[w] : 0;
     if (mode == A_FINAL) {
       uint64_t* ar = P.arena + (uint64_t)r.slot * E;
-      for (uint32_t w = tid; w < E; w += kAnsBlock) ar[w] = row.w[w];
+      for (uint32_t w = tid; w < E; w += NT) ar[w] = row.w[w];
     }
     float d = 0.0f;
     if (has_row && S.q && tid < 8) d = l2_lds(row.f, S.q, S.dim);
@@ -965,23 +1167,99 @@ __global__ void __launch_bounds__(kAnsBlock) k_answer(PmStep S) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint32_t prev = __hip_atomic_fetch_add(&S.done[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = (prev + 1 == S.done[2]);
-    if (s_last) {
+    L.s_last = (prev + 1 == S.np_live);
+    if (L.s_last) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
   }
   __syncthreads();
-  if (!s_last) return;
-  const uint32_t nchain = S.done[1];
-  for (uint32_t k = 0; k < nchain; ++k) decode_chained(S, S.done[3 + k], row);
+  if (!L.s_last) return;
+  finish_step(S, row);
+}
+
+template <int W>
+__global__ void __launch_bounds__(kAnsBlock) k_answer(PmStep S) {
+  __shared__ AnswerLds<kAnsBlock> L;
+  answer_role<W, false, kAnsBlock>(S, blockIdx.x, L);
+}
+
+// ---- k_step: the step in one launch ---------------------------------------
+// Workgroups [0, nsub) match one sub-query each (all its hints), the next np
+// resolve one partition each, the last nsub answer one sub-query each.
+// Dispatch is in workgroup order and a role only waits for lower-numbered
+// ones (resolver: its partition's match workgroups, counted in cnt[p];
+// answer: its resolver's ready[p] == token), so the lowest unfinished
+// workgroup can always run.  At most 240 workgroups of 1024 threads whose LDS
+// admits one per CU: the envelope the sc1 hand-off form of MI355X_MICROARCH.md
+// is measured in.  Producer: sc1 stores, every wave drains (vmcnt(0)),
+// barrier, one lane's counter add / flag store; consumer: sc1 poll, barrier,
+// sc1 loads.
+constexpr int kStepBlock = 1024, kStepHPT = kLdsPH / kStepBlock;
+constexpr uint32_t kLine = kHandStride;   // counters / flags one per 256-B line
+union StepLds {
+  uint32_t s_cand[kStepBlock / 64][6];
+  ResolveLds<2> r;
+  AnswerLds<kStepBlock> a;
+  uint8_t one_per_cu[96 * 1024];
+};
+
+template <int W>
+__global__ void __launch_bounds__(kStepBlock) k_step(PmStep S) {
+  __shared__ StepLds L;
+  const uint32_t b = blockIdx.x;
+  TS(0);
+  TS_HWID();
+  if (b < S.nsub) {
+    PmSub sub = S.subs_a[b];
+    sub.part = __builtin_amdgcn_readfirstlane(sub.part);
+    sub.kind = __builtin_amdgcn_readfirstlane(sub.kind);
+    sub.idx = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(sub.idx >> 32)) << 32) |
+              __builtin_amdgcn_readfirstlane((uint32_t)sub.idx);
+    match_role<kStepBlock, kStepHPT, true>(S, b, 0, sub, L.s_cand);
+    TS(1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __hip_atomic_fetch_add(S.cnt + sub.part * kLine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      st32<true>(S.mflag + b * kLine, S.token);   // this sub-query's record, for its answer's guess
+    }
+    TS(2);
+    return;
+  }
+  if (b < S.nsub + S.np) {
+    const uint32_t p = b - S.nsub, n = S.sb_a[p + 1] - S.sb_a[p];
+    if (n == 0) return;
+    if (threadIdx.x == 0) {
+      while (ld32<true>(S.cnt + p * kLine) != n) __builtin_amdgcn_s_sleep(1);
+      st32<true>(S.cnt + p * kLine, 0);   // every match workgroup of this step is in: re-armed
+    }
+    __syncthreads();
+    TS(1);
+    resolve_role<2, kStepBlock, true>(S, p, L.r);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const uint32_t fin = L.r.fin;
+    if (threadIdx.x == 0) st32<true>(S.ready + p * kLine, S.token);
+    TS(2);
+    if (!fin) return;
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();   // L.r is dead from here: its space holds the decode row
+    finish_step(S, L.a.row);
+    return;
+  }
+  answer_role<W, true, kStepBlock>(S, b - S.nsub - S.np, L.a);
+  TS(2);
 }
 
 }  // namespace pm
 
 namespace pmk {
 static inline unsigned cdiv(uint64_t a, uint64_t b) { return (unsigned)((a + b - 1) / b); }
-uint32_t step_match_blocks(uint32_t maxPH) { return cdiv(maxPH, kBlock * kMatchHPT); }
+uint32_t step_match_blocks(uint32_t maxPH) { return cdiv(maxPH, kMatchHints); }
 // With events, the launch carries them in its own dispatch packet
 // (hipExtLaunchKernelGGL): the kernel's execution time as the profiler sees it.
 #define PM_LAUNCH(ev, kern, grid, blk, st, ...)                                              \
@@ -1002,6 +1280,16 @@ bool step_resolve_lds_ok(uint32_t maxPH, uint32_t max_sub_per_part) {
 void step_answer(hipStream_t st, const PmStep& S, PmEvents ev) {
   if (S.E % 2 == 0) PM_LAUNCH(ev, k_answer<2>, dim3(S.nsub), dim3(kAnsBlock), st, S);
   else PM_LAUNCH(ev, k_answer<1>, dim3(S.nsub), dim3(kAnsBlock), st, S);
+}
+bool step_fused_ok(const PmStep& S, uint32_t maxPH, uint32_t max_sub_per_part) {
+  return S.args_valid && S.cnt && S.ready && max_sub_per_part <= kSpecSubs && maxPH <= kLdsPH &&
+         2 * S.nsub + S.np <= 256;
+}
+void step_fused(hipStream_t st, const PmStep& S, PmEvents ev) {
+  // S.cblk must be 1 (one match record per sub-query)
+  const dim3 grid(2 * S.nsub + S.np);
+  if (S.E % 2 == 0) PM_LAUNCH(ev, k_step<2>, grid, dim3(kStepBlock), st, S);
+  else PM_LAUNCH(ev, k_step<1>, grid, dim3(kStepBlock), st, S);
 }
 uint32_t step_max_sub_per_part() { return kMaxSubPerPart; }
 uint32_t step_max_ss() { return kMaxSSLds; }

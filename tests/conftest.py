@@ -28,3 +28,25 @@ def oracle():
     from oracle import oracle as O
     O.lib()
     return O
+
+
+@pytest.fixture(scope="session")
+def ctx_unfused():
+    """A context that runs every batch-PIR step as the three separate kernels
+    (PM_NO_FUSE=1, read at context creation) instead of the fused k_step."""
+    import pacmann_amd as pm
+    old = os.environ.get("PM_NO_FUSE")
+    os.environ["PM_NO_FUSE"] = "1"
+    try:
+        return pm.Context(0)
+    finally:
+        if old is None:
+            del os.environ["PM_NO_FUSE"]
+        else:
+            os.environ["PM_NO_FUSE"] = old
+
+
+@pytest.fixture(params=["fused", "unfused"])
+def step_ctx(request):
+    """Both step paths: k_step (default) and the three-kernel fallback."""
+    return request.getfixturevalue("ctx" if request.param == "fused" else "ctx_unfused")

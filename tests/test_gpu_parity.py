@@ -184,13 +184,13 @@ def test_pir_dummy_preprocessing(ctx, oracle):
 # ---------------------------------------------------------------------------
 # SimpleBatchPianoPIR
 # ---------------------------------------------------------------------------
-def test_batch_pir_basic(ctx, oracle):
+def test_batch_pir_basic(step_ctx, oracle):
     """TestBatchPIRBasic (pir_test.go:60-202) with the GPU path, plus
     bit-exact parity against the oracle for every response."""
     import pacmann_amd as pm
     N, E, B = 1_000_000, 16, 32
     db = np.repeat(np.arange(N, dtype=np.uint64), E)   # rawDB[i*16+j] = i
-    g = pm.SimpleBatchPianoPIR(N, E * 8, B, db, 20, seed=SEED, ctx=ctx)
+    g = pm.SimpleBatchPianoPIR(N, E * 8, B, db, 20, seed=SEED, ctx=step_ctx)
     o = oracle.SimpleBatchPianoPIR(N, E * 8, B, db, 20, seed=SEED)
     g.Preprocessing()
     o.Preprocessing()
@@ -218,13 +218,13 @@ def test_batch_pir_basic(ctx, oracle):
 
 @pytest.mark.parametrize("N,E,B,n", [(200_000, 80, 32, 96), (50_000, 12, 8, 24), (30_000, 6, 32, 200),
                                      (30_000, 6, 4, 2000)])
-def test_batch_pir_sequence(ctx, oracle, N, E, B, n):
+def test_batch_pir_sequence(step_ctx, oracle, N, E, B, n):
     """Many batches (duplicates, drops, dummies) through the batch layer's
     re-preprocessing trigger (batch-pir.go:239-245) and, for the last case,
     the per-sub-query FinishedQueryNum == MaxQueryNum path (pir.go:527-530)."""
     import pacmann_amd as pm
     db = rand_db(N, E, N + E)
-    g = pm.SimpleBatchPianoPIR(N, E * 8, B, db, 8, seed=SEED, ctx=ctx)
+    g = pm.SimpleBatchPianoPIR(N, E * 8, B, db, 8, seed=SEED, ctx=step_ctx)
     o = oracle.SimpleBatchPianoPIR(N, E * 8, B, db, 8, seed=SEED)
     g.Preprocessing()
     o.Preprocessing()
@@ -271,11 +271,11 @@ def test_search_knn_matches_oracle(ctx, oracle, nonprivate, bench):
     assert g.counts() == o.counts()
 
 
-def test_search_loop_with_maintenance(ctx, oracle):
+def test_search_loop_with_maintenance(step_ctx, oracle):
     import pacmann_amd as pm
     v, graph = small_graph(n=2048, seed=1)
     qs = v[::37][:30] + np.float32(1.0)
-    g = pm.PIRGraphInfo(v, graph, pir_seed=6, search_seed=2, ctx=ctx)
+    g = pm.PIRGraphInfo(v, graph, pir_seed=6, search_seed=2, ctx=step_ctx)
     o = oracle.Graph(v, graph, pir_seed=6, search_seed=2)
     g.Preprocess()
     o.Preprocess()
@@ -287,14 +287,14 @@ def test_search_loop_with_maintenance(ctx, oracle):
 
 
 @pytest.mark.gpu
-def test_batch_query_mask(ctx, oracle):
+def test_batch_query_mask(step_ctx, oracle):
     """pm_batchpir_query_ok: ok => the entry is rawDB[id]; not ok => the id was
     dropped by the bucketing (batch-pir.go:195-200) or failed, entry zero;
     rows identical to the oracle's, across batches with drops and repeats."""
     import pacmann_amd as pm
     N, E, B = 40_000, 8, 16
     db = rand_db(N, E, 99)
-    g = pm.SimpleBatchPianoPIR(N, E * 8, B, db, 8, seed=SEED, ctx=ctx)
+    g = pm.SimpleBatchPianoPIR(N, E * 8, B, db, 8, seed=SEED, ctx=step_ctx)
     o = oracle.SimpleBatchPianoPIR(N, E * 8, B, db, 8, seed=SEED)
     g.Preprocessing()
     o.Preprocessing()
@@ -318,7 +318,7 @@ def test_batch_query_mask(ctx, oracle):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("nshards", [2, 3])
-def test_batch_pir_shards(ctx, oracle, nshards):
+def test_batch_pir_shards(step_ctx, oracle, nshards):
     """pm_batchpir_create_shard: shards fed the same batches; their entries
     summed (and masks OR-ed) equal the unsharded oracle bit for bit, through
     the batch layer's re-preprocessing trigger; each shard's partitions carry
@@ -326,7 +326,7 @@ def test_batch_pir_shards(ctx, oracle, nshards):
     import pacmann_amd as pm
     N, E, B = 30_000, 6, 8
     db = rand_db(N, E, 77)
-    shards = [pm.SimpleBatchPianoPIR(N, E * 8, B, db, 8, seed=SEED, ctx=ctx, shard=r, nshards=nshards)
+    shards = [pm.SimpleBatchPianoPIR(N, E * 8, B, db, 8, seed=SEED, ctx=step_ctx, shard=r, nshards=nshards)
               for r in range(nshards)]
     o = oracle.SimpleBatchPianoPIR(N, E * 8, B, db, 8, seed=SEED)
     for s in shards:
