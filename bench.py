@@ -45,7 +45,8 @@ SYMBOLS = {"prep_fold": "void pm::k_prep_fold_pipe<4, 1, 4>(pm::PmPart const*, u
            "answer": "void pm::k_answer<2>(pm::PmStep)", "step": "void pm::k_step<2>(pm::PmStep)", "resolve": "void pm::k_resolve<true>(pm::PmStep)",
            "hint_match": "pm::k_match(pm::PmStep)", "prep_offsets": "pm::k_prep_offsets(pm::PmPart const*)"}
 HOST = ["host_search_knn", "host_knn_init", "host_knn_final", "host_knn_batch", "host_knn_update",
-        "host_gvi_parse", "host_batch_query", "host_step_launch", "host_step_wait", "host_step_post"]
+        "host_gvi_parse", "host_batch_query", "host_step_launch", "host_step_wait", "host_step_post",
+        "host_wait_first_token", "host_wait_all_tokens"]
 
 
 def make_data(rank: int):

@@ -146,8 +146,8 @@ struct HostBuf {
 };
 
 // Host wall-clock accumulators, read back as "host_*" through pm_timing_get.
-enum HostTimer : int { HT_STEP_LAUNCH, HT_STEP_WAIT, HT_STEP_POST, HT_BATCH_QUERY, HT_GVI_PARSE, HT_SEARCH_KNN, HT_KNN_INIT, HT_KNN_BATCH, HT_KNN_UPDATE, HT_KNN_FINAL, HT_COUNT };
-static const char* const kHostTimerName[HT_COUNT] = {"host_step_launch", "host_step_wait", "host_step_post", "host_batch_query", "host_gvi_parse", "host_search_knn", "host_knn_init", "host_knn_batch", "host_knn_update", "host_knn_final"};
+enum HostTimer : int { HT_STEP_LAUNCH, HT_STEP_WAIT, HT_STEP_POST, HT_BATCH_QUERY, HT_GVI_PARSE, HT_SEARCH_KNN, HT_KNN_INIT, HT_KNN_BATCH, HT_KNN_UPDATE, HT_KNN_FINAL, HT_WAIT_FIRST, HT_WAIT_ALL, HT_COUNT };
+static const char* const kHostTimerName[HT_COUNT] = {"host_step_launch", "host_step_wait", "host_step_post", "host_batch_query", "host_gvi_parse", "host_search_knn", "host_knn_init", "host_knn_batch", "host_knn_update", "host_knn_final", "host_wait_first_token", "host_wait_all_tokens"};
 
 struct TimedLaunch { std::string name; hipEvent_t a, b; double bytes; };
 
@@ -279,7 +279,8 @@ struct Engine {
   uint64_t FBN = 0, QMIP = 0, Support = 0, prepCount = 0;
   double prepTime = 0, storage = 0, commOn = 0, commOff = 0;
 
-  DevBuf db, zero16, parts_d, owned_d, tag, pp, parity, ridx, rval, hist, fqn, arena, tab, tabT, done, hand;
+  DevBuf db, zero16, parts_d, owned_d, tag, pp, parity, ridx, rval, hist, fqn, arena, tab, tabT, done, gran;
+  uint32_t gran_words = 0;
   std::vector<uint32_t> owned_list;   // owned partitions in order (owned_d holds their PmPart)
   DevBuf qoffs, ans_srv;
   DevBuf subs_d, sb_d, bits, cand, meta, spec, res_d, ans, qvec, stamps;
@@ -287,7 +288,7 @@ struct Engine {
   uint64_t stamp_n = 0;
   uint32_t step_token = 0;         // PmStep::token of the last step
   size_t pf_off = 0, pf_len = ~size_t(0);   // bytes of each result row the caller reads next
-  HostBuf desc_h, out_h;
+  HostBuf desc_h, out_h, err_h;
   std::vector<PartHost> parts;
   uint32_t maxH = 0, maxPH = 0, maxSS = 0, maxRepl = 0, maxCS = 0, minCS = ~0u;
 
@@ -421,10 +422,18 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
   CHK(g->tab.reserve(off_tab * 2));
   CHK(g->tabT.reserve(off_tab * 2));
   CHK(g->done.reserve(4 * (3 + 16 * 4096)));
-  HIPCHK(hipMemset(g->done.p, 0, 4 * 3));        // the chain counters start (and end each step) at 0
-  // k_step hand-off counters and flags, one per line: cnt[P], ready[P], mflag[kArgSubs]
-  CHK(g->hand.reserve((2 * g->P + kArgSubs) * 4 * kHandStride));
-  HIPCHK(hipMemset(g->hand.p, 0, (2 * g->P + kArgSubs) * 4 * kHandStride));
+  {   // step completion counter (pm_query.hip chain_add): 2^31 in the low half, 0 chained
+    const uint32_t init[3] = {1u << 31, 0, 0};
+    HIPCHK(hipMemcpy(g->done.p, init, sizeof init, hipMemcpyHostToDevice));
+  }
+  {   // k_step hand-off granules (token 0 never marks a step) and the error word
+    g->gran_words = (g->maxPH + 63) / 64;
+    const size_t n = (size_t)kArgSubs * (8 + 64 + 2 * g->gran_words + 8) * 8;
+    CHK(g->gran.reserve(n));
+    HIPCHK(hipMemset(g->gran.p, 0, n));
+    CHK(g->err_h.reserve(64));
+    memset(g->err_h.p, 0, 64);
+  }
   CHK(g->parts_d.reserve(g->P * sizeof(PmPart)));
   CHK(g->owned_d.reserve(std::max<size_t>(1, g->owned_list.size()) * sizeof(PmPart)));
   for (uint64_t i = 0; i < g->P; ++i) {
@@ -538,6 +547,8 @@ static int wait_step(pm_ctx* c, const PmOutHdr* hdr, uint32_t nsub, uint32_t tok
     uint32_t s = 0;
     for (uint64_t spin = 0; s < nsub; ++spin) {
       if (tok[s * stride] == token) {
+        if (c->timing && s == 0) c->host_add(HT_WAIT_FIRST, ms_since(t0));
+        if (c->timing && s + 1 == nsub) c->host_add(HT_WAIT_ALL, ms_since(t0));
         const char* r = rows + s * row_bytes + pf_off;
         for (size_t b = 0; b < pf_len; b += 64) __builtin_prefetch(r + b);
         ++s;
@@ -632,9 +643,14 @@ static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
   S.cand = g->cand.as<uint32_t>();
   S.meta = g->meta.as<uint32_t>();
   S.spec = g->spec.as<uint32_t>();
-  S.cnt = g->hand.as<uint32_t>();
-  S.ready = g->hand.as<uint32_t>() + g->P * kHandStride;
-  S.mflag = g->hand.as<uint32_t>() + 2 * g->P * kHandStride;
+  if (words <= g->gran_words) {   // k_step granules (sized at creation for maxPH)
+    uint64_t* gb = g->gran.as<uint64_t>();
+    S.recg = gb;
+    S.specg = gb + kArgSubs * 8;
+    S.bitsg = gb + kArgSubs * (8 + 64);
+    S.resg = gb + kArgSubs * (8 + 64 + 2 * (uint64_t)g->gran_words);
+    S.err_h = g->err_h.as<uint32_t>();
+  }
   S.cblk = cblk;
   S.res = g->res_d.as<PmRes>();
   S.ans = g->ans.as<uint64_t>();
@@ -677,18 +693,22 @@ static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
     S.cblk = 1;   // one match workgroup per sub-query
 #ifdef PM_STEP_STAMPS
     const uint32_t grid = 2 * nsub + (uint32_t)g->P;
-    CHK(g->stamps.reserve((uint64_t)grid * 4 * 8));
-    HIPCHK(hipMemsetAsync(g->stamps.p, 0, (uint64_t)grid * 4 * 8, st));
+    CHK(g->stamps.reserve((uint64_t)grid * 8 * 8));
+    HIPCHK(hipMemsetAsync(g->stamps.p, 0, (uint64_t)grid * 8 * 8, st));
     S.stamps = g->stamps.as<uint64_t>();
 #endif
     c->timed_ext("step", ans_bytes, [&](pmk::PmEvents ev) { pmk::step_fused(st, S, ev); }, 2);
     HIPCHK(hipGetLastError());
     c->host_add(HT_STEP_LAUNCH, ms_since(t_begin));
     CHK(wait_and_post(g, S, nsub, t_begin));
+    if (*(volatile uint32_t*)S.err_h) {
+      *(volatile uint32_t*)S.err_h = 0;
+      return fail(PM_EHIP, "k_step: a hand-off wait timed out (results of this step are invalid)");
+    }
 #ifdef PM_STEP_STAMPS
-    if (const char* fn = getenv("PM_STAMP_FILE")) {   // append {grid, nsub, cblk, np} + grid x 4 stamps
+    if (const char* fn = getenv("PM_STAMP_FILE")) {   // append {grid, nsub, cblk, np} + grid x 8 stamps
       HIPCHK(hipStreamSynchronize(st));
-      std::vector<uint64_t> t((uint64_t)grid * 4);
+      std::vector<uint64_t> t((uint64_t)grid * 8);
       HIPCHK(hipMemcpy(t.data(), g->stamps.p, t.size() * 8, hipMemcpyDeviceToHost));
       if (FILE* f = fopen(fn, "ab")) {
         const uint32_t h[4] = {grid, nsub, cblk, (uint32_t)g->P};

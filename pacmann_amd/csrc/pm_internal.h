@@ -100,7 +100,6 @@ struct alignas(16) PmOutHdr {
 #ifndef PM_KARG_SUBS
 #define PM_KARG_SUBS 112
 #endif
-constexpr uint32_t kHandStride = 64;   // u32 words between k_step counters / flags
 constexpr uint32_t kArgSubs = PM_KARG_SUBS, kArgParts = PM_KARG_SUBS > 1 ? 32 : 1;
 struct PmStep {
   const PM_G PmPart* parts;
@@ -113,9 +112,9 @@ struct PmStep {
                                // {hint, tag, program point} x 2 (hint kNone: none)
   PM_G PmRes* res;             // [nsub]
   PM_G uint64_t* ans;          // [nsub][E] raw answers of chained sub-queries
-  PM_G uint32_t* done;         // [0] unified chain counter (resolver_count, pm_query.hip),
-                               // [1] chained sub-queries, [3..] their list (filled by the
-                               // resolvers; re-armed by each step's finisher; zero at creation)
+  PM_G uint32_t* done;         // [0..1] step completion counter (chain_add, pm_query.hip),
+                               // [2] chained sub-queries, [3..] their list (filled by the
+                               // resolvers; re-armed by each step's finisher)
   const PM_G uint64_t* db;
   const PM_G float* q;         // search query (device) or null
   PM_G PmOutHdr* hdr_h;        // pinned host outputs
@@ -123,10 +122,12 @@ struct PmStep {
   PM_G uint64_t* stamps;       // PM_STAMPS diagnostic builds only: s_memtime per phase
   PM_G uint32_t* meta;         // [nsub][2]: chunk QueryHistogram, predicted in-chunk index
   PM_G uint32_t* spec;         // [nsub][64]: predicted re-evaluation values (k_match -> k_resolve)
-  PM_G uint32_t* cnt;          // [np][kHandStride] k_step: match workgroups done per partition
-                               // (re-armed by its resolver), one per 256-B line
-  PM_G uint32_t* ready;
-  PM_G uint32_t* mflag;        // [kArgSubs][kHandStride] k_step: token of the step whose match record is out        // [np] k_step: token of the step whose results the resolver published
+  // k_step hand-off granules {value, token} (pm_query.hip put_g / get_g)
+  PM_G uint64_t* recg;         // [kArgSubs][8] match record + prediction per sub-query
+  PM_G uint64_t* specg;        // [kArgSubs][64] predicted re-evaluation values
+  PM_G uint64_t* bitsg;        // [kArgSubs][words][2] match bits
+  PM_G uint64_t* resg;         // [kArgSubs][8] resolution records
+  PM_G uint32_t* err_h;        // pinned host: set when a hand-off spin timed out        // [np] k_step: token of the step whose results the resolver published
   uint32_t words, E, dim, nsub, np, cblk;
   uint32_t np_live;            // partitions with at least one sub-query in this step
   // Small steps ship the descriptor inside the kernel arguments (no PCIe

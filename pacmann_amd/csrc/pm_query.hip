@@ -75,9 +75,27 @@ constexpr uint32_t kNone = 0xffffffffu;
           ((uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |           \
           (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);                      \
   } while (0)
+// answer workgroups: slot 3 = time the resolver's flag was seen << 1 | guess kept
+#define TS_SEEN(kept)                                                                          \
+  do {                                                                                         \
+    if (threadIdx.x == 0 && S.stamps)                                                          \
+      S.stamps[(uint64_t)blockIdx.x * 4 + 3] = (__builtin_amdgcn_s_memrealtime() << 1) | (kept); \
+  } while (0)
+// match-role phases (k_step only): stamps[gridDim.x * 4 + blockIdx.x * 4 + i],
+// each after draining the loads it follows
+#define MS(i)                                                                              \
+  do {                                                                                     \
+    if (GRAN) {                                                                             \
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                    \
+      if (threadIdx.x == 0 && S.stamps)                                                    \
+        S.stamps[(uint64_t)gridDim.x * 4 + blockIdx.x * 4 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    }                                                                                      \
+  } while (0)
 #else
+#define MS(i) do {} while (0)
 #define TS(i) do {} while (0)
 #define TS_HWID() do {} while (0)
+#define TS_SEEN(kept) do {} while (0)
 #endif
 // slots: k_resolve partition 0: 0..40; k_match block (0,0): 41..47; k_answer block 0: 48..63
 
@@ -135,24 +153,81 @@ template <bool SC1> __device__ __forceinline__ uint64_t ld64(const PM_G uint64_t
   if (SC1) return __hip_atomic_load((uint64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return *p;
 }
-template <bool SC1> __device__ __forceinline__ void st_res(PM_G PmRes* p, const PmRes& r) {
-  const uint64_t* w = reinterpret_cast<const uint64_t*>(&r);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) st64<SC1>(reinterpret_cast<PM_G uint64_t*>(p) + i, w[i]);
+
+// k_step hand-offs: data-tagged 8-byte granules {value, step token}, each
+// written by ONE sc1 store, read with sc1 loads until the token is this
+// step's (MI355X_MICROARCH.md, handoff-1to1: no drain, no flag, no counter).
+// A spin longer than kSpinTicks (20 ms of s_memrealtime) flags an error in
+// pinned host memory, which the host turns into a failed step.
+constexpr uint64_t kSpinTicks = 2000000;
+__device__ __forceinline__ void put_g(PM_G uint64_t* p, uint32_t v, uint32_t tok) {
+  st64<true>(p, ((uint64_t)tok << 32) | v);
 }
-template <bool SC1> __device__ __forceinline__ PmRes ld_res(const PM_G PmRes* p) {
-  PmRes r;
-  uint64_t* w = reinterpret_cast<uint64_t*>(&r);
+__device__ __forceinline__ uint32_t get_g(const PM_G uint64_t* p, const PmStep& S) {
+  uint64_t v = ld64<true>(p);
+  if ((uint32_t)(v >> 32) != S.token) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    do {
+      __builtin_amdgcn_s_sleep(1);
+      v = ld64<true>(p);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {
+        __hip_atomic_store((uint32_t*)S.err_h, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    } while ((uint32_t)(v >> 32) != S.token);
+  }
+  return (uint32_t)v;
+}
+// granule layouts (k_step): rec[s][8] = {c1, t1, p1, c2, t2, p2, hist0, sing};
+// spec[s][64]; bits[s][words][2] (low, high halves); res[s][8] (PmRes fields)
+enum : uint32_t { G_REC = 8, G_RES = 8 };
+template <bool GRAN> __device__ __forceinline__ void put_res(const PmStep& S, uint32_t s, const PmRes& r) {
+  if (GRAN) {
+    const uint32_t* f = reinterpret_cast<const uint32_t*>(&r);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) w[i] = ld64<SC1>(reinterpret_cast<const PM_G uint64_t*>(p) + i);
+    for (int i = 0; i < 8; ++i) put_g(S.resg + (uint64_t)s * G_RES + i, f[i], S.token);
+  } else {
+    S.res[s] = r;
+  }
+}
+// a resolution record read by the step's finisher (granules: sc1, token-checked)
+template <bool GRAN> __device__ __forceinline__ PmRes res_after_acquire(const PmStep& S, uint32_t s) {
+  if (!GRAN) return S.res[s];
+  PmRes r;
+  uint32_t* f = reinterpret_cast<uint32_t*>(&r);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f[i] = get_g(S.resg + (uint64_t)s * G_RES + i, S);
   return r;
 }
 
 constexpr uint32_t kMatchHints = 1024;   // hints per match workgroup (any block size)
 
+// In-chunk index the k-th of a partition's pn sub-queries (those from pb0 on)
+// gets if every earlier one succeeds: its chunk's QueryHistogram h0k plus the
+// earlier valid first occurrences in the same chunk.  One whole wave, pn <= 64;
+// lane t returns sub-query pb0 + t in `st` and whether it is valid in `validt`.
+__device__ __forceinline__ uint32_t predict_ing(const PmStep& S, const PmPart& P, uint32_t pb0, uint32_t pn,
+                                                uint32_t k, uint32_t chunk, uint32_t h0k, PmSub& st,
+                                                bool& validt) {
+  const uint32_t lane = threadIdx.x & 63;
+  st = PmSub{0, SUB_NONE, ~0ull};
+  if (lane < pn) st = desc_sub(S, pb0 + lane);
+  validt = lane < pn && st.kind == SUB_REAL && st.idx < P.N;
+  const uint32_t cht = (uint32_t)(st.idx >> P.log2CS);
+  bool first = validt;
+  for (uint32_t t = 0; t + 1 < pn; ++t) {
+    const uint64_t it = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(st.idx >> 32), t) << 32) |
+                        __builtin_amdgcn_readlane((uint32_t)st.idx, t);
+    const bool rt = __builtin_amdgcn_readlane(st.kind == SUB_REAL ? 1u : 0u, t) != 0;
+    if (t < lane && rt && it == st.idx) first = false;
+  }
+  const uint64_t mk = __ballot(lane < k && validt && first && cht == chunk);
+  return h0k + (uint32_t)__builtin_popcountll(mk);
+}
+
 // One match workgroup (HOT LOOP C): hints [blk*kMatchHints, +kMatchHints) of
 // sub-query s against the state at the start of the step; `sub` is uniform.
-template <int NT, int kMatchHPT, bool SC1>
+template <int NT, int kMatchHPT, bool GRAN>
 __device__ __forceinline__ void match_role(const PmStep& S, uint32_t s, uint32_t blk, PmSub sub,
                                            uint32_t (&s_cand)[NT / 64][6]) {
   const bool stamp_wg = blk == 0 && s == 0;
@@ -170,6 +245,7 @@ __device__ __forceinline__ void match_role(const PmStep& S, uint32_t s, uint32_t
   // QueryHistogram now, the rest below (loads overlap the match loads).
   const bool meta_wg = blk == 0;
   const uint32_t h0k = (meta_wg && live) ? P.hist[chunk] : 0;
+  uint32_t sing_rec = 0;   // GRAN: thread 0's copy for the record
   // kMatchHPT hints per thread, all loads of a kind issued together
   uint32_t tg[kMatchHPT], pv[kMatchHPT];
   uint16_t rv[kMatchHPT];
@@ -179,8 +255,10 @@ __device__ __forceinline__ void match_role(const PmStep& S, uint32_t s, uint32_t
     tg[u] = 0; pv[u] = kDefaultProgramPoint;
     if (live && h < P.PH) { tg[u] = P.tag[h]; pv[u] = P.pp[h]; }
   }
+  MS(0);
 #pragma unroll
   for (int u = 0; u < kMatchHPT; ++u) rv[u] = row[tg[u]];
+  MS(1);
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (meta_wg && wave == 0) {
     // In-chunk index this sub-query gets if every earlier one of its partition
@@ -189,24 +267,20 @@ __device__ __forceinline__ void match_role(const PmStep& S, uint32_t s, uint32_t
     // that refresh would hand out: spec[s][j] (k_resolve's re-evaluation).
     const uint32_t pb0 = desc_sb(S, sub.part), pn = desc_sb(S, sub.part + 1) - pb0, k = s - pb0;
     if (pn <= kSpecSubs) {
-      PmSub st{0, SUB_NONE, ~0ull};
-      if (lane < pn) st = desc_sub(S, pb0 + lane);
-      const bool validt = lane < pn && st.kind == SUB_REAL && st.idx < P.N;
+      PmSub st;
+      bool validt;
+      const uint32_t sing = predict_ing(S, P, pb0, pn, k, chunk, h0k, st, validt);
       const uint32_t cht = (uint32_t)(st.idx >> P.log2CS);
-      bool first = validt;
-      for (uint32_t t = 0; t + 1 < pn; ++t) {
-        const uint64_t it = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(st.idx >> 32), t) << 32) |
-                            __builtin_amdgcn_readlane((uint32_t)st.idx, t);
-        const bool rt = __builtin_amdgcn_readlane(st.kind == SUB_REAL ? 1u : 0u, t) != 0;
-        if (t < lane && rt && it == st.idx) first = false;
-      }
-      const uint64_t mk = __ballot(lane < k && validt && first && cht == chunk);
-      const uint32_t sing = h0k + (uint32_t)__builtin_popcountll(mk);
       const uint32_t pred = (live && sing < P.Qpc && chunk < P.SS) ? P.PH + chunk * P.Qpc + sing : kNone;
       uint32_t v = kSkip;
       if (lane < pn && lane > k && validt && cht < P.SS && pred != kNone) v = P.tab[(uint64_t)cht * P.H + pred];
-      if (lane < pn) st32<SC1>(S.spec + (uint64_t)s * kSpecSubs + lane, v);
-      if (lane == 0) { st32<SC1>(S.meta + 2 * (uint64_t)s, h0k); st32<SC1>(S.meta + 2 * (uint64_t)s + 1, sing); }
+      if (GRAN) {
+        if (lane < pn) put_g(S.specg + (uint64_t)s * kSpecSubs + lane, v, S.token);
+        sing_rec = sing;
+      } else {
+        if (lane < pn) S.spec[(uint64_t)s * kSpecSubs + lane] = v;
+        if (lane == 0) { S.meta[2 * (uint64_t)s] = h0k; S.meta[2 * (uint64_t)s + 1] = sing; }
+      }
     }
   }
   // match bits, and the block's first two matches with the tag / program
@@ -219,7 +293,15 @@ __device__ __forceinline__ void match_role(const PmStep& S, uint32_t s, uint32_t
     const bool m = live && h < P.PH && rv[u] == offset &&
                    (pv[u] == kDefaultProgramPoint || (pv[u] >> P.log2CS) != chunk);
     uint64_t b = __ballot(m);
-    if (lane == 0 && (h - lane) < P.PH) st64<SC1>(S.bits + (uint64_t)s * S.words + (h >> 6), b);
+    if (lane == 0 && (h - lane) < P.PH) {
+      if (GRAN) {
+        PM_G uint64_t* g = S.bitsg + ((uint64_t)s * S.words + (h >> 6)) * 2;
+        put_g(g, (uint32_t)b, S.token);
+        put_g(g + 1, (uint32_t)(b >> 32), S.token);
+      } else {
+        S.bits[(uint64_t)s * S.words + (h >> 6)] = b;
+      }
+    }
     if (b && h1 == kNone) {   // in hint order within this wave
       const uint32_t l = (uint32_t)__builtin_ctzll(b), hl = h - lane + l;
       const uint32_t tl = __builtin_amdgcn_readlane(tg[u], l), pl = __builtin_amdgcn_readlane(pv[u], l);
@@ -237,6 +319,7 @@ __device__ __forceinline__ void match_role(const PmStep& S, uint32_t s, uint32_t
       }
     }
   }
+  MS(2);
   if (lane == 0) {
     s_cand[wave][0] = h0; s_cand[wave][1] = t0; s_cand[wave][2] = p0;
     s_cand[wave][3] = h1; s_cand[wave][4] = t1; s_cand[wave][5] = p1;
@@ -254,8 +337,15 @@ __device__ __forceinline__ void match_role(const PmStep& S, uint32_t s, uint32_t
           o[3] = h; o[4] = s_cand[w][3 * k + 1]; o[5] = s_cand[w][3 * k + 2];
         }
       }
-    PM_G uint32_t* dst = S.cand + ((uint64_t)s * S.cblk + blk) * 6;
-    for (int i = 0; i < 6; ++i) st32<SC1>(dst + i, o[i]);
+    if (GRAN) {   // one record per sub-query (blk 0 covers every hint), prediction included
+      PM_G uint64_t* g = S.recg + (uint64_t)s * G_REC;
+      for (int i = 0; i < 6; ++i) put_g(g + i, o[i], S.token);
+      put_g(g + 6, h0k, S.token);
+      put_g(g + 7, sing_rec, S.token);
+    } else {
+      PM_G uint32_t* dst = S.cand + ((uint64_t)s * S.cblk + blk) * 6;
+      for (int i = 0; i < 6; ++i) dst[i] = o[i];
+    }
   }
   STAMP_AT(stamp_wg, 43);
 }
@@ -304,13 +394,21 @@ __device__ __forceinline__ uint32_t find_next(const uint64_t* __restrict__ bw, u
   return kNone;
 }
 
-// The same over a global bitmask (sc1 loads when handed over inside k_step).
-template <bool SC1>
-__device__ __forceinline__ uint32_t find_next_g(const PM_G uint64_t* bw, uint32_t nw, uint32_t start) {
+// The same over sub-query `sub`'s match bits in global memory (granules in k_step).
+template <bool GRAN>
+__device__ __forceinline__ uint32_t find_next_g(const PmStep& S, uint64_t sub, uint32_t nw, uint32_t start) {
   const uint32_t lane = threadIdx.x & 63;
   for (uint32_t w0 = start >> 6; w0 < nw; w0 += 64) {
     const uint32_t w = w0 + lane;
-    uint64_t v = w < nw ? ld64<SC1>(bw + w) : 0;
+    uint64_t v = 0;
+    if (w < nw) {
+      if (GRAN) {
+        const PM_G uint64_t* g = S.bitsg + (sub * S.words + w) * 2;
+        v = get_g(g, S) | ((uint64_t)get_g(g + 1, S) << 32);
+      } else {
+        v = S.bits[sub * S.words + w];
+      }
+    }
     if (w == (start >> 6)) v &= ~0ull << (start & 63);
     const uint64_t m = __ballot(v != 0);
     if (m) {
@@ -353,12 +451,25 @@ struct ResolveLds {
   uint16_t spec_v[MODE != 0 ? kSpecSubs * kSpecSubs : 1];
 };
 
-// Unified chain counter done[0]: each live partition's resolver adds
-// 1 - (its workgroups involved in refresh chains), each involved answer
-// workgroup adds 1 once its refresh is released.  Every answer arrival
-// follows its own resolver's add, so the running sum reaches np_live exactly
-// at the last add of the step, whichever role makes it: that one decodes the
-// chain list and re-arms the counters.  Called by wave 0 of a resolver.
+// Step completion counter, 64 bits at done[0..1]: the high half counts the
+// live partitions' resolvers, the low half holds (answer workgroups arrived)
+// - (workgroups the resolvers declared involved in refresh chains) + 2^31.
+// A resolver adds 2^32 - (its involved workgroups), an involved answer
+// workgroup adds 1 once its refresh is released; the bias keeps the low half
+// from borrowing, so the value is np_live << 32 | 2^31 exactly after the last
+// add of the step, in any order of the adds.  That add's workgroup decodes
+// the chain list (done[2] entries from done[3]) and re-arms the counters.
+constexpr uint64_t kChainBias = 1ull << 31;
+__device__ __forceinline__ uint64_t chain_add(const PmStep& S, uint64_t d) {
+  const uint64_t prev = __hip_atomic_fetch_add(reinterpret_cast<PM_G uint64_t*>(S.done), d, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+  return (prev + d == (((uint64_t)S.np_live << 32) | kChainBias)) ? 1u : 0u;
+}
+__device__ __forceinline__ void chain_rearm(const PmStep& S) {
+  *reinterpret_cast<PM_G uint64_t*>(S.done) = kChainBias;
+  S.done[2] = 0;
+}
+// Called by wave 0 of a resolver, after its chain list entries.
 template <class LdsT>
 __device__ __forceinline__ void resolver_count(const PmStep& S, LdsT& L, uint32_t nchain, uint32_t cadd) {
   if ((threadIdx.x & 63) != 0) return;
@@ -366,15 +477,13 @@ __device__ __forceinline__ void resolver_count(const PmStep& S, LdsT& L, uint32_
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   }
-  const uint32_t d = 1u - cadd;
-  const uint32_t prev = __hip_atomic_fetch_add(&S.done[0], d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  L.fin = (prev + d == S.np_live) ? 1u : 0u;
+  L.fin = (uint32_t)chain_add(S, (1ull << 32) - cadd);
 }
 
 // One partition's share of Client.Query for every sub-query of the step, in
 // order (wave 0 runs the chain; the other waves only help the prologue and
 // return early).  L.fin: this workgroup made the step's last chain-count add.
-template <int MODE, int NT, bool SC1>
+template <int MODE, int NT, bool GRAN>
 __device__ __forceinline__ void resolve_role(const PmStep& S, uint32_t p, ResolveLds<MODE>& L) {
   constexpr bool LDS = MODE != 0;
   auto& s_idx = L.s_idx; auto& s_kind = L.s_kind; auto& s_chunk = L.s_chunk; auto& s_st = L.s_st;
@@ -398,7 +507,7 @@ __device__ __forceinline__ void resolve_role(const PmStep& S, uint32_t p, Resolv
   const bool staged = MODE == 1 && !fast;
   auto find_bits = [&](uint32_t j, uint32_t start) -> uint32_t {
     if (staged) return find_next(bits_l + (uint64_t)j * nw, nw, start);
-    return find_next_g<SC1>(S.bits + (uint64_t)(b0 + j) * S.words, nw, start);
+    return find_next_g<GRAN>(S, b0 + j, nw, start);
   };
   auto tag_of = [&](uint32_t h) -> uint32_t { return staged ? tag_l[h] : P.tag[h]; };
   auto pp_of = [&](uint32_t h) -> uint32_t { return staged ? pp_l[h] : P.pp[h]; };
@@ -412,8 +521,12 @@ __device__ __forceinline__ void resolve_role(const PmStep& S, uint32_t p, Resolv
         const PmSub sub = step_sub(S, b0 + j);
         uint32_t c1 = kNone, c2 = kNone, t1 = 0, p1 = 0, t2 = 0, p2 = 0;
         if (sub.kind == SUB_REAL && sub.idx < P.N) {
-          const PM_G uint32_t* cr = S.cand + (uint64_t)(b0 + j) * S.cblk * 6;
-          const uint32_t v = lane < nblk * 6 ? ld32<SC1>(cr + lane) : kNone;
+          uint32_t v = kNone;
+          if (GRAN) {
+            if (lane < 6) v = get_g(S.recg + (uint64_t)(b0 + j) * G_REC + lane, S);
+          } else if (lane < nblk * 6) {
+            v = S.cand[(uint64_t)(b0 + j) * S.cblk * 6 + lane];
+          }
           for (uint32_t k = 0; k < 2 * nblk && c2 == kNone; ++k) {   // uniform
             const uint32_t h = __builtin_amdgcn_readlane(v, 3 * k);
             if (h == kNone) { k |= 1; continue; }                    // rest of this block is empty
@@ -432,11 +545,23 @@ __device__ __forceinline__ void resolve_role(const PmStep& S, uint32_t p, Resolv
       PmSub sub{0, SUB_NONE, 0};
       if (k < n) sub = step_sub(S, b0 + k);
       const bool valid = k < n && sub.kind == SUB_REAL && sub.idx < P.N;
-      const uint32_t h0 = valid ? ld32<SC1>(S.meta + 2 * (uint64_t)(b0 + k)) : 0;
-      const uint32_t sg = valid ? ld32<SC1>(S.meta + 2 * (uint64_t)(b0 + k) + 1) : kNone;
+      uint32_t h0 = 0, sg = kNone;
+      if (valid) {
+        if (GRAN) {
+          h0 = get_g(S.recg + (uint64_t)(b0 + k) * G_REC + 6, S);
+          sg = get_g(S.recg + (uint64_t)(b0 + k) * G_REC + 7, S);
+        } else {
+          h0 = S.meta[2 * (uint64_t)(b0 + k)];
+          sg = S.meta[2 * (uint64_t)(b0 + k) + 1];
+        }
+      }
       for (uint32_t e0 = 0; e0 < n * n; e0 += 64) {   // spec_v[kk][j], kk < j
-        const uint32_t e = e0 + lane, kk = e / n, j = e % n;
-        if (e < n * n && kk < j) spec_v[kk * kSpecSubs + j] = (uint16_t)ld32<SC1>(S.spec + (uint64_t)(b0 + kk) * kSpecSubs + j);
+        const uint32_t e = e0 + lane, kk = (e / n) & 63, j = e % n;
+        // written by real sub-queries' match workgroups only (never read for others)
+        const bool rk = __shfl(sub.kind, kk) == SUB_REAL;
+        if (e < n * n && kk < j && rk)
+          spec_v[kk * kSpecSubs + j] = (uint16_t)(GRAN ? get_g(S.specg + (uint64_t)(b0 + kk) * kSpecSubs + j, S)
+                                                       : S.spec[(uint64_t)(b0 + kk) * kSpecSubs + j]);
       }
       if (k < n) {
         s_kind[k] = sub.kind; s_idx[k] = sub.idx; s_chunk[k] = (uint32_t)(sub.idx >> lg); s_st[k] = kNone;
@@ -464,7 +589,7 @@ __device__ __forceinline__ void resolve_role(const PmStep& S, uint32_t p, Resolv
   #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint32_t i = tid + u * NT;
-        if (i < nb) bv[u] = ld64<SC1>(S.bits + (uint64_t)(b0 + i / nw) * S.words + (i % nw));
+        if (i < nb) bv[u] = S.bits[(uint64_t)(b0 + i / nw) * S.words + (i % nw)];
         if (i < ph4) {
           tv[u] = reinterpret_cast<const PM_G u32x4*>(P.tag)[i];
           pv[u] = reinterpret_cast<const PM_G u32x4*>(P.pp)[i];
@@ -711,7 +836,7 @@ __device__ __forceinline__ void resolve_role(const PmStep& S, uint32_t p, Resolv
     // --- flush (one writer per result / hint / chunk) -----------------------
     if (in) {
       const bool ok = st == ST_OK;
-      st_res<SC1>(S.res + b0 + k, PmRes{st, ok ? rhit : 0u, ok ? ch : 0u, ok ? ring : 0u, ok ? rtag : 0u,
+      put_res<GRAN>(S, b0 + k, PmRes{st, ok ? rhit : 0u, ok ? ch : 0u, ok ? ring : 0u, ok ? rtag : 0u,
                             ok ? rpp : 0u, (ok || st == ST_DUP || st == ST_CACHED) ? rslot : 0u, ok ? rfl : 0u});
     }
     if (k < nmod) { P.tag[mh] = mt; P.pp[mh] = mp; }
@@ -721,7 +846,7 @@ __device__ __forceinline__ void resolve_role(const PmStep& S, uint32_t p, Resolv
     if (last) P.hist[ch] = ring + 1;
     if (nchain) {   // this partition's chained sub-queries, contiguous and in order
       uint32_t pos = 0;
-      if (k == 0) pos = atomicAdd(&S.done[1], nchain);
+      if (k == 0) pos = atomicAdd(&S.done[2], nchain);
       pos = __builtin_amdgcn_readfirstlane(pos);
       if (k < nchain) S.done[3 + pos + k] = cl;
     }
@@ -842,7 +967,7 @@ __device__ __forceinline__ void resolve_role(const PmStep& S, uint32_t p, Resolv
     if (j < 32) STAMP(4 + j);
   }
   // --- flush (pir.go:460-470 refresh; one writer per hint / chunk) ----------
-  for (uint32_t k = lane; k < n; k += 64) st_res<SC1>(S.res + b0 + k, s_res[k]);
+  for (uint32_t k = lane; k < n; k += 64) put_res<GRAN>(S, b0 + k, s_res[k]);
   for (uint32_t k = lane; k < nmod; k += 64) {
     P.tag[m_h[k]] = m_tag[k];
     P.pp[m_h[k]] = m_pp[k];
@@ -856,7 +981,7 @@ __device__ __forceinline__ void resolve_role(const PmStep& S, uint32_t p, Resolv
   }
   if (nchain) {   // this partition's chained sub-queries, contiguous and in order
     uint32_t pos = 0;
-    if (lane == 0) pos = atomicAdd(&S.done[1], nchain);
+    if (lane == 0) pos = atomicAdd(&S.done[2], nchain);
     pos = __builtin_amdgcn_readfirstlane(pos);
     for (uint32_t k = lane; k < nchain; k += 64) S.done[3 + pos + k] = s_chain[k];
   }
@@ -874,7 +999,7 @@ __global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
   resolve_role<LDS ? 1 : 0, kBlock, false>(S, p, L);
   __syncthreads();
   // last add here: no answer workgroup is involved in a chain, nothing to decode
-  if (L.fin && threadIdx.x == 0) { S.done[0] = 0; S.done[1] = 0; }
+  if (L.fin && threadIdx.x == 0) chain_rearm(S);
 }
 
 // L2Dist of the first `dim` floats of an LDS row against q (device), one
@@ -919,9 +1044,10 @@ enum : uint32_t { A_ZERO = 0, A_FINAL = 1, A_CHAINED = 2, A_CACHED = 3, A_DUMMY 
 
 // Decode one chained sub-query (its hint was refreshed earlier in this step)
 // once every earlier refresh is visible; the whole workgroup participates.
+template <bool GRAN>
 __device__ void decode_chained(const PmStep& S, uint32_t s, RowBuf& row) {
   const PmSub sub = step_sub(S, s);
-  const PmRes r = S.res[s];
+  const PmRes r = res_after_acquire<GRAN>(S, s);
   const PmPart& P = S.parts[sub.part];
   const uint32_t E = S.E, EX = E & ~3u, tid = threadIdx.x;
   const uint64_t slot = (uint64_t)r.chunk * P.Qpc + r.ing;
@@ -951,14 +1077,16 @@ __device__ void decode_chained(const PmStep& S, uint32_t s, RowBuf& row) {
 
 // The finisher of a step (see resolver_count), after its acquire: decodes the
 // chained sub-queries in list order and re-arms the counters.  Whole workgroup.
+template <bool GRAN>
 __device__ void finish_step(const PmStep& S, RowBuf& row) {
-  const uint32_t nchain = S.done[1];
-  for (uint32_t k = 0; k < nchain; ++k) decode_chained(S, S.done[3 + k], row);
-  if (threadIdx.x == 0) { S.done[0] = 0; S.done[1] = 0; }
+  const uint32_t nchain = S.done[2];
+  for (uint32_t k = 0; k < nchain; ++k) decode_chained<GRAN>(S, S.done[3 + k], row);
+  if (threadIdx.x == 0) chain_rearm(S);
 }
 
 template <int NT>
 struct AnswerLds {
+  uint32_t f[17];   // k_step: granule fields, per-wave first candidates, predicted index
   uint32_t qo[kMaxSSLds];
   uint64_t red[NT * 2];
   __attribute__((aligned(16))) RowBuf row;
@@ -973,7 +1101,7 @@ __device__ __forceinline__ uint32_t answer_mode(const PmRes& r) {
        : r.status == ST_DUMMY ? A_DUMMY : A_ZERO;
 }
 
-// One sub-query's answer (HOT LOOPs D + E, decode, outputs).  SC1: inside
+// One sub-query's answer (HOT LOOPs D + E, decode, outputs).  GRAN: inside
 // k_step.  There the answer starts before its partition's resolver is done:
 // a dummy sub-query's set does not depend on the resolution at all, and a
 // real one's usually is the one its first stale candidate gives (hint c1 with
@@ -982,7 +1110,7 @@ __device__ __forceinline__ uint32_t answer_mode(const PmRes& r) {
 // rows gathered and the decode operands loaded for that guess while the
 // resolver runs; its result then either equals the guess in every field the
 // answer reads (kept) or the work is redone for the actual result.
-template <int W, bool SC1, int NT>
+template <int W, bool GRAN, int NT>
 __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, AnswerLds<NT>& L) {
   uint32_t* const qo = L.qo;
   uint64_t* const red = L.red;
@@ -1074,7 +1202,7 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, AnswerL
   };
   PmRes r;
   uint32_t mode;
-  if (SC1) {
+  if (GRAN) {
     // ---- the guess (see above), from this sub-query's match record ---------
     PmRes g{kNone, 0, 0, 0, 0, 0, 0, 0};
     uint32_t gmode = kNone;
@@ -1082,15 +1210,49 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, AnswerL
       g.status = ST_DUMMY;
       gmode = A_DUMMY;
     } else if (sub.kind == SUB_REAL && sub.idx < P.N) {
-      if (tid == 0)
-        while (ld32<true>(S.mflag + s * kHandStride) != S.token) __builtin_amdgcn_s_sleep(1);
+      // first stale candidate, found here over every hint (the match role's
+      // predicate and state; one tag load and one PRF gather per hint), so
+      // the guess never waits for the match workgroup
+      constexpr int HPT = kLdsPH / NT;   // k_step: PH <= kLdsPH
+      const uint32_t ch = (uint32_t)(sub.idx >> lg), off = (uint32_t)(sub.idx & mask);
+      const uint32_t wave = tid >> 6, lane = tid & 63;
+      uint32_t tg[HPT], pv[HPT], rv[HPT];
+#pragma unroll
+      for (int u = 0; u < HPT; ++u) {
+        const uint32_t h = u * NT + tid;
+        tg[u] = 0; pv[u] = kDefaultProgramPoint;
+        if (h < P.PH) { tg[u] = P.tag[h]; pv[u] = P.pp[h]; }
+      }
+      const uint32_t h0k = wave == 0 ? P.hist[ch] : 0;
+#pragma unroll
+      for (int u = 0; u < HPT; ++u) rv[u] = u * NT + tid < P.PH ? P.tab[(uint64_t)ch * P.H + tg[u]] : kNone;
+      // per wave the lowest matching hint (lower u first: hints u*NT + tid)
+      uint32_t wh = kNone, wt = 0, wp = 0;
+#pragma unroll
+      for (int u = 0; u < HPT; ++u) {
+        const bool m = rv[u] == off && (pv[u] == kDefaultProgramPoint || (pv[u] >> lg) != ch);
+        const uint64_t bm = __ballot(m);
+        if (bm && wh == kNone) {
+          const uint32_t l = (uint32_t)__builtin_ctzll(bm);
+          wh = u * NT + wave * 64 + l;
+          wt = __builtin_amdgcn_readlane(tg[u], l);
+          wp = __builtin_amdgcn_readlane(pv[u], l);
+        }
+      }
+      if (lane == 0) { L.f[wave] = wh; L.red[2 * wave] = wt; L.red[2 * wave + 1] = wp; }
+      if (wave == 0) {
+        const uint32_t pb0 = step_sb(S, sub.part), pn = step_sb(S, sub.part + 1) - pb0;
+        PmSub st;
+        bool validt;
+        const uint32_t sg0 = predict_ing(S, P, pb0, pn, s - pb0, ch, h0k, st, validt);
+        if (lane == 0) L.f[16] = sg0;
+      }
       __syncthreads();
-      const PM_G uint32_t* cr = S.cand + (uint64_t)s * 6;   // one record per sub-query (cblk 1)
-      const uint32_t c1 = __builtin_amdgcn_readfirstlane(ld32<true>(cr));
-      const uint32_t t1 = __builtin_amdgcn_readfirstlane(ld32<true>(cr + 1));
-      const uint32_t p1 = __builtin_amdgcn_readfirstlane(ld32<true>(cr + 2));
-      const uint32_t sg = __builtin_amdgcn_readfirstlane(ld32<true>(S.meta + 2 * (uint64_t)s + 1));
-      const uint32_t ch = (uint32_t)(sub.idx >> lg);
+      uint32_t c1 = kNone, t1 = 0, p1 = 0;
+      const uint32_t sg = L.f[16];
+      for (uint32_t w = 0; w < NT / 64; ++w)
+        if (L.f[w] < c1) { c1 = L.f[w]; t1 = (uint32_t)L.red[2 * w]; p1 = (uint32_t)L.red[2 * w + 1]; }
+      __syncthreads();
       if (c1 != kNone && sg < P.Qpc && ch < P.SS) {
         g = PmRes{ST_OK, c1, ch, sg, t1, p1, 0, 0};
         gmode = A_FINAL;
@@ -1098,21 +1260,21 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, AnswerL
     }
     if (gmode != kNone) gather(g, gmode);
     TS(1);
-    // ---- the resolver's results of this step (sc1 poll, then sc1 loads) ----
-    if (tid == 0)
-      while (ld32<true>(S.ready + sub.part * kHandStride) != S.token) __builtin_amdgcn_s_sleep(1);
+    // ---- the resolver's record of this sub-query ----------------------------
+    if (tid < G_RES) L.f[tid] = get_g(S.resg + (uint64_t)s * G_RES + tid, S);
     __syncthreads();
-    r = ld_res<true>(S.res + s);
+    r = PmRes{L.f[0], L.f[1], L.f[2], L.f[3], L.f[4], L.f[5], L.f[6], L.f[7]};
     mode = answer_mode(r);
     const bool kept = mode == gmode &&
                       (mode == A_DUMMY || (r.hit == g.hit && r.chunk == g.chunk && r.ing == g.ing &&
                                            r.tag == g.tag && r.pp == g.pp));
+    TS_SEEN(kept ? 1u : 0u);
     if (!kept) {
       e_rv = e_bp = e_pp = 0;
       gather(r, mode);
     }
   } else {
-    r = ld_res<false>(S.res + s);
+    r = S.res[s];
     mode = answer_mode(r);
     gather(r, mode);
   }
@@ -1166,8 +1328,7 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, AnswerL
   if (tid == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t prev = __hip_atomic_fetch_add(&S.done[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    L.s_last = (prev + 1 == S.np_live);
+    L.s_last = (uint32_t)chain_add(S, 1);
     if (L.s_last) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1175,7 +1336,7 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, AnswerL
   }
   __syncthreads();
   if (!L.s_last) return;
-  finish_step(S, row);
+  finish_step<GRAN>(S, row);
 }
 
 template <int W>
@@ -1186,17 +1347,14 @@ __global__ void __launch_bounds__(kAnsBlock) k_answer(PmStep S) {
 
 // ---- k_step: the step in one launch ---------------------------------------
 // Workgroups [0, nsub) match one sub-query each (all its hints), the next np
-// resolve one partition each, the last nsub answer one sub-query each.
-// Dispatch is in workgroup order and a role only waits for lower-numbered
-// ones (resolver: its partition's match workgroups, counted in cnt[p];
-// answer: its resolver's ready[p] == token), so the lowest unfinished
-// workgroup can always run.  At most 240 workgroups of 1024 threads whose LDS
-// admits one per CU: the envelope the sc1 hand-off form of MI355X_MICROARCH.md
-// is measured in.  Producer: sc1 stores, every wave drains (vmcnt(0)),
-// barrier, one lane's counter add / flag store; consumer: sc1 poll, barrier,
-// sc1 loads.
+// resolve one partition each, the last nsub answer one sub-query each.  Every
+// hand-off is a set of granules (put_g / get_g): a resolver polls its
+// partition's match records, an answer workgroup its own match record (for
+// its guess) and then its resolution record.  Dispatch is in workgroup order
+// and a role only waits for lower-numbered ones, so the lowest unfinished
+// workgroup can always run; at most 240 workgroups of 1024 threads whose LDS
+// admits one per CU, the envelope the hand-off forms are measured in.
 constexpr int kStepBlock = 1024, kStepHPT = kLdsPH / kStepBlock;
-constexpr uint32_t kLine = kHandStride;   // counters / flags one per 256-B line
 union StepLds {
   uint32_t s_cand[kStepBlock / 64][6];
   ResolveLds<2> r;
@@ -1218,37 +1376,21 @@ __global__ void __launch_bounds__(kStepBlock) k_step(PmStep S) {
               __builtin_amdgcn_readfirstlane((uint32_t)sub.idx);
     match_role<kStepBlock, kStepHPT, true>(S, b, 0, sub, L.s_cand);
     TS(1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __hip_atomic_fetch_add(S.cnt + sub.part * kLine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      st32<true>(S.mflag + b * kLine, S.token);   // this sub-query's record, for its answer's guess
-    }
-    TS(2);
     return;
   }
   if (b < S.nsub + S.np) {
-    const uint32_t p = b - S.nsub, n = S.sb_a[p + 1] - S.sb_a[p];
-    if (n == 0) return;
-    if (threadIdx.x == 0) {
-      while (ld32<true>(S.cnt + p * kLine) != n) __builtin_amdgcn_s_sleep(1);
-      st32<true>(S.cnt + p * kLine, 0);   // every match workgroup of this step is in: re-armed
-    }
-    __syncthreads();
-    TS(1);
+    const uint32_t p = b - S.nsub;
+    if (S.sb_a[p + 1] == S.sb_a[p]) return;
     resolve_role<2, kStepBlock, true>(S, p, L.r);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    const uint32_t fin = L.r.fin;
-    if (threadIdx.x == 0) st32<true>(S.ready + p * kLine, S.token);
     TS(2);
-    if (!fin) return;
+    if (!L.r.fin) return;
     if (threadIdx.x == 0) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();   // L.r is dead from here: its space holds the decode row
-    finish_step(S, L.a.row);
+    finish_step<true>(S, L.a.row);
     return;
   }
   answer_role<W, true, kStepBlock>(S, b - S.nsub - S.np, L.a);
@@ -1282,7 +1424,7 @@ void step_answer(hipStream_t st, const PmStep& S, PmEvents ev) {
   else PM_LAUNCH(ev, k_answer<1>, dim3(S.nsub), dim3(kAnsBlock), st, S);
 }
 bool step_fused_ok(const PmStep& S, uint32_t maxPH, uint32_t max_sub_per_part) {
-  return S.args_valid && S.cnt && S.ready && max_sub_per_part <= kSpecSubs && maxPH <= kLdsPH &&
+  return S.args_valid && S.recg && S.err_h && max_sub_per_part <= kSpecSubs && maxPH <= kLdsPH &&
          2 * S.nsub + S.np <= 256;
 }
 void step_fused(hipStream_t st, const PmStep& S, PmEvents ev) {

@@ -5,9 +5,10 @@ Build the PM_STEP_STAMPS variant here (it travels with the snapshot):
 then on the GPU box:
     PM_LIB=pacmann_amd/libpacmann_ststamps.so PM_STAMP_FILE=gpurun_out/st.bin \\
         python tools/step_stamps.py --run && python tools/step_stamps.py --show gpurun_out/st.bin
-Stamps are s_memrealtime (100 MHz) per workgroup: 0 start, 1 after its wait
-(match: after the role), 2 end; 3: XCC_ID << 32 | HW_ID.  Workgroups: nsub
-match, np resolvers, nsub answers.
+Stamps are s_memrealtime (100 MHz) per workgroup: 0 start, 1 (match: role
+end; answer: guess done), 2 end; 3: XCC_ID << 32 | HW_ID (answer: resolution
+seen << 1 | guess kept); then per workgroup the match phases (tags in,
+gathers in, ballots done).  Workgroups: nsub match, np resolvers, nsub answers.
 """
 import os
 import subprocess
@@ -45,19 +46,28 @@ def show(fn):
     while off < raw.size:
         grid, nsub, cblk, np_ = raw[off:off + 16].view(np.uint32)
         off += 16
-        t = raw[off:off + grid * 32].view(np.uint64).reshape(grid, 4)
-        off += grid * 32
+        t8 = raw[off:off + grid * 64].view(np.uint64)
+        off += grid * 64
+        t, ms = t8[:grid * 4].reshape(grid, 4), t8[grid * 4:].reshape(grid, 4)
         t0 = t[:, 0][t[:, 0] > 0].min()
         rel = np.where(t[:, :3] > 0, t[:, :3].astype(np.int64) - t0, -1) * 10 / 1000.0   # us
         m, r, a = rel[:nsub], rel[nsub:nsub + np_], rel[nsub + np_:]
         live = r[:, 0] >= 0
-        rows.append([m[:, 0].max(), np.median(m[:, 1]), m[:, 1].max(), m[:, 2].max(),
-                     r[live, 1].max(), np.median(r[live, 2] - r[live, 1]), r[live, 2].max(),
-                     a[:, 1].max(), np.median(a[:, 2] - a[:, 1]), a[:, 2].max()])
+        seen = t[nsub + np_:, 3]
+        a_seen = ((seen >> 1).astype(np.int64) - int(t0)) * 0.01
+        kept = (seen & 1).astype(bool)
+        mrel = (ms[:nsub, :3].astype(np.int64) - int(t0)) * 0.01
+        rows.append([np.median(mrel[:, 0]), np.median(mrel[:, 1]), np.median(mrel[:, 2]),
+                     m[:, 0].max(), np.median(m[:, 1]), m[:, 1].max(),
+                     np.median(r[live, 2]), r[live, 2].max(),
+                     a[:, 1].max(), a_seen.max(), np.median((a[:, 2] - a_seen)[kept]) if kept.any() else 0,
+                     np.median((a[:, 2] - a_seen)[~kept]) if (~kept).any() else 0, kept.mean(), a[:, 2].max()])
     rows = np.array(rows[10:])
-    names = ["match last start", "match median role end", "match last role end", "match last counted",
-             "resolver last poll done", "resolver median body", "resolver last end", "answer last poll done",
-             "answer median body", "answer last end"]
+    names = ["match median tags in", "match median gathers in", "match median ballots done",
+             "match last start", "match median role end", "match last role end",
+             "resolver median end", "resolver last end", "answer last guess done",
+             "answer last result seen", "answer after result, kept", "answer after result, redone",
+             "answer fraction kept", "answer last end"]
     print(f"{len(rows)} steps; us since the first workgroup start (median / p10 / p90)")
     for i, n in enumerate(names):
         print(f"  {n:26s} {np.median(rows[:, i]):7.2f} {np.percentile(rows[:, i], 10):7.2f} "
