@@ -156,6 +156,10 @@ struct pm_ctx {
   hipStream_t stream = nullptr;
   int timing = 0;   // 0 off, 1 preprocessing / leaf kernels, 2 also the per-step kernels
   bool no_fuse = false;      // PM_NO_FUSE=1: the three step kernels even when k_step fits
+  bool no_guess = false;
+  bool verify_rows = false;
+  bool debug_cache = false;
+  bool log_steps = false;    // PM_LOG_STEPS=1: one stderr line per sub-query per step  // PM_DEBUG_CACHE=1: check cached answers against the slot's first answer  // PM_VERIFY_ROWS=1: re-read each step's results after the stream drains     // PM_NO_GUESS=1: k_step answers do not start before their resolution
   bool debug_sync = false;   // PM_DEBUG_SYNC=1: synchronise after every launch (fault triage)
   std::string last_kernel;
   // host-side wall-clock accumulators ("host_*" names in pm_timing_get)
@@ -218,6 +222,14 @@ extern "C" int pm_ctx_create(int device, pm_ctx** out) {
   c->debug_sync = dbg && dbg[0] == '1';
   const char* nf = getenv("PM_NO_FUSE");
   c->no_fuse = nf && nf[0] == '1';
+  const char* ls = getenv("PM_LOG_STEPS");
+  c->log_steps = ls && ls[0] == '1';
+  const char* dc = getenv("PM_DEBUG_CACHE");
+  c->debug_cache = dc && dc[0] == '1';
+  const char* vr = getenv("PM_VERIFY_ROWS");
+  c->verify_rows = vr && vr[0] == '1';
+  const char* ng = getenv("PM_NO_GUESS");
+  c->no_guess = ng && ng[0] == '1';
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e != hipSuccess) { delete c; return fail(PM_EHIP, hipGetErrorString(e)); }
   *out = c;
@@ -266,6 +278,7 @@ struct PartHost {
   uint64_t epoch_ctr = 0, fqn = 0, dummy_ctr = 0;
   uint64_t maxq64 = 0;
   FlatMap cache;   // localCache (pir.go:120): idx -> arena slot
+  std::unordered_map<uint64_t, std::vector<uint64_t>> shadow;   // PM_DEBUG_CACHE: slot -> row the host got
 };
 
 struct Engine {
@@ -488,6 +501,7 @@ static int engine_prep(Engine* g, uint64_t p0, uint64_t p1) {
     pm_expand_key(key, ph.d.rk);
     ph.fqn = 0;
     ph.cache.clear();
+    ph.shadow.clear();
   }
   CHK(upload_parts(g));
   const PmPart* dp = p1 - p0 == 1 ? g->parts_d.as<PmPart>() + p0 : g->owned_d.as<PmPart>();
@@ -545,12 +559,21 @@ static int wait_step(pm_ctx* c, const PmOutHdr* hdr, uint32_t nsub, uint32_t tok
     const size_t stride = sizeof(PmOutHdr) / sizeof(uint32_t);
     auto t0 = Clock::now();
     uint32_t s = 0;
+    const size_t w0 = pf_off / 8, w1 = (pf_off + pf_len + 7) / 8;
     for (uint64_t spin = 0; s < nsub; ++spin) {
       if (tok[s * stride] == token) {
         if (c->timing && s == 0) c->host_add(HT_WAIT_FIRST, ms_since(t0));
+        // the row words this caller reads must have landed: their XOR is in the header
+        const volatile uint64_t* rw = (const volatile uint64_t*)(rows + s * row_bytes);
+        const volatile uint64_t* cs = &hdr[s].csum;
+        uint64_t x = token * kCsumMix;
+        for (size_t w = w0; w < w1; ++w) x ^= rw[w];
+        if (x != *cs) {
+          if ((spin & 0xffff) == 0xffff && ms_since(t0) > 5000.0)
+            return fail(PM_EHIP, "step results incomplete (sub-query " + std::to_string(s) + ")");
+          continue;
+        }
         if (c->timing && s + 1 == nsub) c->host_add(HT_WAIT_ALL, ms_since(t0));
-        const char* r = rows + s * row_bytes + pf_off;
-        for (size_t b = 0; b < pf_len; b += 64) __builtin_prefetch(r + b);
         ++s;
         continue;
       }
@@ -573,15 +596,55 @@ static int wait_and_post(Engine* g, const PmStep& S, uint32_t nsub, Clock::time_
   pm_ctx* c = g->ctx;
   const uint64_t E = g->E;
   auto t_wait = Clock::now();
-  CHK(wait_step(c, S.hdr_h, nsub, S.token, (const char*)S.rows_h, E * 8, g->pf_off,
-                std::min<size_t>(g->pf_len, E * 8 - std::min<size_t>(g->pf_off, E * 8))));
+  CHK(wait_step(c, S.hdr_h, nsub, S.token, (const char*)S.rows_h, E * 8, (size_t)S.pf_w0 * 8,
+                (size_t)(S.pf_w1 - S.pf_w0) * 8));
   c->host_add(HT_STEP_WAIT, ms_since(t_wait));
 
+  if (c->verify_rows) {   // diagnostics: what the host saw at token time vs after the stream drains
+    std::vector<uint64_t> seen((const uint64_t*)S.rows_h, (const uint64_t*)S.rows_h + (uint64_t)nsub * E);
+    std::vector<PmOutHdr> hseen(S.hdr_h, S.hdr_h + nsub);
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (uint32_t s = 0; s < nsub; ++s) {
+      const bool rd = memcmp(seen.data() + (uint64_t)s * E, (const uint64_t*)S.rows_h + (uint64_t)s * E, E * 8) != 0;
+      const bool hd = memcmp(&hseen[s], &S.hdr_h[s], sizeof(PmOutHdr)) != 0;
+      if (rd || hd)
+        fprintf(stderr, "[pm] verify: token %u sub %u status %u: %s%s changed after the token was seen\n", S.token, s,
+                S.hdr_h[s].status, rd ? "row " : "", hd ? "header " : "");
+    }
+  }
   auto t_post = Clock::now();
   g->hdr = S.hdr_h;
   g->rows = S.rows_h;
   // host mirrors: FinishedQueryNum and the localCache index (pir.go:469-470);
   // in-step cache hits copy the earlier response
+  if (c->log_steps) {   // diagnostics: every sub-query of the step
+    for (uint32_t s = 0; s < nsub; ++s)
+      fprintf(stderr, "[pm] step %p tok %u s %u part %u kind %u idx %lu -> st %u ref %u row0 %016lx\n", (void*)g,
+              S.token, s, g->subs[s].part, g->subs[s].kind, (unsigned long)g->subs[s].idx, g->hdr[s].status,
+              g->hdr[s].ref, (unsigned long)g->rows[(uint64_t)s * E]);
+  }
+  if (c->debug_cache) {   // diagnostics: cached answers against the rows the host got for their slots
+    for (uint32_t s = 0; s < nsub; ++s) {
+      const PmOutHdr& h = g->hdr[s];
+      PartHost& ph = g->parts[g->subs[s].part];
+      const uint64_t* row = g->rows + (uint64_t)s * E;
+      if (h.status == ST_OK) ph.shadow[h.ref].assign(row, row + E);
+      if (h.status == ST_CACHED) {
+        auto it = ph.shadow.find(h.ref);
+        if (it == ph.shadow.end() || memcmp(it->second.data(), row, E * 8) != 0) {
+          HIPCHK(hipStreamSynchronize(c->stream));
+          std::vector<uint64_t> dev(E);
+          HIPCHK(hipMemcpy(dev.data(), ph.d.arena + (uint64_t)h.ref * E, E * 8, hipMemcpyDeviceToHost));
+          const bool dev_ok = it != ph.shadow.end() && memcmp(it->second.data(), dev.data(), E * 8) == 0;
+          fprintf(stderr, "[pm] cache: token %u sub %u part %u idx %lu slot %u: row differs from the slot's answer%s; "
+                  "device arena now %s the slot's answer; row[0] %016lx shadow[0] %016lx arena[0] %016lx\n",
+                  S.token, s, g->subs[s].part, (unsigned long)g->subs[s].idx, h.ref,
+                  it == ph.shadow.end() ? " (no answer recorded)" : "", dev_ok ? "equals" : "differs from",
+                  (unsigned long)row[0], (unsigned long)(it == ph.shadow.end() ? 0 : it->second[0]), (unsigned long)dev[0]);
+        }
+      }
+    }
+  }
   for (uint32_t s = 0; s < nsub; ++s) {
     const PmOutHdr& h = g->hdr[s];
     if (h.status == ST_OK) {
@@ -668,6 +731,12 @@ static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
   S.args_valid = (nsub <= kArgSubs && g->P <= kArgParts) ? 1u : 0u;
   if (++g->step_token == 0) ++g->step_token;   // 0 never marks a published header
   S.token = g->step_token;
+  {   // row words the consumer reads: checksummed in the header (PmOutHdr)
+    const size_t off = std::min<size_t>(g->pf_off, E * 8);
+    const size_t end = std::min<size_t>(E * 8, off + std::min<size_t>(g->pf_len, E * 8));
+    S.pf_w0 = (uint32_t)(off / 8);
+    S.pf_w1 = (uint32_t)((end + 7) / 8);
+  }
   if (S.args_valid) {
     memcpy(S.subs_a, g->subs.data(), dsub);
     memcpy(S.sb_a, g->sb.data(), (g->P + 1) * 4);
@@ -691,6 +760,7 @@ static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
   // Timing level 2: the kernels carry their events in their own dispatch packets.
   if (!c->no_fuse && !c->debug_sync && pmk::step_fused_ok(S, g->maxPH, max_per_part)) {
     S.cblk = 1;   // one match workgroup per sub-query
+    S.no_guess = c->no_guess ? 1u : 0u;
 #ifdef PM_STEP_STAMPS
     const uint32_t grid = 2 * nsub + (uint32_t)g->P;
     CHK(g->stamps.reserve((uint64_t)grid * 8 * 8));

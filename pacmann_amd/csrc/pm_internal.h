@@ -91,10 +91,19 @@ struct PmRes {
 // Per-sub-query result header, written by the GPU into pinned host memory.
 // One 16-byte store: the step token is written together with the rest, after
 // the row of the sub-query has drained; the host polls it (no stream sync).
+// Result header of one sub-query in pinned host memory.  The device's row
+// writes and this header reach the host in no guaranteed order (a token seen
+// does not mean the row's bytes have landed, measured), so the header also
+// carries the XOR of the row words the host will read ([pf_w0, pf_w1) of
+// PmStep) mixed with the step token (a stale checksum never matches a stale
+// row): the host waits until the row it reads matches.  {status, ref, dist,
+// token} are one 16-B store.
+constexpr uint64_t kCsumMix = 0x9E3779B97F4A7C15ull;
 struct alignas(16) PmOutHdr {
   uint32_t status, ref;
   float dist;
   uint32_t token;
+  uint64_t csum, pad;
 };
 // Arguments of the step kernels (pm_query.hip).
 #ifndef PM_KARG_SUBS
@@ -130,6 +139,8 @@ struct PmStep {
   PM_G uint32_t* err_h;        // pinned host: set when a hand-off spin timed out        // [np] k_step: token of the step whose results the resolver published
   uint32_t words, E, dim, nsub, np, cblk;
   uint32_t np_live;            // partitions with at least one sub-query in this step
+  uint32_t pf_w0, pf_w1;       // row words the host reads (PmOutHdr::csum covers them)
+  uint32_t no_guess;           // k_step diagnostics: answers wait for their resolution (PM_NO_GUESS=1)
   // Small steps ship the descriptor inside the kernel arguments (no PCIe
   // round trip); larger ones use subs_h / sb_h.
   uint32_t args_valid;

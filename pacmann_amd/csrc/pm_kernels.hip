@@ -22,6 +22,12 @@ __device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
 // ---------------------------------------------------------------------------
 constexpr int kOffsChunksPerBlock = 16;
 
+// Initial PRF tables of every hint h < H (its tag is h) at 16 chunks per
+// workgroup, written chunk-major (hint search) and hint-major (set
+// expansion).  Bound by the AES T-table lookups in LDS: the hint-major stores
+// are scattered 2-B writes (every lane on its own line, ~5x their bytes in
+// HBM write traffic), yet staging them through LDS made the kernel 20-25 %
+// slower (375 -> 450-470 us at SIFT1M shape), so they stay direct.
 __global__ void __launch_bounds__(kBlock) k_prep_offsets(const PmPart* __restrict__ parts) {
   __shared__ uint32_t te[kTeLdsWords];
   const PmPart& P = parts[blockIdx.z];

@@ -81,18 +81,15 @@ constexpr uint32_t kNone = 0xffffffffu;
     if (threadIdx.x == 0 && S.stamps)                                                          \
       S.stamps[(uint64_t)blockIdx.x * 4 + 3] = (__builtin_amdgcn_s_memrealtime() << 1) | (kept); \
   } while (0)
-// match-role phases (k_step only): stamps[gridDim.x * 4 + blockIdx.x * 4 + i],
-// each after draining the loads it follows
-#define MS(i)                                                                              \
-  do {                                                                                     \
-    if (GRAN) {                                                                             \
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                    \
-      if (threadIdx.x == 0 && S.stamps)                                                    \
-        S.stamps[(uint64_t)gridDim.x * 4 + blockIdx.x * 4 + (i)] = __builtin_amdgcn_s_memrealtime(); \
-    }                                                                                      \
+// answer phases (k_step): stamps[gridDim.x * 4 + blockIdx.x * 4 + i], at
+// points that follow a barrier anyway (no added waits)
+#define AS(i)                                                                                \
+  do {                                                                                       \
+    if (GRAN && threadIdx.x == 0 && S.stamps)                                                \
+      S.stamps[(uint64_t)gridDim.x * 4 + blockIdx.x * 4 + (i)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 #else
-#define MS(i) do {} while (0)
+#define AS(i) do {} while (0)
 #define TS(i) do {} while (0)
 #define TS_HWID() do {} while (0)
 #define TS_SEEN(kept) do {} while (0)
@@ -255,10 +252,8 @@ __device__ __forceinline__ void match_role(const PmStep& S, uint32_t s, uint32_t
     tg[u] = 0; pv[u] = kDefaultProgramPoint;
     if (live && h < P.PH) { tg[u] = P.tag[h]; pv[u] = P.pp[h]; }
   }
-  MS(0);
 #pragma unroll
   for (int u = 0; u < kMatchHPT; ++u) rv[u] = row[tg[u]];
-  MS(1);
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (meta_wg && wave == 0) {
     // In-chunk index this sub-query gets if every earlier one of its partition
@@ -319,7 +314,6 @@ __device__ __forceinline__ void match_role(const PmStep& S, uint32_t s, uint32_t
       }
     }
   }
-  MS(2);
   if (lane == 0) {
     s_cand[wave][0] = h0; s_cand[wave][1] = t0; s_cand[wave][2] = p0;
     s_cand[wave][3] = h1; s_cand[wave][4] = t1; s_cand[wave][5] = p1;
@@ -1032,11 +1026,22 @@ union RowBuf {   // one decoded entry; the L2 reads its leading floats
 
 // Result header of sub-query s, once every thread's row stores have drained
 // (the host reads the row as soon as it sees the token).  Lane 0 holds `d`.
+// XOR of row words [pf_w0, pf_w1) (the LDS copy of what was written), for
+// PmOutHdr::csum.  Wave 0 only; lane 0 holds the result.
+__device__ __forceinline__ uint64_t row_csum(const PmStep& S, const RowBuf& row, bool has_row) {
+  uint64_t x = 0;
+  if (has_row)
+    for (uint32_t w = S.pf_w0 + (threadIdx.x & 63); w < S.pf_w1; w += 64) x ^= row.w[w];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x ^= __shfl_xor(x, o);
+  return x;
+}
+
 __device__ __forceinline__ void publish_hdr(const PmStep& S, uint32_t s, uint32_t status, uint32_t ref,
-                                            float d) {
+                                            float d, uint64_t csum) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) S.hdr_h[s] = PmOutHdr{status, ref, d, S.token};
+  if (threadIdx.x == 0) S.hdr_h[s] = PmOutHdr{status, ref, d, S.token, csum ^ (S.token * kCsumMix), 0};
 }
 
 // What a k_answer workgroup does for its sub-query.
@@ -1071,7 +1076,9 @@ __device__ void decode_chained(const PmStep& S, uint32_t s, RowBuf& row) {
   for (uint32_t w = tid; w < E; w += blockDim.x) { orow[w] = row.w[w]; ar[w] = row.w[w]; }
   float d = 0.0f;
   if (S.q && tid < 8) d = l2_lds(row.f, S.q, S.dim);
-  publish_hdr(S, s, r.status, r.slot, d);
+  uint64_t cs = 0;
+  if (tid < 64) cs = row_csum(S, row, true);
+  publish_hdr(S, s, r.status, r.slot, d, cs);
   __syncthreads();
 }
 
@@ -1149,6 +1156,7 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, AnswerL
     }
     STAMP_AT(stamp_wg && mode == A_FINAL, 49);
     __syncthreads();
+    AS(1);
     STAMP_AT(stamp_wg, 50);
     // ---- server XOR gather (HOT LOOP E) into row.w[0..EX) ------------------
     if (mode == A_FINAL || mode == A_CHAINED || mode == A_DUMMY) {
@@ -1206,7 +1214,8 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, AnswerL
     // ---- the guess (see above), from this sub-query's match record ---------
     PmRes g{kNone, 0, 0, 0, 0, 0, 0, 0};
     uint32_t gmode = kNone;
-    if (sub.kind == SUB_DUMMY) {
+    if (S.no_guess) {
+    } else if (sub.kind == SUB_DUMMY) {
       g.status = ST_DUMMY;
       gmode = A_DUMMY;
     } else if (sub.kind == SUB_REAL && sub.idx < P.N) {
@@ -1250,6 +1259,7 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, AnswerL
       __syncthreads();
       uint32_t c1 = kNone, t1 = 0, p1 = 0;
       const uint32_t sg = L.f[16];
+      AS(0);
       for (uint32_t w = 0; w < NT / 64; ++w)
         if (L.f[w] < c1) { c1 = L.f[w]; t1 = (uint32_t)L.red[2 * w]; p1 = (uint32_t)L.red[2 * w + 1]; }
       __syncthreads();
@@ -1315,7 +1325,9 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, AnswerL
     }
     float d = 0.0f;
     if (has_row && S.q && tid < 8) d = l2_lds(row.f, S.q, S.dim);
-    publish_hdr(S, s, r.status, r.slot, d);
+    uint64_t cs = 0;
+    if (tid < 64) cs = row_csum(S, row, has_row);
+    publish_hdr(S, s, r.status, r.slot, d, cs);
   }
   STAMP_AT(stamp_wg, 53);
   // ---- arrival: workgroups of refresh chains count in; the last one decodes

@@ -14,6 +14,18 @@ pytestmark = pytest.mark.gpu
 SEED = 20240501
 
 
+def mismatch_report(b, q, got, want, rows, masks=None):
+    """Which ids differ and how (zero row / the true row / other)."""
+    bad = np.where((got != want).any(axis=1))[0]
+    out = [f"batch {b}: {len(bad)} ids differ"]
+    for i in bad[:8]:
+        g = got[i]
+        kind = "zero" if not g.any() else ("db row" if (g == rows[int(q[i])]).all() else "other")
+        out.append(f"  pos {i} id {int(q[i])}: got {kind} {int(g[0]):016x}, want {'zero' if not want[i].any() else 'db row' if (want[i] == rows[int(q[i])]).all() else 'other'} {int(want[i][0]):016x}"
+                   + (f", masks {[bool(m[i]) for m in masks]}" if masks is not None else ""))
+    return "\n".join(out)
+
+
 def rand_db(n, e, seed=1):
     return np.random.default_rng(seed).integers(0, 2**64, size=n * e, dtype=np.uint64)
 
@@ -342,7 +354,18 @@ def test_batch_pir_shards(step_ctx, oracle, nshards):
         got = sum(p[0] for p in parts)
         ok = np.logical_or.reduce([p[1] for p in parts])
         want, _ = o.Query(q)
-        assert np.array_equal(got, want), b
+        if not np.array_equal(got, want):
+            state = []
+            for p in range(P):
+                a, o_ = shards[p % nshards].export_state(p), o.sub(p).export_state()
+                for k in STATE_KEYS:
+                    if not np.array_equal(a[k], o_[k]):
+                        x, y = np.asarray(a[k]).ravel(), np.asarray(o_[k]).ravel()
+                        d = np.where(x != y)[0] if x.shape == y.shape else np.array([-1])
+                        state.append(f"partition {p} {k}: {len(d)} entries differ, first at {d[:6].tolist()} "
+                                     f"(size {x.size})")
+            pytest.fail(mismatch_report(b, q, got, want, db.reshape(N, E), [p[1] for p in parts]) + "\n"
+                        + "\n".join(state or ["client state equal"]))
         assert not got[~ok].any(), b
     for k in ("FinishedBatchNum", "QueriesMadeInPartition", "SupportBatchNum", "PrepCount"):
         assert all(s.stats()[k] == o.stats()[k] for s in shards), k

@@ -7,8 +7,7 @@ then on the GPU box:
         python tools/step_stamps.py --run && python tools/step_stamps.py --show gpurun_out/st.bin
 Stamps are s_memrealtime (100 MHz) per workgroup: 0 start, 1 (match: role
 end; answer: guess done), 2 end; 3: XCC_ID << 32 | HW_ID (answer: resolution
-seen << 1 | guess kept); then per workgroup the match phases (tags in,
-gathers in, ballots done).  Workgroups: nsub match, np resolvers, nsub answers.
+seen << 1 | guess kept).  Workgroups: nsub match, np resolvers, nsub answers.
 """
 import os
 import subprocess
@@ -56,15 +55,16 @@ def show(fn):
         seen = t[nsub + np_:, 3]
         a_seen = ((seen >> 1).astype(np.int64) - int(t0)) * 0.01
         kept = (seen & 1).astype(bool)
-        mrel = (ms[:nsub, :3].astype(np.int64) - int(t0)) * 0.01
-        rows.append([np.median(mrel[:, 0]), np.median(mrel[:, 1]), np.median(mrel[:, 2]),
+        arel = (ms[nsub + np_:, :2].astype(np.int64) - int(t0)) * 0.01
+        okr = ms[nsub + np_:, 0] > 0
+        rows.append([np.median(arel[okr, 0]), arel[okr, 0].max(), np.median(arel[okr, 1]), arel[okr, 1].max(),
                      m[:, 0].max(), np.median(m[:, 1]), m[:, 1].max(),
                      np.median(r[live, 2]), r[live, 2].max(),
                      a[:, 1].max(), a_seen.max(), np.median((a[:, 2] - a_seen)[kept]) if kept.any() else 0,
                      np.median((a[:, 2] - a_seen)[~kept]) if (~kept).any() else 0, kept.mean(), a[:, 2].max()])
     rows = np.array(rows[10:])
-    names = ["match median tags in", "match median gathers in", "match median ballots done",
-             "match last start", "match median role end", "match last role end",
+    names = ["answer median scan done", "answer last scan done", "answer median set done",
+             "answer last set done", "match last start", "match median role end", "match last role end",
              "resolver median end", "resolver last end", "answer last guess done",
              "answer last result seen", "answer after result, kept", "answer after result, redone",
              "answer fraction kept", "answer last end"]
