@@ -75,6 +75,71 @@ def pmc_traffic(kernel_symbol: str):
     return best
 
 
+# BASELINE.json configs[2]: MS-MARCO-shaped batch PIR, the TestBatchPIRPerf
+# shape (pianopir/pir_test.go:204-275): 3,201,821 entries of 112 words, BatchSize
+# 32, FailureProbLog2 8, 300 batches of 32 uniform ids.
+C2_N, C2_E, C2_B, C2_BATCHES = 3_201_821, 112, 32, 300
+
+
+def batch_pir_msmarco(ctx, with_cpu: bool):
+    """Preprocessing time, then batch-query throughput, of the batch-PIR path at
+    the configs[2] shape, with the step kernel's answer-bytes roofline."""
+    import pacmann_amd as pm
+    db = np.random.default_rng(77).integers(0, 2**64, size=C2_N * C2_E, dtype=np.uint64)
+    g = pm.SimpleBatchPianoPIR(C2_N, C2_E * 8, C2_B, db, 8, seed=21, ctx=ctx)
+    ctx.sync()
+    t0 = time.perf_counter()
+    g.Preprocessing()
+    ctx.sync()
+    prep = time.perf_counter() - t0
+    rng = np.random.default_rng(78)
+    batches = rng.integers(0, C2_N, size=(C2_BATCHES + 20, C2_B)).astype(np.uint64)
+    rows = db.reshape(C2_N, C2_E)
+    for b in batches[:10]:   # warm-up
+        g.Query(b)
+    ctx.sync()
+    t0 = time.perf_counter()
+    bad = 0
+    for b in batches[10:10 + C2_BATCHES]:
+        resp, _ = g.Query(b)
+        r0 = resp[0]   # the reference's check: the first response is zero or the entry
+        bad += int(r0.any() and not np.array_equal(r0, rows[int(b[0])]))
+    ctx.sync()
+    online = time.perf_counter() - t0
+    ctx.timing_reset()
+    ctx.timing(2)
+    for b in batches[10 + C2_BATCHES - 10:10 + C2_BATCHES]:
+        g.Query(b)
+    ctx.timing(False)
+    n, ms, by = ctx.timing_get("step")
+    out = {"workload": "TestBatchPIRPerf shape (configs[2], MS-MARCO 3.2M): 3,201,821 x 896 B, BatchSize 32, "
+                       "FailureProbLog2 8, uniform synthetic DB and ids",
+           "preprocessing_s": round(prep, 6), "batches": C2_BATCHES,
+           "batch_queries_per_s": round(C2_BATCHES / online, 1),
+           "ids_per_s": round(C2_BATCHES * C2_B / online, 1), "ms_per_batch": round(online / C2_BATCHES * 1e3, 4),
+           "first_response_mismatches": bad}
+    if n:
+        ach = (by / n) / (ms / n / 1e3) / 1e9
+        out["roofline"] = {"bound": "hbm", "kernel": "step", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "avg_ms": round(ms / n, 5),
+                           "alg_bytes_per_launch": by / n}
+    if with_cpu:
+        from oracle import oracle as O
+        o = O.SimpleBatchPianoPIR(C2_N, C2_E * 8, C2_B, db, 8, seed=21)
+        t0 = time.perf_counter()
+        o.Preprocessing()
+        oprep = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        for b in batches[10:10 + C2_BATCHES]:
+            o.Query(b)
+        oon = time.perf_counter() - t0
+        out["cpu_baseline"] = {"preprocessing_s": round(oprep, 3), "batch_queries_per_s": round(C2_BATCHES / oon, 1),
+                               "cores": 1, "kind": "port",
+                               "sample": f"the same DB, preprocessing and {C2_BATCHES} batches"}
+    del g
+    return out
+
+
 def dist_init():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     if ws == 1:
@@ -106,6 +171,7 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-config2", action="store_true", help="skip the MS-MARCO-shaped batch-PIR block")
     args = ap.parse_args()
 
     dist, rank, ws, local = dist_init()
@@ -217,6 +283,8 @@ def main():
     }
     if not args.no_cpu_baseline and ws == 1:
         out["cpu_baseline"] = cpu_baseline(v, g, queries[args.warmup + args.steps:])
+    if ws == 1 and not args.no_config2:
+        out["config2_batch_pir"] = batch_pir_msmarco(ctx, not args.no_cpu_baseline)
     print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -229,7 +229,8 @@ def test_batch_pir_basic(step_ctx, oracle):
 
 
 @pytest.mark.parametrize("N,E,B,n", [(200_000, 80, 32, 96), (50_000, 12, 8, 24), (30_000, 6, 32, 200),
-                                     (30_000, 6, 4, 2000)])
+                                     (30_000, 6, 4, 2000),
+                                     (320_000, 112, 32, 32)])   # configs[2] entry size (896 B), TestBatchPIRPerf batches
 def test_batch_pir_sequence(step_ctx, oracle, N, E, B, n):
     """Many batches (duplicates, drops, dummies) through the batch layer's
     re-preprocessing trigger (batch-pir.go:239-245) and, for the last case,
