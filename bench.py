@@ -1,6 +1,6 @@
 """bench.py — private queries/sec on the SIFT1M-shaped private search (1 MI355X per rank).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--sessions S] [--no-cpu-baseline] [--no-config2]
 
 Workload (BASELINE.json configs[1], the metric's config): n = 1e6 vectors,
 d = 128, degree m = 32 graph, k = 10, step = 20, parallel = 3, batch PIR with
@@ -9,13 +9,19 @@ private-search.go harness (run-private-search.sh flags).  Data are synthetic
 (no dataset in the image): a clustered SIFT-like mixture with integer values in
 [0,255] and a uniform random degree-32 graph (private-search.go:54-69).
 
-One step = one private query (GraphANNFrontend.SearchKNN over PIRGraphInfo,
-20 batch-PIR rounds of 96 ids) plus, whenever the harness trigger fires
-(private-search.go:226-232), the full hint re-preprocessing — so `value` is
-q / (online + maintenance) wall time, the reference's own accounting.
+Serving: one GPU serves S client sessions at once (--sessions, default 4 =
+the process's hardware queues).  Every session is a full PianoPIR client (own
+keys, hint state, maintenance) over the one server DB on the device, driven by
+its own host thread and stream (pm_search_loop_sessions), so one session's
+step kernels overlap the others' host work.  One step = one private query per
+session (GraphANNFrontend.SearchKNN over PIRGraphInfo, 20 batch-PIR rounds of
+96 ids) plus, whenever the harness trigger fires (private-search.go:226-232),
+that session's full hint re-preprocessing — so `value` is all sessions'
+queries / wall time including maintenance, the reference's own accounting
+summed over clients.  `single_session` reports one client alone (latency view).
 
-Multi-GPU: one process per GPU (torch.distributed.run); every rank runs an
-independent client + server replica on its own GPU and query stream (queries
+Multi-GPU: one process per GPU (torch.distributed.run); every rank runs its
+own server replica and S sessions on its own GPU and query streams (queries
 are independent units, no data-path exchange), so scaling is weak and `value`
 is the sum of queries over the max of the ranks' times.
 """
@@ -40,6 +46,7 @@ PREP_KERNELS = ["prep_offsets", "prep_fold", "prep_repl", "l2_rows"]   # timed i
 STEP_KERNELS = ["step", "hint_match", "resolve", "answer"]          # timed in the profile window
 KERNELS = PREP_KERNELS + STEP_KERNELS
 PROFILE_QUERIES = 8
+SESSIONS = 4   # client sessions per GPU (GPU_MAX_HW_QUEUES = 4 hardware queues per process)
 SYMBOLS = {"prep_fold": "void pm::k_prep_fold_pipe<4, 1, 4>(pm::PmPart const*, unsigned long const*, "
                         "unsigned long const*, unsigned int, unsigned int, unsigned int, unsigned int)",
            "answer": "void pm::k_answer<2>(pm::PmStep)", "step": "void pm::k_step<2>(pm::PmStep)", "resolve": "void pm::k_resolve<true>(pm::PmStep)",
@@ -170,48 +177,84 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--sessions", type=int, default=SESSIONS,
+                    help="client sessions served concurrently per GPU (one host thread + stream each)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-config2", action="store_true", help="skip the MS-MARCO-shaped batch-PIR block")
+    ap.add_argument("--no-single", action="store_true", help="skip the one-client latency block")
     args = ap.parse_args()
+    S = max(1, args.sessions)
 
     dist, rank, ws, local = dist_init()
     import pacmann_amd as pm
 
-    ctx = pm.Context(local)
     v, g = make_data(rank)
-    queries = make_queries(v, args.warmup + args.steps + 64, seed=300 + rank)
-    gi = pm.PIRGraphInfo(v, g, pir_seed=11 + rank, search_seed=12 + rank, ctx=ctx)
-    gi.Preprocess()   # GraphANNFrontend.Preprocess: DB packing + first hint preprocessing
+    nq = args.warmup + args.steps + PROFILE_QUERIES
+    queries = make_queries(v, S * nq + 64, seed=300 + rank)
+    qsess = queries[:S * nq].reshape(S, nq, -1)
+    # session 0 owns the graph and the server DB (GraphANNFrontend.Preprocess:
+    # DB packing + first hint preprocessing); sessions 1..S-1 are further
+    # clients over the same device DB, each with its own keys and hint state
+    base = pm.PIRGraphInfo(v, g, pir_seed=11 + 97 * rank, search_seed=12 + 97 * rank, ctx=pm.Context(local))
+    base.Preprocess()
+    sess = [base] + [base.Session(11 + 97 * rank + i, 12 + 97 * rank + i, pm.Context(local)) for i in range(1, S)]
+    for s_ in sess[1:]:
+        s_.Preprocess()
+    ctxs = [s_.ctx for s_ in sess]
     if args.warmup:
-        gi.SearchLoop(queries[:args.warmup], K_TOP, STEP, PARALLEL)
+        pm.search_loop_sessions(sess, qsess[:, :args.warmup], K_TOP, STEP, PARALLEL)
 
-    ctx.timing_reset()
-    ctx.timing(True)
+    for c in ctxs:
+        c.timing_reset()
+        c.timing(True)
     if dist:
         dist.barrier()
-    ctx.sync()
+    for c in ctxs:
+        c.sync()
     t0 = time.perf_counter()
-    _, online, maint = gi.SearchLoop(queries[args.warmup:args.warmup + args.steps], K_TOP, STEP, PARALLEL)
-    ctx.sync()
+    _, _, online, maint = pm.search_loop_sessions(sess, qsess[:, args.warmup:args.warmup + args.steps],
+                                                  K_TOP, STEP, PARALLEL)
+    for c in ctxs:
+        c.sync()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    ctx.timing(False)
+    for c in ctxs:
+        c.timing(False)
 
-    ktime = {k: ctx.timing_get(k) for k in PREP_KERNELS}
-    htime = {k: ctx.timing_get(k) for k in HOST}
-    nsteps = htime["host_step_launch"][0]   # batch-PIR steps run in the timed region
+    def tsum(name):
+        r = [c.timing_get(name) for c in ctxs]
+        return tuple(sum(x[i] for x in r) for i in range(3))
+
+    ktime = {k: tsum(k) for k in PREP_KERNELS}
+    htime = {k: tsum(k) for k in HOST}
+    nsteps = htime["host_step_launch"][0]   # batch-PIR steps run in the timed region (all sessions)
     # profile window (after the timed region, not part of `value`): per-launch
-    # device time of the three step kernels, bracketed by events on their stream
-    ctx.timing_reset()
-    ctx.timing(2)
+    # device time of the step kernels under the same S-session load, from
+    # events carried in the kernels' own dispatch packets
+    for c in ctxs:
+        c.timing_reset()
+        c.timing(2)
     w0 = args.warmup + args.steps
-    gi.SearchLoop(queries[w0:w0 + PROFILE_QUERIES], K_TOP, STEP, PARALLEL)
-    ctx.timing(False)
+    pm.search_loop_sessions(sess, qsess[:, w0:w0 + PROFILE_QUERIES], K_TOP, STEP, PARALLEL)
+    for c in ctxs:
+        c.timing(False)
     for k in STEP_KERNELS:
-        n, ms, by = ctx.timing_get(k)
+        n, ms, by = tsum(k)
         # scaled to the timed region's step count: launches, device ms, bytes
         ktime[k] = (nsteps, ms / max(n, 1) * nsteps, by / max(n, 1) * nsteps)
+    # the reference's own accounting, one client alone (latency view; not `value`)
+    single = None
+    if rank == 0 and not args.no_single:
+        n1 = min(args.steps, 50)
+        sq = queries[S * nq:S * nq + n1] if S * nq + n1 <= len(queries) else qsess[0, :n1]
+        t1 = time.perf_counter()
+        _, on1, mt1 = base.SearchLoop(sq, K_TOP, STEP, PARALLEL)
+        base.ctx.sync()
+        t1 = time.perf_counter() - t1
+        single = {"queries_per_s": round(n1 / t1, 2), "ms_per_query": round(t1 / n1 * 1e3, 4),
+                  "online_s_per_query": round(on1 / n1, 6), "maintenance_s_per_query": round(mt1 / n1, 6),
+                  "queries": n1}
     if dist:
         import torch
         t = torch.tensor([elapsed], dtype=torch.float64)
@@ -221,7 +264,7 @@ def main():
         dist.destroy_process_group()
         return
 
-    total_q = args.steps * ws
+    total_q = args.steps * S * ws
     value = total_q / elapsed
     # dominant kernel: largest device time over the timed region
     dom = max(KERNELS, key=lambda k: ktime[k][1])
@@ -240,11 +283,11 @@ def main():
             r["note"] = note
         return r
 
-    stats = gi.PIR.stats()
+    stats = base.PIR.stats()
     # the fold against its compulsory bytes too: the DB once plus the parities
     hints = 0
     for p in range(stats["PartitionNum"]):
-        c = gi.PIR.SubConfig(p)
+        c = base.PIR.SubConfig(p)
         hints += c["PrimaryHintNum"] + c["SetSize"] * c["MaxQueryPerChunk"]
     E = (DIM + M) // 2
     fold = roof("prep_fold")
@@ -257,11 +300,17 @@ def main():
     note = None
     if dom == "step":
         note = ("k_step runs hint match, resolution and answer of a batch-PIR step in one launch; "
-                "bytes are the answer's (SURVEY.md §8d: SS*E*8 + 4*SS + 8*E per real/dummy sub-query)")
+                "bytes are the answer's (SURVEY.md §8d: SS*E*8 + 4*SS + 8*E per real/dummy sub-query); "
+                f"avg_ms is per launch with {S} sessions' steps in flight together")
     elif dom not in ("answer", "prep_fold"):
         note = (f"dominant kernel by device time is {dom}, a latency-bound sequential chain with no "
                 f"§8(d) byte figure; the roofline shown is the PIR answer kernel's")
     main_roof = roof(dom, note) if dom in ("answer", "prep_fold", "step") else roof("answer", note)
+    if main_roof and dom == "step":
+        # all sessions' answer bytes over the timed region's wall time (the GPU-wide PIR-scan rate)
+        agg = ktime["step"][2] / elapsed / 1e9
+        main_roof["aggregate"] = {"achieved": round(agg, 1), "frac": round(agg / HBM_PEAK_GBS, 4),
+                                  "note": "answer bytes of every step in the timed region / its wall time"}
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "queries/s", "n_gpus": ws,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
@@ -269,11 +318,13 @@ def main():
         "data": "synthetic (clustered SIFT-like uint8-valued f32 vectors, uniform random degree-32 graph)",
         "config": {"workload": "SIFT1M-shaped private graph search over 16-partition batch PianoPIR",
                    "n": N, "dim": DIM, "m": M, "k": K_TOP, "step": STEP, "parallel": PARALLEL,
-                   "batch_size": M, "failure_prob_log2": F, "parallelism": f"replicas{ws}"},
+                   "batch_size": M, "failure_prob_log2": F, "sessions_per_gpu": S,
+                   "parallelism": f"replicas{ws}"},
         "roofline": main_roof,
         "roofline_prep": fold,
-        "online_s_per_query": round(online / args.steps, 6),
-        "maintenance_s_per_query": round(maint / args.steps, 6),
+        "single_session": single,
+        "online_s_per_query": round(float(np.mean(online)) / args.steps, 6),
+        "maintenance_s_per_query": round(float(np.mean(maint)) / args.steps, 6),
         "preprocessing_s": round(stats["PreprocessingTime"], 6),
         "kernel_ms": {k: round(ktime[k][1], 3) for k in KERNELS},
         "kernel_avg_us": {k: round(ktime[k][1] / ktime[k][0] * 1e3, 3) if ktime[k][0] else None for k in KERNELS},
@@ -282,9 +333,9 @@ def main():
         "dominant_kernel": dom,
     }
     if not args.no_cpu_baseline and ws == 1:
-        out["cpu_baseline"] = cpu_baseline(v, g, queries[args.warmup + args.steps:])
+        out["cpu_baseline"] = cpu_baseline(v, g, queries[S * nq:])
     if ws == 1 and not args.no_config2:
-        out["config2_batch_pir"] = batch_pir_msmarco(ctx, not args.no_cpu_baseline)
+        out["config2_batch_pir"] = batch_pir_msmarco(ctxs[0], not args.no_cpu_baseline)
     print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()

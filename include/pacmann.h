@@ -134,6 +134,14 @@ int  pm_batchpir_create(pm_ctx* ctx, uint64_t DBSize, uint64_t DBEntryByteNum, u
 int  pm_batchpir_create_shard(pm_ctx* ctx, uint64_t DBSize, uint64_t DBEntryByteNum, uint64_t BatchSize,
                               const uint64_t* rawDB, uint64_t FailureProbLog2, uint64_t seed,
                               uint32_t shard, uint32_t nshards, pm_batchpir** out);
+/* Another client of the same server (multi-session serving, SURVEY.md §8f
+ * rank 2): a new SimpleBatchPianoPIR client (own keys from `seed`, own hint
+ * state, counters and local cache) whose server side reads the DB rows of
+ * `server` in place (one device copy of the DB for all its clients; the
+ * reference's server likewise keeps one rawDB alias, pir.go:34-39).  Same
+ * DBSize, entry size, BatchSize, FailureProbLog2 and shard as `server`; same
+ * device as `ctx`.  The DB stays alive while any client holds it. */
+int  pm_batchpir_create_client(pm_ctx* ctx, pm_batchpir* server, uint64_t seed, pm_batchpir** out);
 void pm_batchpir_destroy(pm_batchpir* h);
 int  pm_batchpir_preprocessing(pm_batchpir* h);         /* batch-pir.go:119-155 */
 int  pm_batchpir_dummy_preprocessing(pm_batchpir* h);   /* batch-pir.go:157-166 */
@@ -178,6 +186,19 @@ int  pm_search_knn(pm_graph* g, const float* query, int k, int max_step, int par
 int  pm_search_loop(pm_graph* g, const float* queries, uint64_t q, int k, int step, int parallel,
                     int benchmarking, int64_t* answers, double* online_s, double* maintenance_s);
 int  pm_graph_counts(pm_graph* g, uint64_t* total_queries, uint64_t* succ_queries);
+/* A further client session over a preprocessed `base` (same graph, vectors and
+ * server DB, shared on the device): own context/stream, PIR keys (pir_seed),
+ * hint state, start set and id stream (search_seed).  Call pm_graph_preprocess
+ * on it (client hint preprocessing + GetStartVertex) before searching. */
+int  pm_graph_create_session(pm_ctx* ctx, pm_graph* base, uint64_t pir_seed, uint64_t search_seed,
+                             pm_graph** out);
+/* S sessions served concurrently on one GPU, one host thread each: session i
+ * runs the private-search.go:216-240 loop (incl. its own maintenance trigger)
+ * over queries[i*q*dim ...] into answers[i*q*k ...].  wall_s: wall time from the
+ * common start to the last session's end; online_s / maintenance_s: S entries. */
+int  pm_search_loop_sessions(pm_graph** sessions, uint32_t S, const float* queries, uint64_t q, int k,
+                             int step, int parallel, int64_t* answers, double* wall_s, double* online_s,
+                             double* maintenance_s);
 pm_batchpir* pm_graph_pir(pm_graph* g);
 
 #ifdef __cplusplus

@@ -101,6 +101,10 @@ SIGNATURES = {
                                  C.POINTER(dbl), C.POINTER(dbl)]),
     "pm_graph_counts": (C.c_int, [vp, u64p, u64p]),
     "pm_graph_pir": (vp, [vp]),
+    "pm_batchpir_create_client": (C.c_int, [vp, vp, u64, C.POINTER(vp)]),
+    "pm_graph_create_session": (C.c_int, [vp, vp, u64, u64, C.POINTER(vp)]),
+    "pm_search_loop_sessions": (C.c_int, [C.POINTER(vp), C.c_uint32, f32p, u64, C.c_int, C.c_int, C.c_int,
+                                          i64p, C.POINTER(dbl), C.POINTER(dbl), C.POINTER(dbl)]),
 }
 
 Q_OK, Q_EBUDGET, Q_ECHUNK, Q_ENOHIT, Q_ERANGE = range(5)
@@ -350,6 +354,18 @@ class SimpleBatchPianoPIR:
             lib().pm_batchpir_destroy(self.h)
         self.h = None
 
+    def Client(self, seed: int, ctx: Context | None = None) -> "SimpleBatchPianoPIR":
+        """Another client of this server (pm_batchpir_create_client): own keys
+        (seed), hint state and counters; reads this handle's device DB in place."""
+        c = SimpleBatchPianoPIR.__new__(SimpleBatchPianoPIR)
+        c.ctx = ctx or self.ctx
+        c.E, c.shard, c.nshards, c._owned = self.E, self.shard, self.nshards, True
+        c._server = self
+        h = vp()
+        _check(lib().pm_batchpir_create_client(c.ctx.h, self.h, seed, C.byref(h)))
+        c.h = h
+        return c
+
     def Preprocessing(self):
         _check(lib().pm_batchpir_preprocessing(self.h))
 
@@ -479,6 +495,38 @@ class PIRGraphInfo:
         _check(lib().pm_search_loop(self.h, _p(qs, f32p), qs.shape[0], k, step, parallel,
                                     int(benchmarking), _p(ans, i64p), C.byref(on), C.byref(mt)))
         return ans, on.value, mt.value
+
+
+    def Session(self, pir_seed: int, search_seed: int, ctx: Context | None = None) -> "PIRGraphInfo":
+        """Another client session over this (preprocessed) graph and its server
+        DB (pm_graph_create_session): own context, keys, hint state, start set
+        and id stream; call Preprocess() on it before searching."""
+        s = PIRGraphInfo.__new__(PIRGraphInfo)
+        s.ctx = ctx or Context(self.ctx.device)
+        s.N, s.Dim, s.M = self.N, self.Dim, self.M
+        s._base = self   # the base keeps the shared server alive until the session's preprocessing
+        h = vp()
+        _check(lib().pm_graph_create_session(s.ctx.h, self.h, pir_seed, search_seed, C.byref(h)))
+        s.h = h
+        return s
+
+
+def search_loop_sessions(sessions, queries, k: int, step: int, parallel: int):
+    """Serve len(sessions) client sessions concurrently (pm_search_loop_sessions):
+    queries [S, q, dim].  Returns (answers [S, q, k], wall_s, online_s[S], maint_s[S])."""
+    S = len(sessions)
+    qs = np.ascontiguousarray(queries, dtype=np.float32)
+    if qs.ndim != 3 or qs.shape[0] != S or qs.shape[2] != sessions[0].Dim:
+        raise ValueError("queries must be [len(sessions), q, dim]")
+    q = qs.shape[1]
+    ans = np.zeros((S, q, k), dtype=np.int64)
+    hs = (vp * S)(*[s.h for s in sessions])
+    wall = C.c_double()
+    on = np.zeros(S, dtype=np.float64)
+    mt = np.zeros(S, dtype=np.float64)
+    _check(lib().pm_search_loop_sessions(hs, S, _p(qs, f32p), q, k, step, parallel, _p(ans, i64p), C.byref(wall),
+                                         on.ctypes.data_as(C.POINTER(dbl)), mt.ctypes.data_as(C.POINTER(dbl))))
+    return ans, wall.value, on, mt
 
 
 GraphANNFrontend = PIRGraphInfo

@@ -11,7 +11,9 @@
 #include <chrono>
 #include <cmath>
 #include <cstring>
+#include <memory>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -292,7 +294,8 @@ struct Engine {
   uint64_t FBN = 0, QMIP = 0, Support = 0, prepCount = 0;
   double prepTime = 0, storage = 0, commOn = 0, commOff = 0;
 
-  DevBuf db, zero16, parts_d, owned_d, tag, pp, parity, ridx, rval, hist, fqn, arena, tab, tabT, done, gran;
+  std::shared_ptr<DevBuf> db = std::make_shared<DevBuf>();   // server DB; shared by the clients of pm_batchpir_create_client
+  DevBuf zero16, parts_d, owned_d, tag, pp, parity, ridx, rval, hist, fqn, arena, tab, tabT, done, gran;
   uint32_t gran_words = 0;
   std::vector<uint32_t> owned_list;   // owned partitions in order (owned_d holds their PmPart)
   DevBuf qoffs, ans_srv;
@@ -361,10 +364,11 @@ static double part_comm(const PartHost& p, uint64_t E) { return (double)((uint64
 
 static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, uint64_t B,
                          const uint64_t* rawDB, uint64_t F, uint64_t seed, bool batch,
-                         uint32_t shard = 0, uint32_t nshards = 1) {
+                         uint32_t shard = 0, uint32_t nshards = 1, const Engine* server = nullptr) {
   if (nshards == 0 || shard >= nshards) return fail(PM_EINVAL, "shard must be < nshards");
   if (!ctx) return fail(PM_EINVAL, "ctx is NULL");
-  if (!rawDB && N) return fail(PM_EINVAL, "rawDB is NULL");
+  if (!rawDB && N && !server) return fail(PM_EINVAL, "rawDB is NULL");
+  if (server && server->ctx->device != ctx->device) return fail(PM_EINVAL, "a client shares the server DB of its own device only");
   if (N == 0) return fail(PM_EINVAL, "DBSize must be > 0");
   if (Ebytes < 8) return fail(PM_EINVAL, "DBEntryByteNum must be >= 8");
   HIPCHK(hipSetDevice(ctx->device));
@@ -416,12 +420,13 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
     ph.d.tab = (uint16_t*)(uintptr_t)off_tab; off_tab += (uint64_t)ph.d.H * ph.d.SS;
     ph.cache.reserve(ph.d.MaxQ);
   }
-  CHK(g->db.reserve(std::max<uint64_t>(8, off_db * g->E * 8)));
   CHK(g->zero16.reserve(64));
   HIPCHK(hipMemset(g->zero16.p, 0, 64));
-  for (uint32_t i : g->owned_list) {
+  if (server) g->db = server->db;   // same N, entry size, partitions and shard: same packed rows
+  else CHK(g->db->reserve(std::max<uint64_t>(8, off_db * g->E * 8)));
+  for (uint32_t i : server ? std::vector<uint32_t>{} : g->owned_list) {
     const uint64_t start = (uint64_t)i * g->PS, rows = g->parts[i].d.N;
-    HIPCHK(hipMemcpy(g->db.as<uint64_t>() + g->parts[i].d.row0 * g->E, rawDB + start * g->E, rows * g->E * 8,
+    HIPCHK(hipMemcpy(g->db->as<uint64_t>() + g->parts[i].d.row0 * g->E, rawDB + start * g->E, rows * g->E * 8,
                      hipMemcpyHostToDevice));
   }
   CHK(g->tag.reserve(off_tag * 4));
@@ -524,9 +529,9 @@ static int engine_prep(Engine* g, uint64_t p0, uint64_t p1) {
       HIPCHK(hipMemsetAsync(d.rval, 0, (uint64_t)d.SS * d.Qpc * g->E * 8, st));
     }
   } else {
-    c->timed("prep_fold", fold, [&] { pmk::prep_fold(st, dp, np, g->maxH, g->db.as<uint64_t>(), (uint32_t)g->E, g->minCS, g->maxCS,
+    c->timed("prep_fold", fold, [&] { pmk::prep_fold(st, dp, np, g->maxH, g->db->as<uint64_t>(), (uint32_t)g->E, g->minCS, g->maxCS,
                                                g->zero16.as<uint64_t>()); });
-    c->timed("prep_repl", repl, [&] { pmk::prep_repl(st, dp, np, g->maxRepl, g->db.as<uint64_t>(), (uint32_t)g->E); });
+    c->timed("prep_repl", repl, [&] { pmk::prep_repl(st, dp, np, g->maxRepl, g->db->as<uint64_t>(), (uint32_t)g->E); });
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(st));
@@ -723,7 +728,7 @@ static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
   HIPCHK(hipMemsetAsync(g->stamps.p, 0, g->P * 64 * 8, st));
   S.stamps = g->stamps.as<uint64_t>();
 #endif
-  S.db = g->db.as<uint64_t>();
+  S.db = g->db->as<uint64_t>();
   S.q = q_dev;
   S.hdr_h = g->out_h.as<PmOutHdr>();
   S.rows_h = (uint64_t*)(g->out_h.as<char>() + nsub * sizeof(PmOutHdr));
@@ -916,7 +921,7 @@ extern "C" int pm_pir_server_answer(pm_pir* h, const uint32_t* offsets, uint64_t
   HIPCHK(hipMemcpyAsync(g->qoffs.p, offsets, nq * d.SS * 4, hipMemcpyHostToDevice, c->stream));
   c->timed("answer", (double)nq * (d.SS * (g->E * 8 + 4) + g->E * 8), [&] {
     pmk::server_answer(c->stream, g->parts_d.as<PmPart>(), g->qoffs.as<uint32_t>(), (uint32_t)nq, d.SS,
-                       g->db.as<uint64_t>(), (uint32_t)g->E, g->ans_srv.as<uint64_t>());
+                       g->db->as<uint64_t>(), (uint32_t)g->E, g->ans_srv.as<uint64_t>());
   });
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(out, g->ans_srv.p, nq * g->E * 8, hipMemcpyDeviceToHost, c->stream));
@@ -977,6 +982,16 @@ extern "C" int pm_batchpir_create_shard(pm_ctx* ctx, uint64_t DBSize, uint64_t D
   pm_batchpir* h = new pm_batchpir();
   int r = engine_create(ctx, &h->e, DBSize, DBEntryByteNum, BatchSize, rawDB, F, seed, true, shard, nshards);
   if (r) { delete h; return r; }
+  *out = h;
+  return 0;
+}
+extern "C" int pm_batchpir_create_client(pm_ctx* ctx, pm_batchpir* server, uint64_t seed, pm_batchpir** out) {
+  if (!out || !server) return fail(PM_EINVAL, "NULL argument");
+  const Engine& s = server->e;
+  pm_batchpir* h = new pm_batchpir();
+  int r = engine_create(ctx, &h->e, s.N, s.Ebytes, s.B, nullptr, s.F, seed, true, s.shard, s.nshards, &s);
+  if (r) { delete h; return r; }
+  h->e.pf_off = s.pf_off; h->e.pf_len = s.pf_len;
   *out = h;
   return 0;
 }
@@ -1258,9 +1273,15 @@ struct pm_graph {
   bool nonprivate = false, skipPrep = false;
   uint64_t pir_seed = 0;
   SplitMix rng{0};
-  std::vector<float> vectors;
-  std::vector<uint32_t> graph;
-  DevBuf dvec, dq, dids, ddist;
+  // host vectors and graph (the success check, non-private mode, DB packing)
+  // and their device copy; sessions of one base share them
+  std::shared_ptr<const std::vector<float>> vec_own;
+  std::shared_ptr<const std::vector<uint32_t>> graph_own;
+  const float* vectors = nullptr;
+  const uint32_t* graph = nullptr;
+  std::shared_ptr<DevBuf> dvec = std::make_shared<DevBuf>();
+  pm_batchpir* server = nullptr;   // sessions: the base's batch PIR whose server DB they share
+  DevBuf dq, dids, ddist;
   HostBuf stage_h;                                // pinned: query and start-vertex distances
   pm_batchpir* pir = nullptr;
   std::vector<uint64_t> start;   // StartVertices ids
@@ -1291,13 +1312,37 @@ extern "C" int pm_graph_create(pm_ctx* ctx, uint64_t n, uint64_t dim, uint64_t m
   pm_graph* g = new pm_graph();
   g->ctx = ctx; g->n = n; g->dim = dim; g->m = m; g->nonprivate = nonprivate; g->skipPrep = skip_prep;
   g->pir_seed = pir_seed; g->rng.s = search_seed;
-  g->vectors.assign(vectors, vectors + n * dim);
-  g->graph.assign(graph, graph + n * m);
-  int r = g->dvec.reserve(n * dim * 4);
+  g->vec_own = std::make_shared<const std::vector<float>>(vectors, vectors + n * dim);
+  g->graph_own = std::make_shared<const std::vector<uint32_t>>(graph, graph + n * m);
+  g->vectors = g->vec_own->data();
+  g->graph = g->graph_own->data();
+  int r = g->dvec->reserve(n * dim * 4);
   if (!r) r = g->dq.reserve(dim * 4);
   if (r) { delete g; return r; }
-  hipError_t e = hipMemcpy(g->dvec.p, vectors, n * dim * 4, hipMemcpyHostToDevice);
+  hipError_t e = hipMemcpy(g->dvec->p, vectors, n * dim * 4, hipMemcpyHostToDevice);
   if (e != hipSuccess) { delete g; return fail(PM_EHIP, hipGetErrorString(e)); }
+  *out = g;
+  return 0;
+}
+// A second client session over the same graph and server: shares the host
+// vectors/graph, their device copy and (after pm_graph_preprocess) the server
+// DB of `base`'s batch PIR, with its own context, keys, hint state, start set
+// and id stream.  `base` must be preprocessed and outlive its sessions' preprocessing.
+extern "C" int pm_graph_create_session(pm_ctx* ctx, pm_graph* base, uint64_t pir_seed, uint64_t search_seed,
+                                       pm_graph** out) {
+  if (!ctx || !base || !out) return fail(PM_EINVAL, "NULL argument");
+  if (!base->nonprivate && !base->pir) return fail(PM_EINVAL, "base graph not preprocessed");
+  if (base->ctx->device != ctx->device) return fail(PM_EINVAL, "a session shares its base's device");
+  HIPCHK(hipSetDevice(ctx->device));
+  pm_graph* g = new pm_graph();
+  g->ctx = ctx; g->n = base->n; g->dim = base->dim; g->m = base->m;
+  g->nonprivate = base->nonprivate; g->skipPrep = base->skipPrep;
+  g->pir_seed = pir_seed; g->rng.s = search_seed;
+  g->vec_own = base->vec_own; g->graph_own = base->graph_own;
+  g->vectors = base->vectors; g->graph = base->graph;
+  g->dvec = base->dvec;
+  g->server = base->pir;
+  if (int r = g->dq.reserve(g->dim * 4)) { delete g; return r; }
   *out = g;
   return 0;
 }
@@ -1307,7 +1352,12 @@ extern "C" int pm_graph_counts(pm_graph* g, uint64_t* t, uint64_t* s) { *t = g->
 
 // PIRGraphInfo.Preprocess (private-search.go:355-412) + GetStartVertex (:508-531)
 extern "C" int pm_graph_preprocess(pm_graph* g) {
-  {   // the PIR is built in non-private mode too (private-search.go:405)
+  if (g->server) {   // session: a new client over the base's server DB
+    delete g->pir; g->pir = nullptr;
+    CHK(pm_batchpir_create_client(g->ctx, g->server, g->pir_seed, &g->pir));
+    if (g->skipPrep) CHK(pm_batchpir_dummy_preprocessing(g->pir));
+    else CHK(pm_batchpir_preprocessing(g->pir));
+  } else {   // the PIR is built in non-private mode too (private-search.go:405)
     const uint64_t ebytes = g->dim * 4 + g->m * 4, E = ebytes / 8;
     std::vector<uint64_t> raw(g->n * E);
     for (uint64_t i = 0; i < g->n; ++i) {
@@ -1374,7 +1424,7 @@ static int get_vertex_info(pm_graph* g, bool with_q) {
       CHK(g->dids.reserve(n * 4)); CHK(g->ddist.reserve(n * 4));
       HIPCHK(hipMemcpyAsync(g->dids.p, u.data(), n * 4, hipMemcpyHostToDevice, st));
       g->ctx->timed("l2_rows", (double)n * g->dim * 4, [&] {
-        pmk::l2_rows(st, g->dvec.as<float>(), g->dim, n, g->dids.as<uint32_t>(), g->dq.as<float>(), (uint32_t)g->dim, g->ddist.as<float>());
+        pmk::l2_rows(st, g->dvec->as<float>(), g->dim, n, g->dids.as<uint32_t>(), g->dq.as<float>(), (uint32_t)g->dim, g->ddist.as<float>());
       });
       HIPCHK(hipMemcpyAsync(g->dist.data(), g->ddist.p, n * 4, hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
@@ -1448,7 +1498,7 @@ static int search_knn_impl(pm_graph* g, const float* query, int k, int max_step,
     if (ns) {
       CHK(g->ddist.reserve(ns * 4));
       g->ctx->timed("l2_rows", (double)ns * g->dim * 4, [&] {
-        pmk::l2_rows(st, g->dvec.as<float>(), g->dim, ns, g->dstart.as<uint32_t>(), g->dq.as<float>(), (uint32_t)g->dim, g->ddist.as<float>());
+        pmk::l2_rows(st, g->dvec->as<float>(), g->dim, ns, g->dstart.as<uint32_t>(), g->dq.as<float>(), (uint32_t)g->dim, g->ddist.as<float>());
       });
       HIPCHK(hipMemcpyAsync(sdh, g->ddist.p, ns * 4, hipMemcpyDeviceToHost, st));
     }
@@ -1532,5 +1582,52 @@ extern "C" int pm_search_loop(pm_graph* g, const float* queries, uint64_t q, int
   double total = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   if (online_s) *online_s = total - maint;
   if (maint_s) *maint_s = maint;
+  return 0;
+}
+
+// S client sessions served concurrently on one GPU: session i runs the
+// private-search.go:216-240 loop (search + its own maintenance trigger) over
+// queries[i*q .. (i+1)*q) on its own host thread and stream.  The sessions'
+// step kernels overlap each other's host work.  online_s / maint_s: S entries.
+extern "C" int pm_search_loop_sessions(pm_graph** gs, uint32_t S, const float* queries, uint64_t q, int k,
+                                       int step, int parallel, int64_t* answers, double* wall_s,
+                                       double* online_s, double* maint_s) {
+  if (!gs || !S || (!queries && q) || (!answers && q)) return fail(PM_EINVAL, "NULL argument");
+  for (uint32_t i = 0; i < S; ++i) {
+    if (!gs[i]) return fail(PM_EINVAL, "NULL session");
+    for (uint32_t j = 0; j < i; ++j)
+      if (gs[j] == gs[i] || gs[j]->ctx == gs[i]->ctx) return fail(PM_EINVAL, "sessions need distinct graphs and contexts");
+  }
+  std::vector<int> rc(S, 0);
+  std::vector<std::string> msg(S);
+  std::vector<double> on(S, 0.0), mt(S, 0.0);
+  std::atomic<uint32_t> ready{0};
+  std::atomic<bool> go{false};
+  std::vector<std::thread> th;
+  th.reserve(S);
+  for (uint32_t i = 0; i < S; ++i) {
+    th.emplace_back([&, i] {
+      pm_graph* g = gs[i];
+      if (hipSetDevice(g->ctx->device) != hipSuccess) { rc[i] = PM_EHIP; msg[i] = "hipSetDevice"; ready++; return; }
+      ready++;
+      while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
+      rc[i] = pm_search_loop(g, queries + i * q * g->dim, q, k, step, parallel, 0, answers + i * q * (uint64_t)k,
+                             &on[i], &mt[i]);
+      if (rc[i]) msg[i] = pm_last_error();
+      else if (hipStreamSynchronize(g->ctx->stream) != hipSuccess) { rc[i] = PM_EHIP; msg[i] = "stream sync"; }
+    });
+  }
+  while (ready.load() < S) std::this_thread::yield();
+  auto t0 = std::chrono::steady_clock::now();
+  go.store(true, std::memory_order_release);
+  for (auto& t : th) t.join();
+  const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  if (wall_s) *wall_s = wall;
+  for (uint32_t i = 0; i < S; ++i) {
+    if (online_s) online_s[i] = on[i];
+    if (maint_s) maint_s[i] = mt[i];
+  }
+  for (uint32_t i = 0; i < S; ++i)
+    if (rc[i]) return fail(rc[i], "session " + std::to_string(i) + ": " + msg[i]);
   return 0;
 }

@@ -374,3 +374,61 @@ def test_batch_pir_shards(step_ctx, oracle, nshards):
         assert_state_equal(shards[p % nshards].export_state(p), o.sub(p).export_state())
     with pytest.raises(Exception):
         shards[0].export_state(1)
+
+
+# ---------------------------------------------------------------------------
+# multi-session serving: several clients over one server DB
+# ---------------------------------------------------------------------------
+def test_batch_pir_clients_share_server(ctx, oracle):
+    """pm_batchpir_create_client: clients with their own keys over one device
+    DB answer exactly like independent oracle instances with those keys,
+    interleaved batch by batch, through re-preprocessing; destroying the
+    server handle first leaves the clients' DB alive."""
+    import pacmann_amd as pm
+    N, E, B = 30_000, 6, 8
+    db = rand_db(N, E, 78)
+    srv = pm.SimpleBatchPianoPIR(N, E * 8, B, db, 8, seed=SEED, ctx=ctx)
+    clients = [srv.Client(SEED + 1 + i) for i in range(2)]
+    orc = [oracle.SimpleBatchPianoPIR(N, E * 8, B, db, 8, seed=SEED + 1 + i) for i in range(2)]
+    for c, o in zip(clients, orc):
+        c.Preprocessing()
+        o.Preprocessing()
+    for c in clients:
+        c._server = None
+    del srv
+    rng = np.random.default_rng(12)
+    maxq = clients[0].SubConfig(0)["MaxQueryNum"]
+    for b in range(int(maxq // 3) + 4):
+        for c, o in zip(clients, orc):
+            q = rng.integers(0, N, size=3 * B, dtype=np.uint64)
+            got, _ = c.Query(q)
+            want, _ = o.Query(q)
+            if not np.array_equal(got, want):
+                pytest.fail(mismatch_report(b, q, got, want, db.reshape(N, E)))
+    for c, o in zip(clients, orc):
+        assert c.stats()["PrepCount"] == o.stats()["PrepCount"] > 1
+
+
+def test_search_sessions_concurrent(ctx, oracle):
+    """pm_search_loop_sessions: S sessions over one graph and server DB, each
+    on its own host thread and stream, give every session the answers, PIR
+    counters and maintenance count of an independent oracle run with its seeds."""
+    import pacmann_amd as pm
+    v, graph = small_graph(n=2048, seed=3)
+    base = pm.PIRGraphInfo(v, graph, pir_seed=6, search_seed=2, ctx=ctx)
+    base.Preprocess()
+    seeds = [(7, 3), (8, 4), (9, 5)]
+    sess = [base.Session(p, s) for p, s in seeds]
+    for s in sess:
+        s.Preprocess()
+    rng = np.random.default_rng(4)
+    qs = np.stack([v[rng.integers(0, len(v), size=30)] + np.float32(1.0) for _ in seeds])
+    ans, wall, on, mt = pm.search_loop_sessions(sess, qs, 10, 20, 3)
+    assert wall > 0 and (on > 0).all()
+    for i, (p, s) in enumerate(seeds):
+        o = oracle.Graph(v, graph, pir_seed=p, search_seed=s)
+        o.Preprocess()
+        oa, _, _ = o.SearchLoop(qs[i], 10, 20, 3)
+        assert np.array_equal(ans[i], oa), i
+        assert sess[i].counts() == o.counts(), i
+        assert sess[i].PIR.stats()["PrepCount"] == o.pir().stats()["PrepCount"] > 1, i
