@@ -201,6 +201,25 @@ int  pm_search_loop_sessions(pm_graph** sessions, uint32_t S, const float* queri
                              double* maintenance_s);
 pm_batchpir* pm_graph_pir(pm_graph* g);
 
+/* ---- graph construction + ground truth (graphann/build_graph.go) ------- */
+/* Exact k nearest base rows of each query by (L2Dist, id), k <= 64: the
+ * ground truth ComputeRecall (build_graph.go:821-863) scores against.  ids:
+ * nq x k (-1 padded), dists: nq x k or NULL.  Exact for integer-valued rows
+ * (e.g. SIFT's uint8 values); for general float rows the GPU keeps the 64 best
+ * by bf16-rounded distance before the exact re-rank. */
+int pm_knn(pm_ctx* ctx, const float* base, uint64_t n, uint64_t dim, const float* queries, uint64_t nq,
+           uint32_t k, int64_t* ids, float* dists);
+/* BuildGraph / CreateGraphBasedOnNGT (build_graph.go:97-105,314-523) with the
+ * NGT candidate search (absent here) replaced by exact kNN: candidates =
+ * int(1.5 m) nearest by (L2Dist, id) minus u; robustPrune (alpha); reverse
+ * edges; edge sampling with probability min(1.5 m / inbounds, 1); second
+ * robustPrune; random fill to exactly m.  Sampling and fill draw from
+ * hash4(seed, ...).  graph: n x m.  times (NULL or 4
+ * doubles): kNN, first prune, host edge work, second prune, in seconds.
+ * dim <= 192, m <= 42. */
+int pm_build_graph(pm_ctx* ctx, const float* vectors, uint64_t n, uint64_t dim, uint64_t m, float alpha,
+                   uint64_t seed, uint32_t* graph, double* times);
+
 #ifdef __cplusplus
 }
 #endif

@@ -77,6 +77,9 @@ SIG = {
     "or_search_knn": (None, [vp, f32p, C.c_int, C.c_int, C.c_int, C.c_int, i64p, i64p]),
     "or_graph_counts": (None, [vp, u64p, u64p]),
     "or_graph_pir": (vp, [vp]),
+    "or_knn": (None, [f32p, u64, u64, f32p, u64, C.c_uint32, i64p, f32p]),
+    "or_robust_prune": (None, [f32p, u64, u64, u32p, u64, u64, C.c_float, u32p, C.POINTER(C.c_uint32)]),
+    "or_build_graph": (C.c_int, [f32p, u64, u64, u64, C.c_float, u64, u32p]),
     "or_search_loop": (None, [vp, f32p, u64, C.c_int, C.c_int, C.c_int, C.c_int, i64p,
                               C.POINTER(C.c_double), C.POINTER(C.c_double)]),
 }
@@ -308,3 +311,33 @@ class Graph:
 
     def pir(self) -> SimpleBatchPianoPIR:
         return SimpleBatchPianoPIR(0, 0, 0, None, 0, _handle=lib().or_graph_pir(self.h), _keep=self._v)
+
+
+def knn(base, queries, k):
+    """Exact (L2Dist, id) top k by brute force (or_knn)."""
+    b = np.ascontiguousarray(base, dtype=np.float32)
+    q = np.ascontiguousarray(queries, dtype=np.float32).reshape(-1, b.shape[1])
+    ids = np.zeros((q.shape[0], k), dtype=np.int64)
+    d = np.zeros((q.shape[0], k), dtype=np.float32)
+    lib().or_knn(_p(b, f32p), b.shape[0], b.shape[1], _p(q, f32p), q.shape[0], k, _p(ids, i64p),
+                 _p(d, f32p))
+    return ids, d
+
+
+def robust_prune(X, u, cand, m, alpha=1.2):
+    X = np.ascontiguousarray(X, dtype=np.float32)
+    c = np.ascontiguousarray(cand, dtype=np.uint32)
+    out = np.zeros(max(len(c), m), dtype=np.uint32)
+    n = C.c_uint32()
+    lib().or_robust_prune(_p(X, f32p), X.shape[1], u, _p(c, u32p), len(c), m, C.c_float(alpha),
+                          _p(out, u32p), C.byref(n))
+    return out[:n.value]
+
+
+def build_graph(X, m, alpha=1.2, seed=1):
+    X = np.ascontiguousarray(X, dtype=np.float32)
+    g = np.zeros((X.shape[0], m), dtype=np.uint32)
+    rc = lib().or_build_graph(_p(X, f32p), X.shape[0], X.shape[1], m, C.c_float(alpha), seed, _p(g, u32p))
+    if rc:
+        raise ValueError("or_build_graph: n must be > m")
+    return g

@@ -682,3 +682,121 @@ extern "C" void or_search_loop(or_graph* g, const float* queries, uint64_t q, in
   *online_s = total - maint;
   *maintenance_s = maint;
 }
+
+// ---------------------------------------------------------------------------
+// Graph construction (graphann/build_graph.go:169-236,314-523) with exact kNN
+// candidates in place of NGT (absent here), and the exact kNN ground truth.
+// Spec shared with the product:
+//   candidates(u) = the K = int(1.5 m) smallest (L2Dist(x_u, x_v), v) over all
+//                   v (u included), then u removed       (NGT.Search :398-410)
+//   robustPrune     sort by (L2Dist, list position); greedy alpha test (:169-236)
+//   biGraph, inbounds, edge sampling with U = hash4(seed,7,u,j,0)>>11 * 2^-53,
+//   second robustPrune of lists > m, fill with hash4(seed,8,u,t,0) % n (:421-486)
+// ---------------------------------------------------------------------------
+static void knn_row(const float* base, uint64_t n, uint64_t dim, const float* q, uint32_t K,
+                    std::vector<std::pair<uint64_t, uint32_t>>& tmp, uint32_t* out, float* dist, uint32_t* len) {
+  tmp.resize(n);
+  for (uint64_t v = 0; v < n; ++v) {
+    float d = or_l2dist(base + v * dim, q, dim);
+    uint32_t b;
+    memcpy(&b, &d, 4);
+    tmp[v] = {((uint64_t)b << 32) | v, (uint32_t)v};
+  }
+  const uint64_t k = std::min<uint64_t>(K, n);
+  std::partial_sort(tmp.begin(), tmp.begin() + k, tmp.end());
+  for (uint64_t i = 0; i < k; ++i) {
+    out[i] = tmp[i].second;
+    if (dist) { uint32_t b = (uint32_t)(tmp[i].first >> 32); memcpy(&dist[i], &b, 4); }
+  }
+  *len = (uint32_t)k;
+}
+extern "C" void or_knn(const float* base, uint64_t n, uint64_t dim, const float* queries, uint64_t nq, uint32_t k,
+                       int64_t* ids, float* dists) {
+  std::vector<std::pair<uint64_t, uint32_t>> tmp;
+  std::vector<uint32_t> o(k);
+  std::vector<float> d(k);
+  for (uint64_t i = 0; i < nq; ++i) {
+    uint32_t len = 0;
+    knn_row(base, n, dim, queries + i * dim, k, tmp, o.data(), d.data(), &len);
+    for (uint32_t j = 0; j < k; ++j) {
+      ids[i * k + j] = j < len ? (int64_t)o[j] : -1;
+      if (dists) dists[i * k + j] = j < len ? d[j] : INFINITY;
+    }
+  }
+}
+// robustPrune (build_graph.go:169-236); ties of sort.Slice broken by list position
+static std::vector<uint32_t> robust_prune(const float* X, uint64_t dim, uint64_t u, const std::vector<uint32_t>& c,
+                                          uint64_t m, float alpha) {
+  if (c.size() <= m) return c;
+  std::vector<std::pair<uint64_t, float>> d2u(c.size());
+  for (size_t i = 0; i < c.size(); ++i) {
+    float d = or_l2dist(X + u * dim, X + (uint64_t)c[i] * dim, dim);
+    uint32_t b;
+    memcpy(&b, &d, 4);
+    d2u[i] = {((uint64_t)b << 32) | i, d};
+  }
+  std::sort(d2u.begin(), d2u.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+  std::vector<uint32_t> accept, discarded;
+  for (size_t i = 0; i < d2u.size(); ++i) {
+    const uint32_t v = c[(uint32_t)d2u[i].first];
+    const float duv = d2u[i].second;
+    bool ok = true;
+    for (uint32_t a : accept)
+      if (or_l2dist(X + (uint64_t)a * dim, X + (uint64_t)v * dim, dim) * alpha < duv) { ok = false; break; }
+    if (ok) {
+      accept.push_back(v);
+      if (accept.size() == m) break;
+    } else {
+      discarded.push_back(v);
+    }
+  }
+  for (size_t i = 0; accept.size() < m && i < discarded.size(); ++i) accept.push_back(discarded[i]);
+  return accept;
+}
+extern "C" void or_robust_prune(const float* X, uint64_t dim, uint64_t u, const uint32_t* cand, uint64_t n,
+                                uint64_t m, float alpha, uint32_t* out, uint32_t* len) {
+  std::vector<uint32_t> c(cand, cand + n);
+  std::vector<uint32_t> r = robust_prune(X, dim, u, c, m, alpha);
+  std::copy(r.begin(), r.end(), out);
+  *len = (uint32_t)r.size();
+}
+extern "C" int or_build_graph(const float* X, uint64_t n, uint64_t dim, uint64_t m, float alpha, uint64_t seed,
+                              uint32_t* graph) {
+  const uint32_t K = (uint32_t)((float)m * 1.5f);
+  if (n <= m) return -1;
+  std::vector<std::vector<uint32_t>> g1(n);
+  {
+    std::vector<std::pair<uint64_t, uint32_t>> tmp;
+    std::vector<uint32_t> o(K);
+    for (uint64_t u = 0; u < n; ++u) {
+      uint32_t len = 0;
+      knn_row(X, n, dim, X + u * dim, K, tmp, o.data(), nullptr, &len);
+      std::vector<uint32_t> cand;
+      for (uint32_t i = 0; i < len; ++i) if (o[i] != u) cand.push_back(o[i]);
+      g1[u] = robust_prune(X, dim, u, cand, m, alpha);
+    }
+  }
+  std::vector<std::vector<uint32_t>> bi(n);   // :421-430, literally
+  for (uint64_t u = 0; u < n; ++u)
+    for (uint32_t v : g1[u]) { bi[u].push_back(v); bi[v].push_back((uint32_t)u); }
+  std::vector<uint64_t> inb(n);
+  for (uint64_t i = 0; i < n; ++i) inb[i] = bi[i].size();
+  for (uint64_t u = 0; u < n; ++u) {
+    std::vector<uint32_t> conn;
+    for (size_t j = 0; j < bi[u].size(); ++j) {
+      const uint32_t v = bi[u][j];
+      const double prob = std::min(1.5 * (double)m / (double)inb[v], 1.0);
+      if ((double)(or_hash4(seed, 7, u, j, 0) >> 11) * 0x1.0p-53 < prob) conn.push_back(v);
+    }
+    if (conn.size() > m) conn = robust_prune(X, dim, u, conn, m, alpha);
+    uint64_t t = 0;
+    while (conn.size() < m) {
+      const uint32_t v = (uint32_t)(or_hash4(seed, 8, u, t++, 0) % n);
+      if (v == u) continue;
+      if (std::find(conn.begin(), conn.end(), v) != conn.end()) continue;
+      conn.push_back(v);
+    }
+    std::copy(conn.begin(), conn.end(), graph + u * m);
+  }
+  return 0;
+}

@@ -106,6 +106,14 @@ void     or_search_loop(or_graph*, const float* queries, uint64_t q, int k, int 
                         int parallel, int benchmarking, int64_t* answers,
                         double* online_s, double* maintenance_s);
 
+/* ---- graph construction (graphann/build_graph.go) --------------------- */
+void or_knn(const float* base, uint64_t n, uint64_t dim, const float* queries, uint64_t nq, uint32_t k,
+            int64_t* ids, float* dists);                 /* exact (L2Dist, id) top k */
+void or_robust_prune(const float* X, uint64_t dim, uint64_t u, const uint32_t* cand, uint64_t n,
+                     uint64_t m, float alpha, uint32_t* out, uint32_t* len);
+int  or_build_graph(const float* X, uint64_t n, uint64_t dim, uint64_t m, float alpha, uint64_t seed,
+                    uint32_t* graph);                    /* CreateGraphBasedOnNGT, exact kNN candidates */
+
 #ifdef __cplusplus
 }
 #endif

@@ -103,6 +103,8 @@ SIGNATURES = {
     "pm_graph_pir": (vp, [vp]),
     "pm_batchpir_create_client": (C.c_int, [vp, vp, u64, C.POINTER(vp)]),
     "pm_graph_create_session": (C.c_int, [vp, vp, u64, u64, C.POINTER(vp)]),
+    "pm_knn": (C.c_int, [vp, f32p, u64, u64, f32p, u64, C.c_uint32, i64p, f32p]),
+    "pm_build_graph": (C.c_int, [vp, f32p, u64, u64, u64, C.c_float, u64, u32p, C.POINTER(dbl)]),
     "pm_search_loop_sessions": (C.c_int, [C.POINTER(vp), C.c_uint32, f32p, u64, C.c_int, C.c_int, C.c_int,
                                           i64p, C.POINTER(dbl), C.POINTER(dbl), C.POINTER(dbl)]),
 }
@@ -527,6 +529,30 @@ def search_loop_sessions(sessions, queries, k: int, step: int, parallel: int):
     _check(lib().pm_search_loop_sessions(hs, S, _p(qs, f32p), q, k, step, parallel, _p(ans, i64p), C.byref(wall),
                                          on.ctypes.data_as(C.POINTER(dbl)), mt.ctypes.data_as(C.POINTER(dbl))))
     return ans, wall.value, on, mt
+
+
+def knn(base, queries, k: int, ctx: Context | None = None, with_dist: bool = False):
+    """Exact k nearest base rows of each query by (L2Dist, id) (pm_knn): the
+    ground truth of graphann.ComputeRecall.  ids [nq, k] int64, -1 padded."""
+    ctx = ctx or default_context()
+    b = np.ascontiguousarray(base, dtype=np.float32)
+    q = np.ascontiguousarray(queries, dtype=np.float32).reshape(-1, b.shape[1])
+    ids = np.zeros((q.shape[0], k), dtype=np.int64)
+    d = np.zeros((q.shape[0], k), dtype=np.float32)
+    _check(lib().pm_knn(ctx.h, _p(b, f32p), b.shape[0], b.shape[1], _p(q, f32p), q.shape[0], k, _p(ids, i64p),
+                        _p(d, f32p)))
+    return (ids, d) if with_dist else ids
+
+
+def build_graph(vectors, m: int, alpha: float = 1.2, seed: int = 1, ctx: Context | None = None):
+    """graphann.BuildGraph (build_graph.go:97-105,314-523) on the GPU with exact
+    kNN candidates (pm_build_graph).  Returns (graph [n, m] uint32, times dict)."""
+    ctx = ctx or default_context()
+    v = np.ascontiguousarray(vectors, dtype=np.float32)
+    g = np.zeros((v.shape[0], m), dtype=np.uint32)
+    t = (dbl * 4)()
+    _check(lib().pm_build_graph(ctx.h, _p(v, f32p), v.shape[0], v.shape[1], m, alpha, seed, _p(g, u32p), t))
+    return g, {"knn_s": t[0], "prune1_s": t[1], "host_edges_s": t[2], "prune2_s": t[3]}
 
 
 GraphANNFrontend = PIRGraphInfo

@@ -1631,3 +1631,220 @@ extern "C" int pm_search_loop_sessions(pm_graph** gs, uint32_t S, const float* q
     if (rc[i]) return fail(rc[i], "session " + std::to_string(i) + ": " + msg[i]);
   return 0;
 }
+
+// ---------------------------------------------------------------------------
+// Graph construction and exact kNN ground truth.
+// CreateGraphBasedOnNGT (graphann/build_graph.go:314-523) with the NGT
+// candidate search replaced by exact kNN: GPU bf16 MFMA prefilter (top 64) and
+// an exact re-rank in L2Dist order (pm_graph.hip); robustPrune on the GPU;
+// reverse edges, sampling and the random fill on host threads (O(n m)).
+// Randomness (the reference's per-thread math/rand, :455,473-475) comes from
+// hash4 domains 7 (edge sampling) and 8 (fill), so any thread split gives the
+// same graph.  oracle/pm_oracle.cpp (or_build_graph) restates the same spec.
+// ---------------------------------------------------------------------------
+enum : uint64_t { DOM_GRAPH_SAMPLE = 7, DOM_GRAPH_FILL = 8 };
+
+template <class F> static void par_for(uint64_t n, F&& f) {
+  const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  if (n < 4096 || nt == 1) { f(0, n); return; }
+  std::vector<std::thread> th;
+  const uint64_t per = (n + nt - 1) / nt;
+  for (unsigned t = 0; t < nt; ++t) {
+    const uint64_t a = t * per, b = std::min(n, a + per);
+    if (a < b) th.emplace_back([&, a, b] { f(a, b); });
+  }
+  for (auto& t : th) t.join();
+}
+
+struct KnnDev {   // device copies for the prefilter + re-rank
+  DevBuf x, xb, xn;
+  uint32_t dp = 0;
+};
+static int knn_upload(pm_ctx* c, const float* v, uint64_t n, uint32_t dim, KnnDev& d) {
+  d.dp = pmk::knn_pad_dim(dim);
+  if (!d.dp) return fail(PM_EINVAL, "kNN supports dim <= 192");
+  CHK(d.x.reserve(std::max<uint64_t>(4, n * dim * 4)));
+  CHK(d.xb.reserve(std::max<uint64_t>(4, n * d.dp * 2)));
+  CHK(d.xn.reserve(std::max<uint64_t>(4, n * 4)));
+  HIPCHK(hipMemcpyAsync(d.x.p, v, n * dim * 4, hipMemcpyHostToDevice, c->stream));
+  c->timed("to_bf16", (double)n * dim * 4, [&] { pmk::to_bf16(c->stream, d.x.as<float>(), n, dim, d.dp, d.xb.p, d.xn.as<float>()); });
+  return 0;
+}
+
+// Exact k nearest base rows of each query by (L2Dist, id), k <= 64 (the
+// ground truth of ComputeRecall, build_graph.go:821-863); ids -1 padded.
+extern "C" int pm_knn(pm_ctx* c, const float* base, uint64_t n, uint64_t dim, const float* queries, uint64_t nq,
+                      uint32_t k, int64_t* ids, float* dists) {
+  if (!c || !base || (!queries && nq) || (!ids && nq)) return fail(PM_EINVAL, "NULL argument");
+  if (k == 0 || k > pmk::knn_top()) return fail(PM_EINVAL, "k must be in [1, 64]");
+  if (n == 0 || dim == 0 || n >= (1ull << 32) - 1) return fail(PM_EINVAL, "n must be in [1, 2^32-1)");
+  HIPCHK(hipSetDevice(c->device));
+  KnnDev B, Q;
+  CHK(knn_upload(c, base, n, (uint32_t)dim, B));
+  CHK(knn_upload(c, queries, nq, (uint32_t)dim, Q));
+  DevBuf cand, out, dist, len;
+  CHK(cand.reserve(std::max<uint64_t>(4, nq * pmk::knn_top() * 4)));
+  CHK(out.reserve(std::max<uint64_t>(4, nq * k * 4)));
+  CHK(dist.reserve(std::max<uint64_t>(4, nq * k * 4)));
+  CHK(len.reserve(std::max<uint64_t>(4, nq * 4)));
+  c->timed("knn_prefilter", (double)nq * n * B.dp * 2, [&] {
+    pmk::knn_prefilter(c->stream, B.xb.p, B.xn.as<float>(), n, Q.xb.p, Q.xn.as<float>(), nq, B.dp, cand.as<uint32_t>()); });
+  c->timed("knn_rerank", (double)nq * pmk::knn_top() * dim * 4, [&] {
+    pmk::knn_rerank(c->stream, B.x.as<float>(), n, (uint32_t)dim, Q.x.as<float>(), nq, cand.as<uint32_t>(), k, false,
+                    out.as<uint32_t>(), dist.as<float>(), len.as<uint32_t>()); });
+  std::vector<uint32_t> o(nq * k), l(nq);
+  std::vector<float> dd(nq * k);
+  HIPCHK(hipMemcpyAsync(o.data(), out.p, nq * k * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(dd.data(), dist.p, nq * k * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(l.data(), len.p, nq * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  for (uint64_t i = 0; i < nq; ++i)
+    for (uint32_t j = 0; j < k; ++j) {
+      ids[i * k + j] = j < l[i] ? (int64_t)o[i * k + j] : -1;
+      if (dists) dists[i * k + j] = j < l[i] ? dd[i * k + j] : INFINITY;
+    }
+  return 0;
+}
+
+extern "C" int pm_build_graph(pm_ctx* c, const float* vectors, uint64_t n, uint64_t dim, uint64_t m, float alpha,
+                              uint64_t seed, uint32_t* graph, double* times) {
+  if (!c || !vectors || !graph) return fail(PM_EINVAL, "NULL argument");
+  const uint32_t K = (uint32_t)((float)m * 1.5f);   // int(float32(m)*1.5) NGT results (build_graph.go:398)
+  if (m == 0 || m > pmk::prune_max_m() || K + 1 > pmk::knn_top())
+    return fail(PM_EINVAL, "m must be in [1, 42] (1.5 m candidates + self within the 64-key prefilter)");
+  if (dim == 0 || dim > pmk::prune_max_dim() || !pmk::knn_pad_dim((uint32_t)dim))
+    return fail(PM_EINVAL, "dim must be in [1, 192]");
+  if (n <= m || n >= (1ull << 32) - 1) return fail(PM_EINVAL, "n must be > m (the random fill needs m other vertices)");
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t st = c->stream;
+  auto t0 = Clock::now();
+  KnnDev X;
+  CHK(knn_upload(c, vectors, n, (uint32_t)dim, X));
+  DevBuf cand, ck, clen, g1, len1, err;
+  CHK(cand.reserve(n * pmk::knn_top() * 4));
+  CHK(ck.reserve(n * K * 4));
+  CHK(clen.reserve(n * 4));
+  CHK(g1.reserve(n * m * 4));
+  CHK(len1.reserve(n * 4));
+  CHK(err.reserve(4));
+  HIPCHK(hipMemsetAsync(err.p, 0, 4, st));
+  // candidates: NGT.Search(u, 1.5m) with u removed (:398-410), exact here
+  c->timed("knn_prefilter", (double)n * n * X.dp * 2, [&] {
+    pmk::knn_prefilter(st, X.xb.p, X.xn.as<float>(), n, X.xb.p, X.xn.as<float>(), n, X.dp, cand.as<uint32_t>()); });
+  c->timed("knn_rerank", (double)n * pmk::knn_top() * dim * 4, [&] {
+    pmk::knn_rerank(st, X.x.as<float>(), n, (uint32_t)dim, X.x.as<float>(), n, cand.as<uint32_t>(), K, true,
+                    ck.as<uint32_t>(), nullptr, clen.as<uint32_t>()); });
+  HIPCHK(hipStreamSynchronize(st));
+  auto t1 = Clock::now();
+  // first pass: robustPrune(vectors, u, candidates, m, alpha) (:413-414)
+  c->timed("prune", 0.0, [&] {
+    pmk::prune(st, X.x.as<float>(), (uint32_t)dim, nullptr, n, nullptr, K, clen.as<uint32_t>(), ck.as<uint32_t>(),
+               (uint32_t)m, alpha, g1.as<uint32_t>(), len1.as<uint32_t>(), err.as<uint32_t>()); });
+  std::vector<uint32_t> G(n * m), L1(n);
+  uint32_t e = 0;
+  HIPCHK(hipMemcpyAsync(G.data(), g1.p, n * m * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(L1.data(), len1.p, n * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(&e, err.p, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (e) return fail(PM_EINVAL, "robustPrune: candidate list above the kernel's limit");
+  auto t2 = Clock::now();
+  // bi-directional edges (:421-430): biGraph[x] = [u < x with x in graph[u]] ++
+  // graph[x] ++ [u > x with x in graph[u]], u ascending, with multiplicity
+  std::vector<uint64_t> roff(n + 1, 0);
+  for (uint64_t u = 0; u < n; ++u)
+    for (uint32_t j = 0; j < L1[u]; ++j) roff[G[u * m + j] + 1]++;
+  for (uint64_t x = 0; x < n; ++x) roff[x + 1] += roff[x];
+  std::vector<uint32_t> rev(roff[n]);
+  {
+    std::vector<uint64_t> fillp(roff.begin(), roff.end() - 1);
+    for (uint64_t u = 0; u < n; ++u)
+      for (uint32_t j = 0; j < L1[u]; ++j) rev[fillp[G[u * m + j]]++] = (uint32_t)u;
+  }
+  std::vector<uint32_t> inb(n);   // inbounds = len(biGraph) (:433-436)
+  for (uint64_t x = 0; x < n; ++x) inb[x] = (uint32_t)(L1[x] + roff[x + 1] - roff[x]);
+  // sampling (:448-462): keep edge j of u with probability min(1.5m / inbounds[v], 1)
+  std::vector<uint32_t> clen2(n);
+  std::vector<uint64_t> coff(n + 1, 0);
+  auto visit = [&](uint64_t x, auto&& fn) {   // biGraph[x] in order
+    const uint32_t* r = rev.data() + roff[x];
+    const uint64_t nr = roff[x + 1] - roff[x];
+    uint64_t a = 0, j = 0;
+    while (a < nr && r[a] < x) fn(j++, r[a++]);
+    for (uint32_t i = 0; i < L1[x]; ++i) fn(j++, G[x * m + i]);
+    while (a < nr) fn(j++, r[a++]);
+  };
+  auto keep = [&](uint64_t u, uint64_t j, uint32_t v) {
+    const double prob = std::min(1.5 * (double)m / (double)inb[v], 1.0);
+    const double r = (double)(hash4(seed, DOM_GRAPH_SAMPLE, u, j, 0) >> 11) * 0x1.0p-53;
+    return r < prob;
+  };
+  par_for(n, [&](uint64_t a, uint64_t b) {
+    for (uint64_t u = a; u < b; ++u) {
+      uint32_t cnt = 0;
+      visit(u, [&](uint64_t j, uint32_t v) { cnt += keep(u, j, v); });
+      clen2[u] = cnt;
+    }
+  });
+  for (uint64_t u = 0; u < n; ++u) coff[u + 1] = coff[u] + clen2[u];
+  std::vector<uint32_t> conn(coff[n]);
+  par_for(n, [&](uint64_t a, uint64_t b) {
+    for (uint64_t u = a; u < b; ++u) {
+      uint32_t* o = conn.data() + coff[u];
+      visit(u, [&](uint64_t j, uint32_t v) { if (keep(u, j, v)) *o++ = v; });
+    }
+  });
+  // second pass: robustPrune of the lists above m (:464-466) on the GPU
+  std::vector<uint32_t> big;
+  for (uint64_t u = 0; u < n; ++u) if (clen2[u] > m) big.push_back((uint32_t)u);
+  auto t3 = Clock::now();
+  if (!big.empty()) {
+    DevBuf dv, doff, dlen, dids, dout, dol;
+    CHK(dv.reserve(big.size() * 4));
+    CHK(doff.reserve(n * 8));
+    CHK(dlen.reserve(n * 4));
+    CHK(dids.reserve(std::max<uint64_t>(4, conn.size() * 4)));
+    CHK(dout.reserve(n * m * 4));
+    CHK(dol.reserve(n * 4));
+    HIPCHK(hipMemcpyAsync(dv.p, big.data(), big.size() * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(doff.p, coff.data(), n * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(dlen.p, clen2.data(), n * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(dids.p, conn.data(), conn.size() * 4, hipMemcpyHostToDevice, st));
+    c->timed("prune", 0.0, [&] {
+      pmk::prune(st, X.x.as<float>(), (uint32_t)dim, dv.as<uint32_t>(), big.size(), doff.as<uint64_t>(), 0,
+                 dlen.as<uint32_t>(), dids.as<uint32_t>(), (uint32_t)m, alpha, dout.as<uint32_t>(),
+                 dol.as<uint32_t>(), err.as<uint32_t>()); });
+    std::vector<uint32_t> P(n * m), PL(n);
+    HIPCHK(hipMemcpyAsync(P.data(), dout.p, n * m * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(PL.data(), dol.p, n * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&e, err.p, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (e) return fail(PM_EINVAL, "robustPrune: a sampled connection list exceeds 4096 candidates");
+    for (uint32_t u : big) {   // robustPrune of a list > m returns exactly m
+      memcpy(conn.data() + coff[u], &P[(uint64_t)u * m], m * 4);
+      clen2[u] = PL[u];
+    }
+  }
+  auto t4 = Clock::now();
+  // random fill to exactly m (:468-486)
+  par_for(n, [&](uint64_t a, uint64_t b) {
+    std::vector<uint32_t> cur;
+    for (uint64_t u = a; u < b; ++u) {
+      cur.assign(conn.data() + coff[u], conn.data() + coff[u] + std::min<uint64_t>(clen2[u], m));
+      uint64_t t = 0;
+      while (cur.size() < m) {
+        const uint32_t v = (uint32_t)(hash4(seed, DOM_GRAPH_FILL, u, t++, 0) % n);
+        if (v == u) continue;
+        if (std::find(cur.begin(), cur.end(), v) != cur.end()) continue;
+        cur.push_back(v);
+      }
+      memcpy(graph + u * m, cur.data(), m * 4);
+    }
+  });
+  if (times) {
+    times[0] = std::chrono::duration<double>(t1 - t0).count();   // kNN candidates
+    times[1] = std::chrono::duration<double>(t2 - t1).count();   // first robustPrune
+    times[2] = std::chrono::duration<double>(t3 - t2 + (Clock::now() - t4)).count();   // host edges, sampling, fill
+    times[3] = std::chrono::duration<double>(t4 - t3).count();   // second robustPrune
+  }
+  return 0;
+}

@@ -184,4 +184,18 @@ void ip_rows(hipStream_t st, const uint32_t* rows, uint64_t nrows, const uint32_
 void ip_fill(hipStream_t st, uint32_t* rows, uint64_t N, uint32_t D);
 void prf_batch(hipStream_t st, const uint32_t* rk, const uint64_t* tags, const uint64_t* xs,
                uint64_t n, uint64_t* out);
+// graph construction and ground truth (pm_graph.hip)
+uint32_t knn_pad_dim(uint32_t dim);   // bf16 row width for the prefilter (0: unsupported)
+uint32_t knn_top();                   // prefilter candidates per query row
+uint32_t prune_max_list();
+uint32_t prune_max_dim();
+uint32_t prune_max_m();
+void to_bf16(hipStream_t st, const float* rows, uint64_t n, uint32_t dim, uint32_t dp, void* out, float* norms);
+void knn_prefilter(hipStream_t st, const void* X, const float* xn, uint64_t N, const void* Q, const float* qn,
+                   uint64_t M, uint32_t dp, uint32_t* out);
+void knn_rerank(hipStream_t st, const float* X, uint64_t N, uint32_t dim, const float* Q, uint64_t M,
+                const uint32_t* cand, uint32_t K, bool self_base, uint32_t* out, float* dist, uint32_t* len);
+void prune(hipStream_t st, const float* X, uint32_t dim, const uint32_t* verts, uint64_t nverts,
+           const uint64_t* offs, uint64_t stride, const uint32_t* lens, const uint32_t* ids, uint32_t m,
+           float alpha, uint32_t* out, uint32_t* out_len, uint32_t* err);
 }  // namespace pmk

@@ -158,3 +158,38 @@ def test_msmarco_parameters(oracle):
             sub["MaxQueryPerChunk"]) == (1024, 196, 5460, 7168, 88)
     assert round(s["CommOnline"] * 60 / 1024) == 3150
     assert s["SupportBatchNum"] // 60 == 45
+
+
+def test_oracle_robust_prune_properties():
+    """robustPrune (build_graph.go:169-236) restated: lists of at most m come
+    back unchanged; otherwise exactly m ids, the nearest candidate first, and
+    with alpha = 0 (no candidate ever dominated) the m nearest in order."""
+    import numpy as np
+    from oracle import oracle as O
+    rng = np.random.default_rng(0)
+    X = rng.integers(0, 256, size=(200, 16)).astype(np.float32)
+    cand = np.arange(1, 41, dtype=np.uint32)
+    assert np.array_equal(O.robust_prune(X, 0, cand[:8], 8), cand[:8])
+    r = O.robust_prune(X, 0, cand, 8, 1.2)
+    d = O.l2_batch(X[0], X[cand])
+    assert len(r) == 8 and r[0] == cand[np.argmin(d)]
+    r0 = O.robust_prune(X, 0, cand, 8, 0.0)
+    assert np.array_equal(r0, cand[np.lexsort((np.arange(40), d))][:8])
+
+
+def test_oracle_build_graph_properties():
+    """The graph restatement: m neighbours per row, no self loops, deterministic
+    in the seed, different across seeds (sampling and fill).  A row may repeat
+    an id, as the reference's may: a mutual edge appears twice in biGraph and
+    both copies can survive sampling when the list is not pruned (:445-462)."""
+    import numpy as np
+    from oracle import oracle as O
+    from tests.datagen import clustered_vectors
+    v = clustered_vectors(600, 32, seed=1)
+    g = O.build_graph(v, 12, 1.2, seed=4)
+    assert g.shape == (600, 12)
+    assert (g != np.arange(600)[:, None]).all()
+    assert np.array_equal(g, O.build_graph(v, 12, 1.2, seed=4))
+    assert not np.array_equal(g, O.build_graph(v, 12, 1.2, seed=5))
+    ids, _ = O.knn(v, v[:3], 5)
+    assert (ids[:, 0] == np.arange(3)).all()   # each row's own nearest is itself
