@@ -56,11 +56,21 @@ HOST = ["host_search_knn", "host_knn_init", "host_knn_final", "host_knn_batch", 
         "host_wait_first_token", "host_wait_all_tokens"]
 
 
-def make_data(rank: int):
-    from tests.datagen import clustered_vectors, random_graph
-    v = clustered_vectors(N, DIM, seed=100 + rank)
-    g = random_graph(N, M, seed=200 + rank)
-    return v, g
+def make_data(rank: int, graph: str, ctx):
+    """SIFT1M-shaped synthetic vectors and the degree-32 graph: built on the GPU
+    (pm_build_graph: BuildGraph with exact kNN candidates in place of NGT), or
+    the reference's synthetic-mode genRandomGraph (--graph random)."""
+    import pacmann_amd as pm
+    from tests.datagen import random_graph, sift_like_vectors
+    v = sift_like_vectors(N, DIM, seed=100 + rank)
+    if graph == "random":
+        return v, random_graph(N, M, seed=200 + rank), None
+    ctx.sync()
+    t0 = time.perf_counter()
+    g, tm = pm.build_graph(v, M, 1.2, seed=7 + rank, ctx=ctx)
+    tm = {k: round(x, 4) for k, x in tm.items()}
+    tm["total_s"] = round(time.perf_counter() - t0, 4)
+    return v, g, tm
 
 
 def make_queries(v, n, seed):
@@ -156,18 +166,23 @@ def dist_init():
     return dist, dist.get_rank(), ws, int(os.environ.get("LOCAL_RANK", "0"))
 
 
-def cpu_baseline(v, g, queries):
+def cpu_baseline(v, g, queries, ctx):
     """The oracle (single-thread C++ restatement of the Go/AVX path) on a bounded
     sample of the same workload: one preprocessing, then 46 queries = two
-    23-query maintenance windows, value = q / (online + maintenance)."""
+    23-query maintenance windows, value = q / (online + maintenance); with the
+    recall@10 of its answers."""
+    import pacmann_amd as pm
     from oracle import oracle as O
+    from pacmann_amd.report import compute_recall
     og = O.Graph(v, g, pir_seed=11, search_seed=12)
     t0 = time.perf_counter()
     og.Preprocess()
     prep = time.perf_counter() - t0
     nq = 46
-    _, online, maint = og.SearchLoop(queries[:nq], K_TOP, STEP, PARALLEL)
+    ans, online, maint = og.SearchLoop(queries[:nq], K_TOP, STEP, PARALLEL)
+    rec = compute_recall(pm.knn(v, queries[:nq], K_TOP, ctx), ans, K_TOP)
     return {"value": nq / (online + maint), "unit": "queries/s", "cores": 1, "kind": "port",
+            "recall_at_10": round(float(rec), 4),
             "sample": f"{nq} SIFT1M-shaped private queries (2 maintenance windows) after one "
                       f"{prep:.2f}s preprocessing; online {online:.2f}s + maintenance {maint:.2f}s"}
 
@@ -182,20 +197,23 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-config2", action="store_true", help="skip the MS-MARCO-shaped batch-PIR block")
     ap.add_argument("--no-single", action="store_true", help="skip the one-client latency block")
+    ap.add_argument("--graph", choices=["built", "random"], default="built",
+                    help="GPU-built kNN+robustPrune graph (default) or the reference's synthetic random graph")
     args = ap.parse_args()
     S = max(1, args.sessions)
 
     dist, rank, ws, local = dist_init()
     import pacmann_amd as pm
 
-    v, g = make_data(rank)
+    ctx0 = pm.Context(local)
+    v, g, gbuild = make_data(rank, args.graph, ctx0)
     nq = args.warmup + args.steps + PROFILE_QUERIES
     queries = make_queries(v, S * nq + 64, seed=300 + rank)
     qsess = queries[:S * nq].reshape(S, nq, -1)
     # session 0 owns the graph and the server DB (GraphANNFrontend.Preprocess:
     # DB packing + first hint preprocessing); sessions 1..S-1 are further
     # clients over the same device DB, each with its own keys and hint state
-    base = pm.PIRGraphInfo(v, g, pir_seed=11 + 97 * rank, search_seed=12 + 97 * rank, ctx=pm.Context(local))
+    base = pm.PIRGraphInfo(v, g, pir_seed=11 + 97 * rank, search_seed=12 + 97 * rank, ctx=ctx0)
     base.Preprocess()
     sess = [base] + [base.Session(11 + 97 * rank + i, 12 + 97 * rank + i, pm.Context(local)) for i in range(1, S)]
     for s_ in sess[1:]:
@@ -212,8 +230,8 @@ def main():
     for c in ctxs:
         c.sync()
     t0 = time.perf_counter()
-    _, _, online, maint = pm.search_loop_sessions(sess, qsess[:, args.warmup:args.warmup + args.steps],
-                                                  K_TOP, STEP, PARALLEL)
+    answers, _, online, maint = pm.search_loop_sessions(sess, qsess[:, args.warmup:args.warmup + args.steps],
+                                                        K_TOP, STEP, PARALLEL)
     for c in ctxs:
         c.sync()
     if dist:
@@ -243,6 +261,11 @@ def main():
         n, ms, by = tsum(k)
         # scaled to the timed region's step count: launches, device ms, bytes
         ktime[k] = (nsteps, ms / max(n, 1) * nsteps, by / max(n, 1) * nsteps)
+    # recall@10 of every timed answer against exact kNN (ComputeRecall, build_graph.go:821-863)
+    from pacmann_amd.report import compute_recall
+    tq = qsess[:, args.warmup:args.warmup + args.steps].reshape(-1, DIM)
+    gt = pm.knn(v, tq, K_TOP, ctx0)
+    recall = compute_recall(gt, answers.reshape(-1, K_TOP), K_TOP)
     # the reference's own accounting, one client alone (latency view; not `value`)
     single = None
     if rank == 0 and not args.no_single:
@@ -315,7 +338,9 @@ def main():
         "metric": METRIC, "value": round(value, 2), "unit": "queries/s", "n_gpus": ws,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
-        "data": "synthetic (clustered SIFT-like uint8-valued f32 vectors, uniform random degree-32 graph)",
+        "data": ("synthetic SIFT-like uint8-valued f32 vectors (12-D latent mixture); "
+                 + ("uniform random degree-32 graph (genRandomGraph)" if args.graph == "random"
+                    else "degree-32 graph built on the GPU (exact kNN candidates + robustPrune, alpha 1.2)")),
         "config": {"workload": "SIFT1M-shaped private graph search over 16-partition batch PianoPIR",
                    "n": N, "dim": DIM, "m": M, "k": K_TOP, "step": STEP, "parallel": PARALLEL,
                    "batch_size": M, "failure_prob_log2": F, "sessions_per_gpu": S,
@@ -323,6 +348,9 @@ def main():
         "roofline": main_roof,
         "roofline_prep": fold,
         "single_session": single,
+        "recall_at_10": round(float(recall), 4),
+        "recall_queries": int(tq.shape[0]),
+        "graph_build": gbuild,
         "online_s_per_query": round(float(np.mean(online)) / args.steps, 6),
         "maintenance_s_per_query": round(float(np.mean(maint)) / args.steps, 6),
         "preprocessing_s": round(stats["PreprocessingTime"], 6),
@@ -333,7 +361,7 @@ def main():
         "dominant_kernel": dom,
     }
     if not args.no_cpu_baseline and ws == 1:
-        out["cpu_baseline"] = cpu_baseline(v, g, queries[S * nq:])
+        out["cpu_baseline"] = cpu_baseline(v, g, queries[S * nq:], ctx0)
     if ws == 1 and not args.no_config2:
         out["config2_batch_pir"] = batch_pir_msmarco(ctxs[0], not args.no_cpu_baseline)
     print(json.dumps(out), flush=True)

@@ -22,6 +22,29 @@ def clustered_vectors(n, d, centers=None, sigma=20.0, seed=0):
     return out
 
 
+def sift_like_vectors(n, d, seed=0, latent=12, centers=64):
+    """SIFT1M-shaped stand-in with low intrinsic dimension (real SIFT's is ~10-20):
+    a 12-D Gaussian mixture of overlapping clusters, mapped to d dims by a
+    random linear map plus noise, scaled per dimension and rounded to integer
+    values in [0,255] (bvecs semantics).  Unlike clustered_vectors' isolated
+    blobs, its kNN graph is navigable, so recall@10 means something."""
+    rng = np.random.default_rng(seed)
+    c = rng.normal(0, 2.0, size=(centers, latent))
+    W = rng.normal(0, 1.0, size=(latent, d)).astype(np.float32)
+    # per-dimension affine scaling from the generating distribution's moments
+    mean = c.mean(0) @ W
+    var = ((c.var(0) + 1.0)[:, None] * W.astype(np.float64) ** 2).sum(0) + 1.0
+    scale = (40.0 / np.sqrt(var)).astype(np.float32)
+    out = np.empty((n, d), dtype=np.float32)
+    step = 1 << 17
+    for a in range(0, n, step):
+        b = min(n, a + step)
+        z = (c[rng.integers(0, centers, size=b - a)] + rng.normal(0, 1.0, size=(b - a, latent))).astype(np.float32)
+        x = z @ W + rng.normal(0, 1.0, size=(b - a, d)).astype(np.float32)
+        out[a:b] = np.clip(np.rint((x - mean.astype(np.float32)) * scale + 100.0), 0, 255)
+    return out
+
+
 def knn_graph(v, m):
     """Exact m-NN graph (no self loops) by brute force; small n only."""
     n = v.shape[0]

@@ -18,7 +18,7 @@ import pacmann_amd as pm  # noqa: E402
 
 smax = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 nq = int(sys.argv[2]) if len(sys.argv) > 2 else 100
-v, g = bench.make_data(0)
+v, g, _ = bench.make_data(0, "random", None)
 qs = bench.make_queries(v, smax * nq + 8, seed=300)
 base = pm.PIRGraphInfo(v, g, pir_seed=11, search_seed=12, ctx=pm.Context(0))
 base.Preprocess()
