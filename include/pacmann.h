@@ -134,6 +134,16 @@ int  pm_batchpir_create(pm_ctx* ctx, uint64_t DBSize, uint64_t DBEntryByteNum, u
 int  pm_batchpir_create_shard(pm_ctx* ctx, uint64_t DBSize, uint64_t DBEntryByteNum, uint64_t BatchSize,
                               const uint64_t* rawDB, uint64_t FailureProbLog2, uint64_t seed,
                               uint32_t shard, uint32_t nshards, pm_batchpir** out);
+/* The same shard over a synthetic DB generated on the device (BIGANN-scale
+ * benchmarks, BASELINE.json configs[3]/[4]: tens of GB never cross PCIe).  It
+ * replaces the reference's in-process random DB of TestBatchPIRPerf
+ * (pir_test.go:204-275).  Word w of global row r is
+ *   sm64(sm64(db_seed + 9) ^ (r * DBEntrySize + w)),
+ * sm64 = the splitmix64 finalizer of (x + 0x9e3779b97f4a7c15),
+ * so a caller can recompute any row to check an answer. */
+int  pm_batchpir_create_synth(pm_ctx* ctx, uint64_t DBSize, uint64_t DBEntryByteNum, uint64_t BatchSize,
+                              uint64_t FailureProbLog2, uint64_t seed, uint64_t db_seed, uint32_t shard,
+                              uint32_t nshards, pm_batchpir** out);
 /* Another client of the same server (multi-session serving, SURVEY.md §8f
  * rank 2): a new SimpleBatchPianoPIR client (own keys from `seed`, own hint
  * state, counters and local cache) whose server side reads the DB rows of

@@ -89,6 +89,7 @@ SIGNATURES = {
     "pm_batchpir_query": (C.c_int, [vp, u64p, u64, u64p]),
     "pm_batchpir_query_ok": (C.c_int, [vp, u64p, u64, u64p, C.POINTER(C.c_uint8)]),
     "pm_batchpir_create_shard": (C.c_int, [vp, u64, u64, u64, u64p, u64, u64, C.c_uint32, C.c_uint32, C.POINTER(vp)]),
+    "pm_batchpir_create_synth": (C.c_int, [vp, u64, u64, u64, u64, u64, u64, C.c_uint32, C.c_uint32, C.POINTER(vp)]),
     "pm_batchpir_stats_get": (C.c_int, [vp, C.POINTER(BatchStats)]),
     "pm_batchpir_subconfig": (C.c_int, [vp, u64, C.POINTER(PirConfig)]),
     "pm_pir_export": (C.c_int, [vp, u32p, u64p, u64p, u64p, u64p, u64p, u64p, u64p, u64p]),
@@ -178,7 +179,8 @@ class Context:
     def sync(self):
         _check(lib().pm_ctx_sync(self.h))
 
-    def timing(self, on: bool):
+    def timing(self, on):
+        """0 off, 1 (True) preprocessing and leaf kernels, 2 also the step kernels."""
         _check(lib().pm_timing_enable(self.h, int(on)))
 
     def timing_reset(self):
@@ -328,20 +330,52 @@ class PianoPIR:
         return _export(lib().pm_pir_export, self.h, c)
 
 
+_M64 = (1 << 64) - 1
+
+
+def _sm64(x: np.ndarray) -> np.ndarray:
+    """splitmix64 finalizer of (x + golden), vectorised (pm_internal.h sm64)."""
+    with np.errstate(over="ignore"):
+        z = x + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def synth_rows(db_seed: int, ids, E: int) -> np.ndarray:
+    """Rows of the device-generated DB (pm_batchpir_create_synth): word w of
+    row r = sm64(sm64(db_seed + 9) ^ (r * E + w)).  Returns len(ids) x E u64."""
+    k = _sm64(np.array([(db_seed + 9) & _M64], dtype=np.uint64))[0]
+    ids = np.asarray(ids, dtype=np.uint64).reshape(-1, 1)
+    with np.errstate(over="ignore"):
+        x = ids * np.uint64(E) + np.arange(E, dtype=np.uint64)[None, :]
+    return _sm64(k ^ x)
+
+
 class SimpleBatchPianoPIR:
     """pianopir.SimpleBatchPianoPIR (batch-pir.go:40-276) on the GPU."""
 
     def __init__(self, DBSize: int, DBEntryByteNum: int, BatchSize: int, rawDB,
                  FailureProbLog2: int, seed: int = 1, ctx: Context | None = None, _handle=None,
-                 shard: int = 0, nshards: int = 1):
+                 shard: int = 0, nshards: int = 1, db_seed: int | None = None):
         """shard / nshards: hold only partitions p % nshards == shard
-        (pm_batchpir_create_shard); see ShardedBatchPIR for the combine."""
+        (pm_batchpir_create_shard); see ShardedBatchPIR for the combine.
+        db_seed (with rawDB None): the DB is generated on the device,
+        row r = synth_rows(db_seed, [r], E) (pm_batchpir_create_synth)."""
         self.ctx = ctx or default_context()
         self.E = DBEntryByteNum // 8
         self.shard, self.nshards = shard, nshards
         self._owned = _handle is None
         if _handle is not None:
             self.h = _handle
+            return
+        if db_seed is not None:   # device-generated rows (pm_batchpir_create_synth, synth_rows)
+            if rawDB is not None:
+                raise ValueError("pass rawDB or db_seed, not both")
+            h = vp()
+            _check(lib().pm_batchpir_create_synth(self.ctx.h, DBSize, DBEntryByteNum, BatchSize, FailureProbLog2,
+                                                  seed, db_seed, shard, nshards, C.byref(h)))
+            self.h = h
             return
         db = _u64(rawDB)
         if db.size != DBSize * self.E:   # batch-pir.go:57-59 log.Fatalf

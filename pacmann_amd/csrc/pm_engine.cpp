@@ -158,6 +158,7 @@ struct pm_ctx {
   hipStream_t stream = nullptr;
   int timing = 0;   // 0 off, 1 preprocessing / leaf kernels, 2 also the per-step kernels
   bool no_fuse = false;      // PM_NO_FUSE=1: the three step kernels even when k_step fits
+  bool no_split = false;     // PM_NO_SPLIT=1: k_answer gathers wide sets itself (no k_gather)
   bool no_guess = false;
   bool verify_rows = false;
   bool debug_cache = false;
@@ -224,6 +225,8 @@ extern "C" int pm_ctx_create(int device, pm_ctx** out) {
   c->debug_sync = dbg && dbg[0] == '1';
   const char* nf = getenv("PM_NO_FUSE");
   c->no_fuse = nf && nf[0] == '1';
+  const char* ns = getenv("PM_NO_SPLIT");
+  c->no_split = ns && ns[0] == '1';
   const char* ls = getenv("PM_LOG_STEPS");
   c->log_steps = ls && ls[0] == '1';
   const char* dc = getenv("PM_DEBUG_CACHE");
@@ -299,7 +302,7 @@ struct Engine {
   uint32_t gran_words = 0;
   std::vector<uint32_t> owned_list;   // owned partitions in order (owned_d holds their PmPart)
   DevBuf qoffs, ans_srv;
-  DevBuf subs_d, sb_d, bits, cand, meta, spec, res_d, ans, qvec, stamps;
+  DevBuf subs_d, sb_d, bits, cand, meta, spec, res_d, ans, part_x, qvec, stamps;
   std::vector<double> stamp_sum;   // PM_STAMPS builds: accumulated phase deltas
   uint64_t stamp_n = 0;
   uint32_t step_token = 0;         // PmStep::token of the last step
@@ -364,10 +367,11 @@ static double part_comm(const PartHost& p, uint64_t E) { return (double)((uint64
 
 static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, uint64_t B,
                          const uint64_t* rawDB, uint64_t F, uint64_t seed, bool batch,
-                         uint32_t shard = 0, uint32_t nshards = 1, const Engine* server = nullptr) {
+                         uint32_t shard = 0, uint32_t nshards = 1, const Engine* server = nullptr,
+                         const uint64_t* synth_seed = nullptr) {
   if (nshards == 0 || shard >= nshards) return fail(PM_EINVAL, "shard must be < nshards");
   if (!ctx) return fail(PM_EINVAL, "ctx is NULL");
-  if (!rawDB && N && !server) return fail(PM_EINVAL, "rawDB is NULL");
+  if (!rawDB && N && !server && !synth_seed) return fail(PM_EINVAL, "rawDB is NULL");
   if (server && server->ctx->device != ctx->device) return fail(PM_EINVAL, "a client shares the server DB of its own device only");
   if (N == 0) return fail(PM_EINVAL, "DBSize must be > 0");
   if (Ebytes < 8) return fail(PM_EINVAL, "DBEntryByteNum must be >= 8");
@@ -426,8 +430,16 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
   else CHK(g->db->reserve(std::max<uint64_t>(8, off_db * g->E * 8)));
   for (uint32_t i : server ? std::vector<uint32_t>{} : g->owned_list) {
     const uint64_t start = (uint64_t)i * g->PS, rows = g->parts[i].d.N;
-    HIPCHK(hipMemcpy(g->db->as<uint64_t>() + g->parts[i].d.row0 * g->E, rawDB + start * g->E, rows * g->E * 8,
-                     hipMemcpyHostToDevice));
+    if (synth_seed)
+      pmk::db_synth(ctx->stream, g->db->as<uint64_t>() + g->parts[i].d.row0 * g->E, start, rows, (uint32_t)g->E,
+                    *synth_seed);
+    else
+      HIPCHK(hipMemcpy(g->db->as<uint64_t>() + g->parts[i].d.row0 * g->E, rawDB + start * g->E, rows * g->E * 8,
+                       hipMemcpyHostToDevice));
+  }
+  if (synth_seed) {
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(ctx->stream));
   }
   CHK(g->tag.reserve(off_tag * 4));
   CHK(g->pp.reserve(off_pp * 4));
@@ -812,7 +824,13 @@ static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
               r.tag, r.pp, r.slot, r.flags, bad ? "  <-- BAD" : "");
     }
   }
-  c->timed_ext("answer", ans_bytes, [&](pmk::PmEvents ev) { pmk::step_answer(st, S, ev); }, 2);
+  S.nsplit = c->no_split ? 1 : pmk::step_gather_split(g->maxSS, nsub);
+  if (S.nsplit > 1) {
+    CHK(g->part_x.reserve((uint64_t)nsub * S.nsplit * (E & ~3ull) * 8));
+    S.part_x = g->part_x.as<uint64_t>();
+    c->timed_ext("gather", ans_bytes, [&](pmk::PmEvents ev) { pmk::step_gather(st, S, ev); }, 2);
+  }
+  c->timed_ext("answer", S.nsplit > 1 ? 0 : ans_bytes, [&](pmk::PmEvents ev) { pmk::step_answer(st, S, ev); }, 2);
   HIPCHK(hipGetLastError());
   c->host_add(HT_STEP_LAUNCH, ms_since(t_begin));
   return wait_and_post(g, S, nsub, t_begin);
@@ -981,6 +999,17 @@ extern "C" int pm_batchpir_create_shard(pm_ctx* ctx, uint64_t DBSize, uint64_t D
   if (!out) return fail(PM_EINVAL, "out is NULL");
   pm_batchpir* h = new pm_batchpir();
   int r = engine_create(ctx, &h->e, DBSize, DBEntryByteNum, BatchSize, rawDB, F, seed, true, shard, nshards);
+  if (r) { delete h; return r; }
+  *out = h;
+  return 0;
+}
+extern "C" int pm_batchpir_create_synth(pm_ctx* ctx, uint64_t DBSize, uint64_t DBEntryByteNum,
+                                        uint64_t BatchSize, uint64_t FailureProbLog2, uint64_t seed,
+                                        uint64_t db_seed, uint32_t shard, uint32_t nshards, pm_batchpir** out) {
+  if (!out) return fail(PM_EINVAL, "out is NULL");
+  pm_batchpir* h = new pm_batchpir();
+  int r = engine_create(ctx, &h->e, DBSize, DBEntryByteNum, BatchSize, nullptr, FailureProbLog2, seed, true, shard,
+                        nshards, nullptr, &db_seed);
   if (r) { delete h; return r; }
   *out = h;
   return 0;

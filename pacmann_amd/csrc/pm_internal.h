@@ -25,7 +25,7 @@ constexpr uint16_t kSkip = 0xffffu;                      // prep offset sentinel
 constexpr int kBlock = 256;
 
 // Randomness streams; identical spec to oracle/pm_oracle.cpp.
-enum : uint64_t { DOM_KEY = 1, DOM_REPL = 2, DOM_DUMMY = 3 };
+enum : uint64_t { DOM_KEY = 1, DOM_REPL = 2, DOM_DUMMY = 3, DOM_SYNTH_DB = 9 };
 __host__ __device__ inline uint64_t sm64(uint64_t x) {
   uint64_t z = x + 0x9e3779b97f4a7c15ULL;
   z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
@@ -141,6 +141,10 @@ struct PmStep {
   uint32_t np_live;            // partitions with at least one sub-query in this step
   uint32_t pf_w0, pf_w1;       // row words the host reads (PmOutHdr::csum covers them)
   uint32_t no_guess;           // k_step diagnostics: answers wait for their resolution (PM_NO_GUESS=1)
+  // Split gather (three-kernel path, wide sets): k_gather writes nsplit partial
+  // XORs of each sub-query's set, [nsub][nsplit][E&~3]; k_answer folds them.
+  uint32_t nsplit;             // 0/1: k_answer gathers its set itself
+  PM_G uint64_t* part_x;
   // Small steps ship the descriptor inside the kernel arguments (no PCIe
   // round trip); larger ones use subs_h / sb_h.
   uint32_t args_valid;
@@ -172,6 +176,10 @@ bool step_fused_ok(const PmStep& S, uint32_t maxPH, uint32_t max_sub_per_part);
 void step_fused(hipStream_t st, const PmStep& S, PmEvents ev = {});
 bool step_resolve_lds_ok(uint32_t maxPH, uint32_t max_sub_per_part);
 void step_answer(hipStream_t st, const PmStep& S, PmEvents ev = {});
+// Split gather ahead of k_answer for wide query sets (SetSize >= 256, BIGANN
+// scale): how many workgroups per sub-query (1: no split), and the launch.
+uint32_t step_gather_split(uint32_t maxSS, uint32_t nsub);
+void step_gather(hipStream_t st, const PmStep& S, PmEvents ev = {});
 uint32_t step_max_sub_per_part();
 uint32_t step_max_ss();
 uint32_t step_max_e();
@@ -182,6 +190,9 @@ void l2_rows(hipStream_t st, const float* rows, uint64_t row_stride_floats, uint
 void ip_rows(hipStream_t st, const uint32_t* rows, uint64_t nrows, const uint32_t* q, uint32_t dim,
              uint32_t* per_row, uint32_t* sum);
 void ip_fill(hipStream_t st, uint32_t* rows, uint64_t N, uint32_t D);
+// Synthetic DB rows (pm_batchpir_create_synth): dst row i = global row r0 + i,
+// word w = sm64(sm64(db_seed + DOM_SYNTH_DB) ^ (r * E + w)).
+void db_synth(hipStream_t st, uint64_t* dst, uint64_t r0, uint64_t rows, uint32_t E, uint64_t db_seed);
 void prf_batch(hipStream_t st, const uint32_t* rk, const uint64_t* tags, const uint64_t* xs,
                uint64_t n, uint64_t* out);
 // graph construction and ground truth (pm_graph.hip)

@@ -487,6 +487,15 @@ __global__ void __launch_bounds__(kBlock) k_ip_fill(uint4* __restrict__ rows, ui
   }
 }
 
+// Synthetic DB fill (BIGANN-scale benchmarks: the rows never cross PCIe).
+// Grid-stride over the words of rows [r0, r0 + rows) of the global DB.
+__global__ void __launch_bounds__(kBlock) k_db_synth(uint64_t* __restrict__ dst, uint64_t r0, uint64_t nw,
+                                                     uint32_t E, uint64_t k) {
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock, x0 = r0 * E;
+  for (uint64_t f = (uint64_t)blockIdx.x * kBlock + threadIdx.x; f < nw; f += stride)
+    __builtin_nontemporal_store(sm64(k ^ (x0 + f)), dst + f);
+}
+
 __global__ void __launch_bounds__(kBlock) k_prf_batch(const uint32_t* __restrict__ rk,
                                                       const uint64_t* __restrict__ tags,
                                                       const uint64_t* __restrict__ xs, uint64_t n,
@@ -610,6 +619,13 @@ void ip_fill(hipStream_t st, uint32_t* rows, uint64_t N, uint32_t D) {
   unsigned grid = cdiv(n4, kBlock);
   if (grid > 256 * 16) grid = 256 * 16;
   hipLaunchKernelGGL(k_ip_fill, dim3(grid), dim3(kBlock), 0, st, (uint4*)rows, n4, D);
+}
+void db_synth(hipStream_t st, uint64_t* dst, uint64_t r0, uint64_t rows, uint32_t E, uint64_t db_seed) {
+  const uint64_t nw = rows * E;
+  unsigned grid = cdiv(nw, kBlock);
+  if (grid > 256 * 32) grid = 256 * 32;
+  if (grid == 0) return;
+  hipLaunchKernelGGL(k_db_synth, dim3(grid), dim3(kBlock), 0, st, dst, r0, nw, E, sm64(db_seed + DOM_SYNTH_DB));
 }
 void prf_batch(hipStream_t st, const uint32_t* rk, const uint64_t* tags, const uint64_t* xs, uint64_t n,
                uint64_t* out) {

@@ -1140,6 +1140,18 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, AnswerL
       e_bp = P.parity[((uint64_t)P.PH + dslot) * E + tid];
       e_pp = P.parity[(uint64_t)r.hit * E + tid];
     }
+    if (!GRAN && S.nsplit > 1) {   // k_gather did the set: fold its partial XORs
+      if (mode == A_FINAL || mode == A_CHAINED || mode == A_DUMMY) {
+        const PM_G uint64_t* px = S.part_x + (uint64_t)s * S.nsplit * EX;
+        for (uint32_t w = tid; w < EX; w += NT) {
+          uint64_t x = 0;
+          for (uint32_t j = 0; j < S.nsplit; ++j) x ^= px[(uint64_t)j * EX + w];
+          row.w[w] = x;
+        }
+      }
+      __syncthreads();
+      return;
+    }
     // ---- query set (pir.go:363-371 dummy; :424-444 real) -------------------
     if (mode == A_FINAL || mode == A_CHAINED) {
       const uint32_t pchunk = r.pp != kDefaultProgramPoint ? (r.pp >> lg) : kNone;
@@ -1357,6 +1369,87 @@ __global__ void __launch_bounds__(kAnsBlock) k_answer(PmStep S) {
   answer_role<W, false, kAnsBlock>(S, blockIdx.x, L);
 }
 
+// ---- k_gather: the server's XOR gather of wide sets, split ----------------
+// (HOT LOOP D + E for SetSize >= 256: BIGANN's 764 / 3,816 chunks.)  One
+// workgroup per (sub-query s, chunk range j of nsplit); it expands its range
+// of the query set from the resolution record (pir.go:424-444, dummy
+// :363-371), XORs the rows (PrivateQuery pir.go:65-88) and writes one partial
+// entry.  k_answer folds the nsplit partials, so a sub-query's 0.5-2.4 MB of
+// rows are read by nsplit CUs instead of one.
+constexpr int kGatherBlock = 256;
+template <int W>
+__global__ void __launch_bounds__(kGatherBlock) k_gather(PmStep S) {
+  __shared__ uint64_t red[kGatherBlock * 2];
+  const uint32_t j = blockIdx.x, s = blockIdx.y, tid = threadIdx.x;
+  const PmRes r = S.res[s];
+  const uint32_t mode = answer_mode(r);
+  if (mode != A_FINAL && mode != A_CHAINED && mode != A_DUMMY) return;   // block-uniform
+  const PmSub sub = step_sub(S, s);
+  const PmPart& P = S.parts[sub.part];
+  const uint32_t E = S.E, EX = E & ~3u, NSEG = EX / W, mask = P.CS - 1, lg = P.log2CS;
+  const uint32_t per = (P.SS + S.nsplit - 1) / S.nsplit, c0 = min(P.SS, j * per), c1 = min(P.SS, c0 + per);
+  const bool real = mode != A_DUMMY;
+  const uint32_t pchunk = real && r.pp != kDefaultProgramPoint ? (r.pp >> lg) : kNone;
+  const uint32_t rchunk = real ? r.chunk : kNone;
+  const uint32_t rep = real ? (P.ridx[r.chunk * P.Qpc + r.ing] & mask) : 0;
+  const PM_G uint16_t* trow = P.tabT + (uint64_t)r.tag * P.SS;
+  const PM_G uint64_t* base = S.db + P.row0 * E;
+  PM_G uint64_t* out = S.part_x + ((uint64_t)s * S.nsplit + j) * EX;
+  typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+  for (uint32_t seg0 = 0; seg0 < NSEG; seg0 += kGatherBlock) {
+    const uint32_t nseg = min(NSEG - seg0, (uint32_t)kGatherBlock);
+    const uint32_t nsl = kGatherBlock / nseg;
+    const uint32_t sl = tid / nseg, seg = seg0 + tid % nseg;
+    uint64_t a0 = 0, a1 = 0;
+    if (sl < nsl) {
+      constexpr int kG = 16;   // every row load of a batch in flight together
+      for (uint32_t i0 = c0 + sl; i0 < c1; i0 += kG * nsl) {
+        uint64_t rr[kG];
+#pragma unroll
+        for (int u = 0; u < kG; ++u) {
+          const uint32_t i = i0 + u * nsl;
+          uint32_t o = 0;
+          if (i < c1) {
+            if (real) {
+              o = trow[i];
+              if (i == pchunk) o = r.pp & mask;
+              if (i == rchunk) o = rep;
+            } else {
+              o = (uint32_t)(hash4(P.seed, DOM_DUMMY, P.idx, sub.idx, i) & mask);
+            }
+          }
+          rr[u] = i < c1 ? (uint64_t)i * P.CS + o : P.N;
+        }
+        u64x2 x[kG];
+#pragma unroll
+        for (int u = 0; u < kG; ++u) {
+          x[u] = u64x2{0, 0};
+          if (rr[u] < P.N) {
+            const PM_G uint64_t* q = base + rr[u] * E + (uint64_t)seg * W;
+            if (W == 2) x[u] = *reinterpret_cast<const PM_G u64x2*>(q);
+            else x[u].x = *q;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < kG; ++u) { a0 ^= x[u].x; a1 ^= x[u].y; }
+      }
+    }
+    red[tid * 2] = a0;
+    red[tid * 2 + 1] = a1;
+    __syncthreads();
+    if (tid < nseg) {
+      uint64_t x0 = 0, x1 = 0;
+      for (uint32_t k = 0; k < nsl; ++k) {
+        x0 ^= red[(k * nseg + tid) * 2];
+        x1 ^= red[(k * nseg + tid) * 2 + 1];
+      }
+      out[seg * W] = x0;
+      if (W == 2) out[seg * W + 1] = x1;
+    }
+    __syncthreads();
+  }
+}
+
 // ---- k_step: the step in one launch ---------------------------------------
 // Workgroups [0, nsub) match one sub-query each (all its hints), the next np
 // resolve one partition each, the last nsub answer one sub-query each.  Every
@@ -1434,6 +1527,17 @@ bool step_resolve_lds_ok(uint32_t maxPH, uint32_t max_sub_per_part) {
 void step_answer(hipStream_t st, const PmStep& S, PmEvents ev) {
   if (S.E % 2 == 0) PM_LAUNCH(ev, k_answer<2>, dim3(S.nsub), dim3(kAnsBlock), st, S);
   else PM_LAUNCH(ev, k_answer<1>, dim3(S.nsub), dim3(kAnsBlock), st, S);
+}
+uint32_t step_gather_split(uint32_t maxSS, uint32_t nsub) {
+  if (maxSS < 256 || nsub == 0) return 1;
+  // >= 48 rows per workgroup, about 2,048 workgroups in all, at most 64 per sub-query
+  uint32_t n = std::min(cdiv(maxSS, 48), cdiv(2048, nsub));
+  return std::max(1u, std::min(n, 64u));
+}
+void step_gather(hipStream_t st, const PmStep& S, PmEvents ev) {
+  const dim3 grid(S.nsplit, S.nsub);
+  if (S.E % 2 == 0) PM_LAUNCH(ev, k_gather<2>, grid, dim3(kGatherBlock), st, S);
+  else PM_LAUNCH(ev, k_gather<1>, grid, dim3(kGatherBlock), st, S);
 }
 bool step_fused_ok(const PmStep& S, uint32_t maxPH, uint32_t max_sub_per_part) {
   return S.args_valid && S.recg && S.err_h && max_sub_per_part <= kSpecSubs && maxPH <= kLdsPH &&

@@ -508,3 +508,65 @@ def test_built_graph_search_parity(ctx, oracle):
     oa, _, _ = og.SearchLoop(qs, 10, 20, 3)
     assert np.array_equal(ga, oa)
     assert compute_recall(gt, ga, 10) == compute_recall(oracle.knn(v, qs, 10)[0], oa, 10)
+
+
+# ---------------------------------------------------------------------------
+# BIGANN-shaped partitions (BASELINE.json configs[3]/[4]): ChunkSize 8,192 /
+# 16,384, SetSize 764 / 1,028, PrimaryHintNum > 8,192.  These take the
+# unblocked fold, the three-kernel step and the split gather (k_gather).
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("N,E,nq", [(6_250_000, 12, 400), (16_800_000, 4, 300)])
+def test_pir_bigann_partition(ctx, oracle, N, E, nq):
+    """One PianoPIR the size of a BIGANN-100M partition (CS 8,192, SS 764) and a
+    16,384-chunk one (BIGANN-1B's CS): preprocessing state, every response and
+    status (real and dummy queries, repeats through the local cache) and the
+    final client state bit-exact against the oracle."""
+    import pacmann_amd as pm
+    db = rand_db(N, E, seed=N + 1)
+    g = pm.PianoPIR(N, E * 8, db, 8, seed=SEED, ctx=ctx)
+    o = oracle.PianoPIR(N, E * 8, db, 8, seed=SEED)
+    cfg = g.Config()
+    assert cfg == o.Config() and cfg["ChunkSize"] >= 8192 and cfg["SetSize"] >= 256
+    g.Preprocessing()
+    o.Preprocessing()
+    assert_state_equal(g.export_state(), o.export_state())
+    rng = np.random.default_rng(N)
+    ids = rng.integers(0, N, size=nq)
+    ids[7::23] = ids[2]
+    ids[11::37] = ids[5] ^ 1   # neighbours in the same chunk
+    EX = E & ~3
+    for i, idx in enumerate(ids):
+        real = (i % 9) != 4
+        got, err = g.Query(int(idx), real)
+        want, st = o.Query(int(idx), real)
+        assert (err.code if err else 0) == st, i
+        assert np.array_equal(got, want), i
+        if real and st == 0:
+            assert np.array_equal(got[:EX], db[idx * E: idx * E + EX])
+    assert_state_equal(g.export_state(), o.export_state())
+
+
+def test_batch_synth_db_bigann_shard(ctx):
+    """BIGANN-100M over 4 GPUs, rank 0's shard (4 partitions, 16 GB generated
+    on the device by pm_batchpir_create_synth): pir_test.go's property over
+    search-shaped batches of 96 ids — every successful entry equals its DB row
+    (recomputed on the host from the synth spec), every other entry is zero,
+    and only ids of this shard's partitions succeed."""
+    import pacmann_amd as pm
+    N, E, ns = 100_000_000, 80, 4
+    g = pm.SimpleBatchPianoPIR(N, E * 8, 32, None, 8, seed=SEED, ctx=ctx, shard=0, nshards=ns, db_seed=5)
+    g.Preprocessing()
+    PS = g.Config()["PartitionSize"]
+    rng = np.random.default_rng(9)
+    nok = 0
+    for b in range(25):
+        q = rng.integers(0, N, size=96).astype(np.uint64)
+        out, ok = g.QueryWithMask(q)
+        mine = (q // np.uint64(PS)) % np.uint64(ns) == 0
+        assert not (ok & ~mine).any(), b
+        assert np.array_equal(out[ok], pm.synth_rows(5, q[ok], E)), b
+        assert not out[~ok].any(), b
+        nok += int(ok.sum())
+    assert nok > 25 * 96 // ns // 2
+    rows = pm.synth_rows(5, [0, 1, N - 1], E)
+    assert rows.shape == (3, E) and len({int(r[0]) for r in rows}) == 3
