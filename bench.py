@@ -157,13 +157,167 @@ def batch_pir_msmarco(ctx, with_cpu: bool):
     return out
 
 
+# BASELINE.json configs[3] / configs[4]: BIGANN-shaped batch PIR.  Entries are
+# PIRGraphInfo's wire format for d = 128, m = 32 (private-search.go:418-439):
+# (128 + 32) * 4 B = 640 B = 80 words.  The DB is generated on the device
+# (pm_batchpir_create_synth), uniform like TestBatchPIRPerf's.  A private query
+# of the harness is STEP rounds of PARALLEL * M = 96 ids; the rounds here draw
+# uniform ids (the 100M / 1B graphs cannot be built offline in bench time).
+BIG_E, BIG_ROUNDS, BIG_PROFILE_ROUNDS = 80, 400, 40
+
+
+def bigann_pir(name, n_entries, layout, rank, ws, local, dist, nccl_group, rounds=BIG_ROUNDS):
+    """One BIGANN block on every rank.  `layout` = shards the 16 partitions are
+    split into; rank r holds shard r (layout == ws: the whole DB over the node,
+    combined by an RCCL all-reduce per round; layout > ws: only shards
+    0..ws-1 are measured, one per rank, and no combine is run)."""
+    import gc
+
+    import pacmann_amd as pm
+    ctx = pm.Context(local)
+    t0 = time.perf_counter()
+    g = pm.SimpleBatchPianoPIR(n_entries, BIG_E * 8, M, None, F, seed=31, ctx=ctx, shard=rank, nshards=layout,
+                               db_seed=41)
+    ctx.sync()
+    t_create = time.perf_counter() - t0
+    ctx.timing_reset()
+    ctx.timing(True)
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    g.Preprocessing()
+    ctx.sync()
+    prep = time.perf_counter() - t0
+    ctx.timing(False)
+    kprep = {k: ctx.timing_get(k) for k in ("prep_offsets", "prep_fold", "prep_repl")}
+    stats = g.stats()
+    PS = stats["PartitionSize"]
+    sub = g.SubConfig(rank % layout)
+    rng = np.random.default_rng(4242)
+    ids = rng.integers(0, n_entries, size=(rounds + BIG_PROFILE_ROUNDS + 10, PARALLEL * M)).astype(np.uint64)
+    combine = layout == ws and ws > 1
+    dev = None
+    if combine and nccl_group is not None:
+        import torch
+        dev = torch.device("cuda", local)
+
+    def one(q):
+        out, ok = g.QueryWithMask(q)
+        if combine:
+            import torch
+            rows = torch.from_numpy(out.view(np.int64))
+            mask = torch.from_numpy(ok.astype(np.int32))
+            if dev is not None:
+                rows, mask = rows.to(dev), mask.to(dev)
+            dist.all_reduce(rows, op=dist.ReduceOp.SUM, group=nccl_group)   # disjoint entries: sum == xor
+            dist.all_reduce(mask, op=dist.ReduceOp.MAX, group=nccl_group)
+            return rows.cpu().numpy().view(np.uint64), mask.cpu().numpy().astype(bool)
+        return out, ok
+
+    for q in ids[:10]:
+        one(q)
+    keep = []
+    if dist:
+        dist.barrier()
+    ctx.sync()
+    t0 = time.perf_counter()
+    for q in ids[10:10 + rounds]:
+        keep.append(one(q))
+    ctx.sync()
+    if dist:
+        dist.barrier()
+    online = time.perf_counter() - t0
+    # profile window: per-launch device time of the step kernels
+    ctx.timing_reset()
+    ctx.timing(2)
+    for q in ids[10 + rounds:]:
+        one(q)
+    ctx.timing(False)
+    kstep = {k: ctx.timing_get(k) for k in ("hint_match", "resolve", "gather", "answer", "step")}
+    # the reference's property (pir_test.go:45-49): each successful entry is its row
+    bad = nok = 0
+    for q, (out, ok) in zip(ids[10:10 + rounds], keep):
+        if combine:
+            mine = np.ones(len(q), bool)
+        else:
+            mine = (q // np.uint64(PS)) % np.uint64(layout) == np.uint64(rank % layout)
+        bad += int((ok & ~mine).sum())
+        sel = np.where(ok)[0]
+        nok += len(sel)
+        if len(sel):
+            bad += int((out[sel] != pm.synth_rows(41, q[sel], BIG_E)).any(axis=1).sum())
+        bad += int(out[~ok].any(axis=1).sum())
+    del g, keep
+    gc.collect()
+    ctx.close()
+    if dist:
+        import torch
+        t = torch.tensor([prep, online, t_create], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        prep, online, t_create = (float(x) for x in t)
+        c = torch.tensor([bad, nok], dtype=torch.int64)
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        bad, nok = (int(x) for x in c)
+    ms_round = online / rounds * 1e3
+    online_q = ms_round * STEP / 1e3
+    # amortised maintenance per query, the harness's accounting (private-search.go:298)
+    maint_q = prep / stats["SupportBatchNum"] * STEP * PARALLEL
+
+    def roof(entry, nbytes=None):
+        n, ms, by = entry
+        by = nbytes if nbytes is not None else by
+        if not n or not ms or not by:
+            return None
+        ach = (by / n) / (ms / n / 1e3) / 1e9
+        return {"avg_ms": round(ms / n, 5), "alg_bytes_per_launch": by / n, "achieved": round(ach, 1),
+                "unit": "GB/s", "peak": HBM_PEAK_GBS, "frac": round(ach / HBM_PEAK_GBS, 4)}
+
+    n_part = sum(1 for p in range(16) if p % layout == rank % layout)
+    rows_local = sum(min(PS, n_entries - p * PS) for p in range(16) if p % layout == rank % layout)
+    fold = roof(kprep["prep_fold"])
+    if fold:
+        comp = rows_local * BIG_E * 8
+        fold["compulsory"] = {"bytes": comp, "achieved": round(comp / (fold["avg_ms"] / 1e3) / 1e9, 1),
+                              "frac": round(comp / (fold["avg_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
+    gather_key = "gather" if kstep["gather"][0] else "answer"
+    return {
+        "workload": f"{name}: {n_entries:,} x 640 B entries (d=128 f32 + m=32 u32 ids), BatchSize 32 "
+                    f"(16 partitions), FailureProbLog2 8, device-generated uniform DB; rounds of "
+                    f"{PARALLEL * M} uniform ids, {STEP} rounds per private query",
+        "n_ranks": ws, "layout_shards": layout, "shards_measured": min(ws, layout),
+        "partitions_per_rank": n_part, "rank_db_gb": round(rows_local * BIG_E * 8 / 1e9, 2),
+        "subconfig": {k: sub[k] for k in ("ChunkSize", "SetSize", "PrimaryHintNum", "MaxQueryPerChunk",
+                                          "MaxQueryNum")},
+        "combine": (("RCCL" if dev is not None else "gloo (--combine gloo)")
+                    + " all-reduce of the shards' disjoint entries per round (sum == xor)" if combine
+                    else "none (one rank holds every partition)" if layout == 1
+                    else f"none: each rank runs one shard of the {layout}-way layout; the combine is not run"),
+        "db_create_s": round(t_create, 3), "preprocessing_s": round(prep, 4),
+        "rounds": rounds, "ms_per_round": round(ms_round, 4),
+        "online_s_per_query": round(online_q, 6), "maintenance_s_per_query": round(maint_q, 6),
+        "private_queries_per_s": round(1.0 / (online_q + maint_q), 2),
+        "kernel_avg_us": {k: round(v[1] / v[0] * 1e3, 3) for k, v in {**kprep, **kstep}.items() if v[0]},
+        "pir_scan_fold": fold,
+        "pir_scan_answer": roof(kstep[gather_key]),
+        "check": {"ids_answered": nok, "mismatches": bad},
+    }
+
+
 def dist_init():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     if ws == 1:
         return None, 0, 1, 0
+    import datetime
+
     import torch.distributed as dist
-    dist.init_process_group("gloo")   # control plane only: barrier + max of timings
-    return dist, dist.get_rank(), ws, int(os.environ.get("LOCAL_RANK", "0"))
+    # control plane (barrier, max of timings) over gloo; bounded so a lost rank
+    # ends the run instead of hanging it
+    dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=600))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    ndev = torch.cuda.device_count()   # counting devices does not initialise HIP
+    # more ranks than GPUs (a rehearsal on one GPU): ranks share devices round-robin
+    return dist, dist.get_rank(), ws, local % max(ndev, 1)
 
 
 def cpu_baseline(v, g, queries, ctx):
@@ -197,6 +351,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-config2", action="store_true", help="skip the MS-MARCO-shaped batch-PIR block")
     ap.add_argument("--no-single", action="store_true", help="skip the one-client latency block")
+    ap.add_argument("--no-bigann", action="store_true", help="skip the BIGANN-100M / 1B batch-PIR blocks")
+    ap.add_argument("--combine", choices=["rccl", "gloo"], default="rccl",
+                    help="collective of the sharded BIGANN rounds (gloo: host tensors, e.g. ranks sharing one GPU)")
     ap.add_argument("--graph", choices=["built", "random"], default="built",
                     help="GPU-built kNN+robustPrune graph (default) or the reference's synthetic random graph")
     args = ap.parse_args()
@@ -283,6 +440,25 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    # BASELINE.json configs[3] (BIGANN-100M, sharded over the ranks) and
+    # configs[4] (BIGANN-1B in 8 shards): every rank takes part
+    big = {}
+    if not args.no_bigann:
+        nccl_group = None
+        if dist and args.combine == "rccl":
+            import datetime
+
+            import torch
+            torch.cuda.set_device(local)
+            nccl_group = dist.new_group(backend="nccl", timeout=datetime.timedelta(seconds=180))
+        for key, nm, n_entries, layout in (("config3_bigann_100m", "BIGANN-100M-shaped (configs[3])",
+                                            100_000_000, ws),
+                                           ("config4_bigann_1b", "BIGANN-1B-shaped (configs[4]), 8-way layout",
+                                            1_000_000_000, 8)):
+            try:
+                big[key] = bigann_pir(nm, n_entries, layout, rank, ws, local, dist, nccl_group)
+            except Exception as e:   # recorded, never fatal to the headline line
+                big[key] = {"error": f"{type(e).__name__}: {e}"}
     if rank != 0:
         dist.destroy_process_group()
         return
@@ -364,6 +540,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline(v, g, queries[S * nq:], ctx0)
     if ws == 1 and not args.no_config2:
         out["config2_batch_pir"] = batch_pir_msmarco(ctxs[0], not args.no_cpu_baseline)
+    out.update(big)
     print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
