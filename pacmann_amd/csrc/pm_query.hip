@@ -442,7 +442,7 @@ struct ResolveLds {
   // staging: match bits, tags / program points; speculative re-evaluation values
   uint64_t bits_l[STG ? NB : 1];
   uint32_t tag_l[STG ? kLdsPH : 1], pp_l[STG ? kLdsPH : 1];
-  uint16_t spec_v[MODE != 0 ? kSpecSubs * kSpecSubs : 1];
+  uint16_t spec_v[kSpecSubs * kSpecSubs];
 };
 
 // Step completion counter, 64 bits at done[0..1]: the high half counts the
@@ -495,7 +495,9 @@ __device__ __forceinline__ void resolve_role(const PmStep& S, uint32_t p, Resolv
   const uint32_t wave = tid >> 6, lane = tid & 63;
   // fast prologue (n <= 64 sub-queries, the usual shape): no staging of tags,
   // program points or match bits; two independent chains of two round trips
-  const bool fast = MODE == 2 || (MODE == 1 && n <= kSpecSubs && nw <= 128);
+  // (MODE 0, partitions too large to stage: the same from global memory,
+  // the match records read ten blocks at a time)
+  const bool fast = MODE == 2 || (MODE == 1 && n <= kSpecSubs && nw <= 128) || (MODE == 0 && n <= kSpecSubs);
   // match bits, tags and program points: LDS-staged by the staged prologue,
   // read from global memory on the (rare) paths of the fast one that need them
   const bool staged = MODE == 1 && !fast;
@@ -515,17 +517,40 @@ __device__ __forceinline__ void resolve_role(const PmStep& S, uint32_t p, Resolv
         const PmSub sub = step_sub(S, b0 + j);
         uint32_t c1 = kNone, c2 = kNone, t1 = 0, p1 = 0, t2 = 0, p2 = 0;
         if (sub.kind == SUB_REAL && sub.idx < P.N) {
-          uint32_t v = kNone;
-          if (GRAN) {
-            if (lane < 6) v = get_g(S.recg + (uint64_t)(b0 + j) * G_REC + lane, S);
-          } else if (lane < nblk * 6) {
-            v = S.cand[(uint64_t)(b0 + j) * S.cblk * 6 + lane];
+          // the records of up to 16 x 10 blocks, all loads in flight together
+          // (lanes 6b..6b+5 of window w: block 10w + b's {h, tag, pp} x 2)
+          constexpr uint32_t kWin = 16;
+          const uint32_t nwin = (nblk + 9) / 10;
+          uint32_t vv[kWin];
+#pragma unroll
+          for (uint32_t w = 0; w < kWin; ++w) {
+            vv[w] = kNone;
+            const uint32_t nb = w < nwin ? min(10u, nblk - 10 * w) : 0;
+            if (GRAN) {
+              if (w == 0 && lane < 6) vv[w] = get_g(S.recg + (uint64_t)(b0 + j) * G_REC + lane, S);
+            } else if (lane < nb * 6) {
+              vv[w] = S.cand[((uint64_t)(b0 + j) * S.cblk + 10 * w) * 6 + lane];
+            }
           }
-          for (uint32_t k = 0; k < 2 * nblk && c2 == kNone; ++k) {   // uniform
-            const uint32_t h = __builtin_amdgcn_readlane(v, 3 * k);
-            if (h == kNone) { k |= 1; continue; }                    // rest of this block is empty
-            const uint32_t t = __builtin_amdgcn_readlane(v, 3 * k + 1), pp = __builtin_amdgcn_readlane(v, 3 * k + 2);
-            if (c1 == kNone) { c1 = h; t1 = t; p1 = pp; } else { c2 = h; t2 = t; p2 = pp; }
+          // the first two records in hint order: the non-empty hint slots
+          // (lanes 3k), window by window
+          auto take = [&](uint32_t v) {
+            uint64_t m = __ballot(lane < 60 && lane % 3 == 0 && v != kNone);
+            while (m && c2 == kNone) {
+              const uint32_t l = (uint32_t)__builtin_ctzll(m);
+              m &= m - 1;
+              const uint32_t h = __builtin_amdgcn_readlane(v, l), t = __builtin_amdgcn_readlane(v, l + 1),
+                             pp = __builtin_amdgcn_readlane(v, l + 2);
+              if (c1 == kNone) { c1 = h; t1 = t; p1 = pp; } else { c2 = h; t2 = t; p2 = pp; }
+            }
+          };
+#pragma unroll
+          for (uint32_t w = 0; w < kWin; ++w)
+            if (w < nwin && c2 == kNone) take(vv[w]);   // uniform
+          // beyond 160 blocks (PH > 163,840; none of the configurations): the rest
+          for (uint32_t w = kWin; w < nwin && c2 == kNone; ++w) {
+            const uint32_t nb = min(10u, nblk - 10 * w);
+            take(lane < nb * 6 ? S.cand[((uint64_t)(b0 + j) * S.cblk + 10 * w) * 6 + lane] : kNone);
           }
         }
         if (lane == 0) { s_c1[j] = c1; s_c2[j] = c2; s_t1[j] = t1; s_p1[j] = p1; s_t2[j] = t2; s_p2[j] = p2; }
@@ -686,7 +711,7 @@ __device__ __forceinline__ void resolve_role(const PmStep& S, uint32_t p, Resolv
     const uint32_t c1 = real ? s_c1[k] : kNone, c2 = real ? s_c2[k] : kNone;
     const uint32_t t1 = real ? s_t1[k] : 0, p1 = real ? s_p1[k] : 0;
     const uint32_t t2 = real ? s_t2[k] : 0, p2 = real ? s_p2[k] : 0;
-    const bool spec = LDS && n <= kSpecSubs;
+    const bool spec = n <= kSpecSubs && (LDS || fast);
     const uint32_t sg = (spec && real) ? s_sing[k] : kNone;
     // tag sub k's refresh would hand out if every earlier sub-query succeeds
     const uint32_t pred = (sg < P.Qpc && ch < P.SS) ? P.PH + ch * P.Qpc + sg : kNone;
@@ -985,12 +1010,15 @@ __device__ __forceinline__ void resolve_role(const PmStep& S, uint32_t p, Resolv
   }
 }
 
+// (large partitions, MODE 0: 512 threads, so each sub-query of a partition
+// has a candidate wave of its own)
+constexpr int kResolveBlockG = 512;
 template <bool LDS>
-__global__ void __launch_bounds__(kBlock) k_resolve(PmStep S) {
+__global__ void __launch_bounds__(LDS ? kBlock : kResolveBlockG) k_resolve(PmStep S) {
   __shared__ ResolveLds<LDS ? 1 : 0> L;
   const uint32_t p = blockIdx.x;
   if (step_sb(S, p + 1) == step_sb(S, p)) return;
-  resolve_role<LDS ? 1 : 0, kBlock, false>(S, p, L);
+  resolve_role<LDS ? 1 : 0, LDS ? kBlock : kResolveBlockG, false>(S, p, L);
   __syncthreads();
   // last add here: no answer workgroup is involved in a chain, nothing to decode
   if (L.fin && threadIdx.x == 0) chain_rearm(S);
@@ -1143,10 +1171,26 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, AnswerL
     if (!GRAN && S.nsplit > 1) {   // k_gather did the set: fold its partial XORs
       if (mode == A_FINAL || mode == A_CHAINED || mode == A_DUMMY) {
         const PM_G uint64_t* px = S.part_x + (uint64_t)s * S.nsplit * EX;
-        for (uint32_t w = tid; w < EX; w += NT) {
-          uint64_t x = 0;
-          for (uint32_t j = 0; j < S.nsplit; ++j) x ^= px[(uint64_t)j * EX + w];
-          row.w[w] = x;
+        const uint32_t G = NT >= 2 * EX ? NT / EX : 1;   // partial groups folded side by side
+        if (G == 1) {
+          for (uint32_t w = tid; w < EX; w += NT) {
+            uint64_t x = 0;
+            for (uint32_t j = 0; j < S.nsplit; ++j) x ^= px[(uint64_t)j * EX + w];
+            row.w[w] = x;
+          }
+        } else {
+          if (tid < EX * G) {
+            const uint32_t w = tid % EX, g0 = tid / EX;
+            uint64_t x = 0;
+            for (uint32_t j = g0; j < S.nsplit; j += G) x ^= px[(uint64_t)j * EX + w];
+            red[tid] = x;
+          }
+          __syncthreads();
+          if (tid < EX) {
+            uint64_t x = 0;
+            for (uint32_t g0 = 0; g0 < G; ++g0) x ^= red[g0 * EX + tid];
+            row.w[tid] = x;
+          }
         }
       }
       __syncthreads();
@@ -1519,7 +1563,7 @@ void step_match(hipStream_t st, const PmStep& S, uint32_t maxPH, PmEvents ev) {
 }
 void step_resolve(hipStream_t st, const PmStep& S, bool lds, PmEvents ev) {
   if (lds) PM_LAUNCH(ev, k_resolve<true>, dim3(S.np), dim3(kBlock), st, S);
-  else PM_LAUNCH(ev, k_resolve<false>, dim3(S.np), dim3(kBlock), st, S);
+  else PM_LAUNCH(ev, k_resolve<false>, dim3(S.np), dim3(kResolveBlockG), st, S);
 }
 bool step_resolve_lds_ok(uint32_t maxPH, uint32_t max_sub_per_part) {
   return maxPH <= kLdsPH && max_sub_per_part * ((maxPH + 63) / 64) <= kLdsBitWords;
