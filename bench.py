@@ -175,9 +175,16 @@ def bigann_pir(name, n_entries, layout, rank, ws, local, dist, nccl_group, round
 
     import pacmann_amd as pm
     ctx = pm.Context(local)
+    combine = layout == ws and ws > 1
     t0 = time.perf_counter()
-    g = pm.SimpleBatchPianoPIR(n_entries, BIG_E * 8, M, None, F, seed=31, ctx=ctx, shard=rank, nshards=layout,
-                               db_seed=41)
+    if combine:   # the whole DB over the job: each rank one shard, entries all-reduced per round
+        from pacmann_amd.shard import ShardedBatchPIR
+        sp = ShardedBatchPIR(n_entries, BIG_E * 8, M, None, F, seed=31, group=nccl_group, ctx=ctx, db_seed=41,
+                             device=local)
+        g = sp.pir
+    else:
+        g = pm.SimpleBatchPianoPIR(n_entries, BIG_E * 8, M, None, F, seed=31, ctx=ctx, shard=rank, nshards=layout,
+                                   db_seed=41)
     ctx.sync()
     t_create = time.perf_counter() - t0
     ctx.timing_reset()
@@ -195,24 +202,8 @@ def bigann_pir(name, n_entries, layout, rank, ws, local, dist, nccl_group, round
     sub = g.SubConfig(rank % layout)
     rng = np.random.default_rng(4242)
     ids = rng.integers(0, n_entries, size=(rounds + BIG_PROFILE_ROUNDS + 10, PARALLEL * M)).astype(np.uint64)
-    combine = layout == ws and ws > 1
-    dev = None
-    if combine and nccl_group is not None:
-        import torch
-        dev = torch.device("cuda", local)
-
     def one(q):
-        out, ok = g.QueryWithMask(q)
-        if combine:
-            import torch
-            rows = torch.from_numpy(out.view(np.int64))
-            mask = torch.from_numpy(ok.astype(np.int32))
-            if dev is not None:
-                rows, mask = rows.to(dev), mask.to(dev)
-            dist.all_reduce(rows, op=dist.ReduceOp.SUM, group=nccl_group)   # disjoint entries: sum == xor
-            dist.all_reduce(mask, op=dist.ReduceOp.MAX, group=nccl_group)
-            return rows.cpu().numpy().view(np.uint64), mask.cpu().numpy().astype(bool)
-        return out, ok
+        return sp.QueryWithMask(q) if combine else g.QueryWithMask(q)
 
     for q in ids[:10]:
         one(q)
@@ -247,6 +238,8 @@ def bigann_pir(name, n_entries, layout, rank, ws, local, dist, nccl_group, round
         if len(sel):
             bad += int((out[sel] != pm.synth_rows(41, q[sel], BIG_E)).any(axis=1).sum())
         bad += int(out[~ok].any(axis=1).sum())
+    if combine:
+        del sp
     del g, keep
     gc.collect()
     ctx.close()
@@ -288,7 +281,7 @@ def bigann_pir(name, n_entries, layout, rank, ws, local, dist, nccl_group, round
         "partitions_per_rank": n_part, "rank_db_gb": round(rows_local * BIG_E * 8 / 1e9, 2),
         "subconfig": {k: sub[k] for k in ("ChunkSize", "SetSize", "PrimaryHintNum", "MaxQueryPerChunk",
                                           "MaxQueryNum")},
-        "combine": (("RCCL" if dev is not None else "gloo (--combine gloo)")
+        "combine": (("RCCL" if nccl_group is not None else "gloo (--combine gloo)")
                     + " all-reduce of the shards' disjoint entries per round (sum == xor)" if combine
                     else "none (one rank holds every partition)" if layout == 1
                     else f"none: each rank runs one shard of the {layout}-way layout; the combine is not run"),

@@ -27,7 +27,11 @@ class ShardedBatchPIR:
     for nccl (RCCL)."""
 
     def __init__(self, DBSize: int, DBEntryByteNum: int, BatchSize: int, rawDB, FailureProbLog2: int,
-                 seed: int = 1, group=None, engine=None, ctx=None):
+                 seed: int = 1, group=None, engine=None, ctx=None, db_seed: int | None = None,
+                 device: int | None = None):
+        """db_seed: the shard's rows are generated on its GPU
+        (pm_batchpir_create_synth; rawDB None).  device: the CUDA device of the
+        combine's tensors under nccl (default: the current one)."""
         import torch.distributed as dist
         self._dist = dist
         self.group = group
@@ -38,9 +42,13 @@ class ShardedBatchPIR:
             from . import SimpleBatchPianoPIR
             engine = SimpleBatchPianoPIR
         kw = {"ctx": ctx} if ctx is not None else {}
+        if db_seed is not None:
+            kw["db_seed"] = db_seed
         self.pir = engine(DBSize, DBEntryByteNum, BatchSize, rawDB, FailureProbLog2, seed=seed,
                           shard=self.rank, nshards=self.world, **kw)
-        self._device = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
+        self._device = "cpu"
+        if dist.get_backend(group) == "nccl":
+            self._device = "cuda" if device is None else f"cuda:{device}"
 
     def Preprocessing(self):
         self.pir.Preprocessing()

@@ -86,3 +86,54 @@ def test_sharded_batch_pir_world2(oracle):
         assert np.array_equal(rows[0][i], want), i
         good = db.reshape(N, E)[q.astype(np.int64)]
         assert np.array_equal(rows[0][i][oks[0][i]], good[oks[0][i]]), i
+
+
+class SynthShard:
+    """A shard over the device-generated DB spec (pm_batchpir_create_synth),
+    answered on the host from pacmann_amd.synth_rows: the engine interface the
+    bench's BIGANN blocks drive through ShardedBatchPIR."""
+
+    def __init__(self, DBSize, DBEntryByteNum, BatchSize, rawDB, FailureProbLog2, seed=1, shard=0, nshards=1,
+                 db_seed=None):
+        assert rawDB is None and db_seed is not None
+        self.E, self.db_seed = DBEntryByteNum // 8, db_seed
+        self.PS = (DBSize + BatchSize // 2 - 1) // (BatchSize // 2)
+        self.shard, self.nshards = shard, nshards
+
+    def QueryWithMask(self, idx):
+        from pacmann_amd import synth_rows
+        idx = np.asarray(idx, dtype=np.uint64)
+        mine = (idx // np.uint64(self.PS)) % np.uint64(self.nshards) == np.uint64(self.shard)
+        rows = synth_rows(self.db_seed, idx, self.E)
+        rows[~mine] = 0
+        return rows, mine
+
+
+def _rank_synth(rank, world, port, out_dir):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from pacmann_amd.shard import ShardedBatchPIR
+        pir = ShardedBatchPIR(10**8, 640, 32, None, 8, seed=3, engine=SynthShard, db_seed=41)
+        q = np.random.default_rng(5).integers(0, 10**8, size=96).astype(np.uint64)
+        rows, ok = pir.QueryWithMask(q)
+        np.save(os.path.join(out_dir, f"s{rank}.npy"), rows)
+        np.save(os.path.join(out_dir, f"k{rank}.npy"), ok)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_synth_world2():
+    """BIGANN-shaped combine (the bench's configs[3] path): two ranks, each
+    holding half of the 16 partitions of a 10^8-entry synthetic DB; after the
+    all-reduce both hold every row, equal to synth_rows."""
+    from pacmann_amd import synth_rows
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_rank_synth, args=(2, _free_port(), d), nprocs=2, join=True)
+        rows = [np.load(os.path.join(d, f"s{r}.npy")) for r in range(2)]
+        oks = [np.load(os.path.join(d, f"k{r}.npy")) for r in range(2)]
+    q = np.random.default_rng(5).integers(0, 10**8, size=96).astype(np.uint64)
+    assert oks[0].all() and oks[1].all()
+    assert np.array_equal(rows[0], rows[1])
+    assert np.array_equal(rows[0], synth_rows(41, q, 80))
