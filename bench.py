@@ -80,13 +80,16 @@ def make_queries(v, n, seed):
     return np.clip(np.rint(q), 0, 255).astype(np.float32)
 
 
-def pmc_traffic(kernel_symbol: str):
-    """HBM bytes per dispatch of `kernel_symbol` from the newest committed
-    rocprofv3 PMC summary (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE,
-    collected in separate --pmc passes of this bench); None if absent."""
+def pmc_traffic(kernel_symbol: str, grid: int | None = None):
+    """HBM bytes per dispatch of `kernel_symbol` (of launches of `grid` threads
+    if given) from the newest committed rocprofv3 PMC summary (FETCH_SIZE x2
+    gfx950 correction + WRITE_SIZE, collected in separate --pmc passes of this
+    bench); None if absent."""
     best = None
     for f in sorted((ROOT / "profiles").glob("r*/pmc_summary.json")):
         k = json.loads(f.read_text()).get("kernels", {}).get(kernel_symbol)
+        if k and grid is not None:
+            k = k.get("by_grid", {}).get(str(grid))
         if k and "hbm_bytes_per_dispatch_corrected" in k:
             best = (k["hbm_bytes_per_dispatch_corrected"], str(f.relative_to(ROOT)))
     return best
@@ -273,6 +276,20 @@ def bigann_pir(name, n_entries, layout, rank, ws, local, dist, nccl_group, round
         fold["compulsory"] = {"bytes": comp, "achieved": round(comp / (fold["avg_ms"] / 1e3) / 1e9, 1),
                               "frac": round(comp / (fold["avg_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
     gather_key = "gather" if kstep["gather"][0] else "answer"
+    # PMC HBM bytes of the same launches (profiles/r*/pmc_summary.json, by launch shape)
+    H = sub["PrimaryHintNum"] + sub["SetSize"] * sub["MaxQueryPerChunk"]
+    fold_grid = -(-H * (BIG_E // 2) // 256) * 256 * n_part
+    nsub = PARALLEL * M // 16 * n_part
+    nsplit = max(1, min(-(-sub["SetSize"] // 48), -(-2048 // nsub), 64)) if sub["SetSize"] >= 256 else 1
+    gather_grid = nsplit * nsub * 256
+    if fold:
+        tr = pmc_traffic("void pm::k_prep_fold<2>(pm::PmPart const*, unsigned long const*, unsigned int)", fold_grid)
+        fold["traffic"], fold["traffic_source"] = (tr[0], tr[1]) if tr else (None, None)
+    ans_roof = roof(kstep[gather_key])
+    if ans_roof and gather_key == "gather":
+        tr = pmc_traffic("void pm::k_gather<2>(pm::PmStep)", gather_grid)
+        ans_roof["kernel"] = "gather"
+        ans_roof["traffic"], ans_roof["traffic_source"] = (tr[0], tr[1]) if tr else (None, None)
     return {
         "workload": f"{name}: {n_entries:,} x 640 B entries (d=128 f32 + m=32 u32 ids), BatchSize 32 "
                     f"(16 partitions), FailureProbLog2 8, device-generated uniform DB; rounds of "
@@ -291,7 +308,7 @@ def bigann_pir(name, n_entries, layout, rank, ws, local, dist, nccl_group, round
         "private_queries_per_s": round(1.0 / (online_q + maint_q), 2),
         "kernel_avg_us": {k: round(v[1] / v[0] * 1e3, 3) for k, v in {**kprep, **kstep}.items() if v[0]},
         "pir_scan_fold": fold,
-        "pir_scan_answer": roof(kstep[gather_key]),
+        "pir_scan_answer": ans_roof,
         "check": {"ids_answered": nok, "mismatches": bad},
     }
 

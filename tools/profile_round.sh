@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round profile set (run on the GPU box from the repo root):
-#   bench line, kernel stats and the two PMC passes of the same bench command.
+#   bench line, kernel stats and the two PMC passes of the same bench command
+#   (SIFT1M sessions + the BIGANN-100M / 1B blocks).
 # usage: tools/profile_round.sh OUTDIR
 set -e
 out=$1; mkdir -p "$out"
