@@ -313,6 +313,48 @@ def bigann_pir(name, n_entries, layout, rank, ws, local, dist, nccl_group, round
     }
 
 
+# BASELINE.json configs[0]: graphann_test.go's InnerProduct benchmark
+# (graphann_test.go:221-284): N = 1e8 rows of D = 128 uint32, v[i*D+j] = i+j,
+# q[j] = j, the sum of all row products mod 2^32 (closed form 1,178,525,696).
+C0_N, C0_D, C0_SUM, C0_CPU_ROWS = 100_000_000, 128, 1_178_525_696, 1 << 23
+
+
+def inner_product_scan(ctx, with_cpu: bool):
+    """The scan on the GPU (51.2 GB filled on the device, then one streaming
+    k_ip_scan launch timed with events on its stream; best of 3), against HBM
+    peak; the oracle's AVX-512-equivalent InnerProduct over a materialised
+    sample of the same rows on 1 and on all host cores beside it."""
+    import pacmann_amd as pm
+    runs = [pm.ip_bench(C0_N, C0_D, ctx) for _ in range(3)]
+    ok = all(s == C0_SUM for s, _ in runs)
+    ms = min(m for _, m in runs)
+    nbytes = C0_N * C0_D * 4
+    ach = nbytes / (ms / 1e3) / 1e9
+    tr = pmc_traffic("pm::k_ip_scan(uint4 const*, unsigned long, unsigned int const*, unsigned int, unsigned int*)")
+    out = {"workload": "graphann_test.go InnerProduct bench (configs[0]): 1e8 x 128 uint32 rows v[i*D+j]=i+j, "
+                       "q[j]=j, sum mod 2^32",
+           "sum_ok": ok, "scan_ms": round(ms, 4), "rows_per_s": round(C0_N / (ms / 1e3), 1),
+           "roofline": {"bound": "hbm", "kernel": "ip_scan", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": nbytes,
+                        "traffic": tr[0] if tr else None}}
+    if with_cpu:
+        from oracle import oracle as O
+        rows = np.arange(C0_CPU_ROWS, dtype=np.uint32)[:, None] + np.arange(C0_D, dtype=np.uint32)[None, :]
+        q = np.arange(C0_D, dtype=np.uint32)
+        ncores = min(16, os.cpu_count() or 1)   # the box's CPU share is 16 cores per GPU
+        cpu = {}
+        for th in (1, ncores):
+            t0 = time.perf_counter()
+            O.inner_product_scan(rows, q, th)
+            dt = time.perf_counter() - t0
+            cpu[th] = rows.nbytes / dt / 1e9
+        del rows
+        out["cpu_baseline"] = {"value": round(cpu[1], 2), "unit": "GB/s", "cores": 1, "kind": "port",
+                               "all_cores": {"value": round(cpu[ncores], 2), "cores": ncores},
+                               "sample": f"{C0_CPU_ROWS:,} materialised rows (4.3 GB) of the same fill"}
+    return out
+
+
 def dist_init():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     if ws == 1:
@@ -362,6 +404,7 @@ def main():
     ap.add_argument("--no-config2", action="store_true", help="skip the MS-MARCO-shaped batch-PIR block")
     ap.add_argument("--no-single", action="store_true", help="skip the one-client latency block")
     ap.add_argument("--no-bigann", action="store_true", help="skip the BIGANN-100M / 1B batch-PIR blocks")
+    ap.add_argument("--no-config0", action="store_true", help="skip the InnerProduct scan block")
     ap.add_argument("--combine", choices=["rccl", "gloo"], default="rccl",
                     help="collective of the sharded BIGANN rounds (gloo: host tensors, e.g. ranks sharing one GPU)")
     ap.add_argument("--graph", choices=["built", "random"], default="built",
@@ -550,6 +593,8 @@ def main():
         out["cpu_baseline"] = cpu_baseline(v, g, queries[S * nq:], ctx0)
     if ws == 1 and not args.no_config2:
         out["config2_batch_pir"] = batch_pir_msmarco(ctxs[0], not args.no_cpu_baseline)
+    if ws == 1 and not args.no_config0:
+        out["config0_inner_product"] = inner_product_scan(ctxs[0], not args.no_cpu_baseline)
     out.update(big)
     print(json.dumps(out), flush=True)
     if dist:

@@ -52,6 +52,7 @@ SIG = {
     "or_l2dist_avx": (C.c_float, [f32p, f32p, u64]),
     "or_inner_product": (C.c_uint32, [u32p, u32p, u64]),
     "or_inner_product_bench": (C.c_uint32, [u64, u64, C.c_int]),
+    "or_inner_product_scan": (C.c_uint32, [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), u64, u64, C.c_int]),
     "or_l2_batch": (None, [f32p, f32p, u64, u64, f32p]),
     "or_pir_new": (vp, [u64, u64, u64p, u64, u64, u64]),
     "or_pir_free": (None, [vp]),
@@ -166,6 +167,14 @@ def inner_product(a, b) -> int:
 
 def inner_product_bench(N: int, D: int, nthreads: int = 1) -> int:
     return lib().or_inner_product_bench(N, D, nthreads)
+
+
+def inner_product_scan(rows: np.ndarray, q: np.ndarray, nthreads: int = 1) -> int:
+    """InnerProduct summed over materialised rows (N x D uint32), mod 2^32."""
+    rows = np.ascontiguousarray(rows, np.uint32)
+    q = np.ascontiguousarray(q, np.uint32)
+    return lib().or_inner_product_scan(_p(rows, C.POINTER(C.c_uint32)), _p(q, C.POINTER(C.c_uint32)),
+                                       rows.shape[0], rows.shape[1], nthreads)
 
 
 def _export(h, cfg: dict) -> dict:

@@ -181,6 +181,27 @@ extern "C" uint32_t or_inner_product_bench(uint64_t N, uint64_t D, int nthreads)
   return s;
 }
 
+// The benchmark's scan over materialised rows (graphann_test.go:249-283: the
+// N x D array is allocated and filled first, then InnerProduct runs row by
+// row), split over nthreads contiguous row ranges; sums wrap mod 2^32.
+extern "C" uint32_t or_inner_product_scan(const uint32_t* rows, const uint32_t* q, uint64_t N, uint64_t D,
+                                          int nthreads) {
+  if (nthreads < 1) nthreads = 1;
+  std::vector<uint32_t> part(nthreads, 0);
+  auto work = [&](int t) {
+    uint64_t lo = N * t / nthreads, hi = N * (t + 1) / nthreads;
+    uint32_t s = 0;
+    for (uint64_t i = lo; i < hi; ++i) s += or_inner_product(rows + i * D, q, D);
+    part[t] = s;
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < nthreads; ++t) th.emplace_back(work, t);
+  work(0);
+  for (auto& x : th) x.join();
+  uint32_t s = 0; for (auto v : part) s += v;
+  return s;
+}
+
 // ---------------------------------------------------------------------------
 // PianoPIR (pianopir/pir.go)
 // ---------------------------------------------------------------------------

@@ -45,6 +45,7 @@ float    or_l2dist_avx(const float* a, const float* b, size_t dim);     /* AVX r
 uint32_t or_inner_product(const uint32_t* a, const uint32_t* b, size_t n);
 /* TestInnerProduct scan: vectors[i*D+j]=i+j, query[j]=j, sum over rows. */
 uint32_t or_inner_product_bench(uint64_t N, uint64_t D, int nthreads);
+uint32_t or_inner_product_scan(const uint32_t* rows, const uint32_t* q, uint64_t N, uint64_t D, int nthreads);
 void     or_l2_batch(const float* q, const float* rows, size_t nrows, size_t dim, float* out);
 
 /* ---- PianoPIR (pianopir/pir.go) ---------------------------------------- */

@@ -466,12 +466,32 @@ __global__ void __launch_bounds__(kBlock) k_ip_scan(const uint4* __restrict__ ro
   uint32_t acc = 0;
   const uint64_t stride = (uint64_t)gridDim.x * kBlock;
   const uint32_t dim4 = dim / 4;
-  for (uint64_t f = (uint64_t)blockIdx.x * kBlock + threadIdx.x; f < n4; f += stride) {
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(rows) + f);
-    const uint4 v = make_uint4(t.x, t.y, t.z, t.w);
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4* r4 = reinterpret_cast<const u32x4*>(rows);
+  uint64_t f = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (stride % dim4 == 0) {
+    // the grid stride is whole rows: a thread's column (and query slice) is
+    // fixed, and kU 16-B nontemporal loads are in flight per thread
     const uint32_t j = (uint32_t)(f % dim4) * 4;
-    acc += v.x * qs[j] + v.y * qs[j + 1] + v.z * qs[j + 2] + v.w * qs[j + 3];
+    const uint32_t q0 = qs[j], q1 = qs[j + 1], q2 = qs[j + 2], q3 = qs[j + 3];
+    constexpr int kU = 8;
+    for (; f + (kU - 1) * stride < n4; f += kU * stride) {
+      u32x4 t[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) t[u] = __builtin_nontemporal_load(r4 + f + u * stride);
+#pragma unroll
+      for (int u = 0; u < kU; ++u) acc += t[u].x * q0 + t[u].y * q1 + t[u].z * q2 + t[u].w * q3;
+    }
+    for (; f < n4; f += stride) {
+      const u32x4 t = __builtin_nontemporal_load(r4 + f);
+      acc += t.x * q0 + t.y * q1 + t.z * q2 + t.w * q3;
+    }
+  } else {
+    for (; f < n4; f += stride) {
+      const u32x4 t = __builtin_nontemporal_load(r4 + f);
+      const uint32_t j = (uint32_t)(f % dim4) * 4;
+      acc += t.x * qs[j] + t.y * qs[j + 1] + t.z * qs[j + 2] + t.w * qs[j + 3];
+    }
   }
 #pragma unroll
   for (int m = 1; m < 64; m <<= 1) acc += __shfl_xor(acc, m);
@@ -605,7 +625,7 @@ void ip_rows(hipStream_t st, const uint32_t* rows, uint64_t nrows, const uint32_
   if (!per_row && dim % 4 == 0 && dim <= 4096) {
     const uint64_t n4 = nrows * dim / 4;
     unsigned grid = cdiv(n4, kBlock);
-    if (grid > 256 * 16) grid = 256 * 16;
+    if (grid > 256 * 8) grid = 256 * 8;   // 8 workgroups per CU: 2,048 x 256 threads, 16 waves per CU
     if (grid == 0) return;
     hipLaunchKernelGGL(k_ip_scan, dim3(grid), dim3(kBlock), 0, st, (const uint4*)rows, n4, q, dim, sum);
     return;
