@@ -387,10 +387,42 @@ def cpu_baseline(v, g, queries, ctx):
     nq = 46
     ans, online, maint = og.SearchLoop(queries[:nq], K_TOP, STEP, PARALLEL)
     rec = compute_recall(pm.knn(v, queries[:nq], K_TOP, ctx), ans, K_TOP)
-    return {"value": nq / (online + maint), "unit": "queries/s", "cores": 1, "kind": "port",
-            "recall_at_10": round(float(rec), 4),
-            "sample": f"{nq} SIFT1M-shaped private queries (2 maintenance windows) after one "
-                      f"{prep:.2f}s preprocessing; online {online:.2f}s + maintenance {maint:.2f}s"}
+    out = {"value": nq / (online + maint), "unit": "queries/s", "cores": 1, "kind": "port",
+           "recall_at_10": round(float(rec), 4),
+           "sample": f"{nq} SIFT1M-shaped private queries (2 maintenance windows) after one "
+                     f"{prep:.2f}s preprocessing; online {online:.2f}s + maintenance {maint:.2f}s"}
+    # all host cores (the box's CPU share: 16 per GPU): one independent oracle
+    # client per core, like the GPU's sessions, over the same data; each runs
+    # the same sample shape (one preprocessing, then 46 queries = two
+    # maintenance windows); ctypes releases the GIL, so the C loops run in parallel
+    import threading
+    ncores = min(16, os.cpu_count() or 1)
+    nq1 = nq
+    qall = make_queries(v, ncores * nq1, seed=999)
+    res = [None] * ncores
+
+    def client(i):
+        oc = O.Graph(v, g, pir_seed=1000 + i, search_seed=2000 + i)
+        oc.Preprocess()
+        _, on, mt = oc.SearchLoop(qall[i * nq1:(i + 1) * nq1], K_TOP, STEP, PARALLEL)
+        res[i] = (on, mt)
+        del oc
+
+    th = [threading.Thread(target=client, args=(i,)) for i in range(ncores)]
+    t0 = time.perf_counter()
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    wall = time.perf_counter() - t0
+    on_sum = sum(r[0] for r in res)
+    mt_sum = sum(r[1] for r in res)
+    out["all_cores"] = {"value": round(ncores * nq1 / (on_sum + mt_sum) * ncores, 2), "cores": ncores,
+                        "wall_value": round(ncores * nq1 / wall, 2),
+                        "note": f"{ncores} concurrent oracle clients x {nq1} queries (two maintenance windows each); "
+                                "value = queries / (mean per-client online + maintenance time) summed over "
+                                "clients; wall_value includes each client's first preprocessing"}
+    return out
 
 
 def main():
