@@ -171,3 +171,91 @@ def private_search(frontend, queries, *, k: int = 10, step: int = 20, parallel: 
             with open(report_file, "a") as fh:
                 fh.write(out["report"])
     return out
+
+
+# ---------------------------------------------------------------------------
+# MS-MARCO end-to-end quality: vector ids -> passage ids -> MRR@k
+# (reproduction/msmarco/evaluate.py:26-120)
+# ---------------------------------------------------------------------------
+def read_queries_tsv(path: str) -> list[tuple[str, str]]:
+    """`qid<TAB>text` per line, in file order (evaluate.py:26-34)."""
+    out = []
+    with open(path, encoding="utf-8") as fh:
+        for row, line in enumerate(fh, start=1):
+            parts = line.rstrip("\r\n").split("\t", 1)
+            if len(parts) != 2:
+                raise ValueError(f"query row {row} is malformed")
+            out.append((parts[0], parts[1]))
+    return out
+
+
+def read_qrels(path: str) -> dict[str, str]:
+    """TREC qrels `qid 0 docid rel`: the FIRST relevant docid of each query
+    counts (evaluate.py:37-45)."""
+    rel: dict[str, str] = {}
+    with open(path, encoding="utf-8") as fh:
+        for row, line in enumerate(fh, start=1):
+            f = line.split()
+            if len(f) != 4:
+                raise ValueError(f"qrels row {row} is malformed")
+            if f[0] not in rel:
+                rel[f[0]] = f[2]
+    return rel
+
+
+def read_results(path: str, query_count: int, k: int) -> np.ndarray:
+    """Search results as an int .npy of shape (queries, k) or a text file of k
+    ids per line (evaluate.py:48-71)."""
+    with open(path, "rb") as fh:
+        npy = fh.read(6) == b"\x93NUMPY"
+    if npy:
+        a = np.load(path, allow_pickle=False)
+        if a.shape != (query_count, k):
+            raise ValueError(f"result array has shape {a.shape}; expected {(query_count, k)}")
+        if not np.issubdtype(a.dtype, np.integer):
+            raise ValueError(f"result array must contain integers, found {a.dtype}")
+        return a.astype(np.int64)
+    rows = []
+    with open(path, encoding="utf-8") as fh:
+        for row, line in enumerate(fh, start=1):
+            vals = [int(x) for x in line.split()]
+            if len(vals) != k:
+                raise ValueError(f"result row {row} has {len(vals)} values; expected {k}")
+            rows.append(vals)
+    if len(rows) != query_count:
+        raise ValueError(f"result file has {len(rows)} rows; expected {query_count}")
+    return np.asarray(rows, dtype=np.int64)
+
+
+def mrr_at_k(results, queries: list[tuple[str, str]], qrels: dict[str, str], docids,
+             output_docids: str | None = None) -> dict:
+    """MRR over all queries of 1 / (rank of the first returned passage equal to
+    the query's relevant one), 0 when none is in the list; ids outside the
+    corpus map to "INVALID_VECTOR_ID" and never match (evaluate.py:81-120).
+    A query without qrels is an error, as in the reference.  Optionally writes
+    the per-query docid listing in the reference's format."""
+    results = np.asarray(results)
+    n = len(docids)
+    total = 0.0
+    ranked = 0
+    lines = []
+    for qi, (qid, text) in enumerate(queries):
+        relevant = qrels[qid]
+        lines.append(f"Query: {qid} {text}")
+        hit = None
+        for rank, vid in enumerate(results[qi], start=1):
+            d = str(docids[vid]) if 0 <= vid < n else "INVALID_VECTOR_ID"
+            lines.append(d)
+            if hit is None and d == relevant:
+                hit = rank
+        lines.append("----------")
+        lines.append("")
+        if hit is not None:
+            ranked += 1
+            total += 1.0 / hit
+    if output_docids:
+        with open(output_docids, "w", encoding="utf-8") as fh:
+            fh.write("\n".join(lines) + ("\n" if lines else ""))
+    nq = len(queries)
+    return {"metric": f"MRR@{results.shape[1] if results.ndim == 2 else 0}", "mrr": total / nq if nq else 0.0,
+            "queries": nq, "ranked_queries": ranked}

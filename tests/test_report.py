@@ -51,3 +51,28 @@ def test_int_matrix_files_round_trip(tmp_path):
     rows = np.array([[3, 1, 2, 3], [3, 4, 5, 6]], dtype=np.uint32)   # dim-prefixed uint32 rows
     rows.tofile(str(iv))
     assert np.array_equal(load_int_matrix(str(iv), 2, 3), [[1, 2, 3], [4, 5, 6]])
+
+
+def test_mrr_at_k(tmp_path):
+    """reproduction/msmarco/evaluate.py semantics: first relevant docid per
+    query (qrels setdefault), first hit rank, invalid ids never match, text
+    and .npy result files, the docid listing."""
+    import numpy as np
+    from pacmann_amd.report import mrr_at_k, read_qrels, read_queries_tsv, read_results
+    (tmp_path / "q.tsv").write_text("10\twhat is a\n11\tb c\n12\tnone\n")
+    (tmp_path / "qrels").write_text("10 0 D7 1\n10 0 D9 1\n11 0 D1 1\n12 0 D5 1\n")
+    docids = np.array([f"D{i}" for i in range(10)])
+    res = np.array([[3, 9, 7], [1, -4, 2], [12, 0, 0]])
+    np.save(tmp_path / "r.npy", res)
+    (tmp_path / "r.txt").write_text("\n".join(" ".join(map(str, r)) for r in res) + "\n")
+    qs, qr = read_queries_tsv(tmp_path / "q.tsv"), read_qrels(tmp_path / "qrels")
+    assert qr["10"] == "D7"
+    for f in ("r.npy", "r.txt"):
+        r = read_results(str(tmp_path / f), 3, 3)
+        out = mrr_at_k(r, qs, qr, docids, output_docids=str(tmp_path / "ids.txt"))
+        assert out["ranked_queries"] == 2 and abs(out["mrr"] - (1 / 3 + 1) / 3) < 1e-12
+    listing = (tmp_path / "ids.txt").read_text().splitlines()
+    assert listing[0] == "Query: 10 what is a" and "INVALID_VECTOR_ID" in listing
+    import pytest
+    with pytest.raises(ValueError):
+        read_results(str(tmp_path / "r.npy"), 3, 4)
