@@ -108,6 +108,8 @@ SIGNATURES = {
     "pm_build_graph": (C.c_int, [vp, f32p, u64, u64, u64, C.c_float, u64, u32p, C.POINTER(dbl)]),
     "pm_search_loop_sessions": (C.c_int, [C.POINTER(vp), C.c_uint32, f32p, u64, C.c_int, C.c_int, C.c_int,
                                           i64p, C.POINTER(dbl), C.POINTER(dbl), C.POINTER(dbl)]),
+    "pm_search_loop_batched": (C.c_int, [C.POINTER(vp), C.c_uint32, f32p, u64, C.c_int, C.c_int, C.c_int, C.c_uint32,
+                                         i64p, C.POINTER(dbl), C.POINTER(dbl), C.POINTER(dbl)]),
 }
 
 Q_OK, Q_EBUDGET, Q_ECHUNK, Q_ENOHIT, Q_ERANGE = range(5)
@@ -562,6 +564,26 @@ def search_loop_sessions(sessions, queries, k: int, step: int, parallel: int):
     mt = np.zeros(S, dtype=np.float64)
     _check(lib().pm_search_loop_sessions(hs, S, _p(qs, f32p), q, k, step, parallel, _p(ans, i64p), C.byref(wall),
                                          on.ctypes.data_as(C.POINTER(dbl)), mt.ctypes.data_as(C.POINTER(dbl))))
+    return ans, wall.value, on, mt
+
+
+def search_loop_batched(sessions, queries, k: int, step: int, parallel: int, nthreads: int = 0):
+    """Serve len(sessions) client sessions in lock-step, every round of all of
+    them one shared batch-PIR step (pm_search_loop_batched): queries [S, q, dim].
+    Returns (answers [S, q, k], wall_s, online_s[S], maint_s[S])."""
+    S = len(sessions)
+    qs = np.ascontiguousarray(queries, dtype=np.float32)
+    if qs.ndim != 3 or qs.shape[0] != S or qs.shape[2] != sessions[0].Dim:
+        raise ValueError("queries must be [len(sessions), q, dim]")
+    q = qs.shape[1]
+    ans = np.zeros((S, q, k), dtype=np.int64)
+    hs = (vp * S)(*[s.h for s in sessions])
+    wall = C.c_double()
+    on = np.zeros(S, dtype=np.float64)
+    mt = np.zeros(S, dtype=np.float64)
+    _check(lib().pm_search_loop_batched(hs, S, _p(qs, f32p), q, k, step, parallel, nthreads, _p(ans, i64p),
+                                        C.byref(wall), on.ctypes.data_as(C.POINTER(dbl)),
+                                        mt.ctypes.data_as(C.POINTER(dbl))))
     return ans, wall.value, on, mt
 
 

@@ -323,6 +323,9 @@ struct Engine {
   std::vector<uint64_t> resp_rows;
   std::vector<float> resp_dist;
   std::vector<uint8_t> resp_ok;
+  std::vector<char> slow;           // partitions at their query budget this batch (bq_prepare)
+  uint64_t qn = 0;                  // queryNumToMake of the batch being served
+  uint64_t prep_gen = 0;            // preprocessings run (any range): a shared step re-copies the parts
   std::vector<uint64_t> zero_row;   // response of dropped / failed ids (batch-pir.go:229-236)
 };
 
@@ -521,6 +524,7 @@ static int engine_prep(Engine* g, uint64_t p0, uint64_t p1) {
     ph.shadow.clear();
   }
   CHK(upload_parts(g));
+  g->prep_gen++;
   const PmPart* dp = p1 - p0 == 1 ? g->parts_d.as<PmPart>() + p0 : g->owned_d.as<PmPart>();
   const int np = (int)todo.size();
   c->timed("prep_init", 0, [&] { pmk::prep_init(st, dp, np, g->maxH, g->maxRepl, (uint32_t)g->E, g->skipPrep); });
@@ -607,6 +611,8 @@ static int wait_step(pm_ctx* c, const PmOutHdr* hdr, uint32_t nsub, uint32_t tok
   return 0;
 }
 
+static void post_results(Engine* g, PmOutHdr* hdr, uint64_t* rows, uint32_t nsub, uint32_t base,
+                         uint32_t token);
 // Wait for a step's results (tokens in pinned memory) and update the host
 // mirrors.
 static int wait_and_post(Engine* g, const PmStep& S, uint32_t nsub, Clock::time_point) {
@@ -630,8 +636,24 @@ static int wait_and_post(Engine* g, const PmStep& S, uint32_t nsub, Clock::time_
     }
   }
   auto t_post = Clock::now();
-  g->hdr = S.hdr_h;
-  g->rows = S.rows_h;
+  post_results(g, S.hdr_h, S.rows_h, nsub, 0, S.token);
+  c->host_add(HT_STEP_POST, ms_since(t_post));
+  return 0;
+}
+
+// The host side of a published step for one engine whose sub-queries are
+// [base, base + nsub) of the step (base > 0 when several clients shared the
+// step, pm_search_loop_batched): result pointers, FinishedQueryNum and
+// localCache mirrors (pir.go:469-470), in-step cache hits copied from the
+// earlier response (their reference is a step-wide sub-query index).
+static void post_results(Engine* g, PmOutHdr* hdr, uint64_t* rows, uint32_t nsub, uint32_t base,
+                         uint32_t token) {
+  pm_ctx* c = g->ctx;
+  const uint64_t E = g->E;
+  g->hdr = hdr + base;
+  g->rows = rows + (uint64_t)base * E;
+  PmStep S{};
+  S.token = token;
   // host mirrors: FinishedQueryNum and the localCache index (pir.go:469-470);
   // in-step cache hits copy the earlier response
   if (c->log_steps) {   // diagnostics: every sub-query of the step
@@ -649,9 +671,9 @@ static int wait_and_post(Engine* g, const PmStep& S, uint32_t nsub, Clock::time_
       if (h.status == ST_CACHED) {
         auto it = ph.shadow.find(h.ref);
         if (it == ph.shadow.end() || memcmp(it->second.data(), row, E * 8) != 0) {
-          HIPCHK(hipStreamSynchronize(c->stream));
+          (void)hipStreamSynchronize(c->stream);   // diagnostics only
           std::vector<uint64_t> dev(E);
-          HIPCHK(hipMemcpy(dev.data(), ph.d.arena + (uint64_t)h.ref * E, E * 8, hipMemcpyDeviceToHost));
+          (void)hipMemcpy(dev.data(), ph.d.arena + (uint64_t)h.ref * E, E * 8, hipMemcpyDeviceToHost);
           const bool dev_ok = it != ph.shadow.end() && memcmp(it->second.data(), dev.data(), E * 8) == 0;
           fprintf(stderr, "[pm] cache: token %u sub %u part %u idx %lu slot %u: row differs from the slot's answer%s; "
                   "device arena now %s the slot's answer; row[0] %016lx shadow[0] %016lx arena[0] %016lx\n",
@@ -669,15 +691,15 @@ static int wait_and_post(Engine* g, const PmStep& S, uint32_t nsub, Clock::time_
       ph.fqn++;
       ph.cache.put(g->subs[s].idx, h.ref);
     } else if (h.status == ST_DUP) {
-      memcpy(g->rows + (uint64_t)s * E, g->rows + (uint64_t)h.ref * E, E * 8);
-      g->hdr[s].dist = g->hdr[h.ref].dist;
+      const uint32_t r = h.ref - base;
+      memcpy(g->rows + (uint64_t)s * E, g->rows + (uint64_t)r * E, E * 8);
+      g->hdr[s].dist = g->hdr[r].dist;
     }
   }
-  c->host_add(HT_STEP_POST, ms_since(t_post));
 #ifdef PM_STAMPS
   {   // partition 0's phase deltas in shader clocks, accumulated; printed at exit
     std::vector<uint64_t> t(64);
-    HIPCHK(hipMemcpy(t.data(), g->stamps.p, 64 * 8, hipMemcpyDeviceToHost));
+    (void)hipMemcpy(t.data(), g->stamps.p, 64 * 8, hipMemcpyDeviceToHost);
     g->stamp_sum.resize(64, 0.0);
     for (int i = 1; i < 64; ++i)
     {   // each kernel's stamps relative to its own first one
@@ -687,7 +709,6 @@ static int wait_and_post(Engine* g, const PmStep& S, uint32_t nsub, Clock::time_
     g->stamp_n++;
   }
 #endif
-  return 0;
 }
 
 static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
@@ -1062,23 +1083,92 @@ static int batch_query(Engine* g, const uint64_t* idx, uint64_t n, uint64_t* out
   return r;
 }
 static inline bool status_ok(uint32_t st) { return st == ST_OK || st == ST_CACHED || st == ST_DUP; }
-static int batch_query_impl(Engine* g, const uint64_t* idx, uint64_t n, uint64_t* out, const float* q_dev,
-                            uint32_t dim, float* dist_out, const uint64_t** rows_out, uint8_t* ok) {
+
+// SimpleBatchPianoPIR.Query (batch-pir.go:170-248) in three parts, so that a
+// driver serving several clients can put many clients' steps in one launch
+// (pm_search_loop_batched):
+//   bq_prepare   bucketing (:176-200): ids per partition, dummy padding,
+//                overflow drop; when every partition is clear of its query
+//                budget (the usual case), the one step's sub-queries
+//                (*fast = true);
+//   bq_emit_fast after that step is published: each id's response (the last
+//                one made for it, :187,213), distance and success flag;
+//   bq_tail      FinishedBatchNum / QueriesMadeInPartition and the
+//                re-preprocessing trigger (:238-247).
+static int bq_prepare(Engine* g, const uint64_t* idx, uint64_t n, bool* fast) {
   const uint64_t E = g->E, P = g->P;
   if (g->zero_row.size() != E) g->zero_row.assign(E, 0);
   for (uint64_t i = 0; i < n; ++i)
     if (idx[i] >= g->N) return fail(PM_EINVAL, "id " + std::to_string(idx[i]) + " >= DBSize");
   const uint64_t qn = n / P;
+  g->qn = qn;
   g->pq.resize(P);
   for (auto& v : g->pq) v.clear();
   for (uint64_t i = 0; i < n; ++i) g->pq[idx[i] / g->PS].push_back(idx[i]);
   for (auto& v : g->pq) while (v.size() < qn) v.push_back(kDefaultValue);
-  // responses[id] = last response made for it (batch-pir.go:187,213)
   g->resp_map.clear();
-  size_t nresp = 0;
   g->resp_rows.resize(std::max<size_t>(g->resp_rows.size(), n * E));
   g->resp_dist.resize(std::max<size_t>(g->resp_dist.size(), n));
   g->resp_ok.resize(std::max<size_t>(g->resp_ok.size(), n));
+  g->slow.assign(P, 0);
+  bool any_slow = false;
+  for (uint64_t p = 0; p < P; ++p) {
+    uint64_t nreal = 0;
+    for (uint64_t j = 0; j < qn; ++j) nreal += g->pq[p][j] != kDefaultValue;
+    const PartHost& ph = g->parts[p];
+    g->slow[p] = qn && ph.fqn + nreal >= ph.maxq64;
+    any_slow |= g->slow[p] != 0;
+  }
+  *fast = !any_slow && qn <= pmk::step_max_sub_per_part() && qn > 0;
+  if (*fast) {
+    begin_step(g);
+    for (uint64_t p = 0; p < P; ++p) {
+      for (uint64_t j = 0; j < qn; ++j) {
+        const uint64_t id = g->pq[p][j];
+        add_sub(g, (uint32_t)p, id != kDefaultValue, id - p * g->PS, id);
+      }
+      close_partition(g, (uint32_t)p);
+    }
+  }
+  return 0;
+}
+static void bq_emit_fast(Engine* g, const uint64_t* idx, uint64_t n, uint64_t* out, float* dist_out,
+                         const uint64_t** rows_out, uint8_t* ok) {
+  const uint64_t E = g->E;
+  for (size_t s = 0; s < g->subs.size(); ++s) {
+    const uint32_t k = g->subs[s].kind;
+    if (k == SUB_REAL || k == SUB_HOSTCACHE) g->resp_map.put(g->sub_gid[s], (uint32_t)s);   // last wins
+  }
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint32_t* sp = g->resp_map.find(idx[i]);
+    const uint64_t* row = sp ? g->rows + (uint64_t)*sp * E : g->zero_row.data();
+    if (rows_out) rows_out[i] = row;
+    else memcpy(out + i * E, row, E * 8);
+    if (dist_out) dist_out[i] = sp ? g->hdr[*sp].dist : 0.0f;
+    if (ok) ok[i] = sp && status_ok(g->hdr[*sp].status);
+  }
+}
+static int bq_tail(Engine* g, uint64_t n) {
+  if (g->QMIP >= g->parts[0].maxq64 - 2) {
+    CHK(batch_prep(g));
+  } else {
+    g->FBN += n / g->B;
+    g->QMIP += g->qn;
+  }
+  return 0;
+}
+static int batch_query_impl(Engine* g, const uint64_t* idx, uint64_t n, uint64_t* out, const float* q_dev,
+                            uint32_t dim, float* dist_out, const uint64_t** rows_out, uint8_t* ok) {
+  const uint64_t E = g->E, P = g->P;
+  bool fast = false;
+  CHK(bq_prepare(g, idx, n, &fast));
+  const uint64_t qn = g->qn;
+  if (fast) {   // common case: one step; ids map straight onto the pinned result rows
+    CHK(engine_step(g, q_dev, dim));
+    bq_emit_fast(g, idx, n, out, dist_out, rows_out, ok);
+    return bq_tail(g, n);
+  }
+  size_t nresp = 0;
   auto collect = [&]() {
     for (size_t s = 0; s < g->subs.size(); ++s) {
       const uint32_t k = g->subs[s].kind;
@@ -1090,47 +1180,12 @@ static int batch_query_impl(Engine* g, const uint64_t* idx, uint64_t n, uint64_t
       g->resp_ok[slot] = status_ok(g->hdr[s].status);
     }
   };
-  bool qn_done = false;
-  std::vector<char> slow(P, 0);
-  for (uint64_t p = 0; p < P; ++p) {
-    uint64_t nreal = 0;
-    for (uint64_t j = 0; j < qn; ++j) nreal += g->pq[p][j] != kDefaultValue;
-    const PartHost& ph = g->parts[p];
-    slow[p] = qn && ph.fqn + nreal >= ph.maxq64;
-  }
   const uint64_t kStep = pmk::step_max_sub_per_part();
-  bool any_slow = false;
-  for (uint64_t p = 0; p < P; ++p) any_slow |= slow[p] != 0;
-  if (!any_slow && qn <= kStep && qn > 0) {
-    // common case: one fused step; map ids straight onto the pinned result rows
-    begin_step(g);
-    for (uint64_t p = 0; p < P; ++p) {
-      for (uint64_t j = 0; j < qn; ++j) {
-        const uint64_t id = g->pq[p][j];
-        add_sub(g, (uint32_t)p, id != kDefaultValue, id - p * g->PS, id);
-      }
-      close_partition(g, (uint32_t)p);
-    }
-    CHK(engine_step(g, q_dev, dim));
-    for (size_t s = 0; s < g->subs.size(); ++s) {
-      const uint32_t k = g->subs[s].kind;
-      if (k == SUB_REAL || k == SUB_HOSTCACHE) g->resp_map.put(g->sub_gid[s], (uint32_t)s);   // last wins
-    }
-    for (uint64_t i = 0; i < n; ++i) {
-      const uint32_t* sp = g->resp_map.find(idx[i]);
-      const uint64_t* row = sp ? g->rows + (uint64_t)*sp * E : g->zero_row.data();
-      if (rows_out) rows_out[i] = row;
-      else memcpy(out + i * E, row, E * 8);
-      if (dist_out) dist_out[i] = sp ? g->hdr[*sp].dist : 0.0f;
-      if (ok) ok[i] = sp && status_ok(g->hdr[*sp].status);
-    }
-    qn_done = true;
-  }
-  for (uint64_t j0 = 0; !qn_done && j0 < qn; j0 += kStep) {
+  for (uint64_t j0 = 0; j0 < qn; j0 += kStep) {
     const uint64_t j1 = std::min(qn, j0 + kStep);
     begin_step(g);
     for (uint64_t p = 0; p < P; ++p) {
-      if (!slow[p])
+      if (!g->slow[p])
         for (uint64_t j = j0; j < j1; ++j) {
           const uint64_t id = g->pq[p][j];
           add_sub(g, (uint32_t)p, id != kDefaultValue, id - p * g->PS, id);
@@ -1140,7 +1195,7 @@ static int batch_query_impl(Engine* g, const uint64_t* idx, uint64_t n, uint64_t
     if (!g->subs.empty()) { CHK(engine_step(g, q_dev, dim)); collect(); }
   }
   for (uint64_t p = 0; p < P; ++p) {
-    if (!slow[p]) continue;
+    if (!g->slow[p]) continue;
     for (uint64_t j = 0; j < qn; ++j) {
       PartHost& ph = g->parts[p];
       if (ph.fqn == ph.maxq64) CHK(engine_prep(g, p, p + 1));
@@ -1152,7 +1207,7 @@ static int batch_query_impl(Engine* g, const uint64_t* idx, uint64_t n, uint64_t
       collect();
     }
   }
-  for (uint64_t i = 0; !qn_done && i < n; ++i) {
+  for (uint64_t i = 0; i < n; ++i) {
     const uint32_t* sp = g->resp_map.find(idx[i]);
     const uint64_t* row = sp ? &g->resp_rows[(size_t)*sp * E] : g->zero_row.data();
     if (rows_out) rows_out[i] = row;
@@ -1160,13 +1215,7 @@ static int batch_query_impl(Engine* g, const uint64_t* idx, uint64_t n, uint64_t
     if (dist_out) dist_out[i] = sp ? g->resp_dist[*sp] : 0.0f;
     if (ok) ok[i] = sp && g->resp_ok[*sp];
   }
-  if (g->QMIP >= g->parts[0].maxq64 - 2) {
-    CHK(batch_prep(g));
-  } else {
-    g->FBN += n / g->B;
-    g->QMIP += qn;
-  }
-  return 0;
+  return bq_tail(g, n);
 }
 extern "C" int pm_batchpir_query(pm_batchpir* h, const uint64_t* ids, uint64_t n, uint64_t* out) {
   return batch_query(&h->e, ids, n, out, nullptr, 0, nullptr);
@@ -1328,6 +1377,7 @@ struct pm_graph {
   std::vector<int64_t> known_id, known_reach;
   std::vector<VD> heap, all;
   std::vector<std::pair<VD, uint32_t>> fs;
+  Clock::time_point t_init;
   ~pm_graph() { delete pir; }
 };
 
@@ -1438,28 +1488,36 @@ static VD heap_pop(std::vector<VD>& h) {
 
 // GetVertexInfo (private-search.go:441-506) for g->batch, with the L2 distance
 // of every returned vector to the resident query computed on the GPU next to
-// the decode (k_answer).  Fills g->nb and g->dist.
-static int get_vertex_info(pm_graph* g, bool with_q) {
+// the decode (k_answer).  Fills g->nb and g->dist.  In two halves around the
+// batch-PIR step, so that several sessions' steps can share one launch
+// (pm_search_loop_batched): gvi_pre buckets the ids into this session's
+// sub-queries (*fast: they are ready for a shared step; otherwise the step
+// has already been served on this session's own stream), gvi_post maps the
+// published rows back and parses them.
+static int gvi_nonprivate(pm_graph* g, bool with_q) {
+  const uint64_t n = g->batch.size(), m = g->m;
+  for (uint64_t i = 0; i < n; ++i)
+    memcpy(&g->nb[i * m], &g->graph[(uint64_t)g->batch[i] * m], m * 4);
+  if (with_q && n) {
+    hipStream_t st = g->ctx->stream;
+    std::vector<uint32_t> u(g->batch.begin(), g->batch.end());
+    CHK(g->dids.reserve(n * 4)); CHK(g->ddist.reserve(n * 4));
+    HIPCHK(hipMemcpyAsync(g->dids.p, u.data(), n * 4, hipMemcpyHostToDevice, st));
+    g->ctx->timed("l2_rows", (double)n * g->dim * 4, [&] {
+      pmk::l2_rows(st, g->dvec->as<float>(), g->dim, n, g->dids.as<uint32_t>(), g->dq.as<float>(), (uint32_t)g->dim, g->ddist.as<float>());
+    });
+    HIPCHK(hipMemcpyAsync(g->dist.data(), g->ddist.p, n * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  return 0;
+}
+static int gvi_pre(pm_graph* g, bool with_q, bool* fast) {
   const uint64_t n = g->batch.size(), m = g->m;
   g->total += n;
   g->nb.resize(n * m);
   g->dist.assign(n, 0.0f);
-  if (g->nonprivate) {
-    for (uint64_t i = 0; i < n; ++i)
-      memcpy(&g->nb[i * m], &g->graph[(uint64_t)g->batch[i] * m], m * 4);
-    if (with_q && n) {
-      hipStream_t st = g->ctx->stream;
-      std::vector<uint32_t> u(g->batch.begin(), g->batch.end());
-      CHK(g->dids.reserve(n * 4)); CHK(g->ddist.reserve(n * 4));
-      HIPCHK(hipMemcpyAsync(g->dids.p, u.data(), n * 4, hipMemcpyHostToDevice, st));
-      g->ctx->timed("l2_rows", (double)n * g->dim * 4, [&] {
-        pmk::l2_rows(st, g->dvec->as<float>(), g->dim, n, g->dids.as<uint32_t>(), g->dq.as<float>(), (uint32_t)g->dim, g->ddist.as<float>());
-      });
-      HIPCHK(hipMemcpyAsync(g->dist.data(), g->ddist.p, n * 4, hipMemcpyDeviceToHost, st));
-      HIPCHK(hipStreamSynchronize(st));
-    }
-    return 0;
-  }
+  *fast = false;
+  if (g->nonprivate) return gvi_nonprivate(g, with_q);
   Engine* e = &g->pir->e;
   // the ground-truth rows of the success check (private-search.go:483-497) are
   // pulled into the cache while the GPU answers
@@ -1470,8 +1528,24 @@ static int get_vertex_info(pm_graph* g, bool with_q) {
   }
   g->qids.assign(g->batch.begin(), g->batch.end());
   g->rowp.resize(n);
-  CHK(batch_query(e, g->qids.data(), n, nullptr, with_q ? g->dq.as<float>() : nullptr,
-                  (uint32_t)g->dim, with_q ? g->dist.data() : nullptr, g->rowp.data()));
+  auto t = Clock::now();
+  CHK(bq_prepare(e, g->qids.data(), n, fast));
+  if (!*fast)   // a partition at its query budget: the general path, served now
+    CHK(batch_query_impl(e, g->qids.data(), n, nullptr, with_q ? g->dq.as<float>() : nullptr, (uint32_t)g->dim,
+                         with_q ? g->dist.data() : nullptr, g->rowp.data(), nullptr));
+  e->ctx->host_add(HT_BATCH_QUERY, ms_since(t));
+  return 0;
+}
+static int gvi_post(pm_graph* g, bool with_q, bool fast) {
+  if (g->nonprivate) return 0;
+  const uint64_t n = g->batch.size(), m = g->m;
+  Engine* e = &g->pir->e;
+  if (fast) {
+    auto t = Clock::now();
+    bq_emit_fast(e, g->qids.data(), n, nullptr, with_q ? g->dist.data() : nullptr, g->rowp.data(), nullptr);
+    CHK(bq_tail(e, n));
+    e->ctx->host_add(HT_BATCH_QUERY, ms_since(t));
+  }
   auto t_parse = Clock::now();
   const uint64_t nb_off = g->dim * 4;   // Entry2VectorAndNeighbors (private-search.go:418-439)
   for (uint64_t i = 0; i < n; ++i) {
@@ -1486,6 +1560,17 @@ static int get_vertex_info(pm_graph* g, bool with_q) {
   g->ctx->host_add(HT_GVI_PARSE, ms_since(t_parse));
   return 0;
 }
+static int get_vertex_info(pm_graph* g, bool with_q) {
+  bool fast = false;
+  CHK(gvi_pre(g, with_q, &fast));
+  if (fast) {
+    Engine* e = &g->pir->e;
+    auto t = Clock::now();
+    CHK(engine_step(e, with_q ? g->dq.as<float>() : nullptr, (uint32_t)g->dim));
+    e->ctx->host_add(HT_BATCH_QUERY, ms_since(t));
+  }
+  return gvi_post(g, with_q, fast);
+}
 
 // SearchKNN (graphann/search.go:114-234).  Same tie rules as oracle/pm_oracle.cpp.
 static int search_knn_impl(pm_graph* g, const float* query, int k, int max_step, int parallel,
@@ -1497,85 +1582,100 @@ extern "C" int pm_search_knn(pm_graph* g, const float* query, int k, int max_ste
   g->ctx->host_add(HT_SEARCH_KNN, ms_since(t));
   return r;
 }
-static int search_knn_impl(pm_graph* g, const float* query, int k, int max_step, int parallel,
-                           int benchmarking, int64_t* ids_out, int64_t* steps_out) {
-  if (!g->pir && !g->nonprivate) return fail(PM_EINVAL, "pm_graph_preprocess not called");
-  const int64_t n = (int64_t)g->n;
+// SearchKNN in parts (the loop of search_knn_impl; pm_search_loop_batched
+// interleaves them across sessions):
+//   knn_begin  reset; unless benchmarking, the start set's distances to the
+//              query (GPU, k_l2_rows) and the first `parallel` of them on the heap;
+//   knn_batch  the ids of one step (search.go:150-172);
+//   knn_update the returned vertices with a non-empty neighbour list become
+//              known (search.go:185-218);
+//   knn_end    top k by (dist, id) (search.go:222-233).
+static void knn_add_known(pm_graph* g, int64_t id, const uint32_t* nb, float d, int64_t reach) {
   const uint64_t m = g->m;
+  const uint32_t slot = (uint32_t)g->known_id.size();
+  g->known.put((uint64_t)id, slot);
+  g->known_nb.insert(g->known_nb.end(), nb, nb + m);
+  g->known_dist.push_back(d);
+  g->known_id.push_back(id);
+  g->known_reach.push_back(reach);
+}
+// first half: reset + enqueue the start-set distances (async on the session's
+// stream); knn_begin_finish completes it after the stream is synchronised
+static int knn_begin_enqueue(pm_graph* g, const float* query, int benchmarking) {
+  if (!g->pir && !g->nonprivate) return fail(PM_EINVAL, "pm_graph_preprocess not called");
   hipStream_t st = g->ctx->stream;
   g->known.clear();
   g->known_nb.clear(); g->known_dist.clear(); g->known_id.clear(); g->known_reach.clear();
   g->heap.clear();
-  auto add_known = [&](int64_t id, const uint32_t* nb, float d, int64_t reach) {
-    const uint32_t slot = (uint32_t)g->known_id.size();
-    g->known.put((uint64_t)id, slot);
-    g->known_nb.insert(g->known_nb.end(), nb, nb + m);
-    g->known_dist.push_back(d);
-    g->known_id.push_back(id);
-    g->known_reach.push_back(reach);
-  };
-  if (!benchmarking) {
-    auto t_init = Clock::now();
-    // the query stays resident for every distance this search computes; it and
-    // the start-vertex distances move through pinned staging (async, no bounce)
-    const uint64_t ns = g->start.size();
-    CHK(g->stage_h.reserve(g->dim * 4 + ns * 4));
-    float* qh = g->stage_h.as<float>();
-    float* sdh = qh + g->dim;
-    memcpy(qh, query, g->dim * 4);
-    HIPCHK(hipMemcpyAsync(g->dq.p, qh, g->dim * 4, hipMemcpyHostToDevice, st));
-    if (ns) {
-      CHK(g->ddist.reserve(ns * 4));
-      g->ctx->timed("l2_rows", (double)ns * g->dim * 4, [&] {
-        pmk::l2_rows(st, g->dvec->as<float>(), g->dim, ns, g->dstart.as<uint32_t>(), g->dq.as<float>(), (uint32_t)g->dim, g->ddist.as<float>());
-      });
-      HIPCHK(hipMemcpyAsync(sdh, g->ddist.p, ns * 4, hipMemcpyDeviceToHost, st));
-    }
-    HIPCHK(hipStreamSynchronize(st));
-    // the first `parallel` start vertices in stable distance order (search.go:130-146):
-    // a partial sort on (dist, position) selects exactly those
-    g->fs.clear();
-    for (uint64_t i = 0; i < ns; ++i) g->fs.push_back({{sdh[i], (int64_t)g->start[i]}, (uint32_t)i});
-    const size_t take = std::min<size_t>(g->fs.size(), (size_t)std::max(parallel, 0));
-    std::partial_sort(g->fs.begin(), g->fs.begin() + take, g->fs.end(), [](const auto& a, const auto& b) {
-      return a.first.dist < b.first.dist || (a.first.dist == b.first.dist && a.second < b.second); });
-    g->fs.resize(take);   // start ids are distinct: none of the first `parallel` is skipped as known
-    g->ctx->host_add(HT_KNN_INIT, ms_since(t_init));
-    for (size_t i = 0; (int64_t)g->heap.size() < parallel && i < g->fs.size(); ++i) {
-      const int64_t id = g->fs[i].first.id;
-      if (g->known.find((uint64_t)id)) continue;
-      add_known(id, &g->graph[(uint64_t)id * m], g->fs[i].first.dist, 0);
-      heap_push(g->heap, g->fs[i].first);
+  if (benchmarking) return 0;
+  g->t_init = Clock::now();
+  // the query stays resident for every distance this search computes; it and
+  // the start-vertex distances move through pinned staging (async, no bounce)
+  const uint64_t ns = g->start.size();
+  CHK(g->stage_h.reserve(g->dim * 4 + ns * 4));
+  float* qh = g->stage_h.as<float>();
+  memcpy(qh, query, g->dim * 4);
+  HIPCHK(hipMemcpyAsync(g->dq.p, qh, g->dim * 4, hipMemcpyHostToDevice, st));
+  if (ns) {
+    CHK(g->ddist.reserve(ns * 4));
+    g->ctx->timed("l2_rows", (double)ns * g->dim * 4, [&] {
+      pmk::l2_rows(st, g->dvec->as<float>(), g->dim, ns, g->dstart.as<uint32_t>(), g->dq.as<float>(), (uint32_t)g->dim, g->ddist.as<float>());
+    });
+    HIPCHK(hipMemcpyAsync(qh + g->dim, g->ddist.p, ns * 4, hipMemcpyDeviceToHost, st));
+  }
+  return 0;
+}
+static void knn_begin_finish(pm_graph* g, int parallel, int benchmarking) {
+  if (benchmarking) return;
+  const uint64_t ns = g->start.size(), m = g->m;
+  const float* sdh = g->stage_h.as<float>() + g->dim;
+  // the first `parallel` start vertices in stable distance order (search.go:130-146):
+  // a partial sort on (dist, position) selects exactly those
+  g->fs.clear();
+  for (uint64_t i = 0; i < ns; ++i) g->fs.push_back({{sdh[i], (int64_t)g->start[i]}, (uint32_t)i});
+  const size_t take = std::min<size_t>(g->fs.size(), (size_t)std::max(parallel, 0));
+  std::partial_sort(g->fs.begin(), g->fs.begin() + take, g->fs.end(), [](const auto& a, const auto& b) {
+    return a.first.dist < b.first.dist || (a.first.dist == b.first.dist && a.second < b.second); });
+  g->fs.resize(take);   // start ids are distinct: none of the first `parallel` is skipped as known
+  g->ctx->host_add(HT_KNN_INIT, ms_since(g->t_init));
+  for (size_t i = 0; (int64_t)g->heap.size() < parallel && i < g->fs.size(); ++i) {
+    const int64_t id = g->fs[i].first.id;
+    if (g->known.find((uint64_t)id)) continue;
+    knn_add_known(g, id, &g->graph[(uint64_t)id * m], g->fs[i].first.dist, 0);
+    heap_push(g->heap, g->fs[i].first);
+  }
+}
+static void knn_batch(pm_graph* g, int parallel, int benchmarking) {
+  auto t_batch = Clock::now();
+  const uint64_t m = g->m, n = g->n;
+  g->batch.clear();
+  for (int r = 0; r < parallel; ++r) {
+    if (g->heap.empty() || benchmarking) {
+      for (uint64_t i = 0; i < m; ++i) g->batch.push_back((int64_t)g->rng.intn(n));
+    } else {
+      const VD it = heap_pop(g->heap);
+      const uint32_t* nb = &g->known_nb[(size_t)*g->known.find((uint64_t)it.id) * m];
+      for (uint64_t i = 0; i < m; ++i) g->batch.push_back((int64_t)nb[i]);
     }
   }
-  for (int step = 0; step < max_step; ++step) {
-    auto t_batch = Clock::now();
-    g->batch.clear();
-    for (int r = 0; r < parallel; ++r) {
-      if (g->heap.empty() || benchmarking) {
-        for (uint64_t i = 0; i < m; ++i) g->batch.push_back((int64_t)g->rng.intn((uint64_t)n));
-      } else {
-        const VD it = heap_pop(g->heap);
-        const uint32_t* nb = &g->known_nb[(size_t)*g->known.find((uint64_t)it.id) * m];
-        for (uint64_t i = 0; i < m; ++i) g->batch.push_back((int64_t)nb[i]);
-      }
-    }
-    g->ctx->host_add(HT_KNN_BATCH, ms_since(t_batch));
-    CHK(get_vertex_info(g, !benchmarking));
-    if (benchmarking) continue;
-    auto t_round = Clock::now();
-    for (size_t i = 0; i < g->batch.size(); ++i) {
-      const int64_t id = g->batch[i];
-      if (g->known.find((uint64_t)id)) continue;
-      const uint32_t* nb = &g->nb[i * m];
-      bool ok = false;
-      for (uint64_t j = 0; j < m; ++j) if (nb[j] != 0) { ok = true; break; }
-      if (!ok) continue;
-      add_known(id, nb, g->dist[i], step);
-      heap_push(g->heap, {g->dist[i], id});
-    }
-    g->ctx->host_add(HT_KNN_UPDATE, ms_since(t_round));
+  g->ctx->host_add(HT_KNN_BATCH, ms_since(t_batch));
+}
+static void knn_update(pm_graph* g, int step) {
+  auto t_round = Clock::now();
+  const uint64_t m = g->m;
+  for (size_t i = 0; i < g->batch.size(); ++i) {
+    const int64_t id = g->batch[i];
+    if (g->known.find((uint64_t)id)) continue;
+    const uint32_t* nb = &g->nb[i * m];
+    bool ok = false;
+    for (uint64_t j = 0; j < m; ++j) if (nb[j] != 0) { ok = true; break; }
+    if (!ok) continue;
+    knn_add_known(g, id, nb, g->dist[i], step);
+    heap_push(g->heap, {g->dist[i], id});
   }
+  g->ctx->host_add(HT_KNN_UPDATE, ms_since(t_round));
+}
+static void knn_end(pm_graph* g, int k, int64_t* ids_out, int64_t* steps_out) {
   auto t_fin = Clock::now();
   g->all.clear();
   for (size_t i = 0; i < g->known_id.size(); ++i) g->all.push_back({g->known_dist[i], g->known_id[i]});
@@ -1588,6 +1688,19 @@ static int search_knn_impl(pm_graph* g, const float* query, int k, int max_step,
     else { ids_out[i] = g->all[i].id; if (steps_out) steps_out[i] = g->known_reach[*g->known.find((uint64_t)g->all[i].id)]; }
   }
   g->ctx->host_add(HT_KNN_FINAL, ms_since(t_fin));
+}
+static int search_knn_impl(pm_graph* g, const float* query, int k, int max_step, int parallel,
+                           int benchmarking, int64_t* ids_out, int64_t* steps_out) {
+  CHK(knn_begin_enqueue(g, query, benchmarking));
+  if (!benchmarking) HIPCHK(hipStreamSynchronize(g->ctx->stream));
+  knn_begin_finish(g, parallel, benchmarking);
+  for (int step = 0; step < max_step; ++step) {
+    knn_batch(g, parallel, benchmarking);
+    CHK(get_vertex_info(g, !benchmarking));
+    if (benchmarking) continue;
+    knn_update(g, step);
+  }
+  knn_end(g, k, ids_out, steps_out);
   return 0;
 }
 
@@ -1658,6 +1771,284 @@ extern "C" int pm_search_loop_sessions(pm_graph** gs, uint32_t S, const float* q
   }
   for (uint32_t i = 0; i < S; ++i)
     if (rc[i]) return fail(rc[i], "session " + std::to_string(i) + ": " + msg[i]);
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Batched multi-session serving: S client sessions in
+// lock-step, every batch-PIR round of all of them ONE step over S x 16
+// partitions (k_match -> k_resolve -> [k_gather] -> k_answer), so a round
+// costs one launch sequence for all clients instead of one per client.  Each
+// session keeps its own keys, hint state, cache, counters, search state and
+// maintenance; the shared step only concatenates their sub-queries (a
+// session's partition p is the step's partition s * 16 + p) and scores each
+// decoded row against its own session's query (PmPart::qv).  Host work (the
+// sessions' searches) runs on a pool of worker threads between steps.
+// ---------------------------------------------------------------------------
+struct SpinBarrier {
+  std::atomic<uint32_t> count{0}, gen{0};
+  uint32_t n = 1;
+  void wait() {
+    const uint32_t g0 = gen.load(std::memory_order_acquire);
+    if (count.fetch_add(1, std::memory_order_acq_rel) + 1 == n) {
+      count.store(0, std::memory_order_relaxed);
+      gen.fetch_add(1, std::memory_order_release);
+    } else {
+      while (gen.load(std::memory_order_acquire) == g0) std::this_thread::yield();
+    }
+  }
+};
+
+struct StepGroup {
+  pm_ctx* c = nullptr;   // the shared steps' stream
+  uint32_t S = 0, P = 0, maxPH = 0, maxSS = 0, E = 0, dim = 0;
+  DevBuf parts_d, subs_d, sb_d, bits, cand, meta, spec, res_d, ans, part_x, done;
+  HostBuf desc_h, out_h;
+  uint32_t token = 0;
+  std::vector<PmSub> subs;
+  std::vector<uint32_t> sb, base;
+  std::vector<uint64_t> gen;   // each session's Engine::prep_gen at the last upload of its parts
+};
+
+static int group_upload_parts(StepGroup& G, pm_graph** gs) {
+  std::vector<PmPart> v;
+  v.reserve((size_t)G.S * G.P);
+  for (uint32_t s = 0; s < G.S; ++s) {
+    Engine* e = &gs[s]->pir->e;
+    for (uint32_t p = 0; p < G.P; ++p) {
+      PmPart d = e->parts[p].d;
+      d.qv = gs[s]->dq.as<float>();
+      v.push_back(d);
+    }
+  }
+  HIPCHK(hipMemcpyAsync(G.parts_d.p, v.data(), v.size() * sizeof(PmPart), hipMemcpyHostToDevice, G.c->stream));
+  HIPCHK(hipStreamSynchronize(G.c->stream));
+  G.gen.resize(G.S);
+  for (uint32_t s = 0; s < G.S; ++s) G.gen[s] = gs[s]->pir->e.prep_gen;
+  return 0;
+}
+
+// One shared step over the sessions whose sub-queries are ready (in[s]).
+static int group_step(StepGroup& G, pm_graph** gs, const std::vector<char>& in) {
+  pm_ctx* c = G.c;
+  hipStream_t st = c->stream;
+  G.subs.clear();
+  G.sb.assign(1, 0);
+  G.base.assign(G.S, 0);
+  uint32_t max_per_part = 0, np_live = 0;
+  double ans_bytes = 0;
+  for (uint32_t s = 0; s < G.S; ++s) {
+    Engine* e = &gs[s]->pir->e;
+    G.base[s] = (uint32_t)G.subs.size();
+    for (uint32_t p = 0; p < G.P; ++p) {
+      if (in[s]) {
+        for (uint32_t j = e->sb[p]; j < e->sb[p + 1]; ++j) {
+          PmSub x = e->subs[j];
+          x.part += s * G.P;
+          G.subs.push_back(x);
+          if (x.kind == SUB_REAL || x.kind == SUB_DUMMY)   // rows*E*8 + 4*SS + 8*E
+            ans_bytes += (double)e->parts[p].d.SS * (G.E * 8 + 4) + 8.0 * G.E;
+        }
+        const uint32_t n = e->sb[p + 1] - e->sb[p];
+        max_per_part = std::max(max_per_part, n);
+        np_live += n > 0;
+      }
+      G.sb.push_back((uint32_t)G.subs.size());
+    }
+  }
+  const uint32_t nsub = (uint32_t)G.subs.size(), np = G.S * G.P;
+  if (nsub == 0) return 0;
+  const uint32_t words = (G.maxPH + 63) / 64, cblk = pmk::step_match_blocks(G.maxPH);
+  CHK(G.subs_d.reserve(nsub * sizeof(PmSub)));
+  CHK(G.sb_d.reserve((np + 1) * 4));
+  CHK(G.bits.reserve((uint64_t)nsub * words * 8));
+  CHK(G.cand.reserve((uint64_t)nsub * cblk * 6 * 4));
+  CHK(G.meta.reserve((uint64_t)nsub * 2 * 4));
+  CHK(G.spec.reserve((uint64_t)nsub * 64 * 4));
+  CHK(G.res_d.reserve(nsub * sizeof(PmRes)));
+  CHK(G.ans.reserve((uint64_t)nsub * G.E * 8));
+  const size_t dsub = nsub * sizeof(PmSub);
+  CHK(G.desc_h.reserve(dsub + (np + 1) * 4));
+  CHK(G.out_h.reserve(nsub * sizeof(PmOutHdr) + (size_t)nsub * G.E * 8));
+  char* dh = G.desc_h.as<char>();
+  memcpy(dh, G.subs.data(), dsub);
+  memcpy(dh + dsub, G.sb.data(), (np + 1) * 4);
+  PmStep S{};
+  S.parts = G.parts_d.as<PmPart>();
+  S.subs_h = (const PmSub*)dh;
+  S.sb_h = (const uint32_t*)(dh + dsub);
+  S.subs = G.subs_d.as<PmSub>();
+  S.sb = G.sb_d.as<uint32_t>();
+  S.bits = G.bits.as<uint64_t>();
+  S.cand = G.cand.as<uint32_t>();
+  S.meta = G.meta.as<uint32_t>();
+  S.spec = G.spec.as<uint32_t>();
+  S.cblk = cblk;
+  S.res = G.res_d.as<PmRes>();
+  S.ans = G.ans.as<uint64_t>();
+  S.done = G.done.as<uint32_t>();
+  Engine* e0 = &gs[0]->pir->e;
+  S.db = e0->db->as<uint64_t>();
+  S.q = nullptr;   // each partition's PmPart::qv
+  S.hdr_h = G.out_h.as<PmOutHdr>();
+  S.rows_h = (uint64_t*)(G.out_h.as<char>() + nsub * sizeof(PmOutHdr));
+  S.words = words; S.E = G.E; S.dim = G.dim; S.nsub = nsub; S.np = np;
+  S.np_live = np_live;
+  S.args_valid = (nsub <= kArgSubs && np <= kArgParts) ? 1u : 0u;
+  if (S.args_valid) {
+    memcpy(S.subs_a, G.subs.data(), dsub);
+    memcpy(S.sb_a, G.sb.data(), (np + 1) * 4);
+  }
+  if (++G.token == 0) ++G.token;
+  S.token = G.token;
+  {
+    const size_t off = std::min<size_t>(e0->pf_off, G.E * 8);
+    const size_t end = std::min<size_t>(G.E * 8, off + std::min<size_t>(e0->pf_len, G.E * 8));
+    S.pf_w0 = (uint32_t)(off / 8);
+    S.pf_w1 = (uint32_t)((end + 7) / 8);
+  }
+  auto t0 = Clock::now();
+  uint32_t nreal = 0;
+  for (auto& x : G.subs) nreal += x.kind == SUB_REAL;
+  c->timed_ext("hint_match", (double)nreal * G.maxPH, [&](pmk::PmEvents ev) { pmk::step_match(st, S, G.maxPH, ev); }, 2);
+  const bool lds = pmk::step_resolve_lds_ok(G.maxPH, max_per_part);
+  c->timed_ext("resolve", 0, [&](pmk::PmEvents ev) { pmk::step_resolve(st, S, lds, ev); }, 2);
+  S.nsplit = c->no_split ? 1 : pmk::step_gather_split(G.maxSS, nsub);
+  if (S.nsplit > 1) {
+    CHK(G.part_x.reserve((uint64_t)nsub * S.nsplit * (G.E & ~3u) * 8));
+    S.part_x = G.part_x.as<uint64_t>();
+    c->timed_ext("gather", ans_bytes, [&](pmk::PmEvents ev) { pmk::step_gather(st, S, ev); }, 2);
+  }
+  c->timed_ext("answer", S.nsplit > 1 ? 0 : ans_bytes, [&](pmk::PmEvents ev) { pmk::step_answer(st, S, ev); }, 2);
+  HIPCHK(hipGetLastError());
+  c->host_add(HT_STEP_LAUNCH, ms_since(t0));
+  auto t_wait = Clock::now();
+  CHK(wait_step(c, S.hdr_h, nsub, S.token, (const char*)S.rows_h, (size_t)G.E * 8, (size_t)S.pf_w0 * 8,
+                (size_t)(S.pf_w1 - S.pf_w0) * 8));
+  c->host_add(HT_STEP_WAIT, ms_since(t_wait));
+  return 0;
+}
+
+extern "C" int pm_search_loop_batched(pm_graph** gs, uint32_t S, const float* queries, uint64_t q, int k, int step,
+                                      int parallel, uint32_t nthreads, int64_t* answers, double* wall_s,
+                                      double* online_s, double* maint_s) {
+  if (!gs || !S || (!queries && q) || (!answers && q)) return fail(PM_EINVAL, "NULL argument");
+  for (uint32_t i = 0; i < S; ++i) {
+    if (!gs[i] || !gs[i]->pir || gs[i]->nonprivate) return fail(PM_EINVAL, "sessions must be preprocessed private graphs");
+    const Engine& a = gs[0]->pir->e;
+    const Engine& b = gs[i]->pir->e;
+    if (a.db.get() != b.db.get() || a.P != b.P || a.E != b.E || gs[i]->dim != gs[0]->dim || gs[i]->m != gs[0]->m ||
+        b.nshards != 1 || gs[i]->ctx->device != gs[0]->ctx->device)
+      return fail(PM_EINVAL, "batched sessions must be clients of one server DB on one device");
+    for (uint32_t j = 0; j < i; ++j)
+      if (gs[j] == gs[i] || gs[j]->ctx == gs[i]->ctx) return fail(PM_EINVAL, "sessions need distinct graphs and contexts");
+  }
+  StepGroup G;
+  G.c = gs[0]->ctx;
+  G.S = S;
+  {
+    const Engine& e = gs[0]->pir->e;
+    G.P = (uint32_t)e.P; G.maxPH = e.maxPH; G.maxSS = e.maxSS; G.E = (uint32_t)e.E; G.dim = (uint32_t)gs[0]->dim;
+  }
+  HIPCHK(hipSetDevice(G.c->device));
+  CHK(G.parts_d.reserve((size_t)S * G.P * sizeof(PmPart)));
+  CHK(G.done.reserve(4 * (3 + 65536)));
+  {
+    const uint32_t init[3] = {1u << 31, 0, 0};
+    HIPCHK(hipMemcpy(G.done.p, init, sizeof init, hipMemcpyHostToDevice));
+  }
+  for (uint32_t i = 0; i < S; ++i) HIPCHK(hipStreamSynchronize(gs[i]->ctx->stream));
+  CHK(group_upload_parts(G, gs));
+  const uint32_t T = std::max(1u, std::min<uint32_t>(nthreads ? nthreads : 16u, S));
+  std::vector<char> fast(S, 0);
+  std::vector<double> mt(S, 0.0);
+  std::atomic<int> err{0};
+  std::string err_msg;
+  std::atomic<bool> stop{false};
+  SpinBarrier bar;
+  bar.n = T;
+  auto set_err = [&](int rc, uint32_t s) {
+    int z = 0;
+    if (rc && err.compare_exchange_strong(z, rc)) err_msg = "session " + std::to_string(s) + ": " + pm_last_error();
+  };
+  std::vector<int64_t> steps_buf((size_t)T * std::max(k, 1));
+  // worker w serves sessions s = w, w + T, ...; worker 0 (this thread) also launches the shared steps
+  auto worker = [&](uint32_t w) {
+    if (hipSetDevice(G.c->device) != hipSuccess) set_err(PM_EHIP, w);
+    int64_t* stp = &steps_buf[(size_t)w * std::max(k, 1)];
+    for (uint64_t qi = 0; qi < q; ++qi) {
+      for (uint32_t s = w; s < S && !err.load(); s += T) {   // SearchKNN begin (start set, heap)
+        pm_graph* g = gs[s];
+        int rc = knn_begin_enqueue(g, queries + ((uint64_t)s * q + qi) * g->dim, 0);
+        if (!rc && hipStreamSynchronize(g->ctx->stream) != hipSuccess) rc = fail(PM_EHIP, "start-set distances");
+        if (rc) { set_err(rc, s); break; }
+        knn_begin_finish(g, parallel, 0);
+      }
+      for (int st = 0; st < step; ++st) {
+        for (uint32_t s = w; s < S && !err.load(); s += T) {   // this round's ids -> sub-queries
+          pm_graph* g = gs[s];
+          knn_batch(g, parallel, 0);
+          bool f = false;
+          const int rc = gvi_pre(g, true, &f);
+          fast[s] = f;
+          if (rc) set_err(rc, s);
+        }
+        bar.wait();
+        if (w == 0) {
+          bool stale = false;   // a client re-preprocessed since the parts were copied
+          for (uint32_t s = 0; s < S; ++s) stale |= gs[s]->pir->e.prep_gen != G.gen[s];
+          if (stale && !err.load()) {
+            const int rc = group_upload_parts(G, gs);
+            if (rc) set_err(rc, 0);
+          }
+          if (!err.load()) {
+            const int rc = group_step(G, gs, fast);
+            if (rc) set_err(rc, 0);
+          }
+          stop.store(err.load() != 0);
+        }
+        bar.wait();
+        if (stop.load()) return;
+        for (uint32_t s = w; s < S && !err.load(); s += T) {   // rows -> neighbours, known set
+          pm_graph* g = gs[s];
+          if (fast[s]) {   // this client's share of the shared step's results
+            Engine* e = &g->pir->e;
+            auto tp = Clock::now();
+            post_results(e, G.out_h.as<PmOutHdr>(), (uint64_t*)(G.out_h.as<char>() + G.subs.size() * sizeof(PmOutHdr)),
+                         (uint32_t)e->subs.size(), G.base[s], G.token);
+            g->ctx->host_add(HT_STEP_POST, ms_since(tp));
+          }
+          const int rc = gvi_post(g, true, fast[s]);
+          if (rc) { set_err(rc, s); break; }
+          knn_update(g, st);
+        }
+      }
+      for (uint32_t s = w; s < S && !err.load(); s += T) {   // top k, maintenance (private-search.go:226-232)
+        pm_graph* g = gs[s];
+        knn_end(g, k, answers + ((uint64_t)s * q + qi) * k, stp);
+        Engine* e = &g->pir->e;
+        if (e->FBN + (uint64_t)step * (uint64_t)parallel + 10 >= e->Support) {
+          auto a = Clock::now();
+          const int rc = batch_prep(e);
+          if (rc) { set_err(rc, s); break; }
+          mt[s] += std::chrono::duration<double>(Clock::now() - a).count();
+        }
+      }
+    }
+  };
+  std::vector<std::thread> th;
+  auto t0 = Clock::now();
+  for (uint32_t w = 1; w < T; ++w) th.emplace_back(worker, w);
+  worker(0);
+  for (auto& t : th) t.join();
+  const double wall = std::chrono::duration<double>(Clock::now() - t0).count();
+  if (err.load()) return fail(err.load(), err_msg);
+  HIPCHK(hipStreamSynchronize(G.c->stream));
+  if (wall_s) *wall_s = wall;
+  for (uint32_t s = 0; s < S; ++s) {
+    if (online_s) online_s[s] = wall - mt[s];
+    if (maint_s) maint_s[s] = mt[s];
+  }
   return 0;
 }
 

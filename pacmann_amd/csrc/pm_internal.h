@@ -68,6 +68,10 @@ struct PmPart {
   // preprocessing, holds every PRF value the online phase needs.
   PM_G uint16_t* tab;
   PM_G uint16_t* tabT;    // the same table hint-major: tabT[t*SS + c] (set expansion reads one row)
+  // the search query this client's decoded rows are scored against (L2) when
+  // several clients' steps share one launch (pm_search_loop_batched); null:
+  // the step's PmStep::q
+  const PM_G float* qv;
 };
 
 // Sub-query kinds / statuses for one batched step.

@@ -1103,7 +1103,8 @@ __device__ void decode_chained(const PmStep& S, uint32_t s, RowBuf& row) {
   uint64_t* ar = P.arena + (uint64_t)r.slot * E;
   for (uint32_t w = tid; w < E; w += blockDim.x) { orow[w] = row.w[w]; ar[w] = row.w[w]; }
   float d = 0.0f;
-  if (S.q && tid < 8) d = l2_lds(row.f, S.q, S.dim);
+  const float* qq = P.qv ? P.qv : S.q;
+  if (qq && tid < 8) d = l2_lds(row.f, qq, S.dim);
   uint64_t cs = 0;
   if (tid < 64) cs = row_csum(S, row, true);
   publish_hdr(S, s, r.status, r.slot, d, cs);
@@ -1380,7 +1381,8 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, AnswerL
       for (uint32_t w = tid; w < E; w += NT) ar[w] = row.w[w];
     }
     float d = 0.0f;
-    if (has_row && S.q && tid < 8) d = l2_lds(row.f, S.q, S.dim);
+    const float* qq = P.qv ? P.qv : S.q;
+    if (has_row && qq && tid < 8) d = l2_lds(row.f, qq, S.dim);
     uint64_t cs = 0;
     if (tid < 64) cs = row_csum(S, row, has_row);
     publish_hdr(S, s, r.status, r.slot, d, cs);

@@ -434,6 +434,33 @@ def test_search_sessions_concurrent(ctx, oracle):
         assert sess[i].PIR.stats()["PrepCount"] == o.pir().stats()["PrepCount"] > 1, i
 
 
+@pytest.mark.parametrize("nthreads", [0, 2])
+def test_search_sessions_batched(ctx, oracle, nthreads):
+    """pm_search_loop_batched: five sessions in lock-step, every round of all
+    of them one shared step over 5 x 16 partitions; each session's answers,
+    PIR counters and maintenance count equal an independent oracle run with
+    its seeds (nthreads 2: workers serving several sessions each)."""
+    import pacmann_amd as pm
+    v, graph = small_graph(n=2048, seed=3)
+    base = pm.PIRGraphInfo(v, graph, pir_seed=6, search_seed=2, ctx=ctx)
+    base.Preprocess()
+    seeds = [(7, 3), (8, 4), (9, 5), (10, 6), (11, 7)]
+    sess = [base.Session(p, s) for p, s in seeds]
+    for s in sess:
+        s.Preprocess()
+    rng = np.random.default_rng(5)
+    qs = np.stack([v[rng.integers(0, len(v), size=30)] + np.float32(1.0) for _ in seeds])
+    ans, wall, on, mt = pm.search_loop_batched(sess, qs, 10, 20, 3, nthreads)
+    assert wall > 0 and (on > 0).all() and (mt > 0).all()
+    for i, (p, s) in enumerate(seeds):
+        o = oracle.Graph(v, graph, pir_seed=p, search_seed=s)
+        o.Preprocess()
+        oa, _, _ = o.SearchLoop(qs[i], 10, 20, 3)
+        assert np.array_equal(ans[i], oa), i
+        assert sess[i].counts() == o.counts(), i
+        assert sess[i].PIR.stats()["PrepCount"] == o.pir().stats()["PrepCount"] > 1, i
+
+
 # ---------------------------------------------------------------------------
 # graph construction (build_graph.go) and kNN ground truth
 # ---------------------------------------------------------------------------
