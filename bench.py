@@ -9,11 +9,15 @@ private-search.go harness (run-private-search.sh flags).  Data are synthetic
 (no dataset in the image): a clustered SIFT-like mixture with integer values in
 [0,255] and a uniform random degree-32 graph (private-search.go:54-69).
 
-Serving: one GPU serves S client sessions at once (--sessions, default 4 =
-the process's hardware queues).  Every session is a full PianoPIR client (own
-keys, hint state, maintenance) over the one server DB on the device, driven by
-its own host thread and stream (pm_search_loop_sessions), so one session's
-step kernels overlap the others' host work.  One step = one private query per
+Serving: one GPU serves S client sessions at once (--sessions, default 64).
+Every session is a full PianoPIR client (own keys, hint state, cache,
+maintenance) over the one server DB on the device.  Default (--mode batched,
+pm_search_loop_batched): the sessions run in G lock-step groups (--groups,
+default 4 = the process's hardware queues); every batch-PIR round of a group's
+sessions is ONE shared step over their S/G x 16 partitions, and 8 host worker
+threads (--threads) run the sessions' searches between steps, so one group's
+step overlaps the others' host work.  --mode concurrent: each session on its
+own host thread and stream with its own step launches (pm_search_loop_sessions).  One step = one private query per
 session (GraphANNFrontend.SearchKNN over PIRGraphInfo, 20 batch-PIR rounds of
 96 ids) plus, whenever the harness trigger fires (private-search.go:226-232),
 that session's full hint re-preprocessing — so `value` is all sessions'
@@ -43,14 +47,17 @@ N, DIM, M, K_TOP, STEP, PARALLEL, F = 1_000_000, 128, 32, 10, 20, 3, 8
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 METRIC = "private queries/sec + PIR-scan HBM GB/s, SIFT1M d=128 at 1/2/4/8 GPUs"
 PREP_KERNELS = ["prep_offsets", "prep_fold", "prep_repl", "l2_rows"]   # timed in the measured region
-STEP_KERNELS = ["step", "hint_match", "resolve", "answer"]          # timed in the profile window
+STEP_KERNELS = ["step", "hint_match", "resolve", "gather", "answer"]   # timed in the profile window
 KERNELS = PREP_KERNELS + STEP_KERNELS
 PROFILE_QUERIES = 8
-SESSIONS = 4   # client sessions per GPU (GPU_MAX_HW_QUEUES = 4 hardware queues per process)
+SESSIONS = 64   # client sessions per GPU
+GROUPS = 4      # lock-step groups (GPU_MAX_HW_QUEUES = 4 hardware queues per process)
+THREADS = 8     # host worker threads of the batched loop
 SYMBOLS = {"prep_fold": "void pm::k_prep_fold_pipe<4, 1, 4>(pm::PmPart const*, unsigned long const*, "
                         "unsigned long const*, unsigned int, unsigned int, unsigned int, unsigned int)",
            "answer": "void pm::k_answer<2>(pm::PmStep)", "step": "void pm::k_step<2>(pm::PmStep)", "resolve": "void pm::k_resolve<true>(pm::PmStep)",
-           "hint_match": "pm::k_match(pm::PmStep)", "prep_offsets": "pm::k_prep_offsets(pm::PmPart const*)"}
+           "hint_match": "pm::k_match(pm::PmStep)", "prep_offsets": "pm::k_prep_offsets(pm::PmPart const*)",
+           "gather": "void pm::k_gather<2>(pm::PmStep)"}
 HOST = ["host_search_knn", "host_knn_init", "host_knn_final", "host_knn_batch", "host_knn_update",
         "host_gvi_parse", "host_batch_query", "host_step_launch", "host_step_wait", "host_step_post",
         "host_wait_first_token", "host_wait_all_tokens"]
@@ -430,8 +437,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--sessions", type=int, default=SESSIONS,
-                    help="client sessions served concurrently per GPU (one host thread + stream each)")
+    ap.add_argument("--sessions", type=int, default=SESSIONS, help="client sessions served per GPU")
+    ap.add_argument("--mode", choices=["batched", "concurrent"], default="batched",
+                    help="batched: lock-step groups sharing one step per round (default); "
+                         "concurrent: one host thread + stream + own steps per session")
+    ap.add_argument("--groups", type=int, default=GROUPS, help="lock-step groups (batched mode)")
+    ap.add_argument("--threads", type=int, default=THREADS, help="host worker threads (batched mode)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-config2", action="store_true", help="skip the MS-MARCO-shaped batch-PIR block")
     ap.add_argument("--no-single", action="store_true", help="skip the one-client latency block")
@@ -461,8 +472,13 @@ def main():
     for s_ in sess[1:]:
         s_.Preprocess()
     ctxs = [s_.ctx for s_ in sess]
+
+    def serve(qq):
+        if args.mode == "batched":
+            return pm.search_loop_batched(sess, qq, K_TOP, STEP, PARALLEL, args.groups, args.threads)
+        return pm.search_loop_sessions(sess, qq, K_TOP, STEP, PARALLEL)
     if args.warmup:
-        pm.search_loop_sessions(sess, qsess[:, :args.warmup], K_TOP, STEP, PARALLEL)
+        serve(qsess[:, :args.warmup])
 
     for c in ctxs:
         c.timing_reset()
@@ -472,8 +488,7 @@ def main():
     for c in ctxs:
         c.sync()
     t0 = time.perf_counter()
-    answers, _, online, maint = pm.search_loop_sessions(sess, qsess[:, args.warmup:args.warmup + args.steps],
-                                                        K_TOP, STEP, PARALLEL)
+    answers, _, online, maint = serve(qsess[:, args.warmup:args.warmup + args.steps])
     for c in ctxs:
         c.sync()
     if dist:
@@ -496,7 +511,7 @@ def main():
         c.timing_reset()
         c.timing(2)
     w0 = args.warmup + args.steps
-    pm.search_loop_sessions(sess, qsess[:, w0:w0 + PROFILE_QUERIES], K_TOP, STEP, PARALLEL)
+    serve(qsess[:, w0:w0 + PROFILE_QUERIES])
     for c in ctxs:
         c.timing(False)
     for k in STEP_KERNELS:
@@ -558,7 +573,10 @@ def main():
         if n == 0 or ms == 0 or by == 0:
             return None
         ach = (by / n) / (ms / n / 1e3) / 1e9
-        tr = pmc_traffic(SYMBOLS.get(name, name))
+        grid = None
+        if name == "answer" and args.mode == "batched":   # the PMC summary by launch shape: 512-thread WG per sub-query
+            grid = (S // max(1, args.groups)) * PARALLEL * M * 512
+        tr = pmc_traffic(SYMBOLS.get(name, name), grid)
         r = {"bound": "hbm", "kernel": name, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
              "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
              "traffic": tr[0] if tr else None, "traffic_source": tr[1] if tr else None,
@@ -586,13 +604,17 @@ def main():
         note = ("k_step runs hint match, resolution and answer of a batch-PIR step in one launch; "
                 "bytes are the answer's (SURVEY.md §8d: SS*E*8 + 4*SS + 8*E per real/dummy sub-query); "
                 f"avg_ms is per launch with {S} sessions' steps in flight together")
-    elif dom not in ("answer", "prep_fold"):
-        note = (f"dominant kernel by device time is {dom}, a latency-bound sequential chain with no "
-                f"§8(d) byte figure; the roofline shown is the PIR answer kernel's")
+    elif dom == "answer":
+        note = (f"k_answer of the shared step of {S // max(1, args.groups)} lock-step sessions (set expansion, "
+                "XOR gather, decode, refresh, L2); bytes per SURVEY.md §8d: SS*E*8 + 4*SS + 8*E per sub-query")
+    elif dom != "prep_fold":
+        note = (f"dominant kernel by device time is {dom}, which has no §8(d) byte figure; "
+                f"the roofline shown is the PIR answer kernel's")
     main_roof = roof(dom, note) if dom in ("answer", "prep_fold", "step") else roof("answer", note)
-    if main_roof and dom == "step":
+    ans_k = "step" if args.mode == "concurrent" else "answer"
+    if main_roof and main_roof["kernel"] == ans_k:
         # all sessions' answer bytes over the timed region's wall time (the GPU-wide PIR-scan rate)
-        agg = ktime["step"][2] / elapsed / 1e9
+        agg = ktime[ans_k][2] / elapsed / 1e9
         main_roof["aggregate"] = {"achieved": round(agg, 1), "frac": round(agg / HBM_PEAK_GBS, 4),
                                   "note": "answer bytes of every step in the timed region / its wall time"}
     out = {
@@ -604,7 +626,8 @@ def main():
                     else "degree-32 graph built on the GPU (exact kNN candidates + robustPrune, alpha 1.2)")),
         "config": {"workload": "SIFT1M-shaped private graph search over 16-partition batch PianoPIR",
                    "n": N, "dim": DIM, "m": M, "k": K_TOP, "step": STEP, "parallel": PARALLEL,
-                   "batch_size": M, "failure_prob_log2": F, "sessions_per_gpu": S,
+                   "batch_size": M, "failure_prob_log2": F, "sessions_per_gpu": S, "serving": args.mode,
+                   "lockstep_groups": args.groups if args.mode == "batched" else None,
                    "parallelism": f"replicas{ws}"},
         "roofline": main_roof,
         "roofline_prep": fold,

@@ -215,12 +215,15 @@ int  pm_search_loop_sessions(pm_graph** sessions, uint32_t S, const float* queri
  * session keeps its own keys, hint state, cache, counters, search and
  * maintenance (private-search.go:216-240), and gets exactly the answers it
  * would get alone.  Sessions: clients of one server DB on one device (base +
- * pm_graph_create_session), distinct contexts.  nthreads host workers (0:
- * min(S, 16)) run the sessions' searches between the shared steps.  Outputs
- * as pm_search_loop_sessions; online_s[i] = wall_s - maintenance_s[i]. */
+ * pm_graph_create_session), distinct contexts.  ngroups (0: 1) lock-step
+ * groups of consecutive sessions run concurrently, each with its own shared
+ * steps on its first session's stream, so one group's step overlaps the
+ * others' host work; nthreads host workers in all (0: min(S, 16)) run the
+ * sessions' searches between the steps.  Outputs as pm_search_loop_sessions;
+ * online_s[i] = wall_s - maintenance_s[i]. */
 int  pm_search_loop_batched(pm_graph** sessions, uint32_t S, const float* queries, uint64_t q, int k, int step,
-                            int parallel, uint32_t nthreads, int64_t* answers, double* wall_s, double* online_s,
-                            double* maintenance_s);
+                            int parallel, uint32_t ngroups, uint32_t nthreads, int64_t* answers, double* wall_s,
+                            double* online_s, double* maintenance_s);
 pm_batchpir* pm_graph_pir(pm_graph* g);
 
 /* ---- graph construction + ground truth (graphann/build_graph.go) ------- */

@@ -109,7 +109,7 @@ SIGNATURES = {
     "pm_search_loop_sessions": (C.c_int, [C.POINTER(vp), C.c_uint32, f32p, u64, C.c_int, C.c_int, C.c_int,
                                           i64p, C.POINTER(dbl), C.POINTER(dbl), C.POINTER(dbl)]),
     "pm_search_loop_batched": (C.c_int, [C.POINTER(vp), C.c_uint32, f32p, u64, C.c_int, C.c_int, C.c_int, C.c_uint32,
-                                         i64p, C.POINTER(dbl), C.POINTER(dbl), C.POINTER(dbl)]),
+                                         C.c_uint32, i64p, C.POINTER(dbl), C.POINTER(dbl), C.POINTER(dbl)]),
 }
 
 Q_OK, Q_EBUDGET, Q_ECHUNK, Q_ENOHIT, Q_ERANGE = range(5)
@@ -567,9 +567,10 @@ def search_loop_sessions(sessions, queries, k: int, step: int, parallel: int):
     return ans, wall.value, on, mt
 
 
-def search_loop_batched(sessions, queries, k: int, step: int, parallel: int, nthreads: int = 0):
-    """Serve len(sessions) client sessions in lock-step, every round of all of
-    them one shared batch-PIR step (pm_search_loop_batched): queries [S, q, dim].
+def search_loop_batched(sessions, queries, k: int, step: int, parallel: int, ngroups: int = 1, nthreads: int = 0):
+    """Serve len(sessions) client sessions in `ngroups` concurrent lock-step
+    groups, every round of a group's sessions one shared batch-PIR step
+    (pm_search_loop_batched): queries [S, q, dim].
     Returns (answers [S, q, k], wall_s, online_s[S], maint_s[S])."""
     S = len(sessions)
     qs = np.ascontiguousarray(queries, dtype=np.float32)
@@ -581,7 +582,7 @@ def search_loop_batched(sessions, queries, k: int, step: int, parallel: int, nth
     wall = C.c_double()
     on = np.zeros(S, dtype=np.float64)
     mt = np.zeros(S, dtype=np.float64)
-    _check(lib().pm_search_loop_batched(hs, S, _p(qs, f32p), q, k, step, parallel, nthreads, _p(ans, i64p),
+    _check(lib().pm_search_loop_batched(hs, S, _p(qs, f32p), q, k, step, parallel, ngroups, nthreads, _p(ans, i64p),
                                         C.byref(wall), on.ctypes.data_as(C.POINTER(dbl)),
                                         mt.ctypes.data_as(C.POINTER(dbl))))
     return ans, wall.value, on, mt

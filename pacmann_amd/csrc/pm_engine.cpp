@@ -504,12 +504,13 @@ static int upload_parts(Engine* g) {
 
 // Client.Preprocessing (pir.go:267-301) for partitions [p0, p1): Initialization
 // (new key, reset state) then, unless skipPrep, the full hint fold.
-static int engine_prep(Engine* g, uint64_t p0, uint64_t p1) {
-  pm_ctx* c = g->ctx;
-  hipStream_t st = c->stream;
+// Client.Initialization's host side for the owned partitions in [p0, p1)
+// (pir.go:203-255: new key from the next epoch, reset counters and cache);
+// uploads the parts.  Fills `todo` with the partitions to fold.
+static int engine_prep_host(Engine* g, uint64_t p0, uint64_t p1, std::vector<uint64_t>& todo) {
   // the owned partitions in [p0, p1): all of them (owned_d) or a single one
   if (p1 - p0 > 1 && !(p0 == 0 && p1 == g->P)) return fail(PM_EINVAL, "engine_prep: unsupported range");
-  std::vector<uint64_t> todo;
+  todo.clear();
   for (uint64_t i = p0; i < p1; ++i)
     if (g->parts[i].owned) todo.push_back(i);
   if (todo.empty()) return 0;
@@ -525,12 +526,17 @@ static int engine_prep(Engine* g, uint64_t p0, uint64_t p1) {
   }
   CHK(upload_parts(g));
   g->prep_gen++;
-  const PmPart* dp = p1 - p0 == 1 ? g->parts_d.as<PmPart>() + p0 : g->owned_d.as<PmPart>();
-  const int np = (int)todo.size();
+  return 0;
+}
+// The device side for np parts at dp (of one engine, or of several clients of
+// one server: same parameters and DB): PRF tables, then the hint fold and
+// the replacement rows, or zero hints for DummyPreprocessing.  Synchronous.
+static int engine_prep_launch(pm_ctx* c, const Engine* g, const PmPart* dp, int np, const PmPart* host_parts) {
+  hipStream_t st = c->stream;
   c->timed("prep_init", 0, [&] { pmk::prep_init(st, dp, np, g->maxH, g->maxRepl, (uint32_t)g->E, g->skipPrep); });
   double aes = 0, fold = 0, repl = 0;
-  for (uint64_t i : todo) {
-    const PmPart& d = g->parts[i].d;
+  for (int i = 0; i < np; ++i) {
+    const PmPart& d = host_parts[i];
     aes += (double)d.H * d.SS;
     // algorithmic fold bytes: hpc * SS (hint, chunk) pairs of one E-word entry
     fold += ((double)d.PH + (double)(d.SS - 1) * d.Qpc) * d.SS * (double)g->E * 8;
@@ -539,8 +545,8 @@ static int engine_prep(Engine* g, uint64_t p0, uint64_t p1) {
   // the PRF table is built even by DummyPreprocessing: queries still evaluate the PRF
   c->timed("prep_offsets", aes, [&] { pmk::prep_offsets(st, dp, np, g->maxH, g->maxSS); });
   if (g->skipPrep) {   // DummyPreprocessing (pir.go:520-523): zero hints
-    for (uint64_t i : todo) {
-      const PmPart& d = g->parts[i].d;
+    for (int i = 0; i < np; ++i) {
+      const PmPart& d = host_parts[i];
       HIPCHK(hipMemsetAsync(d.parity, 0, (uint64_t)d.H * g->E * 8, st));
       HIPCHK(hipMemsetAsync(d.rval, 0, (uint64_t)d.SS * d.Qpc * g->E * 8, st));
     }
@@ -552,6 +558,15 @@ static int engine_prep(Engine* g, uint64_t p0, uint64_t p1) {
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(st));
   return 0;
+}
+static int engine_prep(Engine* g, uint64_t p0, uint64_t p1) {
+  std::vector<uint64_t> todo;
+  CHK(engine_prep_host(g, p0, p1, todo));
+  if (todo.empty()) return 0;
+  const PmPart* dp = p1 - p0 == 1 ? g->parts_d.as<PmPart>() + p0 : g->owned_d.as<PmPart>();
+  std::vector<PmPart> hp;
+  for (uint64_t i : todo) hp.push_back(g->parts[i].d);
+  return engine_prep_launch(g->ctx, g, dp, (int)todo.size(), hp.data());
 }
 
 // One batched step over the sub-queries in g->subs (partition-major, ranges in
@@ -1802,7 +1817,7 @@ struct SpinBarrier {
 struct StepGroup {
   pm_ctx* c = nullptr;   // the shared steps' stream
   uint32_t S = 0, P = 0, maxPH = 0, maxSS = 0, E = 0, dim = 0;
-  DevBuf parts_d, subs_d, sb_d, bits, cand, meta, spec, res_d, ans, part_x, done;
+  DevBuf parts_d, subs_d, sb_d, bits, cand, meta, spec, res_d, ans, part_x, done, prep_parts;
   HostBuf desc_h, out_h;
   uint32_t token = 0;
   std::vector<PmSub> subs;
@@ -1929,20 +1944,45 @@ static int group_step(StepGroup& G, pm_graph** gs, const std::vector<char>& in) 
   return 0;
 }
 
-extern "C" int pm_search_loop_batched(pm_graph** gs, uint32_t S, const float* queries, uint64_t q, int k, int step,
-                                      int parallel, uint32_t nthreads, int64_t* answers, double* wall_s,
-                                      double* online_s, double* maint_s) {
-  if (!gs || !S || (!queries && q) || (!answers && q)) return fail(PM_EINVAL, "NULL argument");
-  for (uint32_t i = 0; i < S; ++i) {
-    if (!gs[i] || !gs[i]->pir || gs[i]->nonprivate) return fail(PM_EINVAL, "sessions must be preprocessed private graphs");
-    const Engine& a = gs[0]->pir->e;
-    const Engine& b = gs[i]->pir->e;
-    if (a.db.get() != b.db.get() || a.P != b.P || a.E != b.E || gs[i]->dim != gs[0]->dim || gs[i]->m != gs[0]->m ||
-        b.nshards != 1 || gs[i]->ctx->device != gs[0]->ctx->device)
-      return fail(PM_EINVAL, "batched sessions must be clients of one server DB on one device");
-    for (uint32_t j = 0; j < i; ++j)
-      if (gs[j] == gs[i] || gs[j]->ctx == gs[i]->ctx) return fail(PM_EINVAL, "sessions need distinct graphs and contexts");
+// SimpleBatchPianoPIR.Preprocessing (batch-pir.go:119-155) of every client
+// with need[s], as ONE launch set over all their partitions on the team's
+// stream (the clients share the server DB and parameters).  Each client's
+// maintenance time is the set's wall time.
+static int group_prep(StepGroup& G, pm_graph** gs, const std::vector<char>& need, std::vector<double>& mt) {
+  std::vector<uint32_t> who;
+  for (uint32_t s = 0; s < G.S; ++s)
+    if (need[s]) who.push_back(s);
+  if (who.empty()) return 0;
+  auto t0 = Clock::now();
+  std::vector<PmPart> hp;
+  std::vector<uint64_t> todo;
+  for (uint32_t s : who) {
+    Engine* e = &gs[s]->pir->e;
+    e->FBN = 0; e->QMIP = 0;
+    CHK(engine_prep_host(e, 0, e->P, todo));
+    for (uint64_t i : todo) hp.push_back(e->parts[i].d);
   }
+  const Engine* e0 = &gs[who[0]]->pir->e;
+  bool skip = false;
+  for (uint32_t s : who) skip |= gs[s]->pir->e.skipPrep != e0->skipPrep;
+  if (skip) return fail(PM_EINVAL, "batched sessions mix Preprocessing and DummyPreprocessing");
+  CHK(G.prep_parts.reserve(hp.size() * sizeof(PmPart)));
+  HIPCHK(hipMemcpyAsync(G.prep_parts.p, hp.data(), hp.size() * sizeof(PmPart), hipMemcpyHostToDevice, G.c->stream));
+  CHK(engine_prep_launch(G.c, e0, G.prep_parts.as<PmPart>(), (int)hp.size(), hp.data()));
+  const double t = std::chrono::duration<double>(Clock::now() - t0).count();
+  for (uint32_t s : who) {
+    Engine* e = &gs[s]->pir->e;
+    e->prepCount++;
+    record_stats(e, t);
+    mt[s] += t;
+  }
+  return 0;
+}
+
+// One lock-step team: sessions gs[0..S) share one step stream (gs[0]'s) and T
+// worker threads; maintenance seconds into mt[0..S).  Runs on the calling thread.
+static int run_batched_team(pm_graph** gs, uint32_t S, const float* queries, uint64_t q, int k, int step,
+                            int parallel, uint32_t T, int64_t* answers, double* mt_out) {
   StepGroup G;
   G.c = gs[0]->ctx;
   G.S = S;
@@ -1959,8 +1999,8 @@ extern "C" int pm_search_loop_batched(pm_graph** gs, uint32_t S, const float* qu
   }
   for (uint32_t i = 0; i < S; ++i) HIPCHK(hipStreamSynchronize(gs[i]->ctx->stream));
   CHK(group_upload_parts(G, gs));
-  const uint32_t T = std::max(1u, std::min<uint32_t>(nthreads ? nthreads : 16u, S));
-  std::vector<char> fast(S, 0);
+  T = std::max(1u, std::min(T, S));
+  std::vector<char> fast(S, 0), need_prep(S, 0);
   std::vector<double> mt(S, 0.0);
   std::atomic<int> err{0};
   std::string err_msg;
@@ -2023,27 +2063,73 @@ extern "C" int pm_search_loop_batched(pm_graph** gs, uint32_t S, const float* qu
           knn_update(g, st);
         }
       }
-      for (uint32_t s = w; s < S && !err.load(); s += T) {   // top k, maintenance (private-search.go:226-232)
+      for (uint32_t s = w; s < S && !err.load(); s += T) {   // top k, maintenance trigger (private-search.go:226-232)
         pm_graph* g = gs[s];
         knn_end(g, k, answers + ((uint64_t)s * q + qi) * k, stp);
         Engine* e = &g->pir->e;
-        if (e->FBN + (uint64_t)step * (uint64_t)parallel + 10 >= e->Support) {
-          auto a = Clock::now();
-          const int rc = batch_prep(e);
-          if (rc) { set_err(rc, s); break; }
-          mt[s] += std::chrono::duration<double>(Clock::now() - a).count();
-        }
+        need_prep[s] = e->FBN + (uint64_t)step * (uint64_t)parallel + 10 >= e->Support;
       }
+      bar.wait();
+      if (w == 0) {   // the triggered clients' preprocessings as one launch set
+        if (!err.load()) {
+          const int rc = group_prep(G, gs, need_prep, mt);
+          if (rc) set_err(rc, 0);
+        }
+        stop.store(err.load() != 0);
+      }
+      bar.wait();
+      if (stop.load()) return;
     }
   };
   std::vector<std::thread> th;
-  auto t0 = Clock::now();
   for (uint32_t w = 1; w < T; ++w) th.emplace_back(worker, w);
   worker(0);
   for (auto& t : th) t.join();
-  const double wall = std::chrono::duration<double>(Clock::now() - t0).count();
   if (err.load()) return fail(err.load(), err_msg);
   HIPCHK(hipStreamSynchronize(G.c->stream));
+  for (uint32_t s = 0; s < S; ++s) mt_out[s] = mt[s];
+  return 0;
+}
+
+extern "C" int pm_search_loop_batched(pm_graph** gs, uint32_t S, const float* queries, uint64_t q, int k, int step,
+                                      int parallel, uint32_t ngroups, uint32_t nthreads, int64_t* answers,
+                                      double* wall_s, double* online_s, double* maint_s) {
+  if (!gs || !S || (!queries && q) || (!answers && q)) return fail(PM_EINVAL, "NULL argument");
+  for (uint32_t i = 0; i < S; ++i) {
+    if (!gs[i] || !gs[i]->pir || gs[i]->nonprivate) return fail(PM_EINVAL, "sessions must be preprocessed private graphs");
+    const Engine& a = gs[0]->pir->e;
+    const Engine& b = gs[i]->pir->e;
+    if (a.db.get() != b.db.get() || a.P != b.P || a.E != b.E || gs[i]->dim != gs[0]->dim || gs[i]->m != gs[0]->m ||
+        b.nshards != 1 || gs[i]->ctx->device != gs[0]->ctx->device)
+      return fail(PM_EINVAL, "batched sessions must be clients of one server DB on one device");
+    for (uint32_t j = 0; j < i; ++j)
+      if (gs[j] == gs[i] || gs[j]->ctx == gs[i]->ctx) return fail(PM_EINVAL, "sessions need distinct graphs and contexts");
+  }
+  // teams: sessions split into `ngroups` lock-step groups with their own step
+  // streams, run concurrently (one group's shared step on the GPU while the
+  // others' searches run on the host); threads split evenly
+  const uint32_t NG = std::max(1u, std::min(ngroups ? ngroups : 1u, S));
+  const uint32_t TT = std::max(NG, nthreads ? nthreads : std::min<uint32_t>(S, 16u));
+  std::vector<double> mt(S, 0.0);
+  std::vector<int> rc(NG, 0);
+  std::vector<std::string> msg(NG);
+  std::vector<std::thread> teams;
+  const float* qbase = queries;
+  auto t0 = Clock::now();
+  for (uint32_t g = 0; g < NG; ++g) {
+    const uint32_t s0 = (uint32_t)((uint64_t)S * g / NG), s1 = (uint32_t)((uint64_t)S * (g + 1) / NG);
+    const uint32_t Tg = std::max(1u, std::min(s1 - s0, (uint32_t)((uint64_t)TT * (g + 1) / NG - (uint64_t)TT * g / NG)));
+    teams.emplace_back([&, g, s0, s1, Tg] {
+      if (hipSetDevice(gs[0]->ctx->device) != hipSuccess) { rc[g] = PM_EHIP; msg[g] = "hipSetDevice"; return; }
+      rc[g] = run_batched_team(gs + s0, s1 - s0, qbase + (uint64_t)s0 * q * gs[0]->dim, q, k, step, parallel, Tg,
+                               answers + (uint64_t)s0 * q * (uint64_t)k, mt.data() + s0);
+      if (rc[g]) msg[g] = pm_last_error();
+    });
+  }
+  for (auto& t : teams) t.join();
+  const double wall = std::chrono::duration<double>(Clock::now() - t0).count();
+  for (uint32_t g = 0; g < NG; ++g)
+    if (rc[g]) return fail(rc[g], "group " + std::to_string(g) + ": " + msg[g]);
   if (wall_s) *wall_s = wall;
   for (uint32_t s = 0; s < S; ++s) {
     if (online_s) online_s[s] = wall - mt[s];

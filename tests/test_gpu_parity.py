@@ -434,8 +434,8 @@ def test_search_sessions_concurrent(ctx, oracle):
         assert sess[i].PIR.stats()["PrepCount"] == o.pir().stats()["PrepCount"] > 1, i
 
 
-@pytest.mark.parametrize("nthreads", [0, 2])
-def test_search_sessions_batched(ctx, oracle, nthreads):
+@pytest.mark.parametrize("ngroups,nthreads", [(1, 0), (1, 2), (2, 3)])
+def test_search_sessions_batched(ctx, oracle, ngroups, nthreads):
     """pm_search_loop_batched: five sessions in lock-step, every round of all
     of them one shared step over 5 x 16 partitions; each session's answers,
     PIR counters and maintenance count equal an independent oracle run with
@@ -450,7 +450,7 @@ def test_search_sessions_batched(ctx, oracle, nthreads):
         s.Preprocess()
     rng = np.random.default_rng(5)
     qs = np.stack([v[rng.integers(0, len(v), size=30)] + np.float32(1.0) for _ in seeds])
-    ans, wall, on, mt = pm.search_loop_batched(sess, qs, 10, 20, 3, nthreads)
+    ans, wall, on, mt = pm.search_loop_batched(sess, qs, 10, 20, 3, ngroups, nthreads)
     assert wall > 0 and (on > 0).all() and (mt > 0).all()
     for i, (p, s) in enumerate(seeds):
         o = oracle.Graph(v, graph, pir_seed=p, search_seed=s)
