@@ -9,7 +9,7 @@ private-search.go harness (run-private-search.sh flags).  Data are synthetic
 (no dataset in the image): a clustered SIFT-like mixture with integer values in
 [0,255] and a uniform random degree-32 graph (private-search.go:54-69).
 
-Serving: one GPU serves S client sessions at once (--sessions, default 64).
+Serving: one GPU serves S client sessions at once (--sessions, default 128).
 Every session is a full PianoPIR client (own keys, hint state, cache,
 maintenance) over the one server DB on the device.  Default (--mode batched,
 pm_search_loop_batched): the sessions run in G lock-step groups (--groups,
@@ -50,7 +50,7 @@ PREP_KERNELS = ["prep_offsets", "prep_fold", "prep_repl", "l2_rows"]   # timed i
 STEP_KERNELS = ["step", "hint_match", "resolve", "gather", "answer"]   # timed in the profile window
 KERNELS = PREP_KERNELS + STEP_KERNELS
 PROFILE_QUERIES = 8
-SESSIONS = 64   # client sessions per GPU
+SESSIONS = 128  # client sessions per GPU
 GROUPS = 4      # lock-step groups (GPU_MAX_HW_QUEUES = 4 hardware queues per process)
 THREADS = 8     # host worker threads of the batched loop
 SYMBOLS = {"prep_fold": "void pm::k_prep_fold_pipe<4, 1, 4>(pm::PmPart const*, unsigned long const*, "
