@@ -1375,6 +1375,8 @@ struct pm_graph {
   std::shared_ptr<DevBuf> dvec = std::make_shared<DevBuf>();
   pm_batchpir* server = nullptr;   // sessions: the base's batch PIR whose server DB they share
   DevBuf dq, dids, ddist;
+  float* q_shared = nullptr;   // batched serving: this session's query slot in its group's buffer
+  float* qdev() { return q_shared ? q_shared : dq.as<float>(); }
   HostBuf stage_h;                                // pinned: query and start-vertex distances
   pm_batchpir* pir = nullptr;
   std::vector<uint64_t> start;   // StartVertices ids
@@ -1519,7 +1521,7 @@ static int gvi_nonprivate(pm_graph* g, bool with_q) {
     CHK(g->dids.reserve(n * 4)); CHK(g->ddist.reserve(n * 4));
     HIPCHK(hipMemcpyAsync(g->dids.p, u.data(), n * 4, hipMemcpyHostToDevice, st));
     g->ctx->timed("l2_rows", (double)n * g->dim * 4, [&] {
-      pmk::l2_rows(st, g->dvec->as<float>(), g->dim, n, g->dids.as<uint32_t>(), g->dq.as<float>(), (uint32_t)g->dim, g->ddist.as<float>());
+      pmk::l2_rows(st, g->dvec->as<float>(), g->dim, n, g->dids.as<uint32_t>(), g->qdev(), (uint32_t)g->dim, g->ddist.as<float>());
     });
     HIPCHK(hipMemcpyAsync(g->dist.data(), g->ddist.p, n * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -1546,7 +1548,7 @@ static int gvi_pre(pm_graph* g, bool with_q, bool* fast) {
   auto t = Clock::now();
   CHK(bq_prepare(e, g->qids.data(), n, fast));
   if (!*fast)   // a partition at its query budget: the general path, served now
-    CHK(batch_query_impl(e, g->qids.data(), n, nullptr, with_q ? g->dq.as<float>() : nullptr, (uint32_t)g->dim,
+    CHK(batch_query_impl(e, g->qids.data(), n, nullptr, with_q ? g->qdev() : nullptr, (uint32_t)g->dim,
                          with_q ? g->dist.data() : nullptr, g->rowp.data(), nullptr));
   e->ctx->host_add(HT_BATCH_QUERY, ms_since(t));
   return 0;
@@ -1581,7 +1583,7 @@ static int get_vertex_info(pm_graph* g, bool with_q) {
   if (fast) {
     Engine* e = &g->pir->e;
     auto t = Clock::now();
-    CHK(engine_step(e, with_q ? g->dq.as<float>() : nullptr, (uint32_t)g->dim));
+    CHK(engine_step(e, with_q ? g->qdev() : nullptr, (uint32_t)g->dim));
     e->ctx->host_add(HT_BATCH_QUERY, ms_since(t));
   }
   return gvi_post(g, with_q, fast);
@@ -1616,12 +1618,15 @@ static void knn_add_known(pm_graph* g, int64_t id, const uint32_t* nb, float d, 
 }
 // first half: reset + enqueue the start-set distances (async on the session's
 // stream); knn_begin_finish completes it after the stream is synchronised
-static int knn_begin_enqueue(pm_graph* g, const float* query, int benchmarking) {
-  if (!g->pir && !g->nonprivate) return fail(PM_EINVAL, "pm_graph_preprocess not called");
-  hipStream_t st = g->ctx->stream;
+static void knn_reset(pm_graph* g) {
   g->known.clear();
   g->known_nb.clear(); g->known_dist.clear(); g->known_id.clear(); g->known_reach.clear();
   g->heap.clear();
+}
+static int knn_begin_enqueue(pm_graph* g, const float* query, int benchmarking) {
+  if (!g->pir && !g->nonprivate) return fail(PM_EINVAL, "pm_graph_preprocess not called");
+  hipStream_t st = g->ctx->stream;
+  knn_reset(g);
   if (benchmarking) return 0;
   g->t_init = Clock::now();
   // the query stays resident for every distance this search computes; it and
@@ -1640,10 +1645,11 @@ static int knn_begin_enqueue(pm_graph* g, const float* query, int benchmarking) 
   }
   return 0;
 }
-static void knn_begin_finish(pm_graph* g, int parallel, int benchmarking) {
+// sdh: the start set's distances (null: where knn_begin_enqueue put them)
+static void knn_begin_finish(pm_graph* g, int parallel, int benchmarking, const float* sdh = nullptr) {
   if (benchmarking) return;
   const uint64_t ns = g->start.size(), m = g->m;
-  const float* sdh = g->stage_h.as<float>() + g->dim;
+  if (!sdh) sdh = g->stage_h.as<float>() + g->dim;
   // the first `parallel` start vertices in stable distance order (search.go:130-146):
   // a partial sort on (dist, position) selects exactly those
   g->fs.clear();
@@ -1823,6 +1829,10 @@ struct StepGroup {
   std::vector<PmSub> subs;
   std::vector<uint32_t> sb, base;
   std::vector<uint64_t> gen;   // each session's Engine::prep_gen at the last upload of its parts
+  // the sessions' queries and start sets, scored in ONE k_l2_rows launch per query
+  uint32_t ns = 0;
+  DevBuf qbuf, start_ids, start_dist;
+  HostBuf qstage;   // [S][dim] queries, then [S][ns] start-set distances
 };
 
 static int group_upload_parts(StepGroup& G, pm_graph** gs) {
@@ -1832,7 +1842,7 @@ static int group_upload_parts(StepGroup& G, pm_graph** gs) {
     Engine* e = &gs[s]->pir->e;
     for (uint32_t p = 0; p < G.P; ++p) {
       PmPart d = e->parts[p].d;
-      d.qv = gs[s]->dq.as<float>();
+      d.qv = gs[s]->qdev();
       v.push_back(d);
     }
   }
@@ -1944,6 +1954,24 @@ static int group_step(StepGroup& G, pm_graph** gs, const std::vector<char>& in) 
   return 0;
 }
 
+// The team's queries (staged in G.qstage) to the device and every session's
+// start-set distances (search.go:130-146) in one k_l2_rows launch.
+static int group_start_dist(StepGroup& G, pm_graph** gs) {
+  hipStream_t st = G.c->stream;
+  float* qst = G.qstage.as<float>();
+  HIPCHK(hipMemcpyAsync(G.qbuf.p, qst, (uint64_t)G.S * G.dim * 4, hipMemcpyHostToDevice, st));
+  const uint64_t nrows = (uint64_t)G.S * G.ns;
+  if (nrows) {
+    G.c->timed("l2_rows", (double)nrows * G.dim * 4, [&] {
+      pmk::l2_rows(st, gs[0]->dvec->as<float>(), G.dim, nrows, G.start_ids.as<uint32_t>(), G.qbuf.as<float>(),
+                   G.dim, G.start_dist.as<float>(), G.ns);
+    });
+    HIPCHK(hipMemcpyAsync(qst + (uint64_t)G.S * G.dim, G.start_dist.p, nrows * 4, hipMemcpyDeviceToHost, st));
+  }
+  HIPCHK(hipStreamSynchronize(st));
+  return 0;
+}
+
 // SimpleBatchPianoPIR.Preprocessing (batch-pir.go:119-155) of every client
 // with need[s], as ONE launch set over all their partitions on the team's
 // stream (the clients share the server DB and parameters).  Each client's
@@ -1998,6 +2026,23 @@ static int run_batched_team(pm_graph** gs, uint32_t S, const float* queries, uin
     HIPCHK(hipMemcpy(G.done.p, init, sizeof init, hipMemcpyHostToDevice));
   }
   for (uint32_t i = 0; i < S; ++i) HIPCHK(hipStreamSynchronize(gs[i]->ctx->stream));
+  G.ns = (uint32_t)gs[0]->start.size();
+  for (uint32_t i = 0; i < S; ++i)
+    if (gs[i]->start.size() != G.ns) return fail(PM_EINVAL, "sessions with different start-set sizes");
+  CHK(G.qbuf.reserve((uint64_t)S * G.dim * 4));
+  CHK(G.start_ids.reserve(std::max<uint64_t>(4, (uint64_t)S * G.ns * 4)));
+  CHK(G.start_dist.reserve(std::max<uint64_t>(4, (uint64_t)S * G.ns * 4)));
+  CHK(G.qstage.reserve((uint64_t)S * (G.dim + G.ns) * 4));
+  {
+    std::vector<uint32_t> ids;
+    for (uint32_t i = 0; i < S; ++i) ids.insert(ids.end(), gs[i]->start.begin(), gs[i]->start.end());
+    if (!ids.empty()) HIPCHK(hipMemcpy(G.start_ids.p, ids.data(), ids.size() * 4, hipMemcpyHostToDevice));
+  }
+  struct Unshare {   // the sessions' query pointers point into G.qbuf until the team ends
+    pm_graph** gs; uint32_t S;
+    ~Unshare() { for (uint32_t i = 0; i < S; ++i) gs[i]->q_shared = nullptr; }
+  } unshare{gs, S};
+  for (uint32_t i = 0; i < S; ++i) gs[i]->q_shared = G.qbuf.as<float>() + (uint64_t)i * G.dim;
   CHK(group_upload_parts(G, gs));
   T = std::max(1u, std::min(T, S));
   std::vector<char> fast(S, 0), need_prep(S, 0);
@@ -2017,13 +2062,23 @@ static int run_batched_team(pm_graph** gs, uint32_t S, const float* queries, uin
     if (hipSetDevice(G.c->device) != hipSuccess) set_err(PM_EHIP, w);
     int64_t* stp = &steps_buf[(size_t)w * std::max(k, 1)];
     for (uint64_t qi = 0; qi < q; ++qi) {
-      for (uint32_t s = w; s < S && !err.load(); s += T) {   // SearchKNN begin (start set, heap)
+      // SearchKNN begin: every session's query and start-set distances in one
+      // upload, one k_l2_rows launch and one download for the team
+      float* qst = G.qstage.as<float>();
+      for (uint32_t s = w; s < S; s += T) {
         pm_graph* g = gs[s];
-        int rc = knn_begin_enqueue(g, queries + ((uint64_t)s * q + qi) * g->dim, 0);
-        if (!rc && hipStreamSynchronize(g->ctx->stream) != hipSuccess) rc = fail(PM_EHIP, "start-set distances");
-        if (rc) { set_err(rc, s); break; }
-        knn_begin_finish(g, parallel, 0);
+        knn_reset(g);
+        g->t_init = Clock::now();
+        memcpy(qst + (uint64_t)s * G.dim, queries + ((uint64_t)s * q + qi) * g->dim, G.dim * 4);
       }
+      bar.wait();
+      if (w == 0 && !err.load()) {
+        const int rc = group_start_dist(G, gs);
+        if (rc) set_err(rc, 0);
+      }
+      bar.wait();
+      for (uint32_t s = w; s < S && !err.load(); s += T)
+        knn_begin_finish(gs[s], parallel, 0, qst + (uint64_t)S * G.dim + (uint64_t)s * G.ns);
       for (int st = 0; st < step; ++st) {
         for (uint32_t s = w; s < S && !err.load(); s += T) {   // this round's ids -> sub-queries
           pm_graph* g = gs[s];

@@ -190,7 +190,7 @@ uint32_t step_max_e();
 void server_answer(hipStream_t st, const PmPart* dpart, const uint32_t* offs, uint32_t nq,
                    uint32_t SS, const uint64_t* db, uint32_t E, uint64_t* out);
 void l2_rows(hipStream_t st, const float* rows, uint64_t row_stride_floats, uint64_t nrows,
-             const uint32_t* row_ids, const float* q, uint32_t dim, float* out);
+             const uint32_t* row_ids, const float* q, uint32_t dim, float* out, uint64_t seglen = 0);
 void ip_rows(hipStream_t st, const uint32_t* rows, uint64_t nrows, const uint32_t* q, uint32_t dim,
              uint32_t* per_row, uint32_t* sum);
 void ip_fill(hipStream_t st, uint32_t* rows, uint64_t N, uint32_t D);

@@ -404,15 +404,18 @@ __global__ void __launch_bounds__(kBlock) k_server_answer(const PmPart* __restri
 // elements 8t+k (VSUBPS/VMULPS/VADDPS, each rounded: no FMA), then the
 // VHADDPS tree ((s0+s1)+(s2+s3))+((s4+s5)+(s6+s7)) as xor-1/2/4 shuffles, then
 // the scalar tail of build_graph.go:123-125 on lane 0.
+// seglen > 0: rows [j*seglen, (j+1)*seglen) are scored against query j at
+// q + j*dim (several clients' start sets in one launch, pm_search_loop_batched)
 __global__ void __launch_bounds__(kBlock) k_l2_rows(const float* __restrict__ rows,
                                                     uint64_t stride, uint64_t nrows,
                                                     const uint32_t* __restrict__ ids,
                                                     const float* __restrict__ q, uint32_t dim,
-                                                    float* __restrict__ out) {
+                                                    float* __restrict__ out, uint64_t seglen) {
   const uint64_t g = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 3;
   const uint32_t k = threadIdx.x & 7;
   const bool live = g < nrows;
   const float* r = rows + (live ? (ids ? (uint64_t)ids[g] : g) : 0) * stride;
+  if (seglen && live) q += (g / seglen) * dim;
   const uint32_t dimS = dim & ~7u;
   float acc = 0.0f;
   if (live)
@@ -615,10 +618,10 @@ void server_answer(hipStream_t st, const PmPart* d, const uint32_t* offs, uint32
     hipLaunchKernelGGL(k_server_answer<1>, dim3(nq), dim3(kBlock), 0, st, d, offs, SS, db, E, out);
 }
 void l2_rows(hipStream_t st, const float* rows, uint64_t stride, uint64_t nrows, const uint32_t* ids,
-             const float* q, uint32_t dim, float* out) {
+             const float* q, uint32_t dim, float* out, uint64_t seglen) {
   if (!nrows) return;
   hipLaunchKernelGGL(k_l2_rows, dim3(cdiv(nrows * 8, kBlock)), dim3(kBlock), 0, st, rows, stride, nrows,
-                     ids, q, dim, out);
+                     ids, q, dim, out, seglen);
 }
 void ip_rows(hipStream_t st, const uint32_t* rows, uint64_t nrows, const uint32_t* q, uint32_t dim,
              uint32_t* per_row, uint32_t* sum) {
