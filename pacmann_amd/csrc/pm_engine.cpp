@@ -307,6 +307,7 @@ struct Engine {
   uint64_t stamp_n = 0;
   uint32_t step_token = 0;         // PmStep::token of the last step
   size_t pf_off = 0, pf_len = ~size_t(0);   // bytes of each result row the caller reads next
+  bool rows_partial = false;   // this call's caller reads ONLY those bytes (GetVertexInfo): the rest is not sent
   HostBuf desc_h, out_h, err_h;
   std::vector<PartHost> parts;
   uint32_t maxH = 0, maxPH = 0, maxSS = 0, maxRepl = 0, maxCS = 0, minCS = ~0u;
@@ -789,6 +790,7 @@ static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
     const size_t end = std::min<size_t>(E * 8, off + std::min<size_t>(g->pf_len, E * 8));
     S.pf_w0 = (uint32_t)(off / 8);
     S.pf_w1 = (uint32_t)((end + 7) / 8);
+    S.rows_partial = g->rows_partial && !c->verify_rows && !c->debug_cache ? 1u : 0u;
   }
   if (S.args_valid) {
     memcpy(S.subs_a, g->subs.data(), dsub);
@@ -1546,6 +1548,7 @@ static int gvi_pre(pm_graph* g, bool with_q, bool* fast) {
   g->qids.assign(g->batch.begin(), g->batch.end());
   g->rowp.resize(n);
   auto t = Clock::now();
+  e->rows_partial = true;   // Entry2VectorAndNeighbors reads the neighbour list (the distance is in the header)
   CHK(bq_prepare(e, g->qids.data(), n, fast));
   if (!*fast)   // a partition at its query budget: the general path, served now
     CHK(batch_query_impl(e, g->qids.data(), n, nullptr, with_q ? g->qdev() : nullptr, (uint32_t)g->dim,
@@ -1574,6 +1577,7 @@ static int gvi_post(pm_graph* g, bool with_q, bool fast) {
     memcpy(nbi, (const char*)g->rowp[i] + nb_off, m * 4);
     if (memcmp(nbi, &g->graph[(uint64_t)g->batch[i] * m], m * 4) == 0) g->succ++;
   }
+  e->rows_partial = false;
   g->ctx->host_add(HT_GVI_PARSE, ms_since(t_parse));
   return 0;
 }
@@ -1931,6 +1935,7 @@ static int group_step(StepGroup& G, pm_graph** gs, const std::vector<char>& in) 
     const size_t end = std::min<size_t>(G.E * 8, off + std::min<size_t>(e0->pf_len, G.E * 8));
     S.pf_w0 = (uint32_t)(off / 8);
     S.pf_w1 = (uint32_t)((end + 7) / 8);
+    S.rows_partial = !c->verify_rows && !c->debug_cache ? 1u : 0u;   // graph search: neighbour lists only
   }
   auto t0 = Clock::now();
   uint32_t nreal = 0;

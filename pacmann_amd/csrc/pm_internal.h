@@ -144,6 +144,7 @@ struct PmStep {
   uint32_t words, E, dim, nsub, np, cblk;
   uint32_t np_live;            // partitions with at least one sub-query in this step
   uint32_t pf_w0, pf_w1;       // row words the host reads (PmOutHdr::csum covers them)
+  uint32_t rows_partial;       // 1: only words [pf_w0, pf_w1) of each result row are written to the host
   uint32_t no_guess;           // k_step diagnostics: answers wait for their resolution (PM_NO_GUESS=1)
   // Split gather (three-kernel path, wide sets): k_gather writes nsplit partial
   // XORs of each sub-query's set, [nsub][nsplit][E&~3]; k_answer folds them.

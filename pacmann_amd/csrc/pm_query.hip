@@ -1101,7 +1101,9 @@ __device__ void decode_chained(const PmStep& S, uint32_t s, RowBuf& row) {
   __syncthreads();
   uint64_t* orow = S.rows_h + (uint64_t)s * E;
   uint64_t* ar = P.arena + (uint64_t)r.slot * E;
-  for (uint32_t w = tid; w < E; w += blockDim.x) { orow[w] = row.w[w]; ar[w] = row.w[w]; }
+  for (uint32_t w = tid; w < E; w += blockDim.x) ar[w] = row.w[w];
+  for (uint32_t w = (S.rows_partial ? S.pf_w0 : 0) + tid; w < (S.rows_partial ? S.pf_w1 : E); w += blockDim.x)
+    orow[w] = row.w[w];
   float d = 0.0f;
   const float* qq = P.qv ? P.qv : S.q;
   if (qq && tid < 8) d = l2_lds(row.f, qq, S.dim);
@@ -1375,7 +1377,10 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, AnswerL
   // ---- results: row + header into pinned host memory, arena copy -----------
   if (mode != A_CHAINED) {
     const bool has_row = (mode == A_FINAL || mode == A_CACHED);
-    for (uint32_t w = tid; w < E; w += NT) orow[w] = has_row ? row.w[w] : 0;
+    // to the host: the whole row, or only the words its caller reads (graph search:
+    // the neighbour list; the distance travels in the header)
+    for (uint32_t w = (S.rows_partial ? S.pf_w0 : 0) + tid; w < (S.rows_partial ? S.pf_w1 : E); w += NT)
+      orow[w] = has_row ? row.w[w] : 0;
     if (mode == A_FINAL) {
       uint64_t* ar = P.arena + (uint64_t)r.slot * E;
       for (uint32_t w = tid; w < E; w += NT) ar[w] = row.w[w];
