@@ -30,6 +30,7 @@
 
 #include "pm_aes.h"
 #include "pm_internal.h"
+#include <cstdlib>
 
 namespace pm {
 
@@ -369,6 +370,134 @@ __global__ void __launch_bounds__(kBlock) k_match(PmStep S) {
   sub.idx = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(sub.idx >> 32)) << 32) |
             __builtin_amdgcn_readfirstlane((uint32_t)sub.idx);
   match_role<kBlock, kMatchHints / kBlock, false>(S, s, blockIdx.x, sub, s_cand);
+}
+
+// k_match with the sub-queries of a partition grouped, for steps over many
+// partitions with several sub-queries each (batched serving: S x 16
+// partitions, 6 sub-queries each).  A workgroup owns (partition, block of
+// kMatchHints hints): it loads the hints' state (tag, program point: 8 B per
+// hint) once for all of the partition's sub-queries, gathers each one's
+// PRF-table values (2 B per hint, G sub-queries' loads in flight together)
+// and writes exactly the bits, records and predictions of match_role.
+template <int HPT>
+__global__ void __launch_bounds__(kBlock) k_match_part(PmStep S) {
+  constexpr int NT = kBlock, G = 8;
+  __shared__ uint32_t s_cand[G][NT / 64][6];
+  const uint32_t p = blockIdx.y, blk = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t pb0 = desc_sb(S, p), pn = desc_sb(S, p + 1) - pb0;
+  if (!S.args_valid && blk == 0) {   // stage the descriptor for the later kernels
+    for (uint32_t i = tid; i < pn; i += NT) S.subs[pb0 + i] = S.subs_h[pb0 + i];
+    if (p == 0)
+      for (uint32_t i = tid; i <= S.np; i += NT) S.sb[i] = S.sb_h[i];
+  }
+  if (pn == 0) return;
+  const PmPart P = S.parts[p];
+  const uint32_t base = blk * NT * HPT;
+  if (base >= P.PH) return;
+  const uint32_t mask = P.CS - 1, lg = P.log2CS;
+  // block 0: k_resolve's predictions for every real sub-query, one wave each
+  if (blk == 0 && pn <= kSpecSubs) {
+    for (uint32_t k = wave; k < pn; k += NT / 64) {
+      PmSub sub = desc_sub(S, pb0 + k);
+      sub.kind = __builtin_amdgcn_readfirstlane(sub.kind);
+      if (sub.kind != SUB_REAL) continue;
+      const bool live = sub.idx < P.N;
+      const uint32_t chunk = (uint32_t)(sub.idx >> lg);
+      const uint32_t h0k = live ? P.hist[chunk] : 0;
+      PmSub st;
+      bool validt;
+      const uint32_t sing = predict_ing(S, P, pb0, pn, k, chunk, h0k, st, validt);
+      const uint32_t cht = (uint32_t)(st.idx >> lg);
+      const uint32_t pred = (live && sing < P.Qpc && chunk < P.SS) ? P.PH + chunk * P.Qpc + sing : kNone;
+      uint32_t v = kSkip;
+      if (lane < pn && lane > k && validt && cht < P.SS && pred != kNone) v = P.tab[(uint64_t)cht * P.H + pred];
+      const uint64_t s = pb0 + k;
+      if (lane < pn) S.spec[s * kSpecSubs + lane] = v;
+      if (lane == 0) { S.meta[2 * s] = h0k; S.meta[2 * s + 1] = sing; }
+    }
+  }
+  uint32_t tg[HPT], pv[HPT];
+#pragma unroll
+  for (int u = 0; u < HPT; ++u) {
+    const uint32_t h = base + u * NT + tid;
+    tg[u] = 0; pv[u] = kDefaultProgramPoint;
+    if (h < P.PH) { tg[u] = P.tag[h]; pv[u] = P.pp[h]; }
+  }
+  for (uint32_t j0 = 0; j0 < pn; j0 += G) {
+    uint32_t kind[G], chk[G], off[G];
+    bool lv[G];
+    uint16_t rv[G][HPT];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      PmSub sub{0, SUB_NONE, 0};
+      if (j0 + g < pn) sub = desc_sub(S, pb0 + j0 + g);
+      kind[g] = __builtin_amdgcn_readfirstlane(sub.kind);
+      const uint64_t idx = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(sub.idx >> 32)) << 32) |
+                           __builtin_amdgcn_readfirstlane((uint32_t)sub.idx);
+      lv[g] = kind[g] == SUB_REAL && idx < P.N;
+      chk[g] = (uint32_t)(idx >> lg);
+      off[g] = (uint32_t)(idx & mask);
+      const PM_G uint16_t* row = P.tab + (uint64_t)chk[g] * P.H;
+#pragma unroll
+      for (int u = 0; u < HPT; ++u) rv[g][u] = lv[g] ? row[tg[u]] : (uint16_t)0;
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (j0 + g >= pn || kind[g] != SUB_REAL) continue;   // uniform
+      const uint64_t s = pb0 + j0 + g;
+      uint32_t h0 = kNone, t0 = 0, p0 = 0, h1 = kNone, t1 = 0, p1 = 0;   // wave-uniform
+#pragma unroll
+      for (int u = 0; u < HPT; ++u) {
+        if (base + u * NT >= P.PH) break;
+        const uint32_t h = base + u * NT + tid;
+        const bool m = lv[g] && h < P.PH && rv[g][u] == off[g] &&
+                       (pv[u] == kDefaultProgramPoint || (pv[u] >> lg) != chk[g]);
+        uint64_t b = __ballot(m);
+        if (lane == 0 && (h - lane) < P.PH) S.bits[s * S.words + (h >> 6)] = b;
+        if (b && h1 == kNone) {   // in hint order within this wave
+          const uint32_t l = (uint32_t)__builtin_ctzll(b), hl = h - lane + l;
+          const uint32_t tl = __builtin_amdgcn_readlane(tg[u], l), pl = __builtin_amdgcn_readlane(pv[u], l);
+          if (h0 == kNone) {
+            h0 = hl; t0 = tl; p0 = pl;
+            b &= b - 1;
+            if (b) {
+              const uint32_t l2 = (uint32_t)__builtin_ctzll(b);
+              h1 = h - lane + l2;
+              t1 = __builtin_amdgcn_readlane(tg[u], l2);
+              p1 = __builtin_amdgcn_readlane(pv[u], l2);
+            }
+          } else {
+            h1 = hl; t1 = tl; p1 = pl;
+          }
+        }
+      }
+      if (lane == 0) {
+        s_cand[g][wave][0] = h0; s_cand[g][wave][1] = t0; s_cand[g][wave][2] = p0;
+        s_cand[g][wave][3] = h1; s_cand[g][wave][4] = t1; s_cand[g][wave][5] = p1;
+      }
+    }
+    __syncthreads();
+    if (tid < (uint32_t)G && j0 + tid < pn) {   // merge each sub-query's wave pairs
+      const uint32_t g = tid;
+      const PmSub sub = desc_sub(S, pb0 + j0 + g);
+      if (sub.kind == SUB_REAL) {
+        uint32_t o[6] = {kNone, 0, 0, kNone, 0, 0};
+        for (uint32_t w = 0; w < NT / 64; ++w)
+          for (int k = 0; k < 2; ++k) {
+            const uint32_t h = s_cand[g][w][3 * k];
+            if (h < o[0]) {
+              o[3] = o[0]; o[4] = o[1]; o[5] = o[2];
+              o[0] = h; o[1] = s_cand[g][w][3 * k + 1]; o[2] = s_cand[g][w][3 * k + 2];
+            } else if (h < o[3]) {
+              o[3] = h; o[4] = s_cand[g][w][3 * k + 1]; o[5] = s_cand[g][w][3 * k + 2];
+            }
+          }
+        PM_G uint32_t* dst = S.cand + ((uint64_t)(pb0 + j0 + g) * S.cblk + blk) * 6;
+        for (int i = 0; i < 6; ++i) dst[i] = o[i];
+      }
+    }
+    if (j0 + G < pn) __syncthreads();
+  }
 }
 
 // First set bit at position >= start in a sub-query's match bitmask (one wave).
@@ -1566,7 +1695,14 @@ uint32_t step_match_blocks(uint32_t maxPH) { return cdiv(maxPH, kMatchHints); }
     else hipLaunchKernelGGL(kern, grid, blk, 0, st, __VA_ARGS__);                             \
   } while (0)
 void step_match(hipStream_t st, const PmStep& S, uint32_t maxPH, PmEvents ev) {
-  PM_LAUNCH(ev, k_match, dim3(step_match_blocks(maxPH), S.nsub), dim3(kBlock), st, S);
+  // many partitions with several sub-queries each (batched serving): one
+  // workgroup per (partition, hint block); otherwise one per (sub-query, block)
+  static const int mode = [] { const char* e = getenv("PM_MATCH_PART"); return e ? atoi(e) : -1; }();
+  const bool part = mode == 1 || (mode == -1 && S.np >= 128 && S.nsub >= 4 * S.np);
+  if (part)
+    PM_LAUNCH(ev, k_match_part<kMatchHints / kBlock>, dim3(step_match_blocks(maxPH), S.np), dim3(kBlock), st, S);
+  else
+    PM_LAUNCH(ev, k_match, dim3(step_match_blocks(maxPH), S.nsub), dim3(kBlock), st, S);
 }
 void step_resolve(hipStream_t st, const PmStep& S, bool lds, PmEvents ev) {
   if (lds) PM_LAUNCH(ev, k_resolve<true>, dim3(S.np), dim3(kBlock), st, S);
