@@ -588,9 +588,10 @@ static inline double ms_since(Clock::time_point t) {
 // While polling, the bytes [pf_off, pf_off + pf_len) of each published row are
 // prefetched, so the caller's reads of the results hit the cache.
 static int wait_step(pm_ctx* c, const PmOutHdr* hdr, uint32_t nsub, uint32_t token, const char* rows,
-                     size_t row_bytes, size_t pf_off, size_t pf_len) {
+                     size_t row_bytes, size_t pf_off, size_t pf_len, hipStream_t stream = nullptr) {
+  if (!stream) stream = c->stream;   // the stream the step runs on (c: timing and diagnostics)
   if (c->timing >= 2 || c->debug_sync) {
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipStreamSynchronize(stream));
   } else {
     const volatile uint32_t* tok = &hdr[0].token;
     const size_t stride = sizeof(PmOutHdr) / sizeof(uint32_t);
@@ -615,7 +616,7 @@ static int wait_step(pm_ctx* c, const PmOutHdr* hdr, uint32_t nsub, uint32_t tok
         continue;
       }
       if ((spin & 0xffff) == 0xffff && ms_since(t0) > 5000.0) {
-        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(hipStreamSynchronize(stream));
         HIPCHK(hipGetLastError());
         break;
       }
@@ -1829,7 +1830,7 @@ struct StepGroup {
   uint32_t S = 0, P = 0, maxPH = 0, maxSS = 0, E = 0, dim = 0;
   DevBuf parts_d, subs_d, sb_d, bits, cand, meta, spec, res_d, ans, part_x, done, prep_parts;
   HostBuf desc_h, out_h;
-  uint32_t token = 0;
+  uint32_t token = 0, pf_w0 = 0, pf_w1 = 0;
   std::vector<PmSub> subs;
   std::vector<uint32_t> sb, base;
   std::vector<uint64_t> gen;   // each session's Engine::prep_gen at the last upload of its parts
@@ -1952,10 +1953,25 @@ static int group_step(StepGroup& G, pm_graph** gs, const std::vector<char>& in) 
   c->timed_ext("answer", S.nsplit > 1 ? 0 : ans_bytes, [&](pmk::PmEvents ev) { pmk::step_answer(st, S, ev); }, 2);
   HIPCHK(hipGetLastError());
   c->host_add(HT_STEP_LAUNCH, ms_since(t0));
+  G.pf_w0 = S.pf_w0; G.pf_w1 = S.pf_w1;
+  return 0;
+}
+
+// Session s's share of the last shared step: wait for its results (tokens and
+// row checksums, polled by the session's own worker, so a team checks its
+// sub-queries in parallel) and update its host mirrors.
+static int group_collect(StepGroup& G, pm_graph** gs, uint32_t s) {
+  Engine* e = &gs[s]->pir->e;
+  const uint32_t n = (uint32_t)e->subs.size();
+  PmOutHdr* hdr = G.out_h.as<PmOutHdr>();
+  uint64_t* rows = (uint64_t*)(G.out_h.as<char>() + G.subs.size() * sizeof(PmOutHdr));
   auto t_wait = Clock::now();
-  CHK(wait_step(c, S.hdr_h, nsub, S.token, (const char*)S.rows_h, (size_t)G.E * 8, (size_t)S.pf_w0 * 8,
-                (size_t)(S.pf_w1 - S.pf_w0) * 8));
-  c->host_add(HT_STEP_WAIT, ms_since(t_wait));
+  CHK(wait_step(gs[s]->ctx, hdr + G.base[s], n, G.token, (const char*)(rows + (uint64_t)G.base[s] * G.E),
+                (size_t)G.E * 8, (size_t)G.pf_w0 * 8, (size_t)(G.pf_w1 - G.pf_w0) * 8, G.c->stream));
+  gs[s]->ctx->host_add(HT_STEP_WAIT, ms_since(t_wait));
+  auto tp = Clock::now();
+  post_results(e, hdr, rows, n, G.base[s], G.token);
+  gs[s]->ctx->host_add(HT_STEP_POST, ms_since(tp));
   return 0;
 }
 
@@ -2112,11 +2128,8 @@ static int run_batched_team(pm_graph** gs, uint32_t S, const float* queries, uin
         for (uint32_t s = w; s < S && !err.load(); s += T) {   // rows -> neighbours, known set
           pm_graph* g = gs[s];
           if (fast[s]) {   // this client's share of the shared step's results
-            Engine* e = &g->pir->e;
-            auto tp = Clock::now();
-            post_results(e, G.out_h.as<PmOutHdr>(), (uint64_t*)(G.out_h.as<char>() + G.subs.size() * sizeof(PmOutHdr)),
-                         (uint32_t)e->subs.size(), G.base[s], G.token);
-            g->ctx->host_add(HT_STEP_POST, ms_since(tp));
+            const int rw = group_collect(G, gs, s);
+            if (rw) { set_err(rw, s); break; }
           }
           const int rc = gvi_post(g, true, fast[s]);
           if (rc) { set_err(rc, s); break; }
