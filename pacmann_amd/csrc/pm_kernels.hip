@@ -114,7 +114,8 @@ __global__ void __launch_bounds__(kBlock) k_prep_fold(const PmPart* __restrict__
 // registers, so a DB byte is read from HBM once per hint group instead of once
 // per hint that selects it.  Entry CS of a staged chunk is a zero row (kSkip
 // selects it); rows past N are staged from a 16-byte zero source.
-constexpr int kFoldThreads = 1024, kFoldHPT = 4;
+constexpr int kFoldThreads = 1024, kFoldHPT = 7;   // hints per thread: pipelined fold
+constexpr int kFoldHPTBlk = 4;                      // hints per thread: double-buffered fold (up to 8-word slices)
 constexpr uint32_t kFoldMaxItems = 4;   // 16-B staging items per thread per chunk
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) const void g_cvoid_t;
@@ -129,7 +130,7 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_blk(const PmPart* __
   constexpr uint32_t IPE = SW / 2;   // 16-B items per entry slice
   const PmPart& P = parts[blockIdx.z];
   const uint32_t H = P.H, CS = P.CS, SS = P.SS, tid = threadIdx.x;
-  const uint32_t ng = (H + kFoldThreads * kFoldHPT - 1) / (kFoldThreads * kFoldHPT);
+  const uint32_t ng = (H + kFoldThreads * kFoldHPTBlk - 1) / (kFoldThreads * kFoldHPTBlk);
   if (blockIdx.x >= ng) return;   // block-uniform
   const uint32_t hb = (H + ng - 1) / ng, h0 = blockIdx.x * hb, h1 = min(H, h0 + hb);
   const uint32_t w = w0 + blockIdx.y * SW;
@@ -138,15 +139,15 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_blk(const PmPart* __
   const PM_G uint16_t* tab = P.tab;
   const uint32_t rowWords = (CS + 1) * SW, items = CS * IPE;
   const uint32_t wave_item0 = tid & ~63u;
-  uint32_t hk[kFoldHPT];
-  uint64_t acc[kFoldHPT][SW];
+  uint32_t hk[kFoldHPTBlk];
+  uint64_t acc[kFoldHPTBlk][SW];
 #pragma unroll
-  for (int k = 0; k < kFoldHPT; ++k) {
+  for (int k = 0; k < kFoldHPTBlk; ++k) {
     hk[k] = h0 + tid + k * kFoldThreads;
 #pragma unroll
     for (int x = 0; x < SW; ++x) acc[k][x] = 0;
   }
-  uint32_t v[kFoldHPT], nv[kFoldHPT];
+  uint32_t v[kFoldHPTBlk], nv[kFoldHPTBlk];
   // item it of chunk c: entry it / IPE, 16-B piece it % IPE, LDS byte offset it * 16
   auto stage = [&](uint32_t c, uint32_t buf) {
     uint64_t* L = fold_lds + buf * rowWords;
@@ -163,7 +164,7 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_blk(const PmPart* __
   };
   auto load_tab = [&](uint32_t c, uint32_t* out) {
 #pragma unroll
-    for (int k = 0; k < kFoldHPT; ++k) out[k] = hk[k] < h1 ? tab[(uint64_t)c * H + hk[k]] : kSkip;
+    for (int k = 0; k < kFoldHPTBlk; ++k) out[k] = hk[k] < h1 ? tab[(uint64_t)c * H + hk[k]] : kSkip;
   };
   stage(0, 0);
   load_tab(0, v);
@@ -175,7 +176,7 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_blk(const PmPart* __
     if (more) { stage(c + 1, (c + 1) & 1); load_tab(c + 1, nv); }
     const uint64_t* L = fold_lds + (c & 1) * rowWords;
 #pragma unroll
-    for (int k = 0; k < kFoldHPT; ++k) {
+    for (int k = 0; k < kFoldHPTBlk; ++k) {
       const uint32_t o = v[k] == kSkip ? CS : v[k];
       const uint64_t* row = L + o * SW;
 #pragma unroll
@@ -188,10 +189,10 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_blk(const PmPart* __
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < kFoldHPT; ++k) v[k] = nv[k];
+    for (int k = 0; k < kFoldHPTBlk; ++k) v[k] = nv[k];
   }
 #pragma unroll
-  for (int k = 0; k < kFoldHPT; ++k) {
+  for (int k = 0; k < kFoldHPTBlk; ++k) {
     if (hk[k] >= h1) continue;
     PM_G uint64_t* dst = P.parity + (uint64_t)hk[k] * E + w;
 #pragma unroll
@@ -206,7 +207,7 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_blk(const PmPart* __
 // of the chunk staged through LDS too, so every load of the loop is a direct
 // global->LDS load and the waits are counted per wave (G or G+1 loads per
 // chunk), never vmcnt(0).  One extern __shared__ array; raw s_barrier.
-constexpr uint32_t kPipeTabWords = 1024;   // 8 KB table row (<= 4096 hints per group)
+constexpr uint32_t kPipeTabWords = kFoldThreads * kFoldHPT / 4;   // the group's table row: one u16 per hint
 
 // s_waitcnt vmcnt(n) for a runtime n, n <= 15.  n must be wave-uniform, and is
 // made visibly so: s_waitcnt is a scalar instruction, and in a switch lowered
@@ -249,7 +250,7 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_pipe(const PmPart* _
   const PM_G uint16_t* tab = P.tab;
   constexpr uint32_t TABW = (CS + 1) * SW, BUFW = TABW + kPipeTabWords;
   const uint32_t wave_item0 = tid & ~63u;
-  const bool tab_wave = tid < 512;   // waves 0-7 stage the table row: 3 loads per chunk, others 2
+  const bool tab_wave = tid < kPipeTabWords / 2;   // these waves stage the table row (8 entries per lane)
   uint32_t hk[kFoldHPT];
   uint64_t acc[kFoldHPT][SW];
 #pragma unroll
@@ -560,14 +561,15 @@ void prep_fold(hipStream_t st, const PmPart* d, int np, uint32_t maxH, const uin
   }
   // column-slice width: the widest whose double-buffered chunk fits in LDS and
   // whose staging fits kFoldMaxItems 16-B items per thread
-  const uint32_t ng = cdiv(maxH, (uint64_t)kFoldThreads * kFoldHPT);
+  const uint32_t ng = cdiv(maxH, (uint64_t)kFoldThreads * kFoldHPT);      // pipelined fold
+  const uint32_t ngb = cdiv(maxH, (uint64_t)kFoldThreads * kFoldHPTBlk);  // double-buffered fold
   auto fits = [&](uint32_t sw) {
     return 2ull * (maxCS + 1) * sw * 8 <= 150u * 1024 &&
            (uint64_t)maxCS * (sw / 2) <= (uint64_t)kFoldMaxItems * kFoldThreads;
   };
   auto launch = [&](uint32_t sw, uint32_t w0, uint32_t nsl) {
     const size_t lds = 2ull * (maxCS + 1) * sw * 8;
-    const dim3 grid(ng, nsl, np), blk(kFoldThreads);
+    const dim3 grid(ngb, nsl, np), blk(kFoldThreads);
     if (sw == 8) hipLaunchKernelGGL(k_prep_fold_blk<8>, grid, blk, lds, st, d, db, zero16, E, w0);
     else if (sw == 4) hipLaunchKernelGGL(k_prep_fold_blk<4>, grid, blk, lds, st, d, db, zero16, E, w0);
     else hipLaunchKernelGGL(k_prep_fold_blk<2>, grid, blk, lds, st, d, db, zero16, E, w0);
