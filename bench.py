@@ -594,11 +594,24 @@ def main():
     E = (DIM + M) // 2
     fold = roof("prep_fold")
     if fold:
-        comp = N * E * 8 + hints * E * 8
+        # a launch folds k clients' hints at once (batched serving re-preprocesses a group's
+        # triggered clients together); they share the one DB
+        c0 = base.PIR.SubConfig(0)
+        fold_one = sum(((c["PrimaryHintNum"] + (c["SetSize"] - 1) * c["MaxQueryPerChunk"]) * c["SetSize"] * E * 8)
+                       for c in (base.PIR.SubConfig(p) for p in range(stats["PartitionNum"])))
+        k = max(1, round(fold["alg_bytes_per_launch"] / fold_one))
+        comp = N * E * 8 + k * hints * E * 8
         ach_c = comp / (fold["avg_ms"] / 1e3) / 1e9
+        fold["clients_per_launch"] = k
         fold["compulsory"] = {"bytes": comp, "achieved": round(ach_c, 1), "frac": round(ach_c / HBM_PEAK_GBS, 4)}
+        # PMC bytes of launches of this shape (k_prep_fold_pipe<4,1,4>: 2 hint groups x 20 column slices
+        # per partition, 1,024 threads per workgroup)
+        units = 16 * k * -(-(c0["PrimaryHintNum"] + c0["SetSize"] * c0["MaxQueryPerChunk"]) // 7168)
+        tr = pmc_traffic(SYMBOLS["prep_fold"], -(-units // 8) * 8 * (E // 4) * 1024)
+        fold["traffic"], fold["traffic_source"] = (tr[0], tr[1]) if tr else (None, None)
         fold["note"] = ("fold bytes (hint x chunk entry reads, SURVEY.md §8d) exceed HBM peak because the "
-                        "kernel serves them from LDS; 'compulsory' is the DB read once plus the parity writes")
+                        "kernel serves them from LDS; 'compulsory' is the DB read once plus the parity writes "
+                        "of the clients folded in one launch")
     note = None
     if dom == "step":
         note = ("k_step runs hint match, resolution and answer of a batch-PIR step in one launch; "
