@@ -2009,8 +2009,11 @@ static int group_prep(StepGroup& G, pm_graph** gs, const std::vector<char>& need
     Engine* e = &gs[s]->pir->e;
     e->FBN = 0; e->QMIP = 0;
     CHK(engine_prep_host(e, 0, e->P, todo));
-    for (uint64_t i : todo) hp.push_back(e->parts[i].d);
   }
+  // partition-major: the clients' folds of one partition run side by side and
+  // share its DB rows through the caches instead of re-reading them per client
+  for (uint32_t p = 0; p < G.P; ++p)
+    for (uint32_t s : who) hp.push_back(gs[s]->pir->e.parts[p].d);
   const Engine* e0 = &gs[who[0]]->pir->e;
   bool skip = false;
   for (uint32_t s : who) skip |= gs[s]->pir->e.skipPrep != e0->skipPrep;
