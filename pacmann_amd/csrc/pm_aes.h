@@ -3,9 +3,9 @@
 // Replaces aes128MMO / PRFEvalWithLongKeyAndTag (pianopir/aes_amd64.s:51-82,
 // pianopir/util.go:157-165).  One block per lane, T-table formulation with a
 // single table Te0 (rows 1-3 are byte rotations of it) held in LDS replicated
-// 32x so that lane l always reads bank (l & 31): a random-index ds_read_b32 is
-// then conflict-free (bank = (addr/4) % 32, MI355X_MICROARCH.md §LDS).
-// 32 KiB of LDS per workgroup.  Bit-exact with AES-NI: the state is kept as
+// 64x so that lane l always reads bank (l & 31) of its 32-lane group: a
+// random-index ds_read_b32 is then conflict-free (bank = (addr/4) % 32,
+// MI355X_MICROARCH.md §LDS).  64 KiB of LDS per workgroup.  Bit-exact with AES-NI: the state is kept as
 // four little-endian column words, exactly the byte order AESENC works on.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -51,7 +51,11 @@ struct AesTables {
   static constexpr uint8_t rotl(uint8_t v, int n) { return (uint8_t)((v << n) | (v >> (8 - n))); }
 };
 
-constexpr int kTeLdsWords = 256 * 32;   // 32 KiB replicated Te0
+// Te0 replicated 64x, entry b of lane l's copy at byte (b << 8) | (l << 2): a
+// lookup address is ONE v_perm_b32 (the state byte into byte 1, the lane
+// offset in byte 0), and a ds_read_b32 lane group (32 lanes, bank =
+// (a/4) mod 32) reads 32 distinct banks.  64 KiB.
+constexpr int kTeLdsWords = 256 * 64;
 
 // Device copy of the tables (one per translation unit; read only by aes_lds_init).
 static constexpr AesTables kAesTablesHost{};
@@ -61,14 +65,18 @@ __device__ __forceinline__ uint32_t rotl32(uint32_t x, int n) { return (x << n) 
 
 // Fill the replicated table.  Call with the whole block, then __syncthreads().
 __device__ __forceinline__ void aes_lds_init(uint32_t* te, const uint32_t* __restrict__ g_te0) {
-  for (int i = threadIdx.x; i < kTeLdsWords; i += blockDim.x) te[i] = g_te0[i >> 5];
+  for (int i = threadIdx.x; i < kTeLdsWords; i += blockDim.x) te[i] = g_te0[i >> 6];
 }
 
 struct AesLane {
   const uint32_t* te;
-  uint32_t lane;   // (threadIdx.x & 31)
-  __device__ __forceinline__ uint32_t T(uint32_t b) const { return te[(b << 5) | lane]; }
-  __device__ __forceinline__ uint32_t S(uint32_t b) const { return (T(b) >> 8) & 0xffu; }
+  uint32_t lane;   // (threadIdx.x & 63) << 2: this lane's byte offset within an entry row
+  // Te0[byte k of s] from this lane's copy: address = (byte << 8) | lane, one v_perm_b32
+  template <int K> __device__ __forceinline__ uint32_t Tk(uint32_t s) const {
+    const uint32_t a = __builtin_amdgcn_perm(s, lane, 0x0c0c0000u | ((4u + K) << 8));
+    return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(te) + a);
+  }
+  template <int K> __device__ __forceinline__ uint32_t Sk(uint32_t s) const { return (Tk<K>(s) >> 8) & 0xffu; }
 };
 
 // Nine full rounds on state (s0..s3) with round keys rk[4..39].
@@ -76,14 +84,14 @@ __device__ __forceinline__ void aes_rounds(const AesLane& A, const uint32_t* __r
                                            uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3) {
 #pragma unroll
   for (int r = 1; r < 10; ++r) {
-    uint32_t t0 = A.T(s0 & 0xff) ^ rotl32(A.T((s1 >> 8) & 0xff), 8) ^
-                  rotl32(A.T((s2 >> 16) & 0xff), 16) ^ rotl32(A.T(s3 >> 24), 24) ^ rk[4 * r + 0];
-    uint32_t t1 = A.T(s1 & 0xff) ^ rotl32(A.T((s2 >> 8) & 0xff), 8) ^
-                  rotl32(A.T((s3 >> 16) & 0xff), 16) ^ rotl32(A.T(s0 >> 24), 24) ^ rk[4 * r + 1];
-    uint32_t t2 = A.T(s2 & 0xff) ^ rotl32(A.T((s3 >> 8) & 0xff), 8) ^
-                  rotl32(A.T((s0 >> 16) & 0xff), 16) ^ rotl32(A.T(s1 >> 24), 24) ^ rk[4 * r + 2];
-    uint32_t t3 = A.T(s3 & 0xff) ^ rotl32(A.T((s0 >> 8) & 0xff), 8) ^
-                  rotl32(A.T((s1 >> 16) & 0xff), 16) ^ rotl32(A.T(s2 >> 24), 24) ^ rk[4 * r + 3];
+    uint32_t t0 = A.Tk<0>(s0) ^ rotl32(A.Tk<1>(s1), 8) ^ rotl32(A.Tk<2>(s2), 16) ^ rotl32(A.Tk<3>(s3), 24) ^
+                  rk[4 * r + 0];
+    uint32_t t1 = A.Tk<0>(s1) ^ rotl32(A.Tk<1>(s2), 8) ^ rotl32(A.Tk<2>(s3), 16) ^ rotl32(A.Tk<3>(s0), 24) ^
+                  rk[4 * r + 1];
+    uint32_t t2 = A.Tk<0>(s2) ^ rotl32(A.Tk<1>(s3), 8) ^ rotl32(A.Tk<2>(s0), 16) ^ rotl32(A.Tk<3>(s1), 24) ^
+                  rk[4 * r + 2];
+    uint32_t t3 = A.Tk<0>(s3) ^ rotl32(A.Tk<1>(s0), 8) ^ rotl32(A.Tk<2>(s1), 16) ^ rotl32(A.Tk<3>(s2), 24) ^
+                  rk[4 * r + 3];
     s0 = t0; s1 = t1; s2 = t2; s3 = t3;
   }
 }
@@ -95,10 +103,8 @@ __device__ __forceinline__ uint64_t prf64(const AesLane& A, const uint32_t* __re
   const uint32_t w0 = (uint32_t)b, w1 = (uint32_t)(b >> 32);
   uint32_t s0 = w0 ^ rk[0], s1 = w1 ^ rk[1], s2 = rk[2], s3 = rk[3];
   aes_rounds(A, rk, s0, s1, s2, s3);
-  uint32_t c0 = (A.S(s0 & 0xff) | (A.S((s1 >> 8) & 0xff) << 8) | (A.S((s2 >> 16) & 0xff) << 16) |
-                 (A.S(s3 >> 24) << 24)) ^ rk[40];
-  uint32_t c1 = (A.S(s1 & 0xff) | (A.S((s2 >> 8) & 0xff) << 8) | (A.S((s3 >> 16) & 0xff) << 16) |
-                 (A.S(s0 >> 24) << 24)) ^ rk[41];
+  uint32_t c0 = (A.Sk<0>(s0) | (A.Sk<1>(s1) << 8) | (A.Sk<2>(s2) << 16) | (A.Sk<3>(s3) << 24)) ^ rk[40];
+  uint32_t c1 = (A.Sk<0>(s1) | (A.Sk<1>(s2) << 8) | (A.Sk<2>(s3) << 16) | (A.Sk<3>(s0) << 24)) ^ rk[41];
   return ((uint64_t)(c1 ^ w1) << 32) | (uint64_t)(c0 ^ w0);
 }
 
@@ -109,8 +115,7 @@ __device__ __forceinline__ uint32_t prf_lo32(const AesLane& A, const uint32_t* _
   const uint32_t w0 = (uint32_t)b, w1 = (uint32_t)(b >> 32);
   uint32_t s0 = w0 ^ rk[0], s1 = w1 ^ rk[1], s2 = rk[2], s3 = rk[3];
   aes_rounds(A, rk, s0, s1, s2, s3);
-  uint32_t c0 = (A.S(s0 & 0xff) | (A.S((s1 >> 8) & 0xff) << 8) | (A.S((s2 >> 16) & 0xff) << 16) |
-                 (A.S(s3 >> 24) << 24)) ^ rk[40];
+  uint32_t c0 = (A.Sk<0>(s0) | (A.Sk<1>(s1) << 8) | (A.Sk<2>(s2) << 16) | (A.Sk<3>(s3) << 24)) ^ rk[40];
   return c0 ^ w0;
 }
 

@@ -20,24 +20,28 @@ __device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
 //                 EntryXor), one lane per (hint, 16-B segment), parity held in
 //                 a register for the whole chunk sweep.  Gather-bound.
 // ---------------------------------------------------------------------------
-constexpr int kOffsChunksPerBlock = 16;
+constexpr int kOffsChunksPerBlock = 32;
+constexpr int kOffsBlock = 1024;   // 64 KiB of replicated table per workgroup: 16 waves share it
 
 // Initial PRF tables of every hint h < H (its tag is h) at 16 chunks per
 // workgroup, written chunk-major (hint search) and hint-major (set
 // expansion).  Bound by the AES T-table lookups in LDS: the hint-major stores
 // are scattered 2-B writes (every lane on its own line, ~5x their bytes in
 // HBM write traffic), yet staging them through LDS made the kernel 20-25 %
-// slower (375 -> 450-470 us at SIFT1M shape), so they stay direct.
-__global__ void __launch_bounds__(kBlock) k_prep_offsets(const PmPart* __restrict__ parts) {
+// slower (375 -> 450-470 us at SIFT1M shape), so they stay direct (without
+// them the kernel is only 2 % faster).  1,024-thread workgroups share one 64 KiB
+// table copy (the LDS init is 4 B per PRF, not 16) and keep 16 waves per CU
+// for the lookups' latency: 0.370 -> 0.335 ms at SIFT1M shape.
+__global__ void __launch_bounds__(kOffsBlock) k_prep_offsets(const PmPart* __restrict__ parts) {
   __shared__ uint32_t te[kTeLdsWords];
   const PmPart& P = parts[blockIdx.z];
   const uint32_t H = P.H, SS = P.SS;
   const uint32_t c0 = blockIdx.y * kOffsChunksPerBlock;
-  if (blockIdx.x * kBlock >= H || c0 >= SS) return;   // block-uniform
+  if (blockIdx.x * kOffsBlock >= H || c0 >= SS) return;   // block-uniform
   aes_lds_init(te, g_aes.te0);
   __syncthreads();
-  const AesLane A{te, threadIdx.x & 31u};
-  const uint32_t h = blockIdx.x * kBlock + threadIdx.x;
+  const AesLane A{te, (threadIdx.x & 63u) << 2};
+  const uint32_t h = blockIdx.x * kOffsBlock + threadIdx.x;
   if (h >= H) return;
   const uint32_t mask = P.CS - 1;
   const uint32_t own = h >= P.PH ? (h - P.PH) / P.Qpc : 0xffffffffu;
@@ -529,7 +533,7 @@ __global__ void __launch_bounds__(kBlock) k_prf_batch(const uint32_t* __restrict
   aes_lds_init(te, g_aes.te0);
   if (threadIdx.x < 44) srk[threadIdx.x] = rk[threadIdx.x];
   __syncthreads();
-  const AesLane A{te, threadIdx.x & 31u};
+  const AesLane A{te, (threadIdx.x & 63u) << 2};
   for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock)
     out[i] = prf64(A, srk, tags[i], xs[i]);
 }
@@ -548,8 +552,8 @@ void prep_init(hipStream_t st, const PmPart* d, int np, uint32_t maxH, uint32_t 
   hipLaunchKernelGGL(k_prep_init, dim3(cdiv(n, kBlock), np), dim3(kBlock), 0, st, d);
 }
 void prep_offsets(hipStream_t st, const PmPart* d, int np, uint32_t maxH, uint32_t maxSS) {
-  hipLaunchKernelGGL(k_prep_offsets, dim3(cdiv(maxH, kBlock), cdiv(maxSS, kOffsChunksPerBlock), np),
-                     dim3(kBlock), 0, st, d);
+  hipLaunchKernelGGL(k_prep_offsets, dim3(cdiv(maxH, kOffsBlock), cdiv(maxSS, kOffsChunksPerBlock), np),
+                     dim3(kOffsBlock), 0, st, d);
 }
 void prep_fold(hipStream_t st, const PmPart* d, int np, uint32_t maxH, const uint64_t* db, uint32_t E,
                uint32_t minCS, uint32_t maxCS, const uint64_t* zero16) {
