@@ -1828,7 +1828,7 @@ struct SpinBarrier {
 struct StepGroup {
   pm_ctx* c = nullptr;   // the shared steps' stream
   uint32_t S = 0, P = 0, maxPH = 0, maxSS = 0, E = 0, dim = 0;
-  DevBuf parts_d, subs_d, sb_d, bits, cand, meta, spec, res_d, ans, part_x, done, prep_parts;
+  DevBuf parts_d, subs_d, sb_d, bits, cand, meta, spec, res_d, ans, part_x, done, prep_parts, desc_d;
   HostBuf desc_h, out_h;
   uint32_t token = 0, pf_w0 = 0, pf_w1 = 0;
   std::vector<PmSub> subs;
@@ -1907,6 +1907,14 @@ static int group_step(StepGroup& G, pm_graph** gs, const std::vector<char>& in) 
   S.parts = G.parts_d.as<PmPart>();
   S.subs_h = (const PmSub*)dh;
   S.sb_h = (const uint32_t*)(dh + dsub);
+  if (!(nsub <= kArgSubs && np <= kArgParts)) {
+    // a large descriptor crosses PCIe once, by DMA, instead of as thousands of
+    // zero-copy reads by the match workgroups; k_match* stage it from here
+    CHK(G.desc_d.reserve(dsub + (np + 1) * 4));
+    HIPCHK(hipMemcpyAsync(G.desc_d.p, dh, dsub + (np + 1) * 4, hipMemcpyHostToDevice, st));
+    S.subs_h = G.desc_d.as<PmSub>();
+    S.sb_h = (const uint32_t*)(G.desc_d.as<char>() + dsub);
+  }
   S.subs = G.subs_d.as<PmSub>();
   S.sb = G.sb_d.as<uint32_t>();
   S.bits = G.bits.as<uint64_t>();
