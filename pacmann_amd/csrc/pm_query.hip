@@ -1709,7 +1709,12 @@ void step_resolve(hipStream_t st, const PmStep& S, bool lds, PmEvents ev) {
   else PM_LAUNCH(ev, k_resolve<false>, dim3(S.np), dim3(kResolveBlockG), st, S);
 }
 bool step_resolve_lds_ok(uint32_t maxPH, uint32_t max_sub_per_part) {
-  return maxPH <= kLdsPH && max_sub_per_part * ((maxPH + 63) / 64) <= kLdsBitWords;
+  // the staged (LDS) resolver only for partitions with more sub-queries than
+  // the fast prologue takes; otherwise the global-memory form, whose fast
+  // prologue is the same and whose 36 KB of LDS (not 117) let four
+  // workgroups share a CU
+  return max_sub_per_part > kSpecSubs && maxPH <= kLdsPH &&
+         max_sub_per_part * ((maxPH + 63) / 64) <= kLdsBitWords;
 }
 void step_answer(hipStream_t st, const PmStep& S, PmEvents ev) {
   if (S.E % 2 == 0) PM_LAUNCH(ev, k_answer<2>, dim3(S.nsub), dim3(kAnsBlock), st, S);
