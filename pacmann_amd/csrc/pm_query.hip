@@ -1357,7 +1357,7 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, AnswerL
         if (sl < nsl) {
           // every row load of a batch is issued before the first is consumed: the
           // gather is one HBM round trip per kG rows a thread reads, not one per 4
-          constexpr int kG = 16;
+          constexpr int kG = 12;
           typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
           for (uint32_t i0 = sl; i0 < P.SS; i0 += kG * nsl) {
             uint64_t rr[kG];
