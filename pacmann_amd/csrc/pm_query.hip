@@ -395,9 +395,11 @@ __global__ void __launch_bounds__(kBlock) k_match_part(PmStep S) {
   const uint32_t base = blk * NT * HPT;
   if (base >= P.PH) return;
   const uint32_t mask = P.CS - 1, lg = P.log2CS;
-  // block 0: k_resolve's predictions for every real sub-query, one wave each
-  if (blk == 0 && pn <= kSpecSubs) {
-    for (uint32_t k = wave; k < pn; k += NT / 64) {
+  // k_resolve's predictions for every real sub-query, one wave each, spread
+  // over the partition's hint blocks (sub-query k: block k % nb, wave k / nb)
+  const uint32_t nb = (P.PH + NT * HPT - 1) / (NT * HPT);
+  if (pn <= kSpecSubs) {
+    for (uint32_t k = blk + nb * wave; k < pn; k += nb * (NT / 64)) {
       PmSub sub = desc_sub(S, pb0 + k);
       sub.kind = __builtin_amdgcn_readfirstlane(sub.kind);
       if (sub.kind != SUB_REAL) continue;
