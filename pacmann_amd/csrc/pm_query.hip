@@ -381,7 +381,7 @@ __global__ void __launch_bounds__(kBlock) k_match(PmStep S) {
 // and writes exactly the bits, records and predictions of match_role.
 template <int HPT>
 __global__ void __launch_bounds__(kBlock) k_match_part(PmStep S) {
-  constexpr int NT = kBlock, G = 8;
+  constexpr int NT = kBlock, G = 6;
   __shared__ uint32_t s_cand[G][NT / 64][6];
   const uint32_t p = blockIdx.y, blk = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t pb0 = desc_sb(S, p), pn = desc_sb(S, p + 1) - pb0;
