@@ -461,6 +461,29 @@ def test_search_sessions_batched(ctx, oracle, ngroups, nthreads):
         assert sess[i].PIR.stats()["PrepCount"] == o.pir().stats()["PrepCount"] > 1, i
 
 
+def test_search_sessions_batched_rejects(ctx):
+    """pm_search_loop_batched refuses sessions it cannot share a step between:
+    clients of different server DBs, a session twice, an unpreprocessed one."""
+    import pacmann_amd as pm
+    v, graph = small_graph(n=1024, seed=4)
+    bases = []
+    for seed in (1, 2):
+        b = pm.PIRGraphInfo(v, graph, pir_seed=seed, search_seed=seed, ctx=pm.Context(0))
+        b.Preprocess()
+        bases.append(b)
+    a, b = bases[0].Session(3, 3), bases[1].Session(4, 4)
+    for s_ in (a, b):
+        s_.Preprocess()
+    qs = np.stack([v[:2], v[:2]])
+    with pytest.raises(RuntimeError):
+        pm.search_loop_batched([a, b], qs, 10, 20, 3)
+    with pytest.raises(RuntimeError):
+        pm.search_loop_batched([a, a], qs, 10, 20, 3)
+    c = bases[0].Session(5, 5)   # not preprocessed
+    with pytest.raises(RuntimeError):
+        pm.search_loop_batched([a, c], qs, 10, 20, 3)
+
+
 # ---------------------------------------------------------------------------
 # graph construction (build_graph.go) and kNN ground truth
 # ---------------------------------------------------------------------------
