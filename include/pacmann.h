@@ -164,6 +164,17 @@ int  pm_batchpir_query(pm_batchpir* h, const uint64_t* ids, uint64_t n, uint64_t
  * (the error batch-pir.go:205 swallows); those entries are zero. */
 int  pm_batchpir_query_ok(pm_batchpir* h, const uint64_t* ids, uint64_t n, uint64_t* out, uint8_t* ok);
 int  pm_batchpir_stats_get(pm_batchpir* h, pm_batchpir_stats* s);
+/* Many clients of one server answered together (batched serving, SURVEY.md
+ * §8f rank 2): every pm_batchpir_group_query call makes, for each client s,
+ * exactly the SimpleBatchPianoPIR.Query (batch-pir.go:170-248) call of its batch
+ * ids[s*n .. s*n+n), with all clients' sub-queries in ONE shared step over
+ * S x 16 partitions (on clients[0]'s stream).  out: S x n x DBEntrySize words,
+ * ok (nullable): S x n success flags, as pm_batchpir_query_ok.  Clients: the
+ * server and/or pm_batchpir_create_client handles of one server. */
+typedef struct pm_batchpir_group pm_batchpir_group;
+int  pm_batchpir_group_create(pm_batchpir** clients, uint32_t S, pm_batchpir_group** out);
+int  pm_batchpir_group_query(pm_batchpir_group* g, const uint64_t* ids, uint64_t n, uint64_t* out, uint8_t* ok);
+void pm_batchpir_group_destroy(pm_batchpir_group* g);
 int  pm_batchpir_subconfig(pm_batchpir* h, uint64_t partition, pm_pir_config* cfg);
 
 /* State export of one partition's client (test hook; sizes from the config):

@@ -108,6 +108,9 @@ SIGNATURES = {
     "pm_build_graph": (C.c_int, [vp, f32p, u64, u64, u64, C.c_float, u64, u32p, C.POINTER(dbl)]),
     "pm_search_loop_sessions": (C.c_int, [C.POINTER(vp), C.c_uint32, f32p, u64, C.c_int, C.c_int, C.c_int,
                                           i64p, C.POINTER(dbl), C.POINTER(dbl), C.POINTER(dbl)]),
+    "pm_batchpir_group_create": (C.c_int, [C.POINTER(vp), C.c_uint32, C.POINTER(vp)]),
+    "pm_batchpir_group_query": (C.c_int, [vp, u64p, u64, u64p, C.POINTER(C.c_uint8)]),
+    "pm_batchpir_group_destroy": (None, [vp]),
     "pm_search_loop_batched": (C.c_int, [C.POINTER(vp), C.c_uint32, f32p, u64, C.c_int, C.c_int, C.c_int, C.c_uint32,
                                          C.c_uint32, i64p, C.POINTER(dbl), C.POINTER(dbl), C.POINTER(dbl)]),
 }
@@ -475,6 +478,37 @@ class SimpleBatchPianoPIR:
 # ---------------------------------------------------------------------------
 # graphann
 # ---------------------------------------------------------------------------
+class BatchPIRGroup:
+    """Clients of one server answered together (pm_batchpir_group_*): each
+    Query call is, for every client s, its SimpleBatchPianoPIR.Query of
+    ids[s], with all clients' sub-queries in one shared step."""
+
+    def __init__(self, clients):
+        self.clients = list(clients)   # kept alive while the group exists
+        hs = (vp * len(self.clients))(*[c.h for c in self.clients])
+        h = vp()
+        _check(lib().pm_batchpir_group_create(hs, len(self.clients), C.byref(h)))
+        self.h = h
+        self.E = self.clients[0].E
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().pm_batchpir_group_destroy(self.h)
+        self.h = None
+
+    def QueryWithMask(self, ids):
+        """ids [S, n] -> (entries [S, n, DBEntrySize] uint64, ok [S, n] bool)."""
+        ids = np.ascontiguousarray(ids, dtype=np.uint64)
+        S, n = ids.shape
+        if S != len(self.clients):
+            raise ValueError("one row of ids per client")
+        out = np.zeros((S, n, self.E), dtype=np.uint64)
+        ok = np.zeros((S, n), dtype=np.uint8)
+        _check(lib().pm_batchpir_group_query(self.h, _p(ids, u64p), n, _p(out, u64p),
+                                             ok.ctypes.data_as(C.POINTER(C.c_uint8))))
+        return out, ok.astype(bool)
+
+
 class PIRGraphInfo:
     """PIRGraphInfo (private-search.go:336-531) wrapped in GraphANNFrontend
     (graphann/search.go:69-245).  nonprivate=True gives BasicGraphInfo-style

@@ -1834,41 +1834,62 @@ struct StepGroup {
   std::vector<PmSub> subs;
   std::vector<uint32_t> sb, base;
   std::vector<uint64_t> gen;   // each session's Engine::prep_gen at the last upload of its parts
+  std::vector<Engine*> es;     // the clients (batch PIR engines) sharing the steps
+  std::vector<const float*> qv;   // each client's search query on the device (null: no distances)
+  bool rows_partial = false;   // graph search: only the neighbour words of each row go to the host
   // the sessions' queries and start sets, scored in ONE k_l2_rows launch per query
   uint32_t ns = 0;
   DevBuf qbuf, start_ids, start_dist;
   HostBuf qstage;   // [S][dim] queries, then [S][ns] start-set distances
 };
 
-static int group_upload_parts(StepGroup& G, pm_graph** gs) {
+static int group_upload_parts(StepGroup& G) {
   std::vector<PmPart> v;
   v.reserve((size_t)G.S * G.P);
   for (uint32_t s = 0; s < G.S; ++s) {
-    Engine* e = &gs[s]->pir->e;
+    Engine* e = G.es[s];
     for (uint32_t p = 0; p < G.P; ++p) {
       PmPart d = e->parts[p].d;
-      d.qv = gs[s]->qdev();
+      d.qv = G.qv.empty() ? nullptr : G.qv[s];
       v.push_back(d);
     }
   }
   HIPCHK(hipMemcpyAsync(G.parts_d.p, v.data(), v.size() * sizeof(PmPart), hipMemcpyHostToDevice, G.c->stream));
   HIPCHK(hipStreamSynchronize(G.c->stream));
   G.gen.resize(G.S);
-  for (uint32_t s = 0; s < G.S; ++s) G.gen[s] = gs[s]->pir->e.prep_gen;
+  for (uint32_t s = 0; s < G.S; ++s) G.gen[s] = G.es[s]->prep_gen;
   return 0;
 }
 
-// One shared step over the sessions whose sub-queries are ready (in[s]).
-static int group_step(StepGroup& G, pm_graph** gs, const std::vector<char>& in) {
+// Common setup of a step group over clients of one server (same DB, shard
+// and parameters): device buffers and the clients' parts.
+static int group_init(StepGroup& G, pm_ctx* c) {
+  G.c = c;
+  G.S = (uint32_t)G.es.size();
+  const Engine& e = *G.es[0];
+  G.P = (uint32_t)e.P; G.maxPH = e.maxPH; G.maxSS = e.maxSS; G.E = (uint32_t)e.E;
+  HIPCHK(hipSetDevice(c->device));
+  CHK(G.parts_d.reserve((size_t)G.S * G.P * sizeof(PmPart)));
+  CHK(G.done.reserve(4 * (3 + 65536)));
+  const uint32_t init[3] = {1u << 31, 0, 0};
+  HIPCHK(hipMemcpy(G.done.p, init, sizeof init, hipMemcpyHostToDevice));
+  return group_upload_parts(G);
+}
+
+// One shared step over the clients whose sub-queries are ready (in[s]).
+static int group_step(StepGroup& G, const std::vector<char>& in) {
   pm_ctx* c = G.c;
   hipStream_t st = c->stream;
+  bool stale = false;   // a client re-preprocessed since its parts were copied
+  for (uint32_t s = 0; s < G.S; ++s) stale |= G.es[s]->prep_gen != G.gen[s];
+  if (stale) CHK(group_upload_parts(G));
   G.subs.clear();
   G.sb.assign(1, 0);
   G.base.assign(G.S, 0);
   uint32_t max_per_part = 0, np_live = 0;
   double ans_bytes = 0;
   for (uint32_t s = 0; s < G.S; ++s) {
-    Engine* e = &gs[s]->pir->e;
+    Engine* e = G.es[s];
     G.base[s] = (uint32_t)G.subs.size();
     for (uint32_t p = 0; p < G.P; ++p) {
       if (in[s]) {
@@ -1925,7 +1946,7 @@ static int group_step(StepGroup& G, pm_graph** gs, const std::vector<char>& in) 
   S.res = G.res_d.as<PmRes>();
   S.ans = G.ans.as<uint64_t>();
   S.done = G.done.as<uint32_t>();
-  Engine* e0 = &gs[0]->pir->e;
+  Engine* e0 = G.es[0];
   S.db = e0->db->as<uint64_t>();
   S.q = nullptr;   // each partition's PmPart::qv
   S.hdr_h = G.out_h.as<PmOutHdr>();
@@ -1944,7 +1965,7 @@ static int group_step(StepGroup& G, pm_graph** gs, const std::vector<char>& in) 
     const size_t end = std::min<size_t>(G.E * 8, off + std::min<size_t>(e0->pf_len, G.E * 8));
     S.pf_w0 = (uint32_t)(off / 8);
     S.pf_w1 = (uint32_t)((end + 7) / 8);
-    S.rows_partial = !c->verify_rows && !c->debug_cache ? 1u : 0u;   // graph search: neighbour lists only
+    S.rows_partial = G.rows_partial && !c->verify_rows && !c->debug_cache ? 1u : 0u;
   }
   auto t0 = Clock::now();
   uint32_t nreal = 0;
@@ -1968,18 +1989,18 @@ static int group_step(StepGroup& G, pm_graph** gs, const std::vector<char>& in) 
 // Session s's share of the last shared step: wait for its results (tokens and
 // row checksums, polled by the session's own worker, so a team checks its
 // sub-queries in parallel) and update its host mirrors.
-static int group_collect(StepGroup& G, pm_graph** gs, uint32_t s) {
-  Engine* e = &gs[s]->pir->e;
+static int group_collect(StepGroup& G, uint32_t s) {
+  Engine* e = G.es[s];
   const uint32_t n = (uint32_t)e->subs.size();
   PmOutHdr* hdr = G.out_h.as<PmOutHdr>();
   uint64_t* rows = (uint64_t*)(G.out_h.as<char>() + G.subs.size() * sizeof(PmOutHdr));
   auto t_wait = Clock::now();
-  CHK(wait_step(gs[s]->ctx, hdr + G.base[s], n, G.token, (const char*)(rows + (uint64_t)G.base[s] * G.E),
+  CHK(wait_step(e->ctx, hdr + G.base[s], n, G.token, (const char*)(rows + (uint64_t)G.base[s] * G.E),
                 (size_t)G.E * 8, (size_t)G.pf_w0 * 8, (size_t)(G.pf_w1 - G.pf_w0) * 8, G.c->stream));
-  gs[s]->ctx->host_add(HT_STEP_WAIT, ms_since(t_wait));
+  e->ctx->host_add(HT_STEP_WAIT, ms_since(t_wait));
   auto tp = Clock::now();
   post_results(e, hdr, rows, n, G.base[s], G.token);
-  gs[s]->ctx->host_add(HT_STEP_POST, ms_since(tp));
+  e->ctx->host_add(HT_STEP_POST, ms_since(tp));
   return 0;
 }
 
@@ -2044,19 +2065,10 @@ static int group_prep(StepGroup& G, pm_graph** gs, const std::vector<char>& need
 static int run_batched_team(pm_graph** gs, uint32_t S, const float* queries, uint64_t q, int k, int step,
                             int parallel, uint32_t T, int64_t* answers, double* mt_out) {
   StepGroup G;
-  G.c = gs[0]->ctx;
-  G.S = S;
-  {
-    const Engine& e = gs[0]->pir->e;
-    G.P = (uint32_t)e.P; G.maxPH = e.maxPH; G.maxSS = e.maxSS; G.E = (uint32_t)e.E; G.dim = (uint32_t)gs[0]->dim;
-  }
-  HIPCHK(hipSetDevice(G.c->device));
-  CHK(G.parts_d.reserve((size_t)S * G.P * sizeof(PmPart)));
-  CHK(G.done.reserve(4 * (3 + 65536)));
-  {
-    const uint32_t init[3] = {1u << 31, 0, 0};
-    HIPCHK(hipMemcpy(G.done.p, init, sizeof init, hipMemcpyHostToDevice));
-  }
+  G.dim = (uint32_t)gs[0]->dim;
+  G.rows_partial = true;   // GetVertexInfo reads the neighbour lists only
+  for (uint32_t i = 0; i < S; ++i) G.es.push_back(&gs[i]->pir->e);
+  HIPCHK(hipSetDevice(gs[0]->ctx->device));
   for (uint32_t i = 0; i < S; ++i) HIPCHK(hipStreamSynchronize(gs[i]->ctx->stream));
   G.ns = (uint32_t)gs[0]->start.size();
   for (uint32_t i = 0; i < S; ++i)
@@ -2074,8 +2086,11 @@ static int run_batched_team(pm_graph** gs, uint32_t S, const float* queries, uin
     pm_graph** gs; uint32_t S;
     ~Unshare() { for (uint32_t i = 0; i < S; ++i) gs[i]->q_shared = nullptr; }
   } unshare{gs, S};
-  for (uint32_t i = 0; i < S; ++i) gs[i]->q_shared = G.qbuf.as<float>() + (uint64_t)i * G.dim;
-  CHK(group_upload_parts(G, gs));
+  for (uint32_t i = 0; i < S; ++i) {
+    gs[i]->q_shared = G.qbuf.as<float>() + (uint64_t)i * G.dim;
+    G.qv.push_back(gs[i]->qdev());
+  }
+  CHK(group_init(G, gs[0]->ctx));
   T = std::max(1u, std::min(T, S));
   std::vector<char> fast(S, 0), need_prep(S, 0);
   std::vector<double> mt(S, 0.0);
@@ -2122,14 +2137,8 @@ static int run_batched_team(pm_graph** gs, uint32_t S, const float* queries, uin
         }
         bar.wait();
         if (w == 0) {
-          bool stale = false;   // a client re-preprocessed since the parts were copied
-          for (uint32_t s = 0; s < S; ++s) stale |= gs[s]->pir->e.prep_gen != G.gen[s];
-          if (stale && !err.load()) {
-            const int rc = group_upload_parts(G, gs);
-            if (rc) set_err(rc, 0);
-          }
           if (!err.load()) {
-            const int rc = group_step(G, gs, fast);
+            const int rc = group_step(G, fast);
             if (rc) set_err(rc, 0);
           }
           stop.store(err.load() != 0);
@@ -2139,7 +2148,7 @@ static int run_batched_team(pm_graph** gs, uint32_t S, const float* queries, uin
         for (uint32_t s = w; s < S && !err.load(); s += T) {   // rows -> neighbours, known set
           pm_graph* g = gs[s];
           if (fast[s]) {   // this client's share of the shared step's results
-            const int rw = group_collect(G, gs, s);
+            const int rw = group_collect(G, s);
             if (rw) { set_err(rw, s); break; }
           }
           const int rc = gvi_post(g, true, fast[s]);
@@ -2172,6 +2181,64 @@ static int run_batched_team(pm_graph** gs, uint32_t S, const float* queries, uin
   if (err.load()) return fail(err.load(), err_msg);
   HIPCHK(hipStreamSynchronize(G.c->stream));
   for (uint32_t s = 0; s < S; ++s) mt_out[s] = mt[s];
+  return 0;
+}
+
+// ---- SimpleBatchPianoPIR clients served together (the batch API) --------
+// S clients of one server (pm_batchpir_create_client): every call answers one
+// batch of n ids per client (SimpleBatchPianoPIR.Query, batch-pir.go:170-248,
+// per client) with ONE shared step over all their partitions.
+struct pm_batchpir_group {
+  StepGroup G;
+  std::vector<char> fast;
+};
+extern "C" int pm_batchpir_group_create(pm_batchpir** clients, uint32_t S, pm_batchpir_group** out) {
+  if (!clients || !S || !out) return fail(PM_EINVAL, "NULL argument");
+  for (uint32_t i = 0; i < S; ++i) {
+    if (!clients[i]) return fail(PM_EINVAL, "NULL client");
+    const Engine& a = clients[0]->e;
+    const Engine& b = clients[i]->e;
+    if (a.db.get() != b.db.get() || a.P != b.P || a.E != b.E || a.N != b.N || a.shard != b.shard ||
+        a.nshards != b.nshards || b.ctx->device != a.ctx->device || !b.is_batch)
+      return fail(PM_EINVAL, "grouped clients must be batch PIR clients of one server on one device");
+    for (uint32_t j = 0; j < i; ++j)
+      if (clients[j] == clients[i]) return fail(PM_EINVAL, "a client appears twice");
+  }
+  pm_batchpir_group* h = new pm_batchpir_group();
+  for (uint32_t i = 0; i < S; ++i) h->G.es.push_back(&clients[i]->e);
+  h->fast.assign(S, 0);
+  for (uint32_t i = 0; i < S; ++i) {
+    const hipError_t e = hipStreamSynchronize(clients[i]->e.ctx->stream);
+    if (e != hipSuccess) { delete h; return fail(PM_EHIP, hipGetErrorString(e)); }
+  }
+  if (int r = group_init(h->G, clients[0]->e.ctx)) { delete h; return r; }
+  *out = h;
+  return 0;
+}
+extern "C" void pm_batchpir_group_destroy(pm_batchpir_group* h) { delete h; }
+extern "C" int pm_batchpir_group_query(pm_batchpir_group* h, const uint64_t* ids, uint64_t n, uint64_t* out,
+                                       uint8_t* ok) {
+  if (!h || (!ids && n) || (!out && n)) return fail(PM_EINVAL, "NULL argument");
+  StepGroup& G = h->G;
+  const uint64_t E = G.E;
+  for (uint32_t s = 0; s < G.S; ++s) {   // bucketing; clients at a partition's budget go alone
+    Engine* e = G.es[s];
+    bool f = false;
+    CHK(bq_prepare(e, ids + (uint64_t)s * n, n, &f));
+    h->fast[s] = f;
+    if (!f)
+      CHK(batch_query_impl(e, ids + (uint64_t)s * n, n, out + (uint64_t)s * n * E, nullptr, 0, nullptr, nullptr,
+                           ok ? ok + (uint64_t)s * n : nullptr));
+  }
+  CHK(group_step(G, h->fast));
+  for (uint32_t s = 0; s < G.S; ++s) {
+    if (!h->fast[s]) continue;
+    Engine* e = G.es[s];
+    CHK(group_collect(G, s));
+    bq_emit_fast(e, ids + (uint64_t)s * n, n, out + (uint64_t)s * n * E, nullptr, nullptr,
+                 ok ? ok + (uint64_t)s * n : nullptr);
+    CHK(bq_tail(e, n));
+  }
   return 0;
 }
 

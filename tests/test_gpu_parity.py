@@ -461,6 +461,42 @@ def test_search_sessions_batched(ctx, oracle, ngroups, nthreads):
         assert sess[i].PIR.stats()["PrepCount"] == o.pir().stats()["PrepCount"] > 1, i
 
 
+def test_batch_pir_group(ctx, oracle):
+    """pm_batchpir_group_query: five clients of one server answered with one
+    shared step per call; every client's entries, success flags, counters and
+    re-preprocessing equal an independent oracle SimpleBatchPianoPIR with its
+    seed, through the batch layer's own re-preprocessing trigger."""
+    import pacmann_amd as pm
+    N, E, B = 30_000, 8, 8
+    db = rand_db(N, E, 91)
+    server = pm.SimpleBatchPianoPIR(N, E * 8, B, db, 8, seed=SEED, ctx=ctx)
+    server.Preprocessing()
+    seeds = [SEED, 11, 12, 13, 14]
+    clients = [server] + [server.Client(sd, pm.Context(0)) for sd in seeds[1:]]
+    for c in clients[1:]:
+        c.Preprocessing()
+    grp = pm.BatchPIRGroup(clients)
+    ors = [oracle.SimpleBatchPianoPIR(N, E * 8, B, db, 8, seed=sd) for sd in seeds]
+    for o in ors:
+        o.Preprocessing()
+    rng = np.random.default_rng(21)
+    maxq = server.SubConfig(0)["MaxQueryNum"]
+    for b in range(int(maxq // 3) + 6):
+        q = rng.integers(0, N, size=(len(clients), 3 * B), dtype=np.uint64)
+        q[:, 4] = q[:, 1]
+        out, ok = grp.QueryWithMask(q)
+        for i, o in enumerate(ors):
+            want, _ = o.Query(q[i])
+            assert np.array_equal(out[i], want), (b, i)
+            rows = db.reshape(N, E)[q[i].astype(np.int64)]
+            assert np.array_equal(out[i][ok[i]], rows[ok[i]]), (b, i)
+            assert not out[i][~ok[i]].any(), (b, i)
+    for c, o in zip(clients, ors):
+        for k in ("FinishedBatchNum", "QueriesMadeInPartition", "PrepCount"):
+            assert c.stats()[k] == o.stats()[k], k
+        assert c.stats()["PrepCount"] > 1
+
+
 def test_search_sessions_batched_rejects(ctx):
     """pm_search_loop_batched refuses sessions it cannot share a step between:
     clients of different server DBs, a session twice, an unpreprocessed one."""
