@@ -226,6 +226,9 @@ __device__ __forceinline__ void wait_vmcnt(uint32_t n) {
   }
 }
 
+#ifndef PM_FOLD_FLIP
+#define PM_FOLD_FLIP 1
+#endif
 template <int SW, int G, int NB>   // G = 16-B staging loads per thread per chunk; NB LDS buffers
 __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_pipe(const PmPart* __restrict__ parts,
                                                                  const uint64_t* __restrict__ db,
@@ -291,6 +294,12 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_pipe(const PmPart* _
     __builtin_amdgcn_s_barrier();
   };
   wait_chunk(0);
+  // LDS banking: a ds_read_b128 is served in 16-lane groups, and a SW = 4 row
+  // (32 B) starts on one of 8 of the 16 16-B slots of the 256-B bank row, so 16
+  // random rows pile up ~4.4-deep on 8 slots.  Odd lanes read the row's halves
+  // in the other order (their accumulator holds words 2-3 first): each group's
+  // 8 even and 8 odd lanes then fall on disjoint slot sets (~3.1-deep).
+  const uint32_t fl = (SW == 4 && PM_FOLD_FLIP) ? ((tid & 1u) << 1) : 0u;
 #ifndef PM_FOLD_ABL
 #define PM_FOLD_ABL 0   // diagnostic builds: 1 = no LDS compute, 2 = no staging in the loop
 #endif
@@ -304,7 +313,7 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_pipe(const PmPart* _
       const uint64_t* row = L + (t == kSkip ? CS : t) * SW;
 #pragma unroll
       for (int x = 0; x < SW; x += 2) {
-        const u64x2 y = *reinterpret_cast<const u64x2*>(row + x);
+        const u64x2 y = *reinterpret_cast<const u64x2*>(row + (x ^ fl));
         acc[k][x] ^= y.x;
         acc[k][x + 1] ^= y.y;
       }
@@ -316,7 +325,8 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_pipe(const PmPart* _
     if (hk[k] >= h1) continue;
     PM_G uint64_t* dst = P.parity + (uint64_t)hk[k] * E + w;
 #pragma unroll
-    for (int x = 0; x < SW; x += 2) *reinterpret_cast<PM_G u64x2*>(dst + x) = u64x2{acc[k][x], acc[k][x + 1]};
+    for (int x = 0; x < SW; x += 2)
+      *reinterpret_cast<PM_G u64x2*>(dst + (x ^ fl)) = u64x2{acc[k][x], acc[k][x + 1]};
     if (w == 0)   // xorSlices leaves the words past len&~3 zero
       for (uint32_t t = E & ~3u; t < E; ++t) P.parity[(uint64_t)hk[k] * E + t] = 0;
   }
