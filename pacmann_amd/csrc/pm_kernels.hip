@@ -229,7 +229,9 @@ __device__ __forceinline__ void wait_vmcnt(uint32_t n) {
 #ifndef PM_FOLD_FLIP
 #define PM_FOLD_FLIP 1
 #endif
-template <int SW, int G, int NB>   // G = 16-B staging loads per thread per chunk; NB LDS buffers
+// G = 16-B staging loads per thread per chunk; NB LDS buffers; D chunks folded
+// between two workgroup barriers
+template <int SW, int G, int NB, int D = 1>
 __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_pipe(const PmPart* __restrict__ parts,
                                                                  const uint64_t* __restrict__ db,
                                                                  const uint64_t* __restrict__ zero16,
@@ -284,16 +286,18 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_pipe(const PmPart* _
     }
   };
   for (uint32_t x = tid; x < NB * SW; x += kFoldThreads) fold_lds[(x / SW) * BUFW + CS * SW + x % SW] = 0;
-  // chunks 0 .. NB-2 in flight; chunk c + NB - 1 is issued while chunk c is folded
-  for (uint32_t c = 0; c + 1 < (uint32_t)NB && c < SS; ++c) stage(c, c);
+  // chunks 0 .. NB-D-1 in flight; chunks c+NB-D .. c+NB-1 are issued while
+  // chunks c .. c+D-1 are folded
+  static_assert(NB > D, "fold pipeline: more buffers than chunks per barrier");
+  for (uint32_t c = 0; c + D < (uint32_t)NB && c < SS; ++c) stage(c, c);
   const uint32_t ops = G + (tab_wave ? 1 : 0);   // loads per chunk of this wave
-  auto wait_chunk = [&](uint32_t next) {   // chunk `next` landed; later ones may stay in flight
-    const uint32_t issued = min(SS, next + NB - 1);   // chunks issued so far
-    wait_vmcnt(issued > next + 1 ? (issued - next - 1) * ops : 0);
+  auto wait_chunks = [&](uint32_t next, uint32_t issued) {   // chunks next .. next+D-1 landed
+    const uint32_t need = min(SS, next + D);
+    wait_vmcnt(issued > need ? (issued - need) * ops : 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   };
-  wait_chunk(0);
+  wait_chunks(0, min(SS, (uint32_t)(NB - D)));
   // LDS banking: a ds_read_b128 is served in 16-lane groups, and a SW = 4 row
   // (32 B) starts on one of 8 of the 16 16-B slots of the 256-B bank row, so 16
   // random rows pile up ~4.4-deep on 8 slots.  Odd lanes read the row's halves
@@ -303,8 +307,14 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_pipe(const PmPart* _
 #ifndef PM_FOLD_ABL
 #define PM_FOLD_ABL 0   // diagnostic builds: 1 = no LDS compute, 2 = no staging in the loop
 #endif
-  for (uint32_t c = 0; c < SS; ++c) {
-    if (PM_FOLD_ABL != 2 && c + NB - 1 < SS) stage(c + NB - 1, (c + NB - 1) % NB);
+  for (uint32_t c0 = 0; c0 < SS; c0 += D) {
+#pragma unroll
+    for (int j = 0; j < D; ++j)
+      if (PM_FOLD_ABL != 2 && c0 + NB - D + j < SS) stage(c0 + NB - D + j, (c0 + NB - D + j) % NB);
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+    const uint32_t c = c0 + j;
+    if (D > 1 && c >= SS) break;
     const uint64_t* L = fold_lds + (c % NB) * BUFW;
     const uint16_t* T = reinterpret_cast<const uint16_t*>(L + TABW);
 #pragma unroll
@@ -318,7 +328,8 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_pipe(const PmPart* _
         acc[k][x + 1] ^= y.y;
       }
     }
-    if (c + 1 < SS) wait_chunk(c + 1);
+    }
+    if (c0 + D < SS) wait_chunks(c0 + D, min(SS, c0 + NB));
   }
 #pragma unroll
   for (int k = 0; k < kFoldHPT; ++k) {
@@ -594,11 +605,14 @@ void prep_fold(hipStream_t st, const PmPart* d, int np, uint32_t maxH, const uin
 #ifndef PM_FOLD_NB512
 #define PM_FOLD_NB512 4
 #endif
+#ifndef PM_FOLD_D512
+#define PM_FOLD_D512 1
+#endif
     const uint32_t nb = maxCS == 512 ? PM_FOLD_NB512 : 3;   // LDS buffers: <= 150 KB
     const size_t lds = (size_t)nb * ((maxCS + 1) * psw + kPipeTabWords) * 8;
     const dim3 grid(cdiv(units, 8) * 8 * nsl), blk(kFoldThreads);
     if (maxCS == 512)
-      hipLaunchKernelGGL((k_prep_fold_pipe<4, 1, PM_FOLD_NB512>), grid, blk, lds, st, d, db, zero16, E, ng, nsl,
+      hipLaunchKernelGGL((k_prep_fold_pipe<4, 1, PM_FOLD_NB512, PM_FOLD_D512>), grid, blk, lds, st, d, db, zero16, E, ng, nsl,
                          units);
     else if (maxCS == 1024)
       hipLaunchKernelGGL((k_prep_fold_pipe<4, 2, 3>), grid, blk, lds, st, d, db, zero16, E, ng, nsl, units);
