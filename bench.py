@@ -53,7 +53,7 @@ PROFILE_QUERIES = 8
 SESSIONS = 128  # client sessions per GPU
 GROUPS = 4      # lock-step groups (GPU_MAX_HW_QUEUES = 4 hardware queues per process)
 THREADS = 8     # host worker threads of the batched loop
-SYMBOLS = {"prep_fold": "void pm::k_prep_fold_pipe<4, 1, 4>(pm::PmPart const*, unsigned long const*, "
+SYMBOLS = {"prep_fold": "void pm::k_prep_fold_pipe<4, 1, 4, 1>(pm::PmPart const*, unsigned long const*, "
                         "unsigned long const*, unsigned int, unsigned int, unsigned int, unsigned int)",
            "answer": "void pm::k_answer<2>(pm::PmStep)", "step": "void pm::k_step<2>(pm::PmStep)", "resolve": "void pm::k_resolve<true>(pm::PmStep)",
            "hint_match": "pm::k_match(pm::PmStep)", "prep_offsets": "pm::k_prep_offsets(pm::PmPart const*)",
