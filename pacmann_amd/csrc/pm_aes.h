@@ -1,11 +1,13 @@
 // pm_aes.h — AES-128-MMO PRF for gfx950 VALU + LDS (no AES instructions on CDNA).
 //
 // Replaces aes128MMO / PRFEvalWithLongKeyAndTag (pianopir/aes_amd64.s:51-82,
-// pianopir/util.go:157-165).  One block per lane, T-table formulation with a
-// single table Te0 (rows 1-3 are byte rotations of it) held in LDS replicated
-// 64x so that lane l always reads bank (l & 31) of its 32-lane group: a
-// random-index ds_read_b32 is then conflict-free (bank = (addr/4) % 32,
-// MI355X_MICROARCH.md §LDS).  64 KiB of LDS per workgroup.  Bit-exact with AES-NI: the state is kept as
+// pianopir/util.go:157-165).  One block per lane, T-table formulation with two
+// tables in LDS, Te0 and Te2 = rotl16(Te0), each replicated 32x so that lane l
+// always reads bank (l & 31) of its 32-lane group: a random-index ds_read_b32
+// is then conflict-free (bank = (addr/4) % 32, MI355X_MICROARCH.md §LDS).
+// With Te2 a round column is Te0[a] ^ Te2[c] ^ rotl8(Te0[b] ^ Te2[d]) ^ rk:
+// one rotation instead of three (the kernel is VALU-bound).  64 KiB of LDS per
+// workgroup.  Bit-exact with AES-NI: the state is kept as
 // four little-endian column words, exactly the byte order AESENC works on.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -51,10 +53,10 @@ struct AesTables {
   static constexpr uint8_t rotl(uint8_t v, int n) { return (uint8_t)((v << n) | (v >> (8 - n))); }
 };
 
-// Te0 replicated 64x, entry b of lane l's copy at byte (b << 8) | (l << 2): a
-// lookup address is ONE v_perm_b32 (the state byte into byte 1, the lane
-// offset in byte 0), and a ds_read_b32 lane group (32 lanes, bank =
-// (a/4) mod 32) reads 32 distinct banks.  64 KiB.
+// Entry b of lane l's copies: Te0 at byte (b << 8) | ((l & 31) << 2), Te2 at
+// that | 0x80.  A lookup address is ONE v_perm_b32 (the state byte into byte
+// 1, the lane offset with the table bit in byte 0), and a ds_read_b32 lane
+// group (32 lanes, bank = (a/4) mod 32) reads 32 distinct banks.  64 KiB.
 constexpr int kTeLdsWords = 256 * 64;
 
 // Device copy of the tables (one per translation unit; read only by aes_lds_init).
@@ -65,15 +67,25 @@ __device__ __forceinline__ uint32_t rotl32(uint32_t x, int n) { return (x << n) 
 
 // Fill the replicated table.  Call with the whole block, then __syncthreads().
 __device__ __forceinline__ void aes_lds_init(uint32_t* te, const uint32_t* __restrict__ g_te0) {
-  for (int i = threadIdx.x; i < kTeLdsWords; i += blockDim.x) te[i] = g_te0[i >> 6];
+  for (int i = threadIdx.x; i < kTeLdsWords; i += blockDim.x) {
+    const uint32_t t = g_te0[i >> 6];
+    te[i] = (i & 32) ? rotl32(t, 16) : t;
+  }
 }
+
 
 struct AesLane {
   const uint32_t* te;
-  uint32_t lane;   // (threadIdx.x & 63) << 2: this lane's byte offset within an entry row
-  // Te0[byte k of s] from this lane's copy: address = (byte << 8) | lane, one v_perm_b32
+  uint32_t lane;    // (threadIdx.x & 31) << 2: this lane's byte offset within an entry row
+  uint32_t lane2;   // lane | 0x80: its Te2 copy
+  __device__ AesLane(const uint32_t* t, uint32_t tid) : te(t), lane((tid & 31u) << 2), lane2(((tid & 31u) << 2) | 0x80u) {}
+  // Te0 / Te2 [byte k of s] from this lane's copy: address = (byte << 8) | lane, one v_perm_b32
   template <int K> __device__ __forceinline__ uint32_t Tk(uint32_t s) const {
     const uint32_t a = __builtin_amdgcn_perm(s, lane, 0x0c0c0000u | ((4u + K) << 8));
+    return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(te) + a);
+  }
+  template <int K> __device__ __forceinline__ uint32_t T2k(uint32_t s) const {
+    const uint32_t a = __builtin_amdgcn_perm(s, lane2, 0x0c0c0000u | ((4u + K) << 8));
     return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(te) + a);
   }
   template <int K> __device__ __forceinline__ uint32_t Sk(uint32_t s) const { return (Tk<K>(s) >> 8) & 0xffu; }
@@ -84,14 +96,12 @@ __device__ __forceinline__ void aes_rounds(const AesLane& A, const uint32_t* __r
                                            uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3) {
 #pragma unroll
   for (int r = 1; r < 10; ++r) {
-    uint32_t t0 = A.Tk<0>(s0) ^ rotl32(A.Tk<1>(s1), 8) ^ rotl32(A.Tk<2>(s2), 16) ^ rotl32(A.Tk<3>(s3), 24) ^
-                  rk[4 * r + 0];
-    uint32_t t1 = A.Tk<0>(s1) ^ rotl32(A.Tk<1>(s2), 8) ^ rotl32(A.Tk<2>(s3), 16) ^ rotl32(A.Tk<3>(s0), 24) ^
-                  rk[4 * r + 1];
-    uint32_t t2 = A.Tk<0>(s2) ^ rotl32(A.Tk<1>(s3), 8) ^ rotl32(A.Tk<2>(s0), 16) ^ rotl32(A.Tk<3>(s1), 24) ^
-                  rk[4 * r + 2];
-    uint32_t t3 = A.Tk<0>(s3) ^ rotl32(A.Tk<1>(s0), 8) ^ rotl32(A.Tk<2>(s1), 16) ^ rotl32(A.Tk<3>(s2), 24) ^
-                  rk[4 * r + 3];
+    // Te0[a] ^ rotl8(Te0[b]) ^ rotl16(Te0[c]) ^ rotl24(Te0[d]) ^ rk
+    //   = Te0[a] ^ Te2[c] ^ rotl8(Te0[b] ^ Te2[d]) ^ rk
+    uint32_t t0 = A.Tk<0>(s0) ^ A.T2k<2>(s2) ^ rotl32(A.Tk<1>(s1) ^ A.T2k<3>(s3), 8) ^ rk[4 * r + 0];
+    uint32_t t1 = A.Tk<0>(s1) ^ A.T2k<2>(s3) ^ rotl32(A.Tk<1>(s2) ^ A.T2k<3>(s0), 8) ^ rk[4 * r + 1];
+    uint32_t t2 = A.Tk<0>(s2) ^ A.T2k<2>(s0) ^ rotl32(A.Tk<1>(s3) ^ A.T2k<3>(s1), 8) ^ rk[4 * r + 2];
+    uint32_t t3 = A.Tk<0>(s3) ^ A.T2k<2>(s1) ^ rotl32(A.Tk<1>(s0) ^ A.T2k<3>(s2), 8) ^ rk[4 * r + 3];
     s0 = t0; s1 = t1; s2 = t2; s3 = t3;
   }
 }

@@ -40,7 +40,7 @@ __global__ void __launch_bounds__(kOffsBlock) k_prep_offsets(const PmPart* __res
   if (blockIdx.x * kOffsBlock >= H || c0 >= SS) return;   // block-uniform
   aes_lds_init(te, g_aes.te0);
   __syncthreads();
-  const AesLane A{te, (threadIdx.x & 63u) << 2};
+  const AesLane A(te, threadIdx.x);
   const uint32_t h = blockIdx.x * kOffsBlock + threadIdx.x;
   if (h >= H) return;
   const uint32_t mask = P.CS - 1;
@@ -554,7 +554,7 @@ __global__ void __launch_bounds__(kBlock) k_prf_batch(const uint32_t* __restrict
   aes_lds_init(te, g_aes.te0);
   if (threadIdx.x < 44) srk[threadIdx.x] = rk[threadIdx.x];
   __syncthreads();
-  const AesLane A{te, (threadIdx.x & 63u) << 2};
+  const AesLane A(te, threadIdx.x);
   for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock)
     out[i] = prf64(A, srk, tags[i], xs[i]);
 }
