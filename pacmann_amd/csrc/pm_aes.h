@@ -91,11 +91,12 @@ struct AesLane {
   template <int K> __device__ __forceinline__ uint32_t Sk(uint32_t s) const { return (Tk<K>(s) >> 8) & 0xffu; }
 };
 
-// Nine full rounds on state (s0..s3) with round keys rk[4..39].
+// Full rounds R0..9 on state (s0..s3) with round keys rk[4*R0..39].
+template <int R0 = 1>
 __device__ __forceinline__ void aes_rounds(const AesLane& A, const uint32_t* __restrict__ rk,
                                            uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3) {
 #pragma unroll
-  for (int r = 1; r < 10; ++r) {
+  for (int r = R0; r < 10; ++r) {
     // Te0[a] ^ rotl8(Te0[b]) ^ rotl16(Te0[c]) ^ rotl24(Te0[d]) ^ rk
     //   = Te0[a] ^ Te2[c] ^ rotl8(Te0[b] ^ Te2[d]) ^ rk
     uint32_t t0 = A.Tk<0>(s0) ^ A.T2k<2>(s2) ^ rotl32(A.Tk<1>(s1) ^ A.T2k<3>(s3), 8) ^ rk[4 * r + 0];
@@ -127,6 +128,35 @@ __device__ __forceinline__ uint32_t prf_lo32(const AesLane& A, const uint32_t* _
   aes_rounds(A, rk, s0, s1, s2, s3);
   uint32_t c0 = (A.Sk<0>(s0) | (A.Sk<1>(s1) << 8) | (A.Sk<2>(s2) << 16) | (A.Sk<3>(s3) << 24)) ^ rk[40];
   return c0 ^ w0;
+}
+
+// PRF(tag, x) for a fixed tag over many x (the hint-table expansion, tag = the
+// hint, x = the chunk): block words w0 = x, w1 = tag << 3 (x < 2^32), so after
+// the whitening s0 = x ^ rk0 varies with x only, s1 = (tag << 3) ^ rk1 with the
+// tag only, and s2 = rk2, s3 = rk3 not at all.  Round 1's columns split into a
+// part of s0, s2, s3 (per x: R1Uniform, computed once per x for the whole
+// workgroup) and a part of s1 (per lane: R1Lane, once per tag).
+struct R1Uniform { uint32_t u0, u1, u2, u3; };
+__device__ __forceinline__ R1Uniform r1_uniform(const AesLane& A, const uint32_t* __restrict__ rk, uint32_t x) {
+  const uint32_t s0 = x ^ rk[0], s2 = rk[2], s3 = rk[3];
+  // rotl24(Te0[v]) = rotl8(Te2[v])
+  return R1Uniform{A.Tk<0>(s0) ^ A.T2k<2>(s2) ^ rotl32(A.T2k<3>(s3), 8) ^ rk[4],
+                   A.T2k<2>(s3) ^ rotl32(A.Tk<1>(s2) ^ A.T2k<3>(s0), 8) ^ rk[5],
+                   A.Tk<0>(s2) ^ A.T2k<2>(s0) ^ rotl32(A.Tk<1>(s3), 8) ^ rk[6],
+                   A.Tk<0>(s3) ^ rotl32(A.Tk<1>(s0) ^ A.T2k<3>(s2), 8) ^ rk[7]};
+}
+struct R1Lane { uint32_t v0, v1, v2, v3; };
+__device__ __forceinline__ R1Lane r1_lane(const AesLane& A, const uint32_t* __restrict__ rk, uint64_t tag) {
+  const uint32_t s1 = (uint32_t)(tag << 3) ^ rk[1];
+  return R1Lane{rotl32(A.Tk<1>(s1), 8), A.Tk<0>(s1), rotl32(A.T2k<3>(s1), 8), A.T2k<2>(s1)};
+}
+// = prf_lo32(A, rk, tag, x) given r1_uniform(x) and r1_lane(tag).
+__device__ __forceinline__ uint32_t prf_lo32_split(const AesLane& A, const uint32_t* __restrict__ rk,
+                                                   const R1Uniform& u, const R1Lane& v, uint32_t x) {
+  uint32_t s0 = u.u0 ^ v.v0, s1 = u.u1 ^ v.v1, s2 = u.u2 ^ v.v2, s3 = u.u3 ^ v.v3;
+  aes_rounds<2>(A, rk, s0, s1, s2, s3);
+  const uint32_t c0 = (A.Sk<0>(s0) | (A.Sk<1>(s1) << 8) | (A.Sk<2>(s2) << 16) | (A.Sk<3>(s3) << 24)) ^ rk[40];
+  return c0 ^ x;
 }
 
 }  // namespace pm

@@ -20,10 +20,13 @@ __device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
 //                 EntryXor), one lane per (hint, 16-B segment), parity held in
 //                 a register for the whole chunk sweep.  Gather-bound.
 // ---------------------------------------------------------------------------
-constexpr int kOffsChunksPerBlock = 32;
+#ifndef PM_OFFS_CHUNKS
+#define PM_OFFS_CHUNKS 8
+#endif
+constexpr int kOffsChunksPerBlock = PM_OFFS_CHUNKS;
 constexpr int kOffsBlock = 1024;   // 64 KiB of replicated table per workgroup: 16 waves share it
 
-// Initial PRF tables of every hint h < H (its tag is h) at 16 chunks per
+// Initial PRF tables of every hint h < H (its tag is h) at 8 chunks per
 // workgroup, written chunk-major (hint search) and hint-major (set
 // expansion).  Bound by the AES T-table lookups in LDS: the hint-major stores
 // are scattered 2-B writes (every lane on its own line, ~5x their bytes in
@@ -34,6 +37,7 @@ constexpr int kOffsBlock = 1024;   // 64 KiB of replicated table per workgroup: 
 // for the lookups' latency: 0.370 -> 0.335 ms at SIFT1M shape.
 __global__ void __launch_bounds__(kOffsBlock) k_prep_offsets(const PmPart* __restrict__ parts) {
   __shared__ uint32_t te[kTeLdsWords];
+  __shared__ R1Uniform r1u[kOffsChunksPerBlock];
   const PmPart& P = parts[blockIdx.z];
   const uint32_t H = P.H, SS = P.SS;
   const uint32_t c0 = blockIdx.y * kOffsChunksPerBlock;
@@ -41,15 +45,19 @@ __global__ void __launch_bounds__(kOffsBlock) k_prep_offsets(const PmPart* __res
   aes_lds_init(te, g_aes.te0);
   __syncthreads();
   const AesLane A(te, threadIdx.x);
+  const uint32_t c1 = min(SS, c0 + kOffsChunksPerBlock);
+  // round 1's chunk-dependent half, once per chunk for the workgroup (pm_aes.h)
+  if (threadIdx.x < c1 - c0) r1u[threadIdx.x] = r1_uniform(A, P.rk, c0 + threadIdx.x);
+  __syncthreads();
   const uint32_t h = blockIdx.x * kOffsBlock + threadIdx.x;
   if (h >= H) return;
   const uint32_t mask = P.CS - 1;
   const uint32_t own = h >= P.PH ? (h - P.PH) / P.Qpc : 0xffffffffu;
   uint16_t* o = P.tab;
   uint16_t* oT = P.tabT + (uint64_t)h * SS;
-  const uint32_t c1 = min(SS, c0 + kOffsChunksPerBlock);
+  const R1Lane r1v = r1_lane(A, P.rk, h);   // initial tag of hint h is h
   for (uint32_t c = c0; c < c1; ++c) {
-    uint16_t v = (uint16_t)(prf_lo32(A, P.rk, h, c) & mask);   // initial tag of hint h is h
+    uint16_t v = (uint16_t)(prf_lo32_split(A, P.rk, r1u[c - c0], r1v, c) & mask);
     v = (c == own) ? kSkip : v;
     o[(uint64_t)c * H + h] = v;   // chunk-major: hint search
     oT[c] = v;                    // hint-major: set expansion
