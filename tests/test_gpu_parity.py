@@ -497,6 +497,28 @@ def test_batch_pir_group(ctx, oracle):
         assert c.stats()["PrepCount"] > 1
 
 
+def test_batch_pir_group_rejects(ctx):
+    """pm_batchpir_group_create refuses clients of different servers and a
+    client listed twice; the ids must hold one row per client."""
+    import pacmann_amd as pm
+    N, E, B = 4_000, 4, 8
+    a = pm.SimpleBatchPianoPIR(N, E * 8, B, rand_db(N, E, 1), 8, seed=1, ctx=ctx)
+    b = pm.SimpleBatchPianoPIR(N, E * 8, B, rand_db(N, E, 2), 8, seed=1, ctx=ctx)
+    a.Preprocessing()
+    b.Preprocessing()
+    with pytest.raises(RuntimeError, match="one server"):
+        pm.BatchPIRGroup([a, b])
+    with pytest.raises(RuntimeError, match="twice"):
+        pm.BatchPIRGroup([a, a])
+    c = a.Client(5, pm.Context(0))
+    c.Preprocessing()
+    grp = pm.BatchPIRGroup([a, c])
+    with pytest.raises(ValueError):
+        grp.QueryWithMask(np.zeros((3, B), dtype=np.uint64))
+    out, ok = grp.QueryWithMask(np.arange(2 * B, dtype=np.uint64).reshape(2, B))
+    assert out.shape == (2, B, E) and ok.shape == (2, B)
+
+
 def test_search_sessions_batched_rejects(ctx):
     """pm_search_loop_batched refuses sessions it cannot share a step between:
     clients of different server DBs, a session twice, an unpreprocessed one."""
