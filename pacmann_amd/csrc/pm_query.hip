@@ -379,9 +379,15 @@ __global__ void __launch_bounds__(kBlock) k_match(PmStep S) {
 // hint) once for all of the partition's sub-queries, gathers each one's
 // PRF-table values (2 B per hint, G sub-queries' loads in flight together)
 // and writes exactly the bits, records and predictions of match_role.
+#ifndef PM_MATCHPART_WAVES
+#define PM_MATCHPART_WAVES 6
+#endif
+#ifndef PM_MATCHPART_G
+#define PM_MATCHPART_G 6
+#endif
 template <int HPT>
-__global__ void __launch_bounds__(kBlock) k_match_part(PmStep S) {
-  constexpr int NT = kBlock, G = 6;
+__global__ void __launch_bounds__(kBlock, PM_MATCHPART_WAVES) k_match_part(PmStep S) {
+  constexpr int NT = kBlock, G = PM_MATCHPART_G;
   __shared__ uint32_t s_cand[G][NT / 64][6];
   const uint32_t p = blockIdx.y, blk = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t pb0 = desc_sb(S, p), pn = desc_sb(S, p + 1) - pb0;
