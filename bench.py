@@ -9,12 +9,12 @@ private-search.go harness (run-private-search.sh flags).  Data are synthetic
 (no dataset in the image): a clustered SIFT-like mixture with integer values in
 [0,255] and a uniform random degree-32 graph (private-search.go:54-69).
 
-Serving: one GPU serves S client sessions at once (--sessions, default 128).
+Serving: one GPU serves S client sessions at once (--sessions, default 256).
 Every session is a full PianoPIR client (own keys, hint state, cache,
 maintenance) over the one server DB on the device.  Default (--mode batched,
 pm_search_loop_batched): the sessions run in G lock-step groups (--groups,
 default 4 = the process's hardware queues); every batch-PIR round of a group's
-sessions is ONE shared step over their S/G x 16 partitions, and 8 host worker
+sessions is ONE shared step over their S/G x 16 partitions, and 16 host worker
 threads (--threads) run the sessions' searches between steps, so one group's
 step overlaps the others' host work.  --mode concurrent: each session on its
 own host thread and stream with its own step launches (pm_search_loop_sessions).  One step = one private query per
@@ -50,9 +50,9 @@ PREP_KERNELS = ["prep_offsets", "prep_fold", "prep_repl", "l2_rows"]   # timed i
 STEP_KERNELS = ["step", "hint_match", "resolve", "gather", "answer"]   # timed in the profile window
 KERNELS = PREP_KERNELS + STEP_KERNELS
 PROFILE_QUERIES = 8
-SESSIONS = 128  # client sessions per GPU
+SESSIONS = 256  # client sessions per GPU (128: 9.9K q/s, 256: 11.0K, 384: 11.5K, 512: 11.3K)
 GROUPS = 4      # lock-step groups (GPU_MAX_HW_QUEUES = 4 hardware queues per process)
-THREADS = 8     # host worker threads of the batched loop
+THREADS = 16    # host worker threads of the batched loop (the box gives a GPU 16 host cores)
 SYMBOLS = {"prep_fold": "void pm::k_prep_fold_pipe<4, 1, 4, 1>(pm::PmPart const*, unsigned long const*, "
                         "unsigned long const*, unsigned int, unsigned int, unsigned int, unsigned int)",
            "answer": "void pm::k_answer<2>(pm::PmStep)", "step": "void pm::k_step<2>(pm::PmStep)", "resolve": "void pm::k_resolve<true>(pm::PmStep)",
