@@ -106,6 +106,7 @@ def pmc_traffic(kernel_symbol: str, grid: int | None = None):
 # shape (pianopir/pir_test.go:204-275): 3,201,821 entries of 112 words, BatchSize
 # 32, FailureProbLog2 8, 300 batches of 32 uniform ids.
 C2_N, C2_E, C2_B, C2_BATCHES = 3_201_821, 112, 32, 300
+C2_CLIENTS = 32   # clients of the server answered together (one shared step per round)
 
 
 def batch_pir_msmarco(ctx, with_cpu: bool):
@@ -150,6 +151,31 @@ def batch_pir_msmarco(ctx, with_cpu: bool):
         out["roofline"] = {"bound": "hbm", "kernel": "step", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "avg_ms": round(ms / n, 5),
                            "alg_bytes_per_launch": by / n}
+    # C2_CLIENTS clients of the one server DB, every batch of all of them answered
+    # together (pm_batchpir_group_*: one shared step per round)
+    clients = [g] + [g.Client(1000 + i, pm.Context(0)) for i in range(C2_CLIENTS - 1)]
+    for c in clients[1:]:
+        c.Preprocessing()
+    grp = pm.BatchPIRGroup(clients)
+    gb = rng.integers(0, C2_N, size=(C2_BATCHES + 10, C2_CLIENTS, C2_B)).astype(np.uint64)
+    for b in gb[:10]:
+        grp.QueryWithMask(b)
+    for c in clients:
+        c.ctx.sync()
+    t0 = time.perf_counter()
+    gbad = 0
+    for b in gb[10:]:
+        resp, ok = grp.QueryWithMask(b)
+        r0, ids0 = resp[:, 0], b[:, 0].astype(np.int64)   # every client's first response: zero or its entry
+        gbad += int(((r0 != rows[ids0]).any(axis=1) & ok[:, 0]).sum() + (r0[~ok[:, 0]] != 0).any())
+    for c in clients:
+        c.ctx.sync()
+    gon = time.perf_counter() - t0
+    out["clients_grouped"] = {"clients": C2_CLIENTS, "batches_per_client": C2_BATCHES,
+                              "batch_queries_per_s": round(C2_CLIENTS * C2_BATCHES / gon, 1),
+                              "ids_per_s": round(C2_CLIENTS * C2_BATCHES * C2_B / gon, 1),
+                              "ms_per_round": round(gon / C2_BATCHES * 1e3, 4), "first_response_mismatches": gbad}
+    del grp, clients
     if with_cpu:
         from oracle import oracle as O
         o = O.SimpleBatchPianoPIR(C2_N, C2_E * 8, C2_B, db, 8, seed=21)
