@@ -68,7 +68,7 @@ def make_data(rank: int, graph: str, ctx):
     (pm_build_graph: BuildGraph with exact kNN candidates in place of NGT), or
     the reference's synthetic-mode genRandomGraph (--graph random)."""
     import pacmann_amd as pm
-    from tests.datagen import random_graph, sift_like_vectors
+    from pacmann_amd.synth import random_graph, sift_like_vectors
     v = sift_like_vectors(N, DIM, seed=100 + rank)
     if graph == "random":
         return v, random_graph(N, M, seed=200 + rank), None

@@ -54,6 +54,7 @@ SIG = {
     "or_inner_product_bench": (C.c_uint32, [u64, u64, C.c_int]),
     "or_inner_product_scan": (C.c_uint32, [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), u64, u64, C.c_int]),
     "or_l2_batch": (None, [f32p, f32p, u64, u64, f32p]),
+    "or_set_prep_threads": (None, [C.c_int]),
     "or_pir_new": (vp, [u64, u64, u64p, u64, u64, u64]),
     "or_pir_free": (None, [vp]),
     "or_pir_preprocessing": (None, [vp]),
@@ -98,6 +99,12 @@ def lib():
             f.argtypes = a
         _lib = L
     return _lib
+
+
+def set_prep_threads(n: int) -> None:
+    """Threads of the hint fold in Preprocessing (1 = the reference's loop).
+    They split the hint space, so the client state is identical for any n."""
+    lib().or_set_prep_threads(int(n))
 
 
 def _p(a, t):

@@ -265,21 +265,28 @@ static void initialization(or_pir* c) {
   c->cache.clear();
 }
 
-// UpdatePreprocessing (pir.go:303-352)
-static void update_preprocessing(or_pir* c, uint64_t chunkId, const uint64_t* chunk) {
+// UpdatePreprocessing (pir.go:303-352), split in two: the hint fold of one
+// chunk restricted to hint indices [h0, h1) of the concatenated space
+// (primary hints 0..PH-1, then backup hint (g, j) at PH + g*Qpc + j), and the
+// replacement rows of that chunk.  Every hint's parity is its own XOR chain in
+// chunk order, so splitting the hint space over threads (the reference's
+// "TODO: using multiple threads", pir.go:282) gives bit-identical state.
+static void fold_chunk(or_pir* c, uint64_t chunkId, const uint64_t* chunk, uint64_t h0, uint64_t h1) {
   const uint64_t E = c->E, mask = c->CS - 1;
-  for (uint64_t i = 0; i < c->PH; ++i) {
+  for (uint64_t i = h0; i < std::min(h1, c->PH); ++i) {
     uint64_t off = prf(c->rk, c->ptag[i], chunkId) & mask;
     xor_slices(&c->parity[i * E], chunk + off * E, E);
   }
-  for (uint64_t g = 0; g < c->SS; ++g) {
-    if (g == chunkId) continue;
-    for (uint64_t j = 0; j < c->Qpc; ++j) {
-      uint64_t h = g * c->Qpc + j;
-      uint64_t off = prf(c->rk, c->btag[h], chunkId) & mask;
-      xor_slices(&c->bparity[h * E], chunk + off * E, E);
-    }
+  const uint64_t b0 = h0 > c->PH ? h0 - c->PH : 0, b1 = h1 > c->PH ? h1 - c->PH : 0;
+  for (uint64_t h = b0; h < b1; ++h) {
+    const uint64_t g = h / c->Qpc;
+    if (g == chunkId) continue;   // backup hints skip their own chunk
+    uint64_t off = prf(c->rk, c->btag[h], chunkId) & mask;
+    xor_slices(&c->bparity[h * E], chunk + off * E, E);
   }
+}
+static void replacement_rows(or_pir* c, uint64_t chunkId, const uint64_t* chunk) {
+  const uint64_t E = c->E, mask = c->CS - 1;
   for (uint64_t j = 0; j < c->Qpc; ++j) {
     uint64_t off = or_hash4(c->seed, DOM_REPL, c->partition, c->epoch - 1, chunkId * c->Qpc + j) & mask;
     c->ridx[chunkId * c->Qpc + j] = off + chunkId * c->CS;
@@ -287,21 +294,38 @@ static void update_preprocessing(or_pir* c, uint64_t chunkId, const uint64_t* ch
   }
 }
 
+static int g_prep_threads = 1;   // 1: the reference's single-threaded loop (batch-pir.go:16)
+extern "C" void or_set_prep_threads(int n) { g_prep_threads = n < 1 ? 1 : n; }
+
 // Preprocessing (pir.go:267-301)
 static void client_preprocessing(or_pir* c) {
   initialization(c);
   if (c->skipPrep) return;
-  const uint64_t E = c->E, len = c->N * E;
-  std::vector<uint64_t> tmp(c->CS * E);
-  for (uint64_t i = 0; i < c->SS; ++i) {
+  const uint64_t E = c->E, len = c->N * E, H = c->PH + c->SS * c->Qpc;
+  // chunk i, zero-padded past the end of the DB (pir.go:285-295)
+  std::vector<uint64_t> tail;
+  auto chunk_ptr = [&](uint64_t i) -> const uint64_t* {
     uint64_t start = i * c->CS, end = (i + 1) * c->CS;
-    if (end * E > len) {
-      for (uint64_t j = start * E; j < end * E; ++j) tmp[j - start * E] = j >= len ? 0 : c->rawDB[j];
-      update_preprocessing(c, i, tmp.data());
-    } else {
-      update_preprocessing(c, i, c->rawDB + start * E);
+    if (end * E <= len) return c->rawDB + start * E;
+    return tail.data() + (i - (len / E) / c->CS) * c->CS * E;
+  };
+  {   // every chunk that reaches past the end, padded once
+    const uint64_t first = (len / E) / c->CS;
+    if (first < c->SS) {
+      tail.assign((c->SS - first) * c->CS * E, 0);
+      for (uint64_t j = first * c->CS * E; j < len; ++j) tail[j - first * c->CS * E] = c->rawDB[j];
     }
   }
+  const int T = (int)std::min<uint64_t>((uint64_t)g_prep_threads, std::max<uint64_t>(1, H / 64));
+  auto work = [&](int t) {
+    const uint64_t h0 = H * t / T, h1 = H * (t + 1) / T;
+    for (uint64_t i = 0; i < c->SS; ++i) fold_chunk(c, i, chunk_ptr(i), h0, h1);
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; ++t) th.emplace_back(work, t);
+  work(0);
+  for (auto& x : th) x.join();
+  for (uint64_t i = 0; i < c->SS; ++i) replacement_rows(c, i, chunk_ptr(i));
 }
 
 // PrivateQuery (pir.go:65-88)

@@ -59,6 +59,8 @@ or_pir*  or_pir_new(uint64_t DBSize, uint64_t DBEntryByteNum, const uint64_t* ra
                     uint64_t FailureProbLog2, uint64_t seed, uint64_t partition);
 void     or_pir_free(or_pir*);
 void     or_pir_preprocessing(or_pir*);
+/* hint-fold threads of Preprocessing (default 1): split over hints, identical state */
+void     or_set_prep_threads(int n);
 void     or_pir_dummy_preprocessing(or_pir*);
 /* returns 0 ok, 1 budget exhausted, 2 chunk budget, 3 no hit hint, 4 idx out of range */
 int      or_pir_query(or_pir*, uint64_t idx, int real, uint64_t* out);

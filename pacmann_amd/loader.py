@@ -46,53 +46,67 @@ def _ext(path: str) -> str:
     return os.path.splitext(str(path))[1]
 
 
-def _uniform_records(raw: np.ndarray, item: int):
-    """If every record has the first record's dimension, the record count and
-    that dimension; else None (ragged file)."""
+def _map(path) -> np.ndarray:
+    """The file as a read-only byte map: only the pages a reader touches are
+    read, so asking for the first n records of a 132 GB bigann_base.bvecs
+    reads n records, not the file (loader.go streams them the same way)."""
+    if os.path.getsize(path) == 0:
+        return np.zeros(0, dtype=np.uint8)
+    return np.memmap(path, dtype=np.uint8, mode="r")
+
+
+def _uniform_prefix(raw: np.ndarray, item: int, n: int):
+    """(rows, d) when the first min(n, whole records) records all carry the
+    first record's dimension d and nothing past them could be read as another
+    record of the first n (so the record walk would return the same rows);
+    else None.  Only those rows' prefixes are inspected."""
     if raw.size < 4:
         return None
     d = int(raw[:4].view("<i4")[0])
     if d <= 0:
         return None
     rec = 4 + d * item
-    if raw.size % rec:
-        return None
-    k = raw.size // rec
-    dims = raw.reshape(k, rec)[:, :4].copy().view("<i4").ravel()
+    rows = min(n, raw.size // rec)
+    if rows < n and raw.size - rows * rec >= 4:
+        return None   # a partial tail record: let the walk decide what it holds
+    dims = np.asarray(raw[:rows * rec]).reshape(rows, rec)[:, :4].copy().view("<i4").ravel()
     if not (dims == d).all():
         return None
-    return k, d
+    return rows, d
 
 
-def _records(raw: np.ndarray, item: int):
-    """Yield (dim, payload bytes) per record; stops at a short record."""
+def _records(raw: np.ndarray, item: int, n: int):
+    """Yield (dim, payload bytes) for at most n records; stops at a short one."""
     off = 0
-    while off + 4 <= raw.size:
+    for _ in range(n):
+        if off + 4 > raw.size:
+            return
         d = int(raw[off:off + 4].view("<i4")[0])
         end = off + 4 + d * item
         if d < 0 or end > raw.size:
             return
-        yield d, raw[off + 4:end]
+        yield d, np.asarray(raw[off + 4:end])
         off = end
 
 
+def _body(raw: np.ndarray, rows: int, d: int, item: int) -> np.ndarray:
+    rec = 4 + d * item
+    return np.asarray(raw[:rows * rec]).reshape(rows, rec)[:, 4:]
+
+
 def load_bvecs(path, n: int, dim: int) -> np.ndarray:
-    raw = np.fromfile(path, dtype=np.uint8)
+    raw = _map(path)
     out = np.zeros((n, dim), dtype=np.float32)
-    u = _uniform_records(raw, 1)
+    u = _uniform_prefix(raw, 1, n)
     if u is not None:
-        k, d = u
-        rows = min(n, k)
-        body = raw[:rows * (4 + d)].reshape(rows, 4 + d)[:, 4:]
+        rows, d = u
         w = min(d, dim)
-        out[:rows, :w] = body[:, :w]
+        out[:rows, :w] = _body(raw, rows, d, 1)[:, :w]
         if rows < n:
             print("Unexpected EOF", file=sys.stderr)
         return out
     i = 0
-    for d, payload in _records(raw, 1):
-        if i == n:
-            break
+    for d, payload in _records(raw, 1, n):
         w = min(d, dim)
         out[i, :w] = payload[:w]
         i += 1
@@ -103,17 +117,12 @@ def load_bvecs(path, n: int, dim: int) -> np.ndarray:
 
 def load_fvecs(path, n: int, dim: int) -> np.ndarray:
     """Rows as stored (their own dimension); stops at the first short record."""
-    raw = np.fromfile(path, dtype=np.uint8)
-    u = _uniform_records(raw, 4)
+    raw = _map(path)
+    u = _uniform_prefix(raw, 4, n)
     if u is not None:
-        k, d = u
-        rows = min(n, k)
-        return raw[:rows * (4 + 4 * d)].reshape(rows, 4 + 4 * d)[:, 4:].copy().view("<f4").astype(np.float32)
-    rows = []
-    for d, payload in _records(raw, 4):
-        if len(rows) == n:
-            break
-        rows.append(payload.copy().view("<f4").astype(np.float32))
+        rows, d = u
+        return _body(raw, rows, d, 4).copy().view("<f4").astype(np.float32)
+    rows = [p.copy().view("<f4").astype(np.float32) for _, p in _records(raw, 4, n)]
     if not rows:
         return np.zeros((0, dim), dtype=np.float32)
     if len({r.size for r in rows}) != 1:
@@ -122,18 +131,14 @@ def load_fvecs(path, n: int, dim: int) -> np.ndarray:
 
 
 def load_ivecs(path, n: int, dim: int) -> np.ndarray:
-    raw = np.fromfile(path, dtype=np.uint8)
-    u = _uniform_records(raw, 4)
+    raw = _map(path)
+    u = _uniform_prefix(raw, 4, n)
     if u is not None:
-        k, d = u
-        if k < n:
-            raise LoaderError(f"Error reading vector {k}: unexpected EOF")
-        return raw[:n * (4 + 4 * d)].reshape(n, 4 + 4 * d)[:, 4:].copy().view("<u4").astype(np.int64)
-    rows = []
-    for d, payload in _records(raw, 4):
-        if len(rows) == n:
-            break
-        rows.append(payload.copy().view("<u4").astype(np.int64))
+        rows, d = u
+        if rows < n:
+            raise LoaderError(f"Error reading vector {rows}: unexpected EOF")
+        return _body(raw, rows, d, 4).copy().view("<u4").astype(np.int64)
+    rows = [p.copy().view("<u4").astype(np.int64) for _, p in _records(raw, 4, n)]
     if len(rows) < n:
         raise LoaderError(f"Error reading vector {len(rows)}: unexpected EOF")
     if len({r.size for r in rows}) != 1:

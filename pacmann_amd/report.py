@@ -174,88 +174,85 @@ def private_search(frontend, queries, *, k: int = 10, step: int = 20, parallel: 
 
 
 # ---------------------------------------------------------------------------
-# MS-MARCO end-to-end quality: vector ids -> passage ids -> MRR@k
-# (reproduction/msmarco/evaluate.py:26-120)
+# MS-MARCO end-to-end quality (behaviour of reproduction/msmarco/evaluate.py):
+# the search returns vector ids; a vector id names a passage through the
+# corpus's docid list; a query scores 1/rank of the first returned passage that
+# is its relevant one.  Written from that behaviour, not from the script.
 # ---------------------------------------------------------------------------
-def read_queries_tsv(path: str) -> list[tuple[str, str]]:
-    """`qid<TAB>text` per line, in file order (evaluate.py:26-34)."""
-    out = []
+def _lines(path):
     with open(path, encoding="utf-8") as fh:
-        for row, line in enumerate(fh, start=1):
-            parts = line.rstrip("\r\n").split("\t", 1)
-            if len(parts) != 2:
-                raise ValueError(f"query row {row} is malformed")
-            out.append((parts[0], parts[1]))
-    return out
+        yield from enumerate(fh, start=1)
+
+
+def read_queries_tsv(path: str) -> list[tuple[str, str]]:
+    """(qid, text) pairs of a tab-separated query file, kept in file order.
+    The text is everything after the first tab."""
+    pairs = []
+    for ln, raw in _lines(path):
+        qid, tab, text = raw.rstrip("\r\n").partition("\t")
+        if not tab:
+            raise ValueError(f"{path}:{ln}: expected 'qid<TAB>text'")
+        pairs.append((qid, text))
+    return pairs
 
 
 def read_qrels(path: str) -> dict[str, str]:
-    """TREC qrels `qid 0 docid rel`: the FIRST relevant docid of each query
-    counts (evaluate.py:37-45)."""
-    rel: dict[str, str] = {}
-    with open(path, encoding="utf-8") as fh:
-        for row, line in enumerate(fh, start=1):
-            f = line.split()
-            if len(f) != 4:
-                raise ValueError(f"qrels row {row} is malformed")
-            if f[0] not in rel:
-                rel[f[0]] = f[2]
-    return rel
+    """Relevance judgements in TREC form (`qid iter docid rel`).  A query keeps
+    the docid of its earliest line; later lines for it are ignored."""
+    first: dict[str, str] = {}
+    for ln, raw in _lines(path):
+        cols = raw.split()
+        if len(cols) != 4:
+            raise ValueError(f"{path}:{ln}: expected 4 columns, got {len(cols)}")
+        first.setdefault(cols[0], cols[2])
+    return first
 
 
 def read_results(path: str, query_count: int, k: int) -> np.ndarray:
-    """Search results as an int .npy of shape (queries, k) or a text file of k
-    ids per line (evaluate.py:48-71)."""
+    """The search output as a (query_count, k) int64 matrix, from either an
+    integer .npy array (detected by its magic bytes) or whitespace-separated
+    text with one query per line."""
     with open(path, "rb") as fh:
-        npy = fh.read(6) == b"\x93NUMPY"
-    if npy:
-        a = np.load(path, allow_pickle=False)
-        if a.shape != (query_count, k):
-            raise ValueError(f"result array has shape {a.shape}; expected {(query_count, k)}")
-        if not np.issubdtype(a.dtype, np.integer):
-            raise ValueError(f"result array must contain integers, found {a.dtype}")
-        return a.astype(np.int64)
-    rows = []
-    with open(path, encoding="utf-8") as fh:
-        for row, line in enumerate(fh, start=1):
-            vals = [int(x) for x in line.split()]
-            if len(vals) != k:
-                raise ValueError(f"result row {row} has {len(vals)} values; expected {k}")
-            rows.append(vals)
-    if len(rows) != query_count:
-        raise ValueError(f"result file has {len(rows)} rows; expected {query_count}")
-    return np.asarray(rows, dtype=np.int64)
+        is_npy = fh.read(6) == b"\x93NUMPY"
+    if is_npy:
+        arr = np.load(path, allow_pickle=False)
+        if arr.dtype.kind not in "iu":
+            raise ValueError(f"{path}: integer ids expected, array dtype is {arr.dtype}")
+    else:
+        table = [[int(tok) for tok in raw.split()] for _, raw in _lines(path)]
+        widths = {len(r) for r in table}
+        if widths - {k}:
+            bad = next(i for i, r in enumerate(table, start=1) if len(r) != k)
+            raise ValueError(f"{path}:{bad}: {len(table[bad - 1])} ids on the line, k is {k}")
+        arr = np.asarray(table, dtype=np.int64).reshape(len(table), k)
+    if arr.shape != (query_count, k):
+        raise ValueError(f"{path}: results are {arr.shape}, need {(query_count, k)}")
+    return arr.astype(np.int64)
 
 
 def mrr_at_k(results, queries: list[tuple[str, str]], qrels: dict[str, str], docids,
              output_docids: str | None = None) -> dict:
-    """MRR over all queries of 1 / (rank of the first returned passage equal to
-    the query's relevant one), 0 when none is in the list; ids outside the
-    corpus map to "INVALID_VECTOR_ID" and never match (evaluate.py:81-120).
-    A query without qrels is an error, as in the reference.  Optionally writes
-    the per-query docid listing in the reference's format."""
-    results = np.asarray(results)
-    n = len(docids)
-    total = 0.0
-    ranked = 0
-    lines = []
-    for qi, (qid, text) in enumerate(queries):
-        relevant = qrels[qid]
-        lines.append(f"Query: {qid} {text}")
-        hit = None
-        for rank, vid in enumerate(results[qi], start=1):
-            d = str(docids[vid]) if 0 <= vid < n else "INVALID_VECTOR_ID"
-            lines.append(d)
-            if hit is None and d == relevant:
-                hit = rank
-        lines.append("----------")
-        lines.append("")
-        if hit is not None:
-            ranked += 1
-            total += 1.0 / hit
+    """Mean reciprocal rank of the relevant passage over every query (0 for a
+    query whose passage is not returned).  A vector id outside [0, len(docids))
+    maps to the placeholder "INVALID_VECTOR_ID" and matches nothing.  Every
+    query must have a judgement (KeyError otherwise).  output_docids, if given,
+    receives for each query a "Query: <qid> <text>" line, its returned docids
+    one per line, then a "----------" line and a blank line."""
+    res = np.asarray(results)
+    ncorpus = len(docids)
+    rr_sum, found = 0.0, 0
+    listing: list[str] = []
+    for row, (qid, text) in zip(res, queries):
+        target = qrels[qid]
+        names = [str(docids[v]) if 0 <= v < ncorpus else "INVALID_VECTOR_ID" for v in row]
+        listing += [f"Query: {qid} {text}", *names, "----------", ""]
+        rank = next((r for r, name in enumerate(names, start=1) if name == target), 0)
+        if rank:
+            found += 1
+            rr_sum += 1.0 / rank
     if output_docids:
         with open(output_docids, "w", encoding="utf-8") as fh:
-            fh.write("\n".join(lines) + ("\n" if lines else ""))
+            fh.write("".join(s + "\n" for s in listing))
     nq = len(queries)
-    return {"metric": f"MRR@{results.shape[1] if results.ndim == 2 else 0}", "mrr": total / nq if nq else 0.0,
-            "queries": nq, "ranked_queries": ranked}
+    width = res.shape[1] if res.ndim == 2 else 0
+    return {"metric": f"MRR@{width}", "mrr": rr_sum / nq if nq else 0.0, "queries": nq, "ranked_queries": found}

@@ -27,6 +27,9 @@ def ctx():
 def oracle():
     from oracle import oracle as O
     O.lib()
+    # hint-fold threads of the oracle's preprocessing (identical state for any
+    # count); the GPU box gives a GPU 16 host cores
+    O.set_prep_threads(min(16, os.cpu_count() or 1))
     return O
 
 

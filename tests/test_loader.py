@@ -93,3 +93,28 @@ def test_graph_writers_round_trip(tmp_path):
     np.save(tmp_path / "g64.npy", g.astype(np.int64))
     with pytest.raises(L.LoaderError):
         L.load_graph(tmp_path / "g64.npy", 7, 5)   # GetInt32 needs int32
+
+
+def test_vecs_reads_only_the_first_records(tmp_path, monkeypatch):
+    """A base file much larger than n (bigann_base.bvecs is 132 GB; the SIFT1M
+    run reads its first 1e6 records): the reader maps the file and touches
+    only the first n records, so a ragged or garbled record after them does
+    not matter, and no whole-file array is allocated."""
+    rng = np.random.default_rng(7)
+    head = rng.integers(0, 256, size=(20, 16), dtype=np.uint8)
+    tail = rng.integers(0, 256, size=(5000, 16), dtype=np.uint8)
+    p = tmp_path / "big.bvecs"
+    p.write_bytes(vecs_bytes(head, np.uint8) + vecs_bytes(tail, np.uint8) + b"\x07\x00\x00\x00garbage")
+    calls = []
+    real = np.fromfile
+    monkeypatch.setattr(np, "fromfile", lambda *a, **k: calls.append(a) or real(*a, **k))
+    got = L.load_bvecs(p, 20, 16)
+    assert np.array_equal(got, head.astype(np.float32)) and not calls
+    f = tmp_path / "big.fvecs"
+    fv = rng.standard_normal((3000, 8)).astype(np.float32)
+    f.write_bytes(vecs_bytes(fv, np.float32) + vecs_bytes([np.arange(3)], np.float32))
+    assert np.array_equal(L.load_fvecs(f, 10, 8), fv[:10])   # the ragged last record is never read
+    i = tmp_path / "big.ivecs"
+    iv = rng.integers(0, 2**31, size=(100, 4), dtype=np.uint32)
+    i.write_bytes(vecs_bytes(iv, np.uint32) + b"\x01\x02")
+    assert np.array_equal(L.load_ivecs(i, 7, 4), iv[:7].astype(np.int64))

@@ -13,7 +13,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 import bench  # noqa: E402
 import pacmann_amd as pm  # noqa: E402
 from pacmann_amd.report import compute_recall  # noqa: E402
-from tests.datagen import random_graph, sift_like_vectors  # noqa: E402
+from pacmann_amd.synth import random_graph, sift_like_vectors  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000
 nq = int(sys.argv[2]) if len(sys.argv) > 2 else 100
