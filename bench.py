@@ -60,7 +60,7 @@ SYMBOLS = {"prep_fold": "void pm::k_prep_fold_pipe<4, 1, 4, 1>(pm::PmPart const*
            "gather": "void pm::k_gather<2>(pm::PmStep)"}
 HOST = ["host_search_knn", "host_knn_init", "host_knn_final", "host_knn_batch", "host_knn_update",
         "host_gvi_parse", "host_batch_query", "host_step_launch", "host_step_wait", "host_step_post",
-        "host_wait_first_token", "host_wait_all_tokens"]
+        "host_wait_first_token", "host_wait_all_tokens", "host_rows_seen", "host_rows_torn"]
 
 
 def make_data(rank: int, graph: str, ctx):
@@ -681,6 +681,9 @@ def main():
         "kernel_avg_us": {k: round(ktime[k][1] / ktime[k][0] * 1e3, 3) if ktime[k][0] else None for k in KERNELS},
         "host_ms": {k: round(htime[k][1], 3) for k in HOST},
         "steps_in_region": nsteps,
+        # result rows the host read at token time vs those that failed their header
+        # checksum then (the publication ordering audit, pm_query.hip publish_hdr)
+        "rows_check": {"seen": int(htime["host_rows_seen"][0]), "torn": int(htime["host_rows_torn"][0])},
         "dominant_kernel": dom,
     }
     if not args.no_cpu_baseline and ws == 1:

@@ -55,9 +55,10 @@ int         pm_ctx_sync(pm_ctx* ctx);
 /* Per-kernel timing.  Level 1: HIP events around the preprocessing and leaf
  * kernels on the stream they run on ("prep_offsets", "prep_fold",
  * "prep_repl", "l2_rows", "ip_scan", "prf", server "answer").  Level 2 also
- * times the three kernels of every online step ("hint_match", "resolve",
- * "answer") with events carried in their own dispatch packets
- * (hipExtLaunchKernelGGL), and synchronises each step.  Host wall-clock
+ * times the kernels of every online step ("step", "hint_match", "resolve",
+ * "gather", "answer") with events carried in their own dispatch packets
+ * (hipExtLaunchKernelGGL); steps are not synchronised for it (the events are
+ * read by pm_timing_get).  Host wall-clock
  * accumulators are always on: "host_step_launch", "host_step_wait",
  * "host_step_post", "host_batch_query", "host_gvi_parse", "host_search_knn",
  * "host_knn_init", "host_knn_batch", "host_knn_update", "host_knn_final". */
@@ -163,6 +164,17 @@ int  pm_batchpir_query(pm_batchpir* h, const uint64_t* ids, uint64_t n, uint64_t
  * was dropped by the bucketing (batch-pir.go:195-200) or its sub-query failed
  * (the error batch-pir.go:205 swallows); those entries are zero. */
 int  pm_batchpir_query_ok(pm_batchpir* h, const uint64_t* ids, uint64_t n, uint64_t* out, uint8_t* ok);
+/* The same query with the responses left in DEVICE memory, for an in-place
+ * collective over the shards (the multi-GPU combine, SURVEY.md §8e;
+ * replaces the host round trip of Query's [][]uint64 result, batch-pir.go:
+ * 216-236): dev_out is a device pointer on this handle's GPU of
+ * n x (DBEntrySize + 1) uint64 words; row i holds id i's entry and, in word
+ * DBEntrySize, 1 when it is a successful answer (pm_batchpir_query_ok's flag)
+ * or 0 (entry zero).  Entries are copied HBM to HBM from the partitions'
+ * local caches.  stream: a HIP stream (hipStream_t) of the consumer, made to
+ * wait for the rows without a host synchronisation; NULL: the rows are written
+ * when the call returns. */
+int  pm_batchpir_query_dev(pm_batchpir* h, const uint64_t* ids, uint64_t n, uint64_t* dev_out, void* stream);
 int  pm_batchpir_stats_get(pm_batchpir* h, pm_batchpir_stats* s);
 /* Many clients of one server answered together (batched serving, SURVEY.md
  * §8f rank 2): every pm_batchpir_group_query call makes, for each client s,

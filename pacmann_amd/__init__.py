@@ -88,6 +88,7 @@ SIGNATURES = {
     "pm_batchpir_dummy_preprocessing": (C.c_int, [vp]),
     "pm_batchpir_query": (C.c_int, [vp, u64p, u64, u64p]),
     "pm_batchpir_query_ok": (C.c_int, [vp, u64p, u64, u64p, C.POINTER(C.c_uint8)]),
+    "pm_batchpir_query_dev": (C.c_int, [vp, u64p, u64, vp, vp]),
     "pm_batchpir_create_shard": (C.c_int, [vp, u64, u64, u64, u64p, u64, u64, C.c_uint32, C.c_uint32, C.POINTER(vp)]),
     "pm_batchpir_create_synth": (C.c_int, [vp, u64, u64, u64, u64, u64, u64, C.c_uint32, C.c_uint32, C.POINTER(vp)]),
     "pm_batchpir_stats_get": (C.c_int, [vp, C.POINTER(BatchStats)]),
@@ -146,6 +147,16 @@ def lib() -> C.CDLL:
             f.argtypes = args
         _lib = L
     return _lib
+
+
+def hip_runtimes() -> set[str]:
+    """Paths of the HIP runtime libraries mapped into this process.  torch's
+    ROCm wheel ships its own libamdhip64 (same SONAME as /opt/rocm's): with
+    torch imported first, libpacmann.so binds to that one copy; loading
+    libpacmann.so first and torch later maps a second runtime, whose streams
+    and events the first cannot use (pacmann_amd.shard refuses that case)."""
+    with open("/proc/self/maps") as fh:
+        return {ln.split()[-1] for ln in fh if "libamdhip64" in ln}
 
 
 def _check(rc: int):
@@ -430,6 +441,17 @@ class SimpleBatchPianoPIR:
         _check(lib().pm_batchpir_query_ok(self.h, _p(ids, u64p), len(ids), _p(out, u64p),
                                           ok.ctypes.data_as(C.POINTER(C.c_uint8))))
         return out, ok.astype(bool)
+
+    def QueryDevice(self, idx, dev_out: int, stream: int | None = None):
+        """Query with the responses left in device memory (pm_batchpir_query_dev):
+        dev_out = the address of a device buffer on this handle's GPU of
+        len(idx) x (DBEntrySize + 1) uint64 words (row i: id i's entry, then its
+        success flag).  stream: a HIP stream handle that is made to wait for the
+        rows (e.g. torch.cuda.current_stream().cuda_stream); None: the rows are
+        written when the call returns."""
+        ids = _u64(idx).ravel()
+        _check(lib().pm_batchpir_query_dev(self.h, _p(ids, u64p), len(ids), vp(dev_out),
+                                           vp(stream) if stream else None))
 
     def stats(self) -> dict:
         s = BatchStats()

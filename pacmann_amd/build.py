@@ -44,5 +44,20 @@ def build(force: bool = False, verbose: bool = True) -> Path:
     return LIB
 
 
+def build_variant(name: str, defines: list[str]) -> Path:
+    """An experiment build (e.g. -DPM_PUBLISH=0) at build/libpacmann_<name>.so,
+    loaded instead of the default with PM_LIB=<path>."""
+    out = ROOT / "build" / f"libpacmann_{name}.so"
+    out.parent.mkdir(exist_ok=True)
+    cmd = [HIPCC, *FLAGS, *defines, "-o", str(out), *map(str, SOURCES)]
+    print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True, cwd=CSRC)
+    return out
+
+
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    if "--variant" in sys.argv:
+        i = sys.argv.index("--variant")
+        build_variant(sys.argv[i + 1], sys.argv[i + 2:])
+    else:
+        build(force="--force" in sys.argv)

@@ -148,8 +148,8 @@ struct HostBuf {
 };
 
 // Host wall-clock accumulators, read back as "host_*" through pm_timing_get.
-enum HostTimer : int { HT_STEP_LAUNCH, HT_STEP_WAIT, HT_STEP_POST, HT_BATCH_QUERY, HT_GVI_PARSE, HT_SEARCH_KNN, HT_KNN_INIT, HT_KNN_BATCH, HT_KNN_UPDATE, HT_KNN_FINAL, HT_WAIT_FIRST, HT_WAIT_ALL, HT_COUNT };
-static const char* const kHostTimerName[HT_COUNT] = {"host_step_launch", "host_step_wait", "host_step_post", "host_batch_query", "host_gvi_parse", "host_search_knn", "host_knn_init", "host_knn_batch", "host_knn_update", "host_knn_final", "host_wait_first_token", "host_wait_all_tokens"};
+enum HostTimer : int { HT_STEP_LAUNCH, HT_STEP_WAIT, HT_STEP_POST, HT_BATCH_QUERY, HT_GVI_PARSE, HT_SEARCH_KNN, HT_KNN_INIT, HT_KNN_BATCH, HT_KNN_UPDATE, HT_KNN_FINAL, HT_WAIT_FIRST, HT_WAIT_ALL, HT_ROWS_SEEN, HT_ROWS_TORN, HT_COUNT };
+static const char* const kHostTimerName[HT_COUNT] = {"host_step_launch", "host_step_wait", "host_step_post", "host_batch_query", "host_gvi_parse", "host_search_knn", "host_knn_init", "host_knn_batch", "host_knn_update", "host_knn_final", "host_wait_first_token", "host_wait_all_tokens", "host_rows_seen", "host_rows_torn"};
 
 struct TimedLaunch { std::string name; hipEvent_t a, b; double bytes; };
 
@@ -164,6 +164,10 @@ struct pm_ctx {
   bool debug_cache = false;
   bool log_steps = false;    // PM_LOG_STEPS=1: one stderr line per sub-query per step  // PM_DEBUG_CACHE=1: check cached answers against the slot's first answer  // PM_VERIFY_ROWS=1: re-read each step's results after the stream drains     // PM_NO_GUESS=1: k_step answers do not start before their resolution
   bool debug_sync = false;   // PM_DEBUG_SYNC=1: synchronise after every launch (fault triage)
+  // Result rows vs their header checksum when the token is first seen
+  // (PmOutHdr::csum): 0 = no check, 1 = count a mismatch ("host_rows_torn")
+  // and fail the step, 2 = count it and wait for the row to match (PM_ROWS_CHECK)
+  int rows_check = 2;
   std::string last_kernel;
   // host-side wall-clock accumulators ("host_*" names in pm_timing_get)
   uint64_t host_n[HT_COUNT] = {};
@@ -233,6 +237,7 @@ extern "C" int pm_ctx_create(int device, pm_ctx** out) {
   c->debug_cache = dc && dc[0] == '1';
   const char* vr = getenv("PM_VERIFY_ROWS");
   c->verify_rows = vr && vr[0] == '1';
+  if (const char* rc = getenv("PM_ROWS_CHECK")) c->rows_check = atoi(rc);
   const char* ng = getenv("PM_NO_GUESS");
   c->no_guess = ng && ng[0] == '1';
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
@@ -308,7 +313,10 @@ struct Engine {
   uint32_t step_token = 0;         // PmStep::token of the last step
   size_t pf_off = 0, pf_len = ~size_t(0);   // bytes of each result row the caller reads next
   bool rows_partial = false;   // this call's caller reads ONLY those bytes (GetVertexInfo): the rest is not sent
-  HostBuf desc_h, out_h, err_h;
+  HostBuf desc_h, out_h, err_h, src_h;   // src_h: pm_batchpir_query_dev's row pointers
+  DevBuf stage_d;                        // ... and its rows of a multi-step query
+  hipEvent_t dev_ev = nullptr;           // ... its completion, for the consumer's stream
+  ~Engine() { if (dev_ev) (void)hipEventDestroy(dev_ev); }
   std::vector<PartHost> parts;
   uint32_t maxH = 0, maxPH = 0, maxSS = 0, maxRepl = 0, maxCS = 0, minCS = ~0u;
 
@@ -368,6 +376,15 @@ static double part_storage(const PartHost& p, uint64_t Ebytes) {   // LocalStora
   return s;
 }
 static double part_comm(const PartHost& p, uint64_t E) { return (double)((uint64_t)p.d.SS * 4 + E * 8); }
+// Algorithmic bytes of one answered (real or dummy) sub-query, SURVEY.md §8(d):
+// (#in-range rows)*E*8 + 4*SS + 8*E.  A row i*CS + off_i >= N is padding the
+// server skips (pir.go:78-84); with uniform offsets the expected number of
+// in-range rows is N / CS exactly (every full chunk, plus the partial chunk's
+// share), so padding chunks are not counted.
+static inline double answer_bytes(const PmPart& d, uint64_t E) {
+  const double rows = std::min((double)d.SS, (double)d.N / (double)d.CS);
+  return rows * (double)E * 8 + 4.0 * d.SS + 8.0 * E;
+}
 
 static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, uint64_t B,
                          const uint64_t* rawDB, uint64_t F, uint64_t seed, bool batch,
@@ -583,14 +600,16 @@ static inline double ms_since(Clock::time_point t) {
 // Completion of a step: every result header in pinned memory carries this
 // step's token (k_answer writes it after the row has drained), so the host
 // polls the headers instead of waiting for the kernel's completion signal.
-// Timing / debug runs, and a step not published within 5 s (a fault, or a
-// bug), fall back to the stream synchronisation, which reports errors.
+// Debug runs (PM_DEBUG_SYNC), and a step not published within 5 s (a fault, or
+// a bug), fall back to the stream synchronisation, which reports errors.
+// Timed runs poll like any other: their events ride in the kernels' dispatch
+// packets and are read by pm_timing_get.
 // While polling, the bytes [pf_off, pf_off + pf_len) of each published row are
 // prefetched, so the caller's reads of the results hit the cache.
 static int wait_step(pm_ctx* c, const PmOutHdr* hdr, uint32_t nsub, uint32_t token, const char* rows,
                      size_t row_bytes, size_t pf_off, size_t pf_len, hipStream_t stream = nullptr) {
   if (!stream) stream = c->stream;   // the stream the step runs on (c: timing and diagnostics)
-  if (c->timing >= 2 || c->debug_sync) {
+  if (c->debug_sync) {
     HIPCHK(hipStreamSynchronize(stream));
   } else {
     const volatile uint32_t* tok = &hdr[0].token;
@@ -598,21 +617,32 @@ static int wait_step(pm_ctx* c, const PmOutHdr* hdr, uint32_t nsub, uint32_t tok
     auto t0 = Clock::now();
     uint32_t s = 0;
     const size_t w0 = pf_off / 8, w1 = (pf_off + pf_len + 7) / 8;
+    bool first_look = true;   // the first read of sub-query s's row after its token appeared
     for (uint64_t spin = 0; s < nsub; ++spin) {
       if (tok[s * stride] == token) {
-        if (c->timing && s == 0) c->host_add(HT_WAIT_FIRST, ms_since(t0));
-        // the row words this caller reads must have landed: their XOR is in the header
-        const volatile uint64_t* rw = (const volatile uint64_t*)(rows + s * row_bytes);
-        const volatile uint64_t* cs = &hdr[s].csum;
-        uint64_t x = token * kCsumMix;
-        for (size_t w = w0; w < w1; ++w) x ^= rw[w];
-        if (x != *cs) {
-          if ((spin & 0xffff) == 0xffff && ms_since(t0) > 5000.0)
-            return fail(PM_EHIP, "step results incomplete (sub-query " + std::to_string(s) + ")");
-          continue;
+        if (c->timing && s == 0 && first_look) c->host_add(HT_WAIT_FIRST, ms_since(t0));
+        std::atomic_thread_fence(std::memory_order_acquire);
+        if (c->rows_check) {
+          // the device published the token after a system-scope release of the
+          // row (pm_query.hip publish_hdr); the checksum asserts it
+          const volatile uint64_t* rw = (const volatile uint64_t*)(rows + s * row_bytes);
+          const volatile uint64_t* cs = &hdr[s].csum;
+          uint64_t x = token * kCsumMix;
+          for (size_t w = w0; w < w1; ++w) x ^= row_hash_word(rw[w], w);
+          if (first_look) c->host_add(HT_ROWS_SEEN, 0);
+          if (x != *cs) {
+            if (first_look) c->host_add(HT_ROWS_TORN, 0);
+            first_look = false;
+            if (c->rows_check == 1)
+              return fail(PM_EHIP, "step result row " + std::to_string(s) + " does not match its header checksum");
+            if ((spin & 0xffff) == 0xffff && ms_since(t0) > 5000.0)
+              return fail(PM_EHIP, "step results incomplete (sub-query " + std::to_string(s) + ")");
+            continue;
+          }
         }
         if (c->timing && s + 1 == nsub) c->host_add(HT_WAIT_ALL, ms_since(t0));
         ++s;
+        first_look = true;
         continue;
       }
       if ((spin & 0xffff) == 0xffff && ms_since(t0) > 5000.0) {
@@ -808,10 +838,7 @@ static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
   }
   double ans_bytes = 0;
   for (auto& x : g->subs)
-    if (x.kind == SUB_REAL || x.kind == SUB_DUMMY) {   // rows*E*8 + 4*SS + 8*E
-      const double ss = g->parts[x.part].d.SS;
-      ans_bytes += ss * E * 8 + 4 * ss + 8.0 * E;
-    }
+    if (x.kind == SUB_REAL || x.kind == SUB_DUMMY) ans_bytes += answer_bytes(g->parts[x.part].d, E);
   // One launch (k_step) when the step fits it, else the three kernels.
   // Timing level 2: the kernels carry their events in their own dispatch packets.
   if (!c->no_fuse && !c->debug_sync && pmk::step_fused_ok(S, g->maxPH, max_per_part)) {
@@ -976,7 +1003,7 @@ extern "C" int pm_pir_server_answer(pm_pir* h, const uint32_t* offsets, uint64_t
   CHK(g->ans_srv.reserve(nq * g->E * 8));
   CHK(upload_parts(g));
   HIPCHK(hipMemcpyAsync(g->qoffs.p, offsets, nq * d.SS * 4, hipMemcpyHostToDevice, c->stream));
-  c->timed("answer", (double)nq * (d.SS * (g->E * 8 + 4) + g->E * 8), [&] {
+  c->timed("answer", (double)nq * answer_bytes(d, g->E), [&] {
     pmk::server_answer(c->stream, g->parts_d.as<PmPart>(), g->qoffs.as<uint32_t>(), (uint32_t)nq, d.SS,
                        g->db->as<uint64_t>(), (uint32_t)g->E, g->ans_srv.as<uint64_t>());
   });
@@ -1235,12 +1262,74 @@ static int batch_query_impl(Engine* g, const uint64_t* idx, uint64_t n, uint64_t
   }
   return bq_tail(g, n);
 }
+// the slow path of pm_batchpir_query_dev: batch_query_impl's response rows (host) and flags
+static int batch_query_impl_rows(Engine* g, const uint64_t* idx, uint64_t n, const uint64_t** rows_out, uint8_t* ok) {
+  return batch_query_impl(g, idx, n, nullptr, nullptr, 0, nullptr, rows_out, ok);
+}
 extern "C" int pm_batchpir_query(pm_batchpir* h, const uint64_t* ids, uint64_t n, uint64_t* out) {
   return batch_query(&h->e, ids, n, out, nullptr, 0, nullptr);
 }
 extern "C" int pm_batchpir_query_ok(pm_batchpir* h, const uint64_t* ids, uint64_t n, uint64_t* out,
                                     uint8_t* ok) {
   return batch_query(&h->e, ids, n, out, nullptr, 0, nullptr, nullptr, ok);
+}
+// Query with the responses left in device memory for an in-place collective
+// (the sharded combine): a successful sub-query's entry is the
+// row k_answer stored in its partition's localCache arena (slot = the
+// resolution's, followed through in-step duplicates), so the responses are
+// copied HBM to HBM by one k_gather_rows launch; only the row pointers come
+// from the host.  A query that needed several steps (a partition at its budget
+// mid-batch, pir.go:527-530) has its rows in host memory and uploads them.
+extern "C" int pm_batchpir_query_dev(pm_batchpir* h, const uint64_t* ids, uint64_t n, uint64_t* dev_out,
+                                     void* stream) {
+  Engine* g = &h->e;
+  if (n && (!ids || !dev_out)) return fail(PM_EINVAL, "NULL argument");
+  const uint64_t E = g->E;
+  hipStream_t st = g->ctx->stream;
+  HIPCHK(hipSetDevice(g->ctx->device));
+  bool fast = false;
+  CHK(bq_prepare(g, ids, n, &fast));
+  if (fast) {
+    CHK(engine_step(g, nullptr, 0));
+    for (size_t s = 0; s < g->subs.size(); ++s) {
+      const uint32_t k = g->subs[s].kind;
+      if (k == SUB_REAL || k == SUB_HOSTCACHE) g->resp_map.put(g->sub_gid[s], (uint32_t)s);   // last wins
+    }
+    CHK(g->src_h.reserve(std::max<uint64_t>(1, n) * 8));
+    const uint64_t** src = g->src_h.as<const uint64_t*>();
+    for (uint64_t i = 0; i < n; ++i) {
+      src[i] = nullptr;
+      const uint32_t* sp = g->resp_map.find(ids[i]);
+      if (!sp) continue;
+      uint32_t s = *sp;
+      for (int hop = 0; g->hdr[s].status == ST_DUP && hop < 2; ++hop) s = g->hdr[s].ref;   // step-wide index
+      const uint32_t stt = g->hdr[s].status;
+      if (stt == ST_OK || stt == ST_CACHED)
+        src[i] = g->parts[g->subs[s].part].d.arena + (uint64_t)g->hdr[s].ref * E;
+    }
+    pmk::gather_rows(st, src, n, (uint32_t)E, dev_out);
+    HIPCHK(hipGetLastError());
+  } else {   // rows collected on the host by the multi-step path
+    std::vector<uint64_t> rows(n * (E + 1), 0);
+    std::vector<uint8_t> ok(n);
+    std::vector<const uint64_t*> rp(n);
+    CHK(batch_query_impl_rows(g, ids, n, rp.data(), ok.data()));
+    for (uint64_t i = 0; i < n; ++i) {
+      memcpy(&rows[i * (E + 1)], rp[i], E * 8);
+      rows[i * (E + 1) + E] = ok[i];
+    }
+    HIPCHK(hipMemcpyAsync(dev_out, rows.data(), rows.size() * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return 0;   // batch_query_impl_rows ran the re-preprocessing trigger itself
+  }
+  if (stream) {   // the consumer's stream waits for the rows; no host synchronisation
+    if (!g->dev_ev) HIPCHK(hipEventCreateWithFlags(&g->dev_ev, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(g->dev_ev, st));
+    HIPCHK(hipStreamWaitEvent((hipStream_t)stream, g->dev_ev, 0));
+  } else {
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  return bq_tail(g, n);   // stream-ordered after the copy
 }
 extern "C" int pm_batchpir_stats_get(pm_batchpir* h, pm_batchpir_stats* s) {
   const Engine& g = h->e;
@@ -1897,8 +1986,7 @@ static int group_step(StepGroup& G, const std::vector<char>& in) {
           PmSub x = e->subs[j];
           x.part += s * G.P;
           G.subs.push_back(x);
-          if (x.kind == SUB_REAL || x.kind == SUB_DUMMY)   // rows*E*8 + 4*SS + 8*E
-            ans_bytes += (double)e->parts[p].d.SS * (G.E * 8 + 4) + 8.0 * G.E;
+          if (x.kind == SUB_REAL || x.kind == SUB_DUMMY) ans_bytes += answer_bytes(e->parts[p].d, G.E);
         }
         const uint32_t n = e->sb[p + 1] - e->sb[p];
         max_per_part = std::max(max_per_part, n);

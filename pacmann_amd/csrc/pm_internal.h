@@ -92,17 +92,20 @@ struct PmRes {
   uint32_t flags;                     // bit 0: hint refreshed earlier in this step (chained);
                                       // bit 1: a later sub-query in this step re-hits this hint
 };
-// Per-sub-query result header, written by the GPU into pinned host memory.
-// One 16-byte store: the step token is written together with the rest, after
-// the row of the sub-query has drained; the host polls it (no stream sync).
-// Result header of one sub-query in pinned host memory.  The device's row
-// writes and this header reach the host in no guaranteed order (a token seen
-// does not mean the row's bytes have landed, measured), so the header also
-// carries the XOR of the row words the host will read ([pf_w0, pf_w1) of
-// PmStep) mixed with the step token (a stale checksum never matches a stale
-// row): the host waits until the row it reads matches.  {status, ref, dist,
-// token} are one 16-B store.
+// Per-sub-query result header, written by the GPU into pinned host memory
+// after the sub-query's row.  Write-combined stores to fine-grained host
+// memory reach the host in no guaranteed order (measured: 2.6e-4 of rows are
+// torn when the token is first seen), and ordering them costs 2.8-4.4x the
+// answer kernel's time (a system-scope L2 write-back per workgroup, or
+// write-through stores).  So the header carries a 64-bit
+// position-keyed hash of the row words the host reads ([pf_w0, pf_w1) of
+// PmStep), mixed with the step token: the host accepts a row only when its
+// bytes hash to it, else re-reads.  A torn row passes only if the XOR of
+// row_hash_word() over its stale words cancels: probability 2^-64.
 constexpr uint64_t kCsumMix = 0x9E3779B97F4A7C15ull;
+__host__ __device__ inline uint64_t row_hash_word(uint64_t v, uint64_t w) {
+  return sm64(v ^ (w * 0xD6E8FEB86659FD93ull));
+}
 struct alignas(16) PmOutHdr {
   uint32_t status, ref;
   float dist;
@@ -198,6 +201,8 @@ void ip_fill(hipStream_t st, uint32_t* rows, uint64_t N, uint32_t D);
 // Synthetic DB rows (pm_batchpir_create_synth): dst row i = global row r0 + i,
 // word w = sm64(sm64(db_seed + DOM_SYNTH_DB) ^ (r * E + w)).
 void db_synth(hipStream_t st, uint64_t* dst, uint64_t r0, uint64_t rows, uint32_t E, uint64_t db_seed);
+// out[i] = {E words at src[i] (or zeros when null), success flag}, src in pinned host memory
+void gather_rows(hipStream_t st, const uint64_t* const* src, uint64_t n, uint32_t E, uint64_t* out);
 void prf_batch(hipStream_t st, const uint32_t* rk, const uint64_t* tags, const uint64_t* xs,
                uint64_t n, uint64_t* out);
 // graph construction and ground truth (pm_graph.hip)

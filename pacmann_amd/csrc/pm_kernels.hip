@@ -567,6 +567,19 @@ __global__ void __launch_bounds__(kBlock) k_prf_batch(const uint32_t* __restrict
     out[i] = prf64(A, srk, tags[i], xs[i]);
 }
 
+// Device-resident batch responses (pm_batchpir_query_dev): row i of out
+// (E + 1 words) = the entry at src[i] (a row of a partition's localCache arena
+// in HBM; the pointer list sits in pinned host memory) and the success flag,
+// or zeros.  One workgroup per response; E <= 2048.
+__global__ void __launch_bounds__(kBlock) k_gather_rows(const uint64_t* const* __restrict__ src, uint32_t E,
+                                                         uint64_t* __restrict__ out) {
+  const uint64_t i = blockIdx.x;
+  const uint64_t* r = src[i];
+  uint64_t* o = out + i * (E + 1);
+  for (uint32_t w = threadIdx.x; w < E; w += kBlock) o[w] = r ? r[w] : 0;
+  if (threadIdx.x == 0) o[E] = r ? 1 : 0;
+}
+
 }  // namespace pm
 
 // ---------------------------------------------------------------------------
@@ -687,6 +700,9 @@ void db_synth(hipStream_t st, uint64_t* dst, uint64_t r0, uint64_t rows, uint32_
   if (grid > 256 * 32) grid = 256 * 32;
   if (grid == 0) return;
   hipLaunchKernelGGL(k_db_synth, dim3(grid), dim3(kBlock), 0, st, dst, r0, nw, E, sm64(db_seed + DOM_SYNTH_DB));
+}
+void gather_rows(hipStream_t st, const uint64_t* const* src, uint64_t n, uint32_t E, uint64_t* out) {
+  if (n) hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)n), dim3(kBlock), 0, st, src, E, out);
 }
 void prf_batch(hipStream_t st, const uint32_t* rk, const uint64_t* tags, const uint64_t* xs, uint64_t n,
                uint64_t* out) {

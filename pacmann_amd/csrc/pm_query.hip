@@ -1189,24 +1189,65 @@ union RowBuf {   // one decoded entry; the L2 reads its leading floats
   float f[2 * kMaxELds];
 };
 
-// Result header of sub-query s, once every thread's row stores have drained
-// (the host reads the row as soon as it sees the token).  Lane 0 holds `d`.
-// XOR of row words [pf_w0, pf_w1) (the LDS copy of what was written), for
-// PmOutHdr::csum.  Wave 0 only; lane 0 holds the result.
+// PmOutHdr::csum: the position-keyed hash of the row words [pf_w0, pf_w1)
+// as written (the LDS copy, or zeros), pm_internal.h row_hash_word.  Wave 0
+// only; every lane returns the result.
 __device__ __forceinline__ uint64_t row_csum(const PmStep& S, const RowBuf& row, bool has_row) {
   uint64_t x = 0;
-  if (has_row)
-    for (uint32_t w = S.pf_w0 + (threadIdx.x & 63); w < S.pf_w1; w += 64) x ^= row.w[w];
+  for (uint32_t w = S.pf_w0 + (threadIdx.x & 63); w < S.pf_w1; w += 64)
+    x ^= row_hash_word(has_row ? row.w[w] : 0, w);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) x ^= __shfl_xor(x, o);
   return x;
 }
 
+// Result publication into pinned (fine-grained) host memory.  Every storing
+// thread waits for its row stores (s_waitcnt vmcnt(0)), a workgroup barrier
+// follows, then lane 0 writes the header with the token last.  The default
+// (PM_PUBLISH 0) stores write-combined and leaves ordering to the row hash
+// the host verifies (pm_internal.h PmOutHdr).  Two ordered forms, both
+// measured with 0 torn rows in 49M but 2.8x / 4.4x the kernel time, are kept
+// as build options:
+//   1: lane 0 stores the other header fields, then a SYSTEM-scope release
+//      (buffer_wbl2 sc0 sc1: the XCD L2's dirty lines, every wave's included,
+//      are written back) and an explicit s_waitcnt vmcnt(0) — inline asm, so
+//      the compiler cannot drop the wait after the write-back
+//      (MI355X_MICROARCH.md "Compiler hazard") — then the token as ONE 8-byte
+//      system-scope store {dist, token};
+//   3: every row and header word stored write-through at system scope
+//      (sc0 sc1), each wave's stores acknowledged before the barrier, the
+//      token stored after lane 0's header stores are acknowledged.
+#ifndef PM_PUBLISH
+#define PM_PUBLISH 0
+#endif
+__device__ __forceinline__ void row_store(PM_G uint64_t* p, uint64_t v) {
+  if (PM_PUBLISH >= 2) __hip_atomic_store((uint64_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  else *p = v;
+}
 __device__ __forceinline__ void publish_hdr(const PmStep& S, uint32_t s, uint32_t status, uint32_t ref,
                                             float d, uint64_t csum) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) S.hdr_h[s] = PmOutHdr{status, ref, d, S.token, csum ^ (S.token * kCsumMix), 0};
+  if (threadIdx.x != 0) return;
+  PM_G PmOutHdr* h = S.hdr_h + s;
+  const uint64_t tok = ((uint64_t)S.token << 32) | __float_as_uint(d);   // {dist, token}: bytes 8..15
+  if (PM_PUBLISH == 0) {
+    *h = PmOutHdr{status, ref, d, S.token, csum ^ (S.token * kCsumMix), 0};
+    return;
+  }
+  PM_G uint64_t* w = reinterpret_cast<PM_G uint64_t*>(h);
+  if (PM_PUBLISH == 3) {   // every byte written through at system scope: no L2 write-back needed
+    __hip_atomic_store((uint64_t*)w, ((uint64_t)ref << 32) | status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store((uint64_t*)(w + 2), csum ^ (S.token * kCsumMix), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store((uint64_t*)(w + 1), tok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
+  w[0] = ((uint64_t)ref << 32) | status;
+  w[2] = csum ^ (S.token * kCsumMix);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __hip_atomic_store((uint64_t*)(w + 1), tok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // What a k_answer workgroup does for its sub-query.
@@ -1236,11 +1277,11 @@ __device__ void decode_chained(const PmStep& S, uint32_t s, RowBuf& row) {
     row.w[w] = v;
   }
   __syncthreads();
-  uint64_t* orow = S.rows_h + (uint64_t)s * E;
+  PM_G uint64_t* orow = S.rows_h + (uint64_t)s * E;
   uint64_t* ar = P.arena + (uint64_t)r.slot * E;
   for (uint32_t w = tid; w < E; w += blockDim.x) ar[w] = row.w[w];
   for (uint32_t w = (S.rows_partial ? S.pf_w0 : 0) + tid; w < (S.rows_partial ? S.pf_w1 : E); w += blockDim.x)
-    orow[w] = row.w[w];
+    row_store(orow + w, row.w[w]);
   float d = 0.0f;
   const float* qq = P.qv ? P.qv : S.q;
   if (qq && tid < 8) d = l2_lds(row.f, qq, S.dim);
@@ -1294,7 +1335,7 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, AnswerL
   const uint32_t E = S.E, EX = E & ~3u, NSEG = EX / W;
   const PmSub sub = step_sub(S, s);
   const PmPart& P = S.parts[sub.part];
-  uint64_t* const orow = S.rows_h + (uint64_t)s * E;
+  PM_G uint64_t* const orow = S.rows_h + (uint64_t)s * E;
   const bool stamp_wg = s == 0;
   STAMP_AT(stamp_wg, 48);
   const uint32_t mask = P.CS - 1, lg = P.log2CS;
@@ -1517,7 +1558,7 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, AnswerL
     // to the host: the whole row, or only the words its caller reads (graph search:
     // the neighbour list; the distance travels in the header)
     for (uint32_t w = (S.rows_partial ? S.pf_w0 : 0) + tid; w < (S.rows_partial ? S.pf_w1 : E); w += NT)
-      orow[w] = has_row ? row.w[w] : 0;
+      row_store(orow + w, has_row ? row.w[w] : 0);
     if (mode == A_FINAL) {
       uint64_t* ar = P.arena + (uint64_t)r.slot * E;
       for (uint32_t w = tid; w < E; w += NT) ar[w] = row.w[w];

@@ -5,15 +5,25 @@ of a `world`-rank process group holds the partitions p with p % world == r
 (their DB slice, keys and hint tables: pm_batchpir_create_shard). Every rank is
 fed the same id batches and makes the same bucketing, dummy, drop and
 re-preprocessing decisions. It answers its own partitions and leaves the other
-entries zero, so one all-reduce SUM of the entries (and MAX of the success
-mask) gives every rank the unsharded answer, bit for bit. This is the path's
-only exchange. RCCL has no XOR reduction, but at most one rank contributes a
-non-zero entry per id, so an integer sum is exact.
+entries zero, so one all-reduce SUM of the responses gives every rank the
+unsharded answer, bit for bit: the path's only exchange. RCCL has no XOR
+reduction, but at most one rank contributes a non-zero entry per id, so the
+integer sum equals the XOR (and the per-id success flags, one word per row,
+sum to 0 or 1).
+
+The combine is device-resident: each rank's engine writes its responses, with
+the success flag as an extra word per row, straight into one device tensor
+(pm_batchpir_query_dev copies them HBM to HBM from the partitions' local
+caches); under nccl (RCCL over xGMI) that tensor is all-reduced in place and
+crosses PCIe to the host once, after the collective.  Under gloo the same
+device rows are copied to the host for the CPU collective.
 
 Preprocessing needs no exchange: each rank folds only its own partitions, so
 its wall time drops with the rank count.
 """
 from __future__ import annotations
+
+import os
 
 import numpy as np
 
@@ -22,33 +32,49 @@ class ShardedBatchPIR:
     """The SimpleBatchPianoPIR surface over a torch.distributed group.
 
     `engine` builds this rank's shard; by default the GPU engine
-    (pacmann_amd.SimpleBatchPianoPIR(..., shard=rank, nshards=world)). The
-    combine runs on the group's backend: host tensors for gloo, device tensors
-    for nccl (RCCL)."""
+    (pacmann_amd.SimpleBatchPianoPIR(..., shard=rank, nshards=world)) on this
+    rank's device: `device` if given, else LOCAL_RANK (one process per GPU),
+    else the current CUDA device.  A host engine (e.g. the oracle's, in CPU
+    tests) has no device path: its responses are combined on the host."""
 
     def __init__(self, DBSize: int, DBEntryByteNum: int, BatchSize: int, rawDB, FailureProbLog2: int,
                  seed: int = 1, group=None, engine=None, ctx=None, db_seed: int | None = None,
                  device: int | None = None):
-        """db_seed: the shard's rows are generated on its GPU
-        (pm_batchpir_create_synth; rawDB None).  device: the CUDA device of the
-        combine's tensors under nccl (default: the current one)."""
         import torch.distributed as dist
         self._dist = dist
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.E = DBEntryByteNum // 8
-        if engine is None:
-            from . import SimpleBatchPianoPIR
+        self.nccl = dist.get_backend(group) == "nccl"
+        gpu_engine = engine is None
+        if gpu_engine:
+            from . import Context, SimpleBatchPianoPIR
             engine = SimpleBatchPianoPIR
+            if ctx is None:
+                if device is None:
+                    device = int(os.environ.get("LOCAL_RANK", "-1"))
+                if device < 0:
+                    import torch
+                    device = torch.cuda.current_device()
+                ctx = Context(device)
+        if ctx is not None and device is None:
+            device = getattr(ctx, "device", None)
+        if self.nccl and not gpu_engine:
+            raise ValueError("the nccl combine needs the GPU engine (device-resident responses)")
         kw = {"ctx": ctx} if ctx is not None else {}
         if db_seed is not None:
             kw["db_seed"] = db_seed
         self.pir = engine(DBSize, DBEntryByteNum, BatchSize, rawDB, FailureProbLog2, seed=seed,
                           shard=self.rank, nshards=self.world, **kw)
-        self._device = "cpu"
-        if dist.get_backend(group) == "nccl":
-            self._device = "cuda" if device is None else f"cuda:{device}"
+        self.device = device
+        self.device_path = gpu_engine and hasattr(self.pir, "QueryDevice")
+        if self.device_path:
+            from . import hip_runtimes
+            if len(hip_runtimes()) > 1:
+                raise RuntimeError("two HIP runtimes are mapped (libpacmann.so was loaded before torch): "
+                                   "import torch before creating any pacmann_amd context")
+        self._buf = None
 
     def Preprocessing(self):
         self.pir.Preprocessing()
@@ -56,14 +82,42 @@ class ShardedBatchPIR:
     def DummyPreprocessing(self):
         self.pir.DummyPreprocessing()
 
-    def QueryWithMask(self, idx):
+    def _rows(self, n: int):
         import torch
-        out, ok = self.pir.QueryWithMask(idx)
-        rows = torch.from_numpy(np.ascontiguousarray(out).view(np.int64)).to(self._device)
-        mask = torch.from_numpy(ok.astype(np.int32)).to(self._device)
+        if self._buf is None or self._buf.shape[0] < n:
+            self._buf = torch.empty((max(n, 1), self.E + 1), dtype=torch.int64, device=f"cuda:{self.device}")
+        return self._buf[:n]
+
+    def QueryDevice(self, idx):
+        """The combined responses as one device tensor [len(idx), E + 1] (int64
+        view of the uint64 words; column E = success flag), every rank holding
+        the same values after the in-place all-reduce."""
+        import torch
+        ids = np.ascontiguousarray(idx, dtype=np.uint64).ravel()
+        with torch.cuda.device(self.device):
+            rows = self._rows(len(ids))
+            stream = torch.cuda.current_stream()
+            self.pir.QueryDevice(ids, rows.data_ptr(), stream.cuda_stream)
+            if self.nccl:
+                self._dist.all_reduce(rows, op=self._dist.ReduceOp.SUM, group=self.group)
+            else:   # gloo: the CPU collective over the device rows copied once
+                host = rows.cpu()
+                self._dist.all_reduce(host, op=self._dist.ReduceOp.SUM, group=self.group)
+                rows.copy_(host)
+        return rows
+
+    def QueryWithMask(self, idx):
+        ids = np.ascontiguousarray(idx, dtype=np.uint64).ravel()
+        if self.device_path:
+            rows = self.QueryDevice(ids).cpu().numpy().view(np.uint64)   # the one D2H copy
+            return np.ascontiguousarray(rows[:, :self.E]), rows[:, self.E].astype(bool)
+        import torch   # host engine: combine on the host
+        out, ok = self.pir.QueryWithMask(ids)
+        rows = torch.from_numpy(np.ascontiguousarray(out).view(np.int64).copy())
+        mask = torch.from_numpy(ok.astype(np.int64))
         self._dist.all_reduce(rows, op=self._dist.ReduceOp.SUM, group=self.group)
-        self._dist.all_reduce(mask, op=self._dist.ReduceOp.MAX, group=self.group)
-        return rows.cpu().numpy().view(np.uint64), mask.cpu().numpy().astype(bool)
+        self._dist.all_reduce(mask, op=self._dist.ReduceOp.SUM, group=self.group)
+        return rows.numpy().view(np.uint64), mask.numpy().astype(bool)
 
     def Query(self, idx):
         out, _ = self.QueryWithMask(idx)
