@@ -46,8 +46,8 @@ sys.path.insert(0, str(ROOT))
 N, DIM, M, K_TOP, STEP, PARALLEL, F = 1_000_000, 128, 32, 10, 20, 3, 8
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 METRIC = "private queries/sec + PIR-scan HBM GB/s, SIFT1M d=128 at 1/2/4/8 GPUs"
-PREP_KERNELS = ["prep_offsets", "prep_fold", "prep_repl", "l2_rows"]   # timed in the measured region
-STEP_KERNELS = ["step", "hint_match", "resolve", "gather", "answer"]   # timed in the profile window
+PREP_KERNELS = ["prep_offsets", "prep_fold", "prep_repl", "l2_rows"]
+STEP_KERNELS = ["step", "hint_match", "resolve", "gather", "answer"]   # timed in the measured region too
 KERNELS = PREP_KERNELS + STEP_KERNELS
 PROFILE_QUERIES = 8
 SESSIONS = 256  # client sessions per GPU (128: 9.9K q/s, 256: 11.0K, 384: 11.5K, 512: 11.3K)
@@ -126,6 +126,10 @@ def batch_pir_msmarco(ctx, with_cpu: bool):
     for b in batches[:10]:   # warm-up
         g.Query(b)
     ctx.sync()
+    # the step kernels are timed over the timed batches themselves (events in
+    # their dispatch packets; no synchronisation added)
+    ctx.timing_reset()
+    ctx.timing(2)
     t0 = time.perf_counter()
     bad = 0
     for b in batches[10:10 + C2_BATCHES]:
@@ -134,10 +138,6 @@ def batch_pir_msmarco(ctx, with_cpu: bool):
         bad += int(r0.any() and not np.array_equal(r0, rows[int(b[0])]))
     ctx.sync()
     online = time.perf_counter() - t0
-    ctx.timing_reset()
-    ctx.timing(2)
-    for b in batches[10 + C2_BATCHES - 10:10 + C2_BATCHES]:
-        g.Query(b)
     ctx.timing(False)
     n, ms, by = ctx.timing_get("step")
     out = {"workload": "TestBatchPIRPerf shape (configs[2], MS-MARCO 3.2M): 3,201,821 x 896 B, BatchSize 32, "
@@ -150,7 +150,9 @@ def batch_pir_msmarco(ctx, with_cpu: bool):
         ach = (by / n) / (ms / n / 1e3) / 1e9
         out["roofline"] = {"bound": "hbm", "kernel": "step", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "avg_ms": round(ms / n, 5),
-                           "alg_bytes_per_launch": by / n}
+                           "launches": n, "alg_bytes_per_launch": by / n,
+                           "note": "k_step of one 32-id batch (32 sub-queries over 16 partitions: latency-bound, "
+                                   "one workgroup per sub-query gathers 196 rows); every launch of the timed batches"}
     # C2_CLIENTS clients of the one server DB, every batch of all of them answered
     # together (pm_batchpir_group_*: one shared step per round)
     clients = [g] + [g.Client(1000 + i, pm.Context(0)) for i in range(C2_CLIENTS - 1)]
@@ -162,6 +164,8 @@ def batch_pir_msmarco(ctx, with_cpu: bool):
         grp.QueryWithMask(b)
     for c in clients:
         c.ctx.sync()
+    clients[0].ctx.timing_reset()
+    clients[0].ctx.timing(2)   # the shared steps run on the first client's stream
     t0 = time.perf_counter()
     gbad = 0
     for b in gb[10:]:
@@ -171,10 +175,20 @@ def batch_pir_msmarco(ctx, with_cpu: bool):
     for c in clients:
         c.ctx.sync()
     gon = time.perf_counter() - t0
+    clients[0].ctx.timing(False)
     out["clients_grouped"] = {"clients": C2_CLIENTS, "batches_per_client": C2_BATCHES,
                               "batch_queries_per_s": round(C2_CLIENTS * C2_BATCHES / gon, 1),
                               "ids_per_s": round(C2_CLIENTS * C2_BATCHES * C2_B / gon, 1),
                               "ms_per_round": round(gon / C2_BATCHES * 1e3, 4), "first_response_mismatches": gbad}
+    n, ms, by = clients[0].ctx.timing_get("answer")
+    if n:
+        ach = (by / n) / (ms / n / 1e3) / 1e9
+        out["clients_grouped"]["roofline"] = {
+            "bound": "hbm", "kernel": "answer", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "avg_ms": round(ms / n, 5), "launches": n,
+            "alg_bytes_per_launch": by / n,
+            "kernel_avg_us": {k: round(v[1] / v[0] * 1e3, 3) for k, v in
+                              ((k, clients[0].ctx.timing_get(k)) for k in ("hint_match", "resolve", "answer")) if v[0]}}
     del grp, clients
     if with_cpu:
         from oracle import oracle as O
@@ -193,6 +207,85 @@ def batch_pir_msmarco(ctx, with_cpu: bool):
     return out
 
 
+# MS-MARCO-shaped private search (BASELINE.json metric's second dataset;
+# reproduction/msmarco/reproduce.sh:224-230: private-search -n 3201821 -d 192
+# -m 32 -k 100 -q 1000 -step 20 -parallel 3): synthetic d=192 vectors ~
+# N(0, sigma_j), a degree-32 graph built on the GPU, k = 100,
+# and every session runs past its 45-query maintenance window.
+MS_N, MS_DIM, MS_K, MS_SESSIONS, MS_GROUPS, MS_QUERIES, MS_WARMUP = 3_201_821, 192, 100, 64, 2, 48, 2
+
+
+def private_search_msmarco(local, args, with_cpu: bool):
+    import gc
+
+    import pacmann_amd as pm
+    from pacmann_amd.report import compute_recall
+    from pacmann_amd.synth import msmarco_like_vectors
+    ctx = pm.Context(local)
+    v = msmarco_like_vectors(MS_N, MS_DIM, seed=501)
+    ctx.sync()
+    t0 = time.perf_counter()
+    g, tm = pm.build_graph(v, M, 1.2, seed=502, ctx=ctx)
+    build = {k: round(x, 4) for k, x in tm.items()}
+    build["total_s"] = round(time.perf_counter() - t0, 4)
+    S2, nq = MS_SESSIONS, MS_WARMUP + MS_QUERIES
+    rng = np.random.default_rng(503)
+    qs = (v[rng.integers(0, MS_N, S2 * nq)] + rng.normal(0, 0.1, (S2 * nq, MS_DIM))).astype(np.float32)
+    qs = qs.reshape(S2, nq, MS_DIM)
+    base = pm.PIRGraphInfo(v, g, pir_seed=601, search_seed=602, ctx=ctx)
+    base.Preprocess()
+    sess = [base] + [base.Session(601 + i, 602 + i, pm.Context(local)) for i in range(1, S2)]
+    for s_ in sess[1:]:
+        s_.Preprocess()
+    ctxs = [s_.ctx for s_ in sess]
+    pm.search_loop_batched(sess, qs[:, :MS_WARMUP], MS_K, STEP, PARALLEL, MS_GROUPS, args.threads)
+    for c in ctxs:
+        c.sync()
+        c.timing_reset()
+        c.timing(2)
+    t0 = time.perf_counter()
+    ans, _, online, maint = pm.search_loop_batched(sess, qs[:, MS_WARMUP:], MS_K, STEP, PARALLEL, MS_GROUPS,
+                                                   args.threads)
+    for c in ctxs:
+        c.sync()
+    wall = time.perf_counter() - t0
+    for c in ctxs:
+        c.timing(False)
+
+    def tsum(name):
+        r = [c.timing_get(name) for c in ctxs]
+        return tuple(sum(x[i] for x in r) for i in range(3))
+    kt = {k: tsum(k) for k in ("prep_offsets", "prep_fold", "prep_repl", "hint_match", "resolve", "answer")}
+    preps = [s_.PIR.stats()["PrepCount"] for s_ in sess]
+    tq = qs[:, MS_WARMUP:].reshape(-1, MS_DIM)
+    gt = pm.knn(v, tq, K_TOP, ctx)
+    recall = compute_recall(gt, ans.reshape(-1, MS_K)[:, :K_TOP], K_TOP)
+    out = {"workload": "MS-MARCO-shaped private search (reproduce.sh:224-230): 3,201,821 x d=192 synthetic "
+                       "N(0, sigma_j) vectors, degree-32 graph built on the GPU, 896-B PIR entries "
+                       "(16 partitions, CS 1,024 / SS 196), k = 100, step 20, parallel 3",
+           "sessions": S2, "lockstep_groups": MS_GROUPS, "queries_per_session": MS_QUERIES,
+           "private_queries_per_s": round(S2 * MS_QUERIES / wall, 2), "wall_s": round(wall, 4),
+           "online_s_per_query": round(float(np.mean(online)) / MS_QUERIES, 6),
+           "maintenance_s_per_query": round(float(np.mean(maint)) / MS_QUERIES, 6),
+           "maintenances_in_region": int(sum(preps) - S2),   # PrepCount is 1 after the first preprocessing
+           "recall_at_10": round(float(recall), 4), "graph_build": build,
+           "kernel_avg_us": {k: round(x[1] / x[0] * 1e3, 3) for k, x in kt.items() if x[0]}}
+    n, ms, by = kt["answer"]
+    if n and by:
+        ach = (by / n) / (ms / n / 1e3) / 1e9
+        out["roofline"] = {"bound": "hbm", "kernel": "answer", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "avg_ms": round(ms / n, 5),
+                           "launches": n, "alg_bytes_per_launch": by / n,
+                           "aggregate": {"achieved": round(by / wall / 1e9, 1),
+                                         "frac": round(by / wall / 1e9 / HBM_PEAK_GBS, 4)}}
+    if with_cpu:   # the oracle replaying session 0's workload, one core
+        cb = cpu_baseline(v, g, qs[0], MS_WARMUP, ans[0], ctx, 601, 602, k=MS_K)
+        out["cpu_baseline"] = cb
+    del sess, base, ctxs
+    gc.collect()
+    return out
+
+
 # BASELINE.json configs[3] / configs[4]: BIGANN-shaped batch PIR.  Entries are
 # PIRGraphInfo's wire format for d = 128, m = 32 (private-search.go:418-439):
 # (128 + 32) * 4 B = 640 B = 80 words.  The DB is generated on the device
@@ -204,9 +297,54 @@ BIG_E, BIG_ROUNDS, BIG_PROFILE_ROUNDS = 80, 400, 40
 
 def bigann_pir(name, n_entries, layout, rank, ws, local, dist, nccl_group, rounds=BIG_ROUNDS):
     """One BIGANN block on every rank.  `layout` = shards the 16 partitions are
-    split into; rank r holds shard r (layout == ws: the whole DB over the node,
-    combined by an RCCL all-reduce per round; layout > ws: only shards
-    0..ws-1 are measured, one per rank, and no combine is run)."""
+    split into.  layout == ws: rank r holds shard r, the whole DB over the
+    node, combined by an RCCL all-reduce per round.  layout > ws (the 1B DB
+    on fewer than 8 GPUs: 640 GB does not fit one GPU's 288 GB): each rank
+    measures the shards r, r + ws, ... one after another, and the block
+    reports the layout's round time as the slowest shard's (modelled: the
+    shards of a real 8-GPU run answer concurrently; its all-reduce is not
+    included)."""
+    if layout <= ws:
+        return bigann_shard(name, n_entries, layout, rank, rank, ws, local, dist, nccl_group, rounds)
+    per = [bigann_shard(name, n_entries, layout, sh, rank, ws, local, dist, nccl_group, rounds, reduce=False)
+           for sh in range(rank, layout, ws)]
+    out = dict(per[0])
+    if dist:   # every rank's shards, on rank 0
+        import torch
+        t = torch.zeros((layout, 4), dtype=torch.float64)
+        for sh, r in zip(range(rank, layout, ws), per):
+            t[sh] = torch.tensor([r["ms_per_round"], r["preprocessing_s"], r["check"]["mismatches"],
+                                  r["check"]["ids_answered"]], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        rows = t.tolist()
+    else:
+        rows = [[r["ms_per_round"], r["preprocessing_s"], r["check"]["mismatches"], r["check"]["ids_answered"]]
+                for r in per]
+    ms_round = max(r[0] for r in rows)
+    prep = max(r[1] for r in rows)
+    support = per[0]["support_batch_num"]
+    online_q = ms_round * STEP / 1e3
+    maint_q = prep / support * STEP * PARALLEL
+    out["shards_measured"] = layout
+    out["per_shard"] = [{"shard": i, "ms_per_round": round(r[0], 4), "preprocessing_s": round(r[1], 4)}
+                        for i, r in enumerate(rows)]
+    out["check"] = {"ids_answered": int(sum(r[3] for r in rows)), "mismatches": int(sum(r[2] for r in rows))}
+    out["modelled_layout"] = {
+        "ms_per_round": round(ms_round, 4), "preprocessing_s": round(prep, 4),
+        "online_s_per_query": round(online_q, 6), "maintenance_s_per_query": round(maint_q, 6),
+        "private_queries_per_s": round(1.0 / (online_q + maint_q), 2),
+        "note": f"all {layout} shards measured one after another on {ws} GPU(s); a {layout}-GPU node answers "
+                "a round in the slowest shard's time (taken here) plus one RCCL all-reduce of the round's "
+                "96 x 81 words (not included: unmeasured on one GPU)"}
+    out["combine"] = (f"none measured: the {layout} shards ran one after another on this GPU; at {layout} GPUs "
+                      "the rounds combine through ShardedBatchPIR's device-resident RCCL all-reduce")
+    return out
+
+
+def bigann_shard(name, n_entries, layout, shard, rank, ws, local, dist, nccl_group, rounds=BIG_ROUNDS,
+                 reduce=True):
+    """Shard `shard` of the layout on this rank (see bigann_pir); reduce: the
+    times are the max and the checks the sum over the ranks (one shard each)."""
     import gc
 
     import pacmann_amd as pm
@@ -219,8 +357,8 @@ def bigann_pir(name, n_entries, layout, rank, ws, local, dist, nccl_group, round
                              device=local)
         g = sp.pir
     else:
-        g = pm.SimpleBatchPianoPIR(n_entries, BIG_E * 8, M, None, F, seed=31, ctx=ctx, shard=rank, nshards=layout,
-                                   db_seed=41)
+        g = pm.SimpleBatchPianoPIR(n_entries, BIG_E * 8, M, None, F, seed=31, ctx=ctx, shard=shard,
+                                   nshards=layout, db_seed=41)
     ctx.sync()
     t_create = time.perf_counter() - t0
     ctx.timing_reset()
@@ -235,7 +373,7 @@ def bigann_pir(name, n_entries, layout, rank, ws, local, dist, nccl_group, round
     kprep = {k: ctx.timing_get(k) for k in ("prep_offsets", "prep_fold", "prep_repl")}
     stats = g.stats()
     PS = stats["PartitionSize"]
-    sub = g.SubConfig(rank % layout)
+    sub = g.SubConfig(shard)
     rng = np.random.default_rng(4242)
     ids = rng.integers(0, n_entries, size=(rounds + BIG_PROFILE_ROUNDS + 10, PARALLEL * M)).astype(np.uint64)
     def one(q):
@@ -267,7 +405,7 @@ def bigann_pir(name, n_entries, layout, rank, ws, local, dist, nccl_group, round
         if combine:
             mine = np.ones(len(q), bool)
         else:
-            mine = (q // np.uint64(PS)) % np.uint64(layout) == np.uint64(rank % layout)
+            mine = (q // np.uint64(PS)) % np.uint64(layout) == np.uint64(shard)
         bad += int((ok & ~mine).sum())
         sel = np.where(ok)[0]
         nok += len(sel)
@@ -279,7 +417,7 @@ def bigann_pir(name, n_entries, layout, rank, ws, local, dist, nccl_group, round
     del g, keep
     gc.collect()
     ctx.close()
-    if dist:
+    if dist and reduce:
         import torch
         t = torch.tensor([prep, online, t_create], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -301,8 +439,8 @@ def bigann_pir(name, n_entries, layout, rank, ws, local, dist, nccl_group, round
         return {"avg_ms": round(ms / n, 5), "alg_bytes_per_launch": by / n, "achieved": round(ach, 1),
                 "unit": "GB/s", "peak": HBM_PEAK_GBS, "frac": round(ach / HBM_PEAK_GBS, 4)}
 
-    n_part = sum(1 for p in range(16) if p % layout == rank % layout)
-    rows_local = sum(min(PS, n_entries - p * PS) for p in range(16) if p % layout == rank % layout)
+    n_part = sum(1 for p in range(16) if p % layout == shard)
+    rows_local = sum(min(PS, n_entries - p * PS) for p in range(16) if p % layout == shard)
     fold = roof(kprep["prep_fold"])
     if fold:
         comp = rows_local * BIG_E * 8
@@ -327,7 +465,8 @@ def bigann_pir(name, n_entries, layout, rank, ws, local, dist, nccl_group, round
         "workload": f"{name}: {n_entries:,} x 640 B entries (d=128 f32 + m=32 u32 ids), BatchSize 32 "
                     f"(16 partitions), FailureProbLog2 8, device-generated uniform DB; rounds of "
                     f"{PARALLEL * M} uniform ids, {STEP} rounds per private query",
-        "n_ranks": ws, "layout_shards": layout, "shards_measured": min(ws, layout),
+        "n_ranks": ws, "layout_shards": layout, "shards_measured": min(ws, layout), "shard": shard,
+        "support_batch_num": stats["SupportBatchNum"],
         "partitions_per_rank": n_part, "rank_db_gb": round(rows_local * BIG_E * 8 / 1e9, 2),
         "subconfig": {k: sub[k] for k in ("ChunkSize", "SetSize", "PrimaryHintNum", "MaxQueryPerChunk",
                                           "MaxQueryNum")},
@@ -405,25 +544,43 @@ def dist_init():
     return dist, dist.get_rank(), ws, local % max(ndev, 1)
 
 
-def cpu_baseline(v, g, queries, ctx):
-    """The oracle (single-thread C++ restatement of the Go/AVX path) on a bounded
-    sample of the same workload: one preprocessing, then 46 queries = two
-    23-query maintenance windows, value = q / (online + maintenance); with the
-    recall@10 of its answers."""
+def cpu_baseline(v, g, q0, warmup, answers0, ctx, pir_seed, search_seed, k=K_TOP):
+    """The oracle (single-thread C++ restatement of the Go/AVX path; its hint
+    fold on one thread like the reference's ThreadNum = 1) replaying session
+    0's exact workload: same graph, same PIR and search seeds, the same
+    warm-up queries and then the same timed queries q0[warmup:].  value =
+    queries / (online + maintenance) over the replay; its answers are compared
+    with session 0's timed answers one by one, and both recalls are computed
+    on those identical queries."""
     import pacmann_amd as pm
     from oracle import oracle as O
     from pacmann_amd.report import compute_recall
-    og = O.Graph(v, g, pir_seed=11, search_seed=12)
+    O.set_prep_threads(1)
+    og = O.Graph(v, g, pir_seed=pir_seed, search_seed=search_seed)
     t0 = time.perf_counter()
     og.Preprocess()
     prep = time.perf_counter() - t0
-    nq = 46
-    ans, online, maint = og.SearchLoop(queries[:nq], K_TOP, STEP, PARALLEL)
-    rec = compute_recall(pm.knn(v, queries[:nq], K_TOP, ctx), ans, K_TOP)
+    nq = q0.shape[0]
+    ans, online, maint = og.SearchLoop(q0, k, STEP, PARALLEL)
+    timed = ans[warmup:]
+    gt = pm.knn(v, q0[warmup:], K_TOP, ctx)
+    same = (timed == answers0).all(axis=1)
     out = {"value": nq / (online + maint), "unit": "queries/s", "cores": 1, "kind": "port",
-           "recall_at_10": round(float(rec), 4),
-           "sample": f"{nq} SIFT1M-shaped private queries (2 maintenance windows) after one "
-                     f"{prep:.2f}s preprocessing; online {online:.2f}s + maintenance {maint:.2f}s"}
+           "identical_answers": {"queries": int(len(same)), "identical": int(same.sum()),
+                                 "frac": round(float(same.mean()), 6)},
+           "recall_at_10": round(float(compute_recall(gt, timed, K_TOP)), 4),
+           "gpu_recall_at_10_same_queries": round(float(compute_recall(gt, answers0, K_TOP)), 4),
+           "sample": f"session 0's workload replayed: {nq} private queries ({warmup} warm-up + {nq - warmup} timed, "
+                     f"same seeds) after one {prep:.2f}s preprocessing; online {online:.2f}s + "
+                     f"maintenance {maint:.2f}s"}
+    return out
+
+
+def cpu_baseline_all_cores(v, g, out):
+    """The oracle on all the box's host cores (16 per GPU): one independent
+    client per core over the same data, like the GPU's sessions."""
+    from oracle import oracle as O
+    nq = 46
     # all host cores (the box's CPU share: 16 per GPU): one independent oracle
     # client per core, like the GPU's sessions, over the same data; each runs
     # the same sample shape (one preprocessing, then 46 queries = two
@@ -476,6 +633,9 @@ def main():
     ap.add_argument("--no-config0", action="store_true", help="skip the InnerProduct scan block")
     ap.add_argument("--combine", choices=["rccl", "gloo"], default="rccl",
                     help="collective of the sharded BIGANN rounds (gloo: host tensors, e.g. ranks sharing one GPU)")
+    ap.add_argument("--no-kernel-timing", action="store_true",
+                    help="no per-launch events in the timed region (to check they cost nothing)")
+    ap.add_argument("--no-msmarco-search", action="store_true", help="skip the MS-MARCO d=192 private-search block")
     ap.add_argument("--graph", choices=["built", "random"], default="built",
                     help="GPU-built kNN+robustPrune graph (default) or the reference's synthetic random graph")
     args = ap.parse_args()
@@ -506,9 +666,13 @@ def main():
     if args.warmup:
         serve(qsess[:, :args.warmup])
 
+    # every kernel of the timed region is timed where it runs: events on the
+    # streams the kernels are launched on, the step kernels' carried in their
+    # own dispatch packets (hipExtLaunchKernelGGL); nothing is synchronised
+    # for it, so this is the load `value` is measured under
     for c in ctxs:
         c.timing_reset()
-        c.timing(True)
+        c.timing(0 if args.no_kernel_timing else 2)
     if dist:
         dist.barrier()
     for c in ctxs:
@@ -523,27 +687,45 @@ def main():
     for c in ctxs:
         c.timing(False)
 
-    def tsum(name):
-        r = [c.timing_get(name) for c in ctxs]
+    def tsum(name, cs=ctxs):
+        r = [c.timing_get(name) for c in cs]
         return tuple(sum(x[i] for x in r) for i in range(3))
 
-    ktime = {k: tsum(k) for k in PREP_KERNELS}
+    ktime = {k: tsum(k) for k in KERNELS}
     htime = {k: tsum(k) for k in HOST}
     nsteps = htime["host_step_launch"][0]   # batch-PIR steps run in the timed region (all sessions)
-    # profile window (after the timed region, not part of `value`): per-launch
-    # device time of the step kernels under the same S-session load, from
-    # events carried in the kernels' own dispatch packets
-    for c in ctxs:
-        c.timing_reset()
-        c.timing(2)
-    w0 = args.warmup + args.steps
-    serve(qsess[:, w0:w0 + PROFILE_QUERIES])
-    for c in ctxs:
-        c.timing(False)
-    for k in STEP_KERNELS:
-        n, ms, by = tsum(k)
-        # scaled to the timed region's step count: launches, device ms, bytes
-        ktime[k] = (nsteps, ms / max(n, 1) * nsteps, by / max(n, 1) * nsteps)
+    # the same kernels with ONE lock-step group alone on the GPU (no other
+    # group's kernels beside them), and one client's maintenance alone: the
+    # isolated per-launch times beside the contended ones above
+    isolated = None
+    if args.mode == "batched" and not args.no_kernel_timing:
+        gsz = max(1, S // max(1, args.groups))
+        grp = sess[:gsz]
+        for c in ctxs:
+            c.timing_reset()
+        grp[0].ctx.timing(2)
+        w0 = args.warmup + args.steps
+        pm.search_loop_batched(grp, qsess[:gsz, w0:w0 + PROFILE_QUERIES], K_TOP, STEP, PARALLEL, 1,
+                               min(args.threads, gsz))
+        grp[0].ctx.timing(False)
+        one = sess[-1]
+        one.ctx.timing_reset()
+        one.ctx.timing(1)
+        one.PIR.Preprocessing()
+        one.ctx.timing(False)
+        isolated = {"sessions": gsz, "queries_each": PROFILE_QUERIES, "kernel_avg_us": {}}
+        for k in ("hint_match", "resolve", "answer"):
+            n, ms, by = grp[0].ctx.timing_get(k)
+            if n:
+                isolated["kernel_avg_us"][k] = round(ms / n * 1e3, 3)
+                if by:
+                    ach = (by / n) / (ms / n / 1e3) / 1e9
+                    isolated[f"{k}_roofline"] = {"achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
+                                                 "alg_bytes_per_launch": by / n}
+        for k in ("prep_offsets", "prep_fold", "prep_repl"):
+            n, ms, _ = one.ctx.timing_get(k)
+            if n:
+                isolated["kernel_avg_us"][f"{k}_one_client"] = round(ms / n * 1e3, 3)
     # recall@10 of every timed answer against exact kNN (ComputeRecall, build_graph.go:821-863)
     from pacmann_amd.report import compute_recall
     tq = qsess[:, args.warmup:args.warmup + args.steps].reshape(-1, DIM)
@@ -566,29 +748,6 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    # BASELINE.json configs[3] (BIGANN-100M, sharded over the ranks) and
-    # configs[4] (BIGANN-1B in 8 shards): every rank takes part
-    big = {}
-    if not args.no_bigann:
-        nccl_group = None
-        if dist and args.combine == "rccl":
-            import datetime
-
-            import torch
-            torch.cuda.set_device(local)
-            nccl_group = dist.new_group(backend="nccl", timeout=datetime.timedelta(seconds=180))
-        for key, nm, n_entries, layout in (("config3_bigann_100m", "BIGANN-100M-shaped (configs[3])",
-                                            100_000_000, ws),
-                                           ("config4_bigann_1b", "BIGANN-1B-shaped (configs[4]), 8-way layout",
-                                            1_000_000_000, 8)):
-            try:
-                big[key] = bigann_pir(nm, n_entries, layout, rank, ws, local, dist, nccl_group)
-            except Exception as e:   # recorded, never fatal to the headline line
-                big[key] = {"error": f"{type(e).__name__}: {e}"}
-    if rank != 0:
-        dist.destroy_process_group()
-        return
-
     total_q = args.steps * S * ws
     value = total_q / elapsed
     # dominant kernel: largest device time over the timed region
@@ -686,14 +845,53 @@ def main():
         "rows_check": {"seen": int(htime["host_rows_seen"][0]), "torn": int(htime["host_rows_torn"][0])},
         "dominant_kernel": dom,
     }
+    if isolated:
+        out["isolated"] = isolated
     if not args.no_cpu_baseline and ws == 1:
-        out["cpu_baseline"] = cpu_baseline(v, g, queries[S * nq:], ctx0)
+        cb = cpu_baseline(v, g, qsess[0, :args.warmup + args.steps], args.warmup, answers[0], ctx0,
+                          11 + 97 * rank, 12 + 97 * rank)
+        cpu_baseline_all_cores(v, g, cb)
+        out["cpu_baseline"] = cb
+    # the SIFT1M serving state is done with: free its device memory (HBM) for the other blocks
+    import gc
+    del sess, base, ctxs, ktime
+    gc.collect()
     if ws == 1 and not args.no_config2:
-        out["config2_batch_pir"] = batch_pir_msmarco(ctxs[0], not args.no_cpu_baseline)
+        c2 = pm.Context(local)
+        out["config2_batch_pir"] = batch_pir_msmarco(c2, not args.no_cpu_baseline)
+        del c2
+        gc.collect()
+    if ws == 1 and not args.no_msmarco_search:
+        try:
+            out["config2_private_search"] = private_search_msmarco(local, args, not args.no_cpu_baseline)
+        except Exception as e:   # recorded, never fatal to the headline line
+            out["config2_private_search"] = {"error": f"{type(e).__name__}: {e}"}
+        gc.collect()
     if ws == 1 and not args.no_config0:
-        out["config0_inner_product"] = inner_product_scan(ctxs[0], not args.no_cpu_baseline)
-    out.update(big)
-    print(json.dumps(out), flush=True)
+        c0 = pm.Context(local)
+        out["config0_inner_product"] = inner_product_scan(c0, not args.no_cpu_baseline)
+        del c0
+        gc.collect()
+    # BASELINE.json configs[3] (BIGANN-100M, sharded over the ranks) and
+    # configs[4] (BIGANN-1B in 8 shards): every rank takes part
+    if not args.no_bigann:
+        nccl_group = None
+        if dist and args.combine == "rccl":
+            import datetime
+
+            import torch
+            torch.cuda.set_device(local)
+            nccl_group = dist.new_group(backend="nccl", timeout=datetime.timedelta(seconds=180))
+        for key, nm, n_entries, layout in (("config3_bigann_100m", "BIGANN-100M-shaped (configs[3])",
+                                            100_000_000, ws),
+                                           ("config4_bigann_1b", "BIGANN-1B-shaped (configs[4]), 8-way layout",
+                                            1_000_000_000, 8)):
+            try:
+                out[key] = bigann_pir(nm, n_entries, layout, rank, ws, local, dist, nccl_group)
+            except Exception as e:   # recorded, never fatal to the headline line
+                out[key] = {"error": f"{type(e).__name__}: {e}"}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
 

@@ -168,6 +168,7 @@ struct pm_ctx {
   // (PmOutHdr::csum): 0 = no check, 1 = count a mismatch ("host_rows_torn")
   // and fail the step, 2 = count it and wait for the row to match (PM_ROWS_CHECK)
   int rows_check = 2;
+  std::vector<uint64_t> hash_mult;   // row_hash_mult(w) for every word a row can have
   std::string last_kernel;
   // host-side wall-clock accumulators ("host_*" names in pm_timing_get)
   uint64_t host_n[HT_COUNT] = {};
@@ -238,6 +239,8 @@ extern "C" int pm_ctx_create(int device, pm_ctx** out) {
   const char* vr = getenv("PM_VERIFY_ROWS");
   c->verify_rows = vr && vr[0] == '1';
   if (const char* rc = getenv("PM_ROWS_CHECK")) c->rows_check = atoi(rc);
+  c->hash_mult.resize(pmk::step_max_e());
+  for (size_t w = 0; w < c->hash_mult.size(); ++w) c->hash_mult[w] = row_hash_mult(w);
   const char* ng = getenv("PM_NO_GUESS");
   c->no_guess = ng && ng[0] == '1';
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
@@ -628,7 +631,7 @@ static int wait_step(pm_ctx* c, const PmOutHdr* hdr, uint32_t nsub, uint32_t tok
           const volatile uint64_t* rw = (const volatile uint64_t*)(rows + s * row_bytes);
           const volatile uint64_t* cs = &hdr[s].csum;
           uint64_t x = token * kCsumMix;
-          for (size_t w = w0; w < w1; ++w) x ^= row_hash_word(rw[w], w);
+          for (size_t w = w0; w < w1; ++w) x += rw[w] * c->hash_mult[w];
           if (first_look) c->host_add(HT_ROWS_SEEN, 0);
           if (x != *cs) {
             if (first_look) c->host_add(HT_ROWS_TORN, 0);
@@ -2538,19 +2541,26 @@ extern "C" int pm_build_graph(pm_ctx* c, const float* vectors, uint64_t n, uint6
       visit(u, [&](uint64_t j, uint32_t v) { if (keep(u, j, v)) *o++ = v; });
     }
   });
-  // second pass: robustPrune of the lists above m (:464-466) on the GPU
-  std::vector<uint32_t> big;
-  for (uint64_t u = 0; u < n; ++u) if (clen2[u] > m) big.push_back((uint32_t)u);
+  // second pass: robustPrune of the lists above m (:464-466) on the GPU.  Lists
+  // above the kernel's LDS sort (hub vertices: every in-edge of a popular
+  // vertex is kept, :448-462 sample by the TARGET's inbounds) get their
+  // candidate distances on the GPU, their (L2Dist, position) order by a host
+  // sort of those exact keys, and the same greedy pass (presorted k_prune).
+  std::vector<uint32_t> big, huge;
+  for (uint64_t u = 0; u < n; ++u)
+    if (clen2[u] > pmk::prune_max_list()) huge.push_back((uint32_t)u);
+    else if (clen2[u] > m) big.push_back((uint32_t)u);
   auto t3 = Clock::now();
-  if (!big.empty()) {
-    DevBuf dv, doff, dlen, dids, dout, dol;
-    CHK(dv.reserve(big.size() * 4));
+  if (!big.empty() || !huge.empty()) {
+    DevBuf dv, dh, doff, dlen, dids, dout, dol, dd, dpos;
+    CHK(dv.reserve(std::max<size_t>(1, big.size()) * 4));
+    CHK(dh.reserve(std::max<size_t>(1, huge.size()) * 4));
     CHK(doff.reserve(n * 8));
     CHK(dlen.reserve(n * 4));
     CHK(dids.reserve(std::max<uint64_t>(4, conn.size() * 4)));
     CHK(dout.reserve(n * m * 4));
     CHK(dol.reserve(n * 4));
-    HIPCHK(hipMemcpyAsync(dv.p, big.data(), big.size() * 4, hipMemcpyHostToDevice, st));
+    if (!big.empty()) HIPCHK(hipMemcpyAsync(dv.p, big.data(), big.size() * 4, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(doff.p, coff.data(), n * 8, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(dlen.p, clen2.data(), n * 4, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(dids.p, conn.data(), conn.size() * 4, hipMemcpyHostToDevice, st));
@@ -2558,16 +2568,48 @@ extern "C" int pm_build_graph(pm_ctx* c, const float* vectors, uint64_t n, uint6
       pmk::prune(st, X.x.as<float>(), (uint32_t)dim, dv.as<uint32_t>(), big.size(), doff.as<uint64_t>(), 0,
                  dlen.as<uint32_t>(), dids.as<uint32_t>(), (uint32_t)m, alpha, dout.as<uint32_t>(),
                  dol.as<uint32_t>(), err.as<uint32_t>()); });
+    if (!huge.empty()) {
+      CHK(dd.reserve(conn.size() * 4));
+      CHK(dpos.reserve(conn.size() * 4));
+      HIPCHK(hipMemcpyAsync(dh.p, huge.data(), huge.size() * 4, hipMemcpyHostToDevice, st));
+      pmk::cand_dist(st, X.x.as<float>(), (uint32_t)dim, dh.as<uint32_t>(), huge.size(), doff.as<uint64_t>(),
+                     dlen.as<uint32_t>(), dids.as<uint32_t>(), dd.as<float>());
+      std::vector<float> hd(conn.size());
+      HIPCHK(hipMemcpyAsync(hd.data(), dd.p, conn.size() * 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      std::vector<uint32_t> pos(conn.size());
+      par_for(huge.size(), [&](uint64_t a, uint64_t b) {
+        std::vector<uint64_t> key;
+        for (uint64_t i = a; i < b; ++i) {   // sort.Slice by distance; ties by position (as the LDS sort)
+          const uint32_t u = huge[i];
+          const uint64_t o = coff[u], len = clen2[u];
+          key.resize(len);
+          for (uint64_t j = 0; j < len; ++j) {
+            uint32_t bits;
+            memcpy(&bits, &hd[o + j], 4);
+            key[j] = ((uint64_t)bits << 32) | j;
+          }
+          std::sort(key.begin(), key.end());
+          for (uint64_t j = 0; j < len; ++j) pos[o + j] = (uint32_t)key[j];
+        }
+      });
+      HIPCHK(hipMemcpyAsync(dpos.p, pos.data(), pos.size() * 4, hipMemcpyHostToDevice, st));
+      c->timed("prune", 0.0, [&] {
+        pmk::prune(st, X.x.as<float>(), (uint32_t)dim, dh.as<uint32_t>(), huge.size(), doff.as<uint64_t>(), 0,
+                   dlen.as<uint32_t>(), dids.as<uint32_t>(), (uint32_t)m, alpha, dout.as<uint32_t>(),
+                   dol.as<uint32_t>(), err.as<uint32_t>(), dpos.as<uint32_t>(), dd.as<float>()); });
+    }
     std::vector<uint32_t> P(n * m), PL(n);
     HIPCHK(hipMemcpyAsync(P.data(), dout.p, n * m * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(PL.data(), dol.p, n * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(&e, err.p, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    if (e) return fail(PM_EINVAL, "robustPrune: a sampled connection list exceeds 4096 candidates");
-    for (uint32_t u : big) {   // robustPrune of a list > m returns exactly m
-      memcpy(conn.data() + coff[u], &P[(uint64_t)u * m], m * 4);
-      clen2[u] = PL[u];
-    }
+    if (e) return fail(PM_EINVAL, "robustPrune: a connection list above the kernel's limit");
+    for (const auto* lst : {&big, &huge})
+      for (uint32_t u : *lst) {   // robustPrune of a list > m returns exactly m
+        memcpy(conn.data() + coff[u], &P[(uint64_t)u * m], m * 4);
+        clen2[u] = PL[u];
+      }
   }
   auto t4 = Clock::now();
   // random fill to exactly m (:468-486)

@@ -284,13 +284,19 @@ struct PruneLds {
 // vertex verts[b] (or b): candidates ids[offs[u] .. offs[u] + lens[u]) (offs
 // null: u * stride).  Lists of at most m are kept as they are (:170-172).
 // Writes out[u][0..len) and out_len[u]; err = 1 if a list exceeds kPruneMaxL.
+// Presorted mode (lists above kPruneMaxL, hub vertices): sorted_pos[off + s]
+// is the position of the s-th candidate in (L2Dist, position) order and
+// dist_g[off + pos] its distance (k_cand_dist, sorted on the host); only the
+// first kPruneMaxL discards are kept (the top-up needs at most m).
 __global__ void __launch_bounds__(kBlock) k_prune(const float* __restrict__ X, uint32_t dim,
                                                   const uint32_t* __restrict__ verts, uint64_t nverts,
                                                   const uint64_t* __restrict__ offs, uint64_t stride,
                                                   const uint32_t* __restrict__ lens,
                                                   const uint32_t* __restrict__ ids, uint32_t m, float alpha,
                                                   uint32_t* __restrict__ out, uint32_t* __restrict__ out_len,
-                                                  uint32_t* __restrict__ err) {
+                                                  uint32_t* __restrict__ err,
+                                                  const uint32_t* __restrict__ sorted_pos,
+                                                  const float* __restrict__ dist_g) {
   __shared__ PruneLds L;
   const uint64_t b = blockIdx.x;
   if (b >= nverts) return;
@@ -304,46 +310,49 @@ __global__ void __launch_bounds__(kBlock) k_prune(const float* __restrict__ X, u
     if (tid == 0) out_len[u] = n;
     return;
   }
-  if (n > kPruneMaxL) {
+  const bool pre = sorted_pos != nullptr;
+  if (n > kPruneMaxL && !pre) {
     if (tid == 0) { atomicOr(err, 1u); out_len[u] = 0; }
     return;
   }
   const float* xu = X + u * dim;
-  // dist2u (:176-182) in L2Dist order; 32 candidates per round
-  for (uint32_t r = 0; r < n; r += kBlock / 8) {
-    const uint32_t i = r + g;
-    const uint32_t id = i < n ? c[i] : 0;
-    const float d = l2_group8(xu, X + (uint64_t)id * dim, dim, k);
-    if (i < n && k == 0) {
-      L.dist[i] = d;
-      L.key[i] = ((uint64_t)__float_as_uint(d) << 32) | i;
-    }
-  }
-  uint32_t np2 = 64;
-  while (np2 < n) np2 <<= 1;
-  for (uint32_t i = n + tid; i < np2; i += kBlock) L.key[i] = kNoKey;
-  __syncthreads();
-  // sort.Slice by distance (:184-186); ties by position (stable)
-  for (uint32_t kk = 2; kk <= np2; kk <<= 1) {
-    for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
-      for (uint32_t i = tid; i < np2; i += kBlock) {
-        const uint32_t p = i ^ j;
-        if (p > i) {
-          const uint64_t x = L.key[i], y = L.key[p];
-          const bool up = (i & kk) == 0;
-          if ((x > y) == up) { L.key[i] = y; L.key[p] = x; }
-        }
+  if (!pre) {
+    // dist2u (:176-182) in L2Dist order; 32 candidates per round
+    for (uint32_t r = 0; r < n; r += kBlock / 8) {
+      const uint32_t i = r + g;
+      const uint32_t id = i < n ? c[i] : 0;
+      const float d = l2_group8(xu, X + (uint64_t)id * dim, dim, k);
+      if (i < n && k == 0) {
+        L.dist[i] = d;
+        L.key[i] = ((uint64_t)__float_as_uint(d) << 32) | i;
       }
-      __syncthreads();
     }
-  }
+    uint32_t np2 = 64;
+    while (np2 < n) np2 <<= 1;
+    for (uint32_t i = n + tid; i < np2; i += kBlock) L.key[i] = kNoKey;
+    __syncthreads();
+    // sort.Slice by distance (:184-186); ties by position (stable)
+    for (uint32_t kk = 2; kk <= np2; kk <<= 1) {
+      for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+        for (uint32_t i = tid; i < np2; i += kBlock) {
+          const uint32_t p = i ^ j;
+          if (p > i) {
+            const uint64_t x = L.key[i], y = L.key[p];
+            const bool up = (i & kk) == 0;
+            if ((x > y) == up) { L.key[i] = y; L.key[p] = x; }
+          }
+        }
+        __syncthreads();
+      }
+    }
+  }   // !pre
   // the greedy pass (:188-212): candidate v is accepted unless an accepted a_j
   // has L2Dist(a_j, v) * alpha < dist(u, v); all a_j are tested at once
   uint32_t na = 0, nd = 0;
   for (uint32_t s = 0; s < n; ++s) {
-    const uint32_t pos = (uint32_t)L.key[s];
+    const uint32_t pos = pre ? sorted_pos[off + s] : (uint32_t)L.key[s];
     const uint32_t v = c[pos];
-    const float duv = L.dist[pos];
+    const float duv = pre ? dist_g[off + pos] : L.dist[pos];
     const float* xv = X + (uint64_t)v * dim;
     for (uint32_t i = tid; i < dim; i += kBlock) L.acc[na][i] = xv[i];
     __syncthreads();
@@ -358,7 +367,7 @@ __global__ void __launch_bounds__(kBlock) k_prune(const float* __restrict__ X, u
       ++na;
       if (na == m) break;
     } else {
-      if (tid == 0) L.disc[nd] = v;
+      if (tid == 0 && nd < kPruneMaxL) L.disc[nd] = v;
       ++nd;
     }
   }
@@ -368,6 +377,24 @@ __global__ void __launch_bounds__(kBlock) k_prune(const float* __restrict__ X, u
   const uint32_t fill = na < m ? (m - na < nd ? m - na : nd) : 0;
   for (uint32_t i = tid; i < fill; i += kBlock) out[u * m + na + i] = L.disc[i];
   if (tid == 0) out_len[u] = na + fill;
+}
+
+// L2Dist(x_u, x_v) of every candidate v of vertex verts[b]'s list, in the
+// reference's order (dist2u, build_graph.go:176-182), into dist_g[offs[u] + i]:
+// the keys the host sorts for the presorted k_prune of hub vertices.
+__global__ void __launch_bounds__(kBlock) k_cand_dist(const float* __restrict__ X, uint32_t dim,
+                                                      const uint32_t* __restrict__ verts,
+                                                      const uint64_t* __restrict__ offs,
+                                                      const uint32_t* __restrict__ lens,
+                                                      const uint32_t* __restrict__ ids, float* __restrict__ dist_g) {
+  const uint64_t u = verts[blockIdx.x];
+  const uint32_t g = threadIdx.x >> 3, k = threadIdx.x & 7, n = lens[u];
+  const uint64_t off = offs[u];
+  const float* xu = X + u * dim;
+  for (uint32_t i = g; i < n; i += kBlock / 8) {
+    const float d = l2_group8(xu, X + (uint64_t)ids[off + i] * dim, dim, k);
+    if (k == 0) dist_g[off + i] = d;
+  }
 }
 
 }  // namespace pm
@@ -405,9 +432,15 @@ void knn_rerank(hipStream_t st, const float* X, uint64_t N, uint32_t dim, const 
 }
 void prune(hipStream_t st, const float* X, uint32_t dim, const uint32_t* verts, uint64_t nverts,
            const uint64_t* offs, uint64_t stride, const uint32_t* lens, const uint32_t* ids, uint32_t m,
-           float alpha, uint32_t* out, uint32_t* out_len, uint32_t* err) {
+           float alpha, uint32_t* out, uint32_t* out_len, uint32_t* err, const uint32_t* sorted_pos,
+           const float* dist_g) {
   if (!nverts) return;
   hipLaunchKernelGGL(k_prune, dim3((unsigned)nverts), dim3(kBlock), 0, st, X, dim, verts, nverts, offs, stride, lens,
-                     ids, m, alpha, out, out_len, err);
+                     ids, m, alpha, out, out_len, err, sorted_pos, dist_g);
+}
+void cand_dist(hipStream_t st, const float* X, uint32_t dim, const uint32_t* verts, uint64_t nverts,
+               const uint64_t* offs, const uint32_t* lens, const uint32_t* ids, float* dist_g) {
+  if (!nverts) return;
+  hipLaunchKernelGGL(k_cand_dist, dim3((unsigned)nverts), dim3(kBlock), 0, st, X, dim, verts, offs, lens, ids, dist_g);
 }
 }  // namespace pmk

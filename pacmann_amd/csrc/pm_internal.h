@@ -97,15 +97,15 @@ struct PmRes {
 // memory reach the host in no guaranteed order (measured: 2.6e-4 of rows are
 // torn when the token is first seen), and ordering them costs 2.8-4.4x the
 // answer kernel's time (a system-scope L2 write-back per workgroup, or
-// write-through stores).  So the header carries a 64-bit
-// position-keyed hash of the row words the host reads ([pf_w0, pf_w1) of
-// PmStep), mixed with the step token: the host accepts a row only when its
-// bytes hash to it, else re-reads.  A torn row passes only if the XOR of
-// row_hash_word() over its stale words cancels: probability 2^-64.
+// write-through stores).  So the header carries a multilinear
+// hash of the row words the host reads ([pf_w0, pf_w1) of PmStep):
+//   csum = token * kCsumMix + sum_w row[w] * row_hash_mult(w)   (mod 2^64)
+// with odd multipliers, and the host accepts a row only when its bytes hash
+// to it, else re-reads.  One stale word changes the sum by (new - old) * odd
+// != 0: always detected; several cancel only if their weighted differences
+// sum to 0 mod 2^64.  A stale header (previous step's token) never matches.
 constexpr uint64_t kCsumMix = 0x9E3779B97F4A7C15ull;
-__host__ __device__ inline uint64_t row_hash_word(uint64_t v, uint64_t w) {
-  return sm64(v ^ (w * 0xD6E8FEB86659FD93ull));
-}
+__host__ __device__ inline uint64_t row_hash_mult(uint64_t w) { return sm64(w ^ 0x5851F42D4C957F2Dull) | 1ull; }
 struct alignas(16) PmOutHdr {
   uint32_t status, ref;
   float dist;
@@ -218,5 +218,9 @@ void knn_rerank(hipStream_t st, const float* X, uint64_t N, uint32_t dim, const 
                 const uint32_t* cand, uint32_t K, bool self_base, uint32_t* out, float* dist, uint32_t* len);
 void prune(hipStream_t st, const float* X, uint32_t dim, const uint32_t* verts, uint64_t nverts,
            const uint64_t* offs, uint64_t stride, const uint32_t* lens, const uint32_t* ids, uint32_t m,
-           float alpha, uint32_t* out, uint32_t* out_len, uint32_t* err);
+           float alpha, uint32_t* out, uint32_t* out_len, uint32_t* err, const uint32_t* sorted_pos = nullptr,
+           const float* dist_g = nullptr);
+// L2Dist of every candidate of the listed vertices (hub lists above prune_max_list())
+void cand_dist(hipStream_t st, const float* X, uint32_t dim, const uint32_t* verts, uint64_t nverts,
+               const uint64_t* offs, const uint32_t* lens, const uint32_t* ids, float* dist_g);
 }  // namespace pmk

@@ -1190,14 +1190,14 @@ union RowBuf {   // one decoded entry; the L2 reads its leading floats
 };
 
 // PmOutHdr::csum: the position-keyed hash of the row words [pf_w0, pf_w1)
-// as written (the LDS copy, or zeros), pm_internal.h row_hash_word.  Wave 0
+// as written (the LDS copy, or zeros), pm_internal.h row_hash_mult.  Wave 0
 // only; every lane returns the result.
 __device__ __forceinline__ uint64_t row_csum(const PmStep& S, const RowBuf& row, bool has_row) {
   uint64_t x = 0;
   for (uint32_t w = S.pf_w0 + (threadIdx.x & 63); w < S.pf_w1; w += 64)
-    x ^= row_hash_word(has_row ? row.w[w] : 0, w);
+    x += (has_row ? row.w[w] : 0) * row_hash_mult(w);
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) x ^= __shfl_xor(x, o);
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
   return x;
 }
 
@@ -1232,19 +1232,19 @@ __device__ __forceinline__ void publish_hdr(const PmStep& S, uint32_t s, uint32_
   PM_G PmOutHdr* h = S.hdr_h + s;
   const uint64_t tok = ((uint64_t)S.token << 32) | __float_as_uint(d);   // {dist, token}: bytes 8..15
   if (PM_PUBLISH == 0) {
-    *h = PmOutHdr{status, ref, d, S.token, csum ^ (S.token * kCsumMix), 0};
+    *h = PmOutHdr{status, ref, d, S.token, csum + S.token * kCsumMix, 0};
     return;
   }
   PM_G uint64_t* w = reinterpret_cast<PM_G uint64_t*>(h);
   if (PM_PUBLISH == 3) {   // every byte written through at system scope: no L2 write-back needed
     __hip_atomic_store((uint64_t*)w, ((uint64_t)ref << 32) | status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store((uint64_t*)(w + 2), csum ^ (S.token * kCsumMix), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store((uint64_t*)(w + 2), csum + S.token * kCsumMix, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_store((uint64_t*)(w + 1), tok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     return;
   }
   w[0] = ((uint64_t)ref << 32) | status;
-  w[2] = csum ^ (S.token * kCsumMix);
+  w[2] = csum + S.token * kCsumMix;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __hip_atomic_store((uint64_t*)(w + 1), tok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

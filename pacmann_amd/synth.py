@@ -71,17 +71,31 @@ def random_graph(n, m, seed=0):
     return g.astype(np.uint32)
 
 
-def msmarco_like_vectors(n, d=192, seed=0, sigma_hi=0.82, sigma_lo=0.29, block=1 << 17):
+def msmarco_like_vectors(n, d=192, seed=0, sigma_hi=0.82, sigma_lo=0.29, latent=16, centers=256, block=1 << 17):
     """MS-MARCO-shaped stand-in: the reference's corpus is
     768-d TAS-B embeddings reduced to 192 dims by PCA
-    (reproduction/msmarco/embed_and_reduce.py), so dimension j is centred with
-    a standard deviation that decays along the principal axes — 0.82 at j = 0
-    to 0.29 at j = d-1 in the reference's validation fixture.  Here x_j ~
-    N(0, sigma_j) with sigma_j geometric between those ends, float32."""
+    (reproduction/msmarco/embed_and_reduce.py).  Dimension j is centred with
+    a standard deviation decaying along the principal axes — 0.82 at j = 0 to
+    0.29 at j = d-1 in the reference's validation fixture — and, like real
+    embeddings, the points have a low intrinsic dimension (iid Gaussian
+    coordinates in 192-d would make every point nearly equidistant from every
+    other, and no graph index works on that).  Here: a `latent`-dim Gaussian
+    mixture of `centers` overlapping clusters, mapped to d dims by a random
+    linear map plus isotropic noise, then every dimension standardised and
+    scaled to sigma_j (geometric between the two ends), float32."""
     rng = np.random.default_rng(seed)
-    sig = (sigma_hi * (sigma_lo / sigma_hi) ** (np.arange(d) / max(1, d - 1))).astype(np.float32)
+    c = rng.normal(0, 1.5, size=(centers, latent))
+    W = rng.normal(0, 1.0, size=(latent, d))
+    noise = 0.35
+    mean = c.mean(0) @ W
+    var = ((c.var(0) + 1.0)[:, None] * W ** 2).sum(0) + noise ** 2
+    sig = sigma_hi * (sigma_lo / sigma_hi) ** (np.arange(d) / max(1, d - 1))
+    scale = (sig / np.sqrt(var)).astype(np.float32)
+    W, mean = W.astype(np.float32), mean.astype(np.float32)
     out = np.empty((n, d), dtype=np.float32)
     for a in range(0, n, block):
         b = min(n, a + block)
-        out[a:b] = rng.standard_normal((b - a, d), dtype=np.float32) * sig
+        z = (c[rng.integers(0, centers, size=b - a)] + rng.normal(0, 1.0, size=(b - a, latent))).astype(np.float32)
+        x = z @ W + rng.normal(0, noise, size=(b - a, d)).astype(np.float32)
+        out[a:b] = (x - mean) * scale
     return out

@@ -678,3 +678,27 @@ def test_batch_synth_db_bigann_shard(ctx):
     assert nok > 25 * 96 // ns // 2
     rows = pm.synth_rows(5, [0, 1, N - 1], E)
     assert rows.shape == (3, E) and len({int(r[0]) for r in rows}) == 3
+
+
+def test_build_graph_hub_list_matches_oracle(ctx, oracle):
+    """A hub vertex (the centre of a shell of points in 64-d: every vertex's
+    nearest) collects every in-edge, so its sampled connection list is longer
+    than the prune kernel's LDS sort (4,096): that list takes the presorted
+    path (GPU distances, host sort of the exact keys, the same greedy pass).
+    The graph is bit-identical to the oracle's restatement."""
+    import pacmann_amd as pm
+    rng = np.random.default_rng(31)
+    n, d = 8000, 64
+    u = rng.standard_normal((n, d))
+    u /= np.linalg.norm(u, axis=1, keepdims=True)
+    v = np.clip(np.rint(128 + 100 * u), 0, 255).astype(np.float32)
+    v[0] = 128   # the hub
+    # the hub is in (nearly) every vertex's 1.5m candidates, so robustPrune
+    # keeps it first and its bi-directional list holds that many in-edges
+    ids, _ = oracle.knn(v, v, 49)
+    assert (ids == 0).any(axis=1).sum() > 6000
+    g, _ = pm.build_graph(v, 32, 1.2, seed=5, ctx=ctx)
+    o = oracle.build_graph(v, 32, 1.2, seed=5)
+    if not np.array_equal(g, o):
+        bad = np.where((g != o).any(axis=1))[0]
+        pytest.fail(f"{len(bad)} rows differ, first {bad[:5].tolist()}")
