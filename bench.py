@@ -54,13 +54,21 @@ SESSIONS = 256  # client sessions per GPU (128: 9.9K q/s, 256: 11.0K, 384: 11.5K
 GROUPS = 4      # lock-step groups (GPU_MAX_HW_QUEUES = 4 hardware queues per process)
 THREADS = 16    # host worker threads of the batched loop (the box gives a GPU 16 host cores)
 SYMBOLS = {"prep_fold": "void pm::k_prep_fold_pipe<4, 1, 4, 1>(pm::PmPart const*, unsigned long const*, "
-                        "unsigned long const*, unsigned int, unsigned int, unsigned int, unsigned int)",
+                        "unsigned long const*, unsigned int, unsigned int, unsigned int, unsigned int, unsigned int)",
            "answer": "void pm::k_answer<2>(pm::PmStep)", "step": "void pm::k_step<2>(pm::PmStep)", "resolve": "void pm::k_resolve<true>(pm::PmStep)",
            "hint_match": "pm::k_match(pm::PmStep)", "prep_offsets": "pm::k_prep_offsets(pm::PmPart const*)",
            "gather": "void pm::k_gather<2>(pm::PmStep)"}
 HOST = ["host_search_knn", "host_knn_init", "host_knn_final", "host_knn_batch", "host_knn_update",
         "host_gvi_parse", "host_batch_query", "host_step_launch", "host_step_wait", "host_step_post",
         "host_wait_first_token", "host_wait_all_tokens", "host_rows_seen", "host_rows_torn"]
+
+
+T_START = time.perf_counter()
+
+
+def progress(msg: str):
+    """One line per phase on stderr (long profiler runs show they are alive)."""
+    print(f"[bench {time.perf_counter() - T_START:7.1f}s] {msg}", file=sys.stderr, flush=True)
 
 
 def make_data(rank: int, graph: str, ctx):
@@ -100,6 +108,16 @@ def pmc_traffic(kernel_symbol: str, grid: int | None = None):
         if k and "hbm_bytes_per_dispatch_corrected" in k:
             best = (k["hbm_bytes_per_dispatch_corrected"], str(f.relative_to(ROOT)))
     return best
+
+
+def attach_traffic(roof: dict | None, symbol: str, grid: int) -> None:
+    """roof["traffic"]: PMC HBM bytes per dispatch of `symbol` at launch shape
+    `grid` (threads) from the committed profiles (pmc_traffic), with its source."""
+    if not roof:
+        return
+    tr = pmc_traffic(symbol, grid)
+    roof["traffic"], roof["traffic_source"] = (tr[0], tr[1]) if tr else (None, None)
+    roof["symbol"], roof["grid_threads"] = symbol, grid
 
 
 # BASELINE.json configs[2]: MS-MARCO-shaped batch PIR, the TestBatchPIRPerf
@@ -153,6 +171,7 @@ def batch_pir_msmarco(ctx, with_cpu: bool):
                            "launches": n, "alg_bytes_per_launch": by / n,
                            "note": "k_step of one 32-id batch (32 sub-queries over 16 partitions: latency-bound, "
                                    "one workgroup per sub-query gathers 196 rows); every launch of the timed batches"}
+        attach_traffic(out["roofline"], SYMBOLS["step"], (2 * C2_B + 16) * 1024)
     # C2_CLIENTS clients of the one server DB, every batch of all of them answered
     # together (pm_batchpir_group_*: one shared step per round)
     clients = [g] + [g.Client(1000 + i, pm.Context(0)) for i in range(C2_CLIENTS - 1)]
@@ -189,6 +208,7 @@ def batch_pir_msmarco(ctx, with_cpu: bool):
             "alg_bytes_per_launch": by / n,
             "kernel_avg_us": {k: round(v[1] / v[0] * 1e3, 3) for k, v in
                               ((k, clients[0].ctx.timing_get(k)) for k in ("hint_match", "resolve", "answer")) if v[0]}}
+        attach_traffic(out["clients_grouped"]["roofline"], SYMBOLS["answer"], C2_CLIENTS * C2_B * 512)
     del grp, clients
     if with_cpu:
         from oracle import oracle as O
@@ -261,7 +281,8 @@ def private_search_msmarco(local, args, with_cpu: bool):
     gt = pm.knn(v, tq, K_TOP, ctx)
     recall = compute_recall(gt, ans.reshape(-1, MS_K)[:, :K_TOP], K_TOP)
     out = {"workload": "MS-MARCO-shaped private search (reproduce.sh:224-230): 3,201,821 x d=192 synthetic "
-                       "N(0, sigma_j) vectors, degree-32 graph built on the GPU, 896-B PIR entries "
+                       "vectors (16-d latent mixture, per-dimension sigma 0.82 -> 0.29 as the reference's PCA "
+                       "fixture), degree-32 graph built on the GPU, 896-B PIR entries "
                        "(16 partitions, CS 1,024 / SS 196), k = 100, step 20, parallel 3",
            "sessions": S2, "lockstep_groups": MS_GROUPS, "queries_per_session": MS_QUERIES,
            "private_queries_per_s": round(S2 * MS_QUERIES / wall, 2), "wall_s": round(wall, 4),
@@ -278,6 +299,7 @@ def private_search_msmarco(local, args, with_cpu: bool):
                            "launches": n, "alg_bytes_per_launch": by / n,
                            "aggregate": {"achieved": round(by / wall / 1e9, 1),
                                          "frac": round(by / wall / 1e9 / HBM_PEAK_GBS, 4)}}
+        attach_traffic(out["roofline"], SYMBOLS["answer"], (S2 // MS_GROUPS) * PARALLEL * M * 512)
     if with_cpu:   # the oracle replaying session 0's workload, one core
         cb = cpu_baseline(v, g, qs[0], MS_WARMUP, ans[0], ctx, 601, 602, k=MS_K)
         out["cpu_baseline"] = cb
@@ -345,6 +367,7 @@ def bigann_shard(name, n_entries, layout, shard, rank, ws, local, dist, nccl_gro
                  reduce=True):
     """Shard `shard` of the layout on this rank (see bigann_pir); reduce: the
     times are the max and the checks the sum over the ranks (one shard each)."""
+    progress(f"  {name}: shard {shard} of {layout}")
     import gc
 
     import pacmann_amd as pm
@@ -454,13 +477,12 @@ def bigann_shard(name, n_entries, layout, shard, rank, ws, local, dist, nccl_gro
     nsplit = max(1, min(-(-sub["SetSize"] // 48), -(-2048 // nsub), 64)) if sub["SetSize"] >= 256 else 1
     gather_grid = nsplit * nsub * 256
     if fold:
-        tr = pmc_traffic("void pm::k_prep_fold<2>(pm::PmPart const*, unsigned long const*, unsigned int)", fold_grid)
-        fold["traffic"], fold["traffic_source"] = (tr[0], tr[1]) if tr else (None, None)
+        attach_traffic(fold, "void pm::k_prep_fold<2>(pm::PmPart const*, unsigned long const*, unsigned int)",
+                       fold_grid)
     ans_roof = roof(kstep[gather_key])
     if ans_roof and gather_key == "gather":
-        tr = pmc_traffic("void pm::k_gather<2>(pm::PmStep)", gather_grid)
         ans_roof["kernel"] = "gather"
-        ans_roof["traffic"], ans_roof["traffic_source"] = (tr[0], tr[1]) if tr else (None, None)
+        attach_traffic(ans_roof, "void pm::k_gather<2>(pm::PmStep)", gather_grid)
     return {
         "workload": f"{name}: {n_entries:,} x 640 B entries (d=128 f32 + m=32 u32 ids), BatchSize 32 "
                     f"(16 partitions), FailureProbLog2 8, device-generated uniform DB; rounds of "
@@ -489,26 +511,28 @@ def bigann_shard(name, n_entries, layout, shard, rank, ws, local, dist, nccl_gro
 # (graphann_test.go:221-284): N = 1e8 rows of D = 128 uint32, v[i*D+j] = i+j,
 # q[j] = j, the sum of all row products mod 2^32 (closed form 1,178,525,696).
 C0_N, C0_D, C0_SUM, C0_CPU_ROWS = 100_000_000, 128, 1_178_525_696, 1 << 23
+IP_SCAN_SYMBOL = "pm::k_ip_scan(uint4 const*, unsigned long, unsigned int const*, unsigned int, unsigned int*)"
+IP_SCAN_GRID = 2048 * 256   # pmk::ip_rows' scan launch: 2,048 workgroups of 256 threads (pm_kernels.hip)
 
 
 def inner_product_scan(ctx, with_cpu: bool):
     """The scan on the GPU (51.2 GB filled on the device, then one streaming
-    k_ip_scan launch timed with events on its stream; best of 3), against HBM
+    k_ip_scan launch timed with events on its stream; mean of 3), against HBM
     peak; the oracle's AVX-512-equivalent InnerProduct over a materialised
     sample of the same rows on 1 and on all host cores beside it."""
     import pacmann_amd as pm
     runs = [pm.ip_bench(C0_N, C0_D, ctx) for _ in range(3)]
     ok = all(s == C0_SUM for s, _ in runs)
-    ms = min(m for _, m in runs)
+    ms = sum(m for _, m in runs) / len(runs)   # the mean, like rocprof's average over the same launches
     nbytes = C0_N * C0_D * 4
     ach = nbytes / (ms / 1e3) / 1e9
-    tr = pmc_traffic("pm::k_ip_scan(uint4 const*, unsigned long, unsigned int const*, unsigned int, unsigned int*)")
     out = {"workload": "graphann_test.go InnerProduct bench (configs[0]): 1e8 x 128 uint32 rows v[i*D+j]=i+j, "
                        "q[j]=j, sum mod 2^32",
            "sum_ok": ok, "scan_ms": round(ms, 4), "rows_per_s": round(C0_N / (ms / 1e3), 1),
            "roofline": {"bound": "hbm", "kernel": "ip_scan", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": nbytes,
-                        "traffic": tr[0] if tr else None}}
+                        "avg_ms": round(ms, 5), "launches": len(runs)}}
+    attach_traffic(out["roofline"], IP_SCAN_SYMBOL, IP_SCAN_GRID)
     if with_cpu:
         from oracle import oracle as O
         rows = np.arange(C0_CPU_ROWS, dtype=np.uint32)[:, None] + np.arange(C0_D, dtype=np.uint32)[None, :]
@@ -665,6 +689,7 @@ def main():
         return pm.search_loop_sessions(sess, qq, K_TOP, STEP, PARALLEL)
     if args.warmup:
         serve(qsess[:, :args.warmup])
+    progress(f"SIFT1M: {S} sessions ready, warm-up done; timed region")
 
     # every kernel of the timed region is timed where it runs: events on the
     # streams the kernels are launched on, the step kernels' carried in their
@@ -761,11 +786,10 @@ def main():
         grid = None
         if name == "answer" and args.mode == "batched":   # the PMC summary by launch shape: 512-thread WG per sub-query
             grid = (S // max(1, args.groups)) * PARALLEL * M * 512
-        tr = pmc_traffic(SYMBOLS.get(name, name), grid)
         r = {"bound": "hbm", "kernel": name, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
              "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-             "traffic": tr[0] if tr else None, "traffic_source": tr[1] if tr else None,
              "launches": n, "avg_ms": round(ms / n, 5), "alg_bytes_per_launch": by / n}
+        attach_traffic(r, SYMBOLS.get(name, name), grid)
         if note:
             r["note"] = note
         return r
@@ -792,8 +816,7 @@ def main():
         # PMC bytes of launches of this shape (k_prep_fold_pipe<4,1,4>: 2 hint groups x 20 column slices
         # per partition, 1,024 threads per workgroup)
         units = 16 * k * -(-(c0["PrimaryHintNum"] + c0["SetSize"] * c0["MaxQueryPerChunk"]) // 7168)
-        tr = pmc_traffic(SYMBOLS["prep_fold"], -(-units // 8) * 8 * (E // 4) * 1024)
-        fold["traffic"], fold["traffic_source"] = (tr[0], tr[1]) if tr else (None, None)
+        attach_traffic(fold, SYMBOLS["prep_fold"], -(-units // 8) * 8 * (E // 4) * 1024)
         fold["note"] = ("fold bytes (hint x chunk entry reads, SURVEY.md §8d) exceed HBM peak because the "
                         "kernel serves them from LDS; 'compulsory' is the DB read once plus the parity writes "
                         "of the clients folded in one launch")
@@ -848,6 +871,7 @@ def main():
     if isolated:
         out["isolated"] = isolated
     if not args.no_cpu_baseline and ws == 1:
+        progress("SIFT1M cpu_baseline")
         cb = cpu_baseline(v, g, qsess[0, :args.warmup + args.steps], args.warmup, answers[0], ctx0,
                           11 + 97 * rank, 12 + 97 * rank)
         cpu_baseline_all_cores(v, g, cb)
@@ -858,17 +882,20 @@ def main():
     gc.collect()
     if ws == 1 and not args.no_config2:
         c2 = pm.Context(local)
+        progress("config2 batch PIR")
         out["config2_batch_pir"] = batch_pir_msmarco(c2, not args.no_cpu_baseline)
         del c2
         gc.collect()
     if ws == 1 and not args.no_msmarco_search:
         try:
+            progress("config2 MS-MARCO private search")
             out["config2_private_search"] = private_search_msmarco(local, args, not args.no_cpu_baseline)
         except Exception as e:   # recorded, never fatal to the headline line
             out["config2_private_search"] = {"error": f"{type(e).__name__}: {e}"}
         gc.collect()
     if ws == 1 and not args.no_config0:
         c0 = pm.Context(local)
+        progress("config0 inner product")
         out["config0_inner_product"] = inner_product_scan(c0, not args.no_cpu_baseline)
         del c0
         gc.collect()
@@ -887,6 +914,7 @@ def main():
                                            ("config4_bigann_1b", "BIGANN-1B-shaped (configs[4]), 8-way layout",
                                             1_000_000_000, 8)):
             try:
+                progress(key)
                 out[key] = bigann_pir(nm, n_entries, layout, rank, ws, local, dist, nccl_group)
             except Exception as e:   # recorded, never fatal to the headline line
                 out[key] = {"error": f"{type(e).__name__}: {e}"}

@@ -13,6 +13,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <mutex>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -306,7 +307,7 @@ struct Engine {
   double prepTime = 0, storage = 0, commOn = 0, commOff = 0;
 
   std::shared_ptr<DevBuf> db = std::make_shared<DevBuf>();   // server DB; shared by the clients of pm_batchpir_create_client
-  DevBuf zero16, parts_d, owned_d, tag, pp, parity, ridx, rval, hist, fqn, arena, tab, tabT, done, gran;
+  DevBuf zero16, parts_d, owned_d, tag, pp, parity, ridx, rval, hist, fqn, arena, tab, tabT, cur, done, gran;
   uint32_t gran_words = 0;
   std::vector<uint32_t> owned_list;   // owned partitions in order (owned_d holds their PmPart)
   DevBuf qoffs, ans_srv;
@@ -414,7 +415,7 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
   if (g->E > pmk::step_max_e()) return fail(PM_EINVAL, "DBEntrySize above the step kernel's LDS limit");
   g->shard = shard; g->nshards = nshards;
   uint64_t off_tag = 0, off_pp = 0, off_par = 0, off_ridx = 0, off_rval = 0, off_hist = 0, off_ar = 0,
-           off_tab = 0, off_db = 0;
+           off_tab = 0, off_cur = 0, off_db = 0;
   for (uint64_t i = 0; i < g->P; ++i) {
     PartHost& ph = g->parts[i];
     uint64_t start = i * g->PS, end = std::min((i + 1) * g->PS, N);
@@ -446,6 +447,7 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
     ph.d.hist = (uint32_t*)(uintptr_t)off_hist; off_hist += ph.d.SS;
     ph.d.arena = (uint64_t*)(uintptr_t)off_ar; off_ar += (uint64_t)ph.d.MaxQ * g->E;
     ph.d.tab = (uint16_t*)(uintptr_t)off_tab; off_tab += (uint64_t)ph.d.H * ph.d.SS;
+    ph.d.cur = (uint16_t*)(uintptr_t)off_cur; off_cur += (uint64_t)ph.d.PH * ph.d.SS;
     ph.cache.reserve(ph.d.MaxQ);
   }
   CHK(g->zero16.reserve(64));
@@ -475,6 +477,7 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
   CHK(g->arena.reserve(std::max<uint64_t>(8, off_ar * 8)));
   CHK(g->tab.reserve(off_tab * 2));
   CHK(g->tabT.reserve(off_tab * 2));
+  CHK(g->cur.reserve(std::max<uint64_t>(2, off_cur * 2)));
   CHK(g->done.reserve(4 * (3 + 16 * 4096)));
   {   // step completion counter (pm_query.hip chain_add): 2^31 in the low half, 0 chained
     const uint32_t init[3] = {1u << 31, 0, 0};
@@ -503,6 +506,7 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
     d.arena = g->arena.as<uint64_t>() + (uintptr_t)d.arena;
     d.tabT = g->tabT.as<uint16_t>() + (uintptr_t)d.tab;
     d.tab = g->tab.as<uint16_t>() + (uintptr_t)d.tab;
+    d.cur = g->cur.as<uint16_t>() + (uintptr_t)d.cur;
   }
   HIPCHK(hipMemsetAsync(g->fqn.p, 0, g->P * 4, ctx->stream));
   HIPCHK(hipMemsetAsync(g->hist.p, 0, off_hist * 4, ctx->stream));
@@ -552,7 +556,8 @@ static int engine_prep_host(Engine* g, uint64_t p0, uint64_t p1, std::vector<uin
 // The device side for np parts at dp (of one engine, or of several clients of
 // one server: same parameters and DB): PRF tables, then the hint fold and
 // the replacement rows, or zero hints for DummyPreprocessing.  Synchronous.
-static int engine_prep_launch(pm_ctx* c, const Engine* g, const PmPart* dp, int np, const PmPart* host_parts) {
+static int engine_prep_launch(pm_ctx* c, const Engine* g, const PmPart* dp, int np, const PmPart* host_parts,
+                              uint32_t clients = 1) {
   hipStream_t st = c->stream;
   c->timed("prep_init", 0, [&] { pmk::prep_init(st, dp, np, g->maxH, g->maxRepl, (uint32_t)g->E, g->skipPrep); });
   double aes = 0, fold = 0, repl = 0;
@@ -573,7 +578,7 @@ static int engine_prep_launch(pm_ctx* c, const Engine* g, const PmPart* dp, int 
     }
   } else {
     c->timed("prep_fold", fold, [&] { pmk::prep_fold(st, dp, np, g->maxH, g->db->as<uint64_t>(), (uint32_t)g->E, g->minCS, g->maxCS,
-                                               g->zero16.as<uint64_t>()); });
+                                               g->zero16.as<uint64_t>(), clients); });
     c->timed("prep_repl", repl, [&] { pmk::prep_repl(st, dp, np, g->maxRepl, g->db->as<uint64_t>(), (uint32_t)g->E); });
   }
   HIPCHK(hipGetLastError());
@@ -1920,7 +1925,7 @@ struct SpinBarrier {
 struct StepGroup {
   pm_ctx* c = nullptr;   // the shared steps' stream
   uint32_t S = 0, P = 0, maxPH = 0, maxSS = 0, E = 0, dim = 0;
-  DevBuf parts_d, subs_d, sb_d, bits, cand, meta, spec, res_d, ans, part_x, done, prep_parts, desc_d;
+  DevBuf parts_d, subs_d, sb_d, bits, cand, meta, spec, res_d, ans, part_x, done, prep_parts, desc_d, stamps;
   HostBuf desc_h, out_h;
   uint32_t token = 0, pf_w0 = 0, pf_w1 = 0;
   std::vector<PmSub> subs;
@@ -2070,8 +2075,33 @@ static int group_step(StepGroup& G, const std::vector<char>& in) {
     S.part_x = G.part_x.as<uint64_t>();
     c->timed_ext("gather", ans_bytes, [&](pmk::PmEvents ev) { pmk::step_gather(st, S, ev); }, 2);
   }
+#ifdef PM_ANSWER_STAMPS
+  static const char* stamp_file = getenv("PM_ANSWER_STAMPS");   // append {nsub} + nsub x 8 stamps per step
+  static std::atomic<int> stamp_steps{0};   // the first 40 steps of the run (file size)
+  const bool stamp_this = stamp_file && stamp_steps.fetch_add(1) < 40;
+  if (stamp_this) {
+    CHK(G.stamps.reserve((uint64_t)nsub * 8 * 8));
+    HIPCHK(hipMemsetAsync(G.stamps.p, 0, (uint64_t)nsub * 8 * 8, st));
+    S.stamps = G.stamps.as<uint64_t>();
+  }
+#endif
   c->timed_ext("answer", S.nsplit > 1 ? 0 : ans_bytes, [&](pmk::PmEvents ev) { pmk::step_answer(st, S, ev); }, 2);
   HIPCHK(hipGetLastError());
+#ifdef PM_ANSWER_STAMPS
+  if (stamp_this) {
+    HIPCHK(hipStreamSynchronize(st));
+    std::vector<uint64_t> t((uint64_t)nsub * 8);
+    HIPCHK(hipMemcpy(t.data(), G.stamps.p, t.size() * 8, hipMemcpyDeviceToHost));
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lk(mu);
+    if (FILE* f = fopen(stamp_file, "ab")) {
+      const uint64_t h = nsub;
+      fwrite(&h, 8, 1, f);
+      fwrite(t.data(), 8, t.size(), f);
+      fclose(f);
+    }
+  }
+#endif
   c->host_add(HT_STEP_LAUNCH, ms_since(t0));
   G.pf_w0 = S.pf_w0; G.pf_w1 = S.pf_w1;
   return 0;
@@ -2140,7 +2170,7 @@ static int group_prep(StepGroup& G, pm_graph** gs, const std::vector<char>& need
   if (skip) return fail(PM_EINVAL, "batched sessions mix Preprocessing and DummyPreprocessing");
   CHK(G.prep_parts.reserve(hp.size() * sizeof(PmPart)));
   HIPCHK(hipMemcpyAsync(G.prep_parts.p, hp.data(), hp.size() * sizeof(PmPart), hipMemcpyHostToDevice, G.c->stream));
-  CHK(engine_prep_launch(G.c, e0, G.prep_parts.as<PmPart>(), (int)hp.size(), hp.data()));
+  CHK(engine_prep_launch(G.c, e0, G.prep_parts.as<PmPart>(), (int)hp.size(), hp.data(), (uint32_t)who.size()));
   const double t = std::chrono::duration<double>(Clock::now() - t0).count();
   for (uint32_t s : who) {
     Engine* e = &gs[s]->pir->e;

@@ -68,6 +68,12 @@ struct PmPart {
   // preprocessing, holds every PRF value the online phase needs.
   PM_G uint16_t* tab;
   PM_G uint16_t* tabT;    // the same table hint-major: tabT[t*SS + c] (set expansion reads one row)
+  // The hint search's row: cur[c*PH + h] = PRF(current tag of primary hint h,
+  // chunk c) & (CS-1), i.e. tab[c][tag[h]] kept in hint order, so matching a
+  // (chunk, offset) streams PH contiguous u16 instead of gathering through
+  // the tags.  k_prep_offsets seeds it (tags are h); the final refresh of a
+  // hint in a step rewrites its column from tabT[new tag] (pm_query.hip refresh_cur).
+  PM_G uint16_t* cur;
   // the search query this client's decoded rows are scored against (L2) when
   // several clients' steps share one launch (pm_search_loop_batched); null:
   // the step's PmStep::q
@@ -169,8 +175,9 @@ using namespace pm;
 void prep_init(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxH, uint32_t maxRepl,
                uint32_t E, bool zero_state);
 void prep_offsets(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxH, uint32_t maxSS);
+// dparts: `clients` clients of each partition, partition-major (nparts = partitions x clients)
 void prep_fold(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxH, const uint64_t* db,
-               uint32_t E, uint32_t minCS, uint32_t maxCS, const uint64_t* zero16);
+               uint32_t E, uint32_t minCS, uint32_t maxCS, const uint64_t* zero16, uint32_t clients = 1);
 void prep_repl(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxRepl,
                const uint64_t* db, uint32_t E);
 // Timing events carried by a launch's own dispatch packet (null: untimed)

@@ -59,8 +59,9 @@ __global__ void __launch_bounds__(kOffsBlock) k_prep_offsets(const PmPart* __res
   for (uint32_t c = c0; c < c1; ++c) {
     uint16_t v = (uint16_t)(prf_lo32_split(A, P.rk, r1u[c - c0], r1v, c) & mask);
     v = (c == own) ? kSkip : v;
-    o[(uint64_t)c * H + h] = v;   // chunk-major: hint search
+    o[(uint64_t)c * H + h] = v;   // chunk-major: refreshed tags' re-evaluation, fold
     oT[c] = v;                    // hint-major: set expansion
+    if (h < P.PH) P.cur[(uint64_t)c * P.PH + h] = v;   // hint search (tags start at h)
   }
 }
 
@@ -244,21 +245,27 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_pipe(const PmPart* _
                                                                  const uint64_t* __restrict__ db,
                                                                  const uint64_t* __restrict__ zero16,
                                                                  uint32_t E, uint32_t ngmax, uint32_t nsl,
-                                                                 uint32_t units) {
+                                                                 uint32_t npg, uint32_t K) {
   extern __shared__ __attribute__((aligned(16))) uint64_t fold_lds[];   // [NB][(CS+1)*SW + 1024]
   typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
   constexpr uint32_t IPE = SW / 2, CS = G * kFoldThreads / IPE;
-  // XCD-aware order: workgroups b and b + 8 share an XCD (MI355X_MICROARCH.md
-  // § Workgroup dispatch), so the nsl column slices of one (partition, hint
-  // group) unit are dealt to one XCD back to back and the 128-B lines they
-  // split are fetched into that XCD's L2 once.
+  // XCD-aware order (workgroups b and b + 8 share an XCD, MI355X_MICROARCH.md
+  // § Workgroup dispatch).  parts holds K clients of each partition, partition-
+  // major; pg = (partition, hint group) runs on XCD pg % 8.  There, for each
+  // group of LW column slices that split one 128-B line of every row, the
+  // workgroups of all K clients follow each other, so the lines they stage are
+  // fetched into that XCD's L2 once for K x LW workgroups instead of once per
+  // client (the same DB, read by every client's fold).
+  constexpr uint32_t LW = 16 / SW;   // slices per 128-B line
+  const uint32_t ngl = (nsl + LW - 1) / LW, per_pg = K * ngl * LW;
   const uint32_t xcd = blockIdx.x % 8, k = blockIdx.x / 8;
-  const uint32_t unit = xcd + 8 * (k / nsl), slice = k % nsl;
-  if (unit >= units) return;   // block-uniform
-  const PmPart& P = parts[unit / ngmax];
+  const uint32_t pg = xcd + 8 * (k / per_pg), r = k % per_pg;
+  const uint32_t client = (r / LW) % K, slice = (r / (K * LW)) * LW + r % LW;
+  if (pg >= npg || slice >= nsl) return;   // block-uniform
+  const PmPart& P = parts[(pg / ngmax) * K + client];
   const uint32_t H = P.H, SS = P.SS, tid = threadIdx.x;
   const uint32_t ng = (H + kFoldThreads * kFoldHPT - 1) / (kFoldThreads * kFoldHPT);
-  const uint32_t grp = unit % ngmax;
+  const uint32_t grp = pg % ngmax;
   if (grp >= ng) return;   // block-uniform
   const uint32_t hb = (((H + ng - 1) / ng) + 7) & ~7u, h0 = grp * hb, h1 = min(H, h0 + hb);
   const uint32_t w = slice * SW;
@@ -598,7 +605,7 @@ void prep_offsets(hipStream_t st, const PmPart* d, int np, uint32_t maxH, uint32
                      dim3(kOffsBlock), 0, st, d);
 }
 void prep_fold(hipStream_t st, const PmPart* d, int np, uint32_t maxH, const uint64_t* db, uint32_t E,
-               uint32_t minCS, uint32_t maxCS, const uint64_t* zero16) {
+               uint32_t minCS, uint32_t maxCS, const uint64_t* zero16, uint32_t clients) {
   const uint32_t EX = E & ~3u;
   if (EX == 0) {
     hipLaunchKernelGGL(k_prep_fold<2>, dim3(cdiv((uint64_t)maxH * E, kBlock), np), dim3(kBlock), 0,
@@ -622,7 +629,9 @@ void prep_fold(hipStream_t st, const PmPart* d, int np, uint32_t maxH, const uin
   };
   if (minCS == maxCS && (maxCS == 512 || maxCS == 1024 || maxCS == 2048) && E % 2 == 0) {
     // (SW, G): CS 512 -> (4, 1), 1024 -> (4, 2), 2048 -> (2, 2); EX % SW == 0
-    const uint32_t psw = maxCS == 2048 ? 2 : 4, nsl = EX / psw, units = np * ng;
+    const uint32_t psw = maxCS == 2048 ? 2 : 4, nsl = EX / psw;
+    const uint32_t K = clients && np % clients == 0 ? clients : 1, npg = (np / K) * ng;
+    const uint32_t lw = 16 / psw, per_pg = K * cdiv(nsl, lw) * lw;
 #ifndef PM_FOLD_NB512
 #define PM_FOLD_NB512 4
 #endif
@@ -631,14 +640,14 @@ void prep_fold(hipStream_t st, const PmPart* d, int np, uint32_t maxH, const uin
 #endif
     const uint32_t nb = maxCS == 512 ? PM_FOLD_NB512 : 3;   // LDS buffers: <= 150 KB
     const size_t lds = (size_t)nb * ((maxCS + 1) * psw + kPipeTabWords) * 8;
-    const dim3 grid(cdiv(units, 8) * 8 * nsl), blk(kFoldThreads);
+    const dim3 grid(cdiv(npg, 8) * 8 * per_pg), blk(kFoldThreads);
     if (maxCS == 512)
       hipLaunchKernelGGL((k_prep_fold_pipe<4, 1, PM_FOLD_NB512, PM_FOLD_D512>), grid, blk, lds, st, d, db, zero16, E, ng, nsl,
-                         units);
+                         npg, K);
     else if (maxCS == 1024)
-      hipLaunchKernelGGL((k_prep_fold_pipe<4, 2, 3>), grid, blk, lds, st, d, db, zero16, E, ng, nsl, units);
+      hipLaunchKernelGGL((k_prep_fold_pipe<4, 2, 3>), grid, blk, lds, st, d, db, zero16, E, ng, nsl, npg, K);
     else
-      hipLaunchKernelGGL((k_prep_fold_pipe<2, 2, 3>), grid, blk, lds, st, d, db, zero16, E, ng, nsl, units);
+      hipLaunchKernelGGL((k_prep_fold_pipe<2, 2, 3>), grid, blk, lds, st, d, db, zero16, E, ng, nsl, npg, K);
     return;
   }
   uint32_t sw = 8;

@@ -35,6 +35,9 @@
 namespace pm {
 
 constexpr int kAnsBlock = 512;
+#ifndef PM_ANSWER_KG
+#define PM_ANSWER_KG 8   // k_answer gather: rows per thread in flight together (12: 27 VGPRs spill at 8 waves)
+#endif
 constexpr uint32_t kNone = 0xffffffffu;
 
 #ifdef PM_STAMPS
@@ -96,6 +99,20 @@ constexpr uint32_t kNone = 0xffffffffu;
 #define TS_SEEN(kept) do {} while (0)
 #endif
 // slots: k_resolve partition 0: 0..40; k_match block (0,0): 41..47; k_answer block 0: 48..63
+
+// PM_ANSWER_STAMPS diagnostic builds: k_answer (three-kernel path) records
+// s_memrealtime (100 MHz, one clock for all XCDs) at its phase boundaries,
+// stamps[blockIdx * 8 + i]: 0 start, 1 resolution read, 2 query set in LDS,
+// 3 gather reduced, 4 decoded, 5 results issued, 6 XCC_ID << 16 | CU/SE ids.
+#ifdef PM_ANSWER_STAMPS
+#define AST(i)                                                                                   \
+  do {                                                                                           \
+    if (!GRAN && threadIdx.x == 0 && S.stamps)                                                   \
+      S.stamps[(uint64_t)blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime();               \
+  } while (0)
+#else
+#define AST(i) do {} while (0)
+#endif
 
 
 // ---------------------------------------------------------------------------
@@ -237,24 +254,23 @@ __device__ __forceinline__ void match_role(const PmStep& S, uint32_t s, uint32_t
   STAMP_AT(stamp_wg, 42);
   const uint32_t mask = P.CS - 1, chunk = (uint32_t)(sub.idx >> P.log2CS),
                  offset = (uint32_t)(sub.idx & mask);
-  const PM_G uint16_t* row = P.tab + (uint64_t)chunk * P.H;
+  const PM_G uint16_t* crow = P.cur + (uint64_t)chunk * P.PH;   // the hint search row of this chunk
   const bool live = sub.idx < P.N;
   // Block 0 of a sub-query also prepares k_resolve's prediction: its chunk's
   // QueryHistogram now, the rest below (loads overlap the match loads).
   const bool meta_wg = blk == 0;
   const uint32_t h0k = (meta_wg && live) ? P.hist[chunk] : 0;
   uint32_t sing_rec = 0;   // GRAN: thread 0's copy for the record
-  // kMatchHPT hints per thread, all loads of a kind issued together
-  uint32_t tg[kMatchHPT], pv[kMatchHPT];
+  // kMatchHPT hints per thread: their search-row values (contiguous u16).  A
+  // hint matches iff its value is the offset: a refreshed hint's programmed
+  // chunk is its backup tag's own chunk, kSkip in its row, so the program
+  // point check (pir.go:407) needs no load.
   uint16_t rv[kMatchHPT];
 #pragma unroll
   for (int u = 0; u < kMatchHPT; ++u) {
     const uint32_t h = base + u * NT + threadIdx.x;
-    tg[u] = 0; pv[u] = kDefaultProgramPoint;
-    if (live && h < P.PH) { tg[u] = P.tag[h]; pv[u] = P.pp[h]; }
+    rv[u] = (live && h < P.PH) ? crow[h] : kSkip;
   }
-#pragma unroll
-  for (int u = 0; u < kMatchHPT; ++u) rv[u] = row[tg[u]];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (meta_wg && wave == 0) {
     // In-chunk index this sub-query gets if every earlier one of its partition
@@ -279,15 +295,14 @@ __device__ __forceinline__ void match_role(const PmStep& S, uint32_t s, uint32_t
       }
     }
   }
-  // match bits, and the block's first two matches with the tag / program
-  // point this thread already holds (k_resolve's usual candidates)
+  // match bits, and the wave's first two matches with their tag / program
+  // point (k_resolve's usual candidates)
   uint32_t h0 = kNone, t0 = 0, p0 = 0, h1 = kNone, t1 = 0, p1 = 0;   // wave-uniform
 #pragma unroll
   for (int u = 0; u < kMatchHPT; ++u) {
     if (base + u * NT >= P.PH) break;
     const uint32_t h = base + u * NT + threadIdx.x;
-    const bool m = live && h < P.PH && rv[u] == offset &&
-                   (pv[u] == kDefaultProgramPoint || (pv[u] >> P.log2CS) != chunk);
+    const bool m = rv[u] == offset;
     uint64_t b = __ballot(m);
     if (lane == 0 && (h - lane) < P.PH) {
       if (GRAN) {
@@ -299,22 +314,18 @@ __device__ __forceinline__ void match_role(const PmStep& S, uint32_t s, uint32_t
       }
     }
     if (b && h1 == kNone) {   // in hint order within this wave
-      const uint32_t l = (uint32_t)__builtin_ctzll(b), hl = h - lane + l;
-      const uint32_t tl = __builtin_amdgcn_readlane(tg[u], l), pl = __builtin_amdgcn_readlane(pv[u], l);
+      const uint32_t hl = h - lane + (uint32_t)__builtin_ctzll(b);
       if (h0 == kNone) {
-        h0 = hl; t0 = tl; p0 = pl;
+        h0 = hl;
         b &= b - 1;
-        if (b) {
-          const uint32_t l2 = (uint32_t)__builtin_ctzll(b);
-          h1 = h - lane + l2;
-          t1 = __builtin_amdgcn_readlane(tg[u], l2);
-          p1 = __builtin_amdgcn_readlane(pv[u], l2);
-        }
+        if (b) h1 = h - lane + (uint32_t)__builtin_ctzll(b);
       } else {
-        h1 = hl; t1 = tl; p1 = pl;
+        h1 = hl;
       }
     }
   }
+  if (h0 != kNone) { t0 = P.tag[h0]; p0 = P.pp[h0]; }
+  if (h1 != kNone) { t1 = P.tag[h1]; p1 = P.pp[h1]; }
   if (lane == 0) {
     s_cand[wave][0] = h0; s_cand[wave][1] = t0; s_cand[wave][2] = p0;
     s_cand[wave][3] = h1; s_cand[wave][4] = t1; s_cand[wave][5] = p1;
@@ -424,17 +435,13 @@ __global__ void __launch_bounds__(kBlock, PM_MATCHPART_WAVES) k_match_part(PmSte
       if (lane == 0) { S.meta[2 * s] = h0k; S.meta[2 * s + 1] = sing; }
     }
   }
-  uint32_t tg[HPT], pv[HPT];
-#pragma unroll
-  for (int u = 0; u < HPT; ++u) {
-    const uint32_t h = base + u * NT + tid;
-    tg[u] = 0; pv[u] = kDefaultProgramPoint;
-    if (h < P.PH) { tg[u] = P.tag[h]; pv[u] = P.pp[h]; }
-  }
   for (uint32_t j0 = 0; j0 < pn; j0 += G) {
     uint32_t kind[G], chk[G], off[G];
     bool lv[G];
     uint16_t rv[G][HPT];
+    // each sub-query's search-row values of this block's hints (contiguous
+    // u16: 2 B per hint; a hint matches iff its value is the offset, see
+    // match_role); the loads of all G sub-queries in flight together
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       PmSub sub{0, SUB_NONE, 0};
@@ -445,9 +452,12 @@ __global__ void __launch_bounds__(kBlock, PM_MATCHPART_WAVES) k_match_part(PmSte
       lv[g] = kind[g] == SUB_REAL && idx < P.N;
       chk[g] = (uint32_t)(idx >> lg);
       off[g] = (uint32_t)(idx & mask);
-      const PM_G uint16_t* row = P.tab + (uint64_t)chk[g] * P.H;
+      const PM_G uint16_t* crow = P.cur + (uint64_t)chk[g] * P.PH;
 #pragma unroll
-      for (int u = 0; u < HPT; ++u) rv[g][u] = lv[g] ? row[tg[u]] : (uint16_t)0;
+      for (int u = 0; u < HPT; ++u) {
+        const uint32_t h = base + u * NT + tid;
+        rv[g][u] = (lv[g] && h < P.PH) ? crow[h] : kSkip;
+      }
     }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
@@ -458,27 +468,21 @@ __global__ void __launch_bounds__(kBlock, PM_MATCHPART_WAVES) k_match_part(PmSte
       for (int u = 0; u < HPT; ++u) {
         if (base + u * NT >= P.PH) break;
         const uint32_t h = base + u * NT + tid;
-        const bool m = lv[g] && h < P.PH && rv[g][u] == off[g] &&
-                       (pv[u] == kDefaultProgramPoint || (pv[u] >> lg) != chk[g]);
-        uint64_t b = __ballot(m);
+        uint64_t b = __ballot(rv[g][u] == off[g]);   // kSkip never equals an offset
         if (lane == 0 && (h - lane) < P.PH) S.bits[s * S.words + (h >> 6)] = b;
         if (b && h1 == kNone) {   // in hint order within this wave
-          const uint32_t l = (uint32_t)__builtin_ctzll(b), hl = h - lane + l;
-          const uint32_t tl = __builtin_amdgcn_readlane(tg[u], l), pl = __builtin_amdgcn_readlane(pv[u], l);
+          const uint32_t hl = h - lane + (uint32_t)__builtin_ctzll(b);
           if (h0 == kNone) {
-            h0 = hl; t0 = tl; p0 = pl;
+            h0 = hl;
             b &= b - 1;
-            if (b) {
-              const uint32_t l2 = (uint32_t)__builtin_ctzll(b);
-              h1 = h - lane + l2;
-              t1 = __builtin_amdgcn_readlane(tg[u], l2);
-              p1 = __builtin_amdgcn_readlane(pv[u], l2);
-            }
+            if (b) h1 = h - lane + (uint32_t)__builtin_ctzll(b);
           } else {
-            h1 = hl; t1 = tl; p1 = pl;
+            h1 = hl;
           }
         }
       }
+      if (h0 != kNone) { t0 = P.tag[h0]; p0 = P.pp[h0]; }
+      if (h1 != kNone) { t1 = P.tag[h1]; p1 = P.pp[h1]; }
       if (lane == 0) {
         s_cand[g][wave][0] = h0; s_cand[g][wave][1] = t0; s_cand[g][wave][2] = p0;
         s_cand[g][wave][3] = h1; s_cand[g][wave][4] = t1; s_cand[g][wave][5] = p1;
@@ -1167,6 +1171,7 @@ __device__ __forceinline__ float l2_lds(const float* row, const float* __restric
   const uint32_t k = threadIdx.x & 7;
   const uint32_t dimS = dim & ~7u;
   float acc = 0.0f;
+#pragma unroll 8   // the loads of 8 terms issued ahead of the (ordered) sum
   for (uint32_t t = k; t < dimS; t += 8) {
     const float d = __fsub_rn(row[t], q[t]);
     acc = __fadd_rn(acc, __fmul_rn(d, d));
@@ -1201,11 +1206,12 @@ __device__ __forceinline__ uint64_t row_csum(const PmStep& S, const RowBuf& row,
   return x;
 }
 
-// Result publication into pinned (fine-grained) host memory.  Every storing
-// thread waits for its row stores (s_waitcnt vmcnt(0)), a workgroup barrier
-// follows, then lane 0 writes the header with the token last.  The default
-// (PM_PUBLISH 0) stores write-combined and leaves ordering to the row hash
-// the host verifies (pm_internal.h PmOutHdr).  Two ordered forms, both
+// Result publication into pinned (fine-grained) host memory.  The default
+// (PM_PUBLISH 0) leaves ordering to the row hash the host verifies
+// (pm_internal.h PmOutHdr): lane 0 stores the header as soon as the row is
+// final in LDS, and no wave waits for its write-combined row stores to be
+// acknowledged (4: they are, before a workgroup barrier and the header, as in
+// round 1 — which still tears, measured).  Two ordered forms, both
 // measured with 0 torn rows in 49M but 2.8x / 4.4x the kernel time, are kept
 // as build options:
 //   1: lane 0 stores the other header fields, then a SYSTEM-scope release
@@ -1226,12 +1232,16 @@ __device__ __forceinline__ void row_store(PM_G uint64_t* p, uint64_t v) {
 }
 __device__ __forceinline__ void publish_hdr(const PmStep& S, uint32_t s, uint32_t status, uint32_t ref,
                                             float d, uint64_t csum) {
+  PM_G PmOutHdr* h = S.hdr_h + s;
+  if (PM_PUBLISH == 0) {   // lane 0 (it holds d and csum) as soon as the row is final in LDS
+    if (threadIdx.x == 0) *h = PmOutHdr{status, ref, d, S.token, csum + S.token * kCsumMix, 0};
+    return;
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x != 0) return;
-  PM_G PmOutHdr* h = S.hdr_h + s;
   const uint64_t tok = ((uint64_t)S.token << 32) | __float_as_uint(d);   // {dist, token}: bytes 8..15
-  if (PM_PUBLISH == 0) {
+  if (PM_PUBLISH == 4) {   // round 1's drained form: row stores acknowledged, then the plain header
     *h = PmOutHdr{status, ref, d, S.token, csum + S.token * kCsumMix, 0};
     return;
   }
@@ -1252,6 +1262,16 @@ __device__ __forceinline__ void publish_hdr(const PmStep& S, uint32_t s, uint32_
 
 // What a k_answer workgroup does for its sub-query.
 enum : uint32_t { A_ZERO = 0, A_FINAL = 1, A_CHAINED = 2, A_CACHED = 3, A_DUMMY = 4 };
+
+// The hint search row of a refreshed hint (PmPart::cur): hint r.hit now carries
+// backup hint (r.chunk, r.ing)'s tag, whose PRF values tabT holds (pir.go:
+// 460-462).  Written by the hint's final holder in this step (flags bit 1
+// clear); read by the next step's hint search, after this launch ends.
+__device__ __forceinline__ void refresh_cur(const PmPart& P, const PmRes& r, uint32_t tid, uint32_t nt) {
+  const uint32_t ntag = P.PH + r.chunk * P.Qpc + r.ing;
+  const PM_G uint16_t* src = P.tabT + (uint64_t)ntag * P.SS;
+  for (uint32_t c = tid; c < P.SS; c += nt) P.cur[(uint64_t)c * P.PH + r.hit] = src[c];
+}
 
 // Decode one chained sub-query (its hint was refreshed earlier in this step)
 // once every earlier refresh is visible; the whole workgroup participates.
@@ -1276,6 +1296,7 @@ __device__ void decode_chained(const PmStep& S, uint32_t s, RowBuf& row) {
     }
     row.w[w] = v;
   }
+  if (!(r.flags & 2u)) refresh_cur(P, r, tid, blockDim.x);
   __syncthreads();
   PM_G uint64_t* orow = S.rows_h + (uint64_t)s * E;
   uint64_t* ar = P.arena + (uint64_t)r.slot * E;
@@ -1303,7 +1324,7 @@ __device__ void finish_step(const PmStep& S, RowBuf& row) {
 template <int NT>
 struct AnswerLds {
   uint32_t f[17];   // k_step: granule fields, per-wave first candidates, predicted index
-  uint32_t qo[kMaxSSLds];
+  uint16_t qo[kMaxSSLds];   // the query set: in-chunk offsets < ChunkSize <= 32768
   uint64_t red[NT * 2];
   __attribute__((aligned(16))) RowBuf row;
   uint32_t s_last;
@@ -1328,7 +1349,7 @@ __device__ __forceinline__ uint32_t answer_mode(const PmRes& r) {
 // answer reads (kept) or the work is redone for the actual result.
 template <int W, bool GRAN, int NT>
 __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, AnswerLds<NT>& L) {
-  uint32_t* const qo = L.qo;
+  uint16_t* const qo = L.qo;
   uint64_t* const red = L.red;
   RowBuf& row = L.row;
   const uint32_t tid = threadIdx.x;
@@ -1338,12 +1359,30 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, AnswerL
   PM_G uint64_t* const orow = S.rows_h + (uint64_t)s * E;
   const bool stamp_wg = s == 0;
   STAMP_AT(stamp_wg, 48);
+  AST(0);
+#ifdef PM_ANSWER_STAMPS
+  if (!GRAN && threadIdx.x == 0 && S.stamps)
+    S.stamps[(uint64_t)blockIdx.x * 8 + 6] = ((uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
+                                             (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+#endif
   const uint32_t mask = P.CS - 1, lg = P.log2CS;
+  // the search query the decoded row is scored against (L2): loaded now, in
+  // flight with everything else, and put into LDS once the gather is done
+  const float* const qq = P.qv ? P.qv : S.q;
+  const bool q_lds = qq && S.dim <= 2 * NT;   // red[] holds 2 * NT floats... as NT u64 pairs
+  float qreg0 = 0.0f, qreg1 = 0.0f;
+  if (q_lds) {
+    if (tid < S.dim) qreg0 = qq[tid];
+    if (tid + NT < S.dim) qreg1 = qq[tid + NT];
+  }
   uint64_t e_rv = 0, e_bp = 0, e_pp = 0;
+  uint32_t e_cur = kSkip;   // the refreshed hint's new search-row value at chunk tid (refresh_cur)
   // set expansion + gather into row.w[0..EX) and the decode operands for (r, mode)
   auto gather = [&](const PmRes& r, uint32_t mode) {
     // decode operands: independent of the gather, issued first (pir.go:450-468)
     const uint64_t dslot = (uint64_t)r.chunk * P.Qpc + r.ing;
+    if (mode == A_FINAL && !(r.flags & 2u) && tid < P.SS)   // the new tag's PRF row (backup hint (chunk, ing))
+      e_cur = P.tabT[(uint64_t)(P.PH + r.chunk * P.Qpc + r.ing) * P.SS + tid];
     if (mode == A_FINAL && tid < E) {
       e_rv = P.rval[dslot * E + tid];
       e_bp = P.parity[((uint64_t)P.PH + dslot) * E + tid];
@@ -1385,16 +1424,17 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, AnswerL
         uint32_t o = trow[i];
         if (i == pchunk) o = r.pp & mask;
         if (i == r.chunk) o = P.ridx[r.chunk * P.Qpc + r.ing] & mask;
-        qo[i] = o;
+        qo[i] = (uint16_t)o;
       }
     } else if (mode == A_DUMMY) {
       for (uint32_t i = tid; i < P.SS; i += NT)
-        qo[i] = (uint32_t)(hash4(P.seed, DOM_DUMMY, P.idx, sub.idx, i) & mask);
+        qo[i] = (uint16_t)(hash4(P.seed, DOM_DUMMY, P.idx, sub.idx, i) & mask);
     }
     STAMP_AT(stamp_wg && mode == A_FINAL, 49);
     __syncthreads();
     AS(1);
     STAMP_AT(stamp_wg, 50);
+    AST(2);
     // ---- server XOR gather (HOT LOOP E) into row.w[0..EX) ------------------
     if (mode == A_FINAL || mode == A_CHAINED || mode == A_DUMMY) {
       const PM_G uint64_t* base = S.db + P.row0 * E;
@@ -1406,21 +1446,21 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, AnswerL
         if (sl < nsl) {
           // every row load of a batch is issued before the first is consumed: the
           // gather is one HBM round trip per kG rows a thread reads, not one per 4
-          constexpr int kG = 12;
+          constexpr int kG = PM_ANSWER_KG;
           typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
           for (uint32_t i0 = sl; i0 < P.SS; i0 += kG * nsl) {
-            uint64_t rr[kG];
+            uint32_t rr[kG];   // partition rows (< 2^32): 32-bit, so the batch fits 64 VGPRs
 #pragma unroll
             for (int u = 0; u < kG; ++u) {
               const uint32_t i = i0 + u * nsl;
-              rr[u] = i < P.SS ? (uint64_t)i * P.CS + qo[i] : P.N;
+              rr[u] = i < P.SS ? i * P.CS + qo[i] : ~0u;
             }
             u64x2 x[kG];
 #pragma unroll
             for (int u = 0; u < kG; ++u) {
               x[u] = u64x2{0, 0};
               if (rr[u] < P.N) {
-                const PM_G uint64_t* q = base + rr[u] * E + (uint64_t)seg * W;
+                const PM_G uint64_t* q = base + (uint64_t)rr[u] * E + (uint64_t)seg * W;
                 if (W == 2) x[u] = *reinterpret_cast<const PM_G u64x2*>(q);
                 else x[u].x = *q;
               }
@@ -1462,29 +1502,19 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, AnswerL
       constexpr int HPT = kLdsPH / NT;   // k_step: PH <= kLdsPH
       const uint32_t ch = (uint32_t)(sub.idx >> lg), off = (uint32_t)(sub.idx & mask);
       const uint32_t wave = tid >> 6, lane = tid & 63;
-      uint32_t tg[HPT], pv[HPT], rv[HPT];
+      uint32_t rv[HPT];
+      const PM_G uint16_t* crow = P.cur + (uint64_t)ch * P.PH;   // match: value == offset (see match_role)
 #pragma unroll
-      for (int u = 0; u < HPT; ++u) {
-        const uint32_t h = u * NT + tid;
-        tg[u] = 0; pv[u] = kDefaultProgramPoint;
-        if (h < P.PH) { tg[u] = P.tag[h]; pv[u] = P.pp[h]; }
-      }
+      for (int u = 0; u < HPT; ++u) rv[u] = u * NT + tid < P.PH ? crow[u * NT + tid] : kNone;
       const uint32_t h0k = wave == 0 ? P.hist[ch] : 0;
-#pragma unroll
-      for (int u = 0; u < HPT; ++u) rv[u] = u * NT + tid < P.PH ? P.tab[(uint64_t)ch * P.H + tg[u]] : kNone;
       // per wave the lowest matching hint (lower u first: hints u*NT + tid)
       uint32_t wh = kNone, wt = 0, wp = 0;
 #pragma unroll
       for (int u = 0; u < HPT; ++u) {
-        const bool m = rv[u] == off && (pv[u] == kDefaultProgramPoint || (pv[u] >> lg) != ch);
-        const uint64_t bm = __ballot(m);
-        if (bm && wh == kNone) {
-          const uint32_t l = (uint32_t)__builtin_ctzll(bm);
-          wh = u * NT + wave * 64 + l;
-          wt = __builtin_amdgcn_readlane(tg[u], l);
-          wp = __builtin_amdgcn_readlane(pv[u], l);
-        }
+        const uint64_t bm = __ballot(rv[u] == off);
+        if (bm && wh == kNone) wh = u * NT + wave * 64 + (uint32_t)__builtin_ctzll(bm);
       }
+      if (wh != kNone) { wt = P.tag[wh]; wp = P.pp[wh]; }
       if (lane == 0) { L.f[wave] = wh; L.red[2 * wave] = wt; L.red[2 * wave + 1] = wp; }
       if (wave == 0) {
         const uint32_t pb0 = step_sb(S, sub.part), pn = step_sb(S, sub.part + 1) - pb0;
@@ -1523,6 +1553,7 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, AnswerL
   } else {
     r = S.res[s];
     mode = answer_mode(r);
+    AST(1);
     gather(r, mode);
   }
   const uint64_t dslot = (uint64_t)r.chunk * P.Qpc + r.ing;
@@ -1530,8 +1561,13 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, AnswerL
   const uint64_t* bp = P.parity + ((uint64_t)P.PH + dslot) * E;
   uint64_t* pp = P.parity + (uint64_t)r.hit * E;
   STAMP_AT(stamp_wg, 51);
+  AST(3);
   // ---- decode + refresh, or the cached row -----------------------------
   if (mode == A_FINAL) {
+    if (!(r.flags & 2u)) {   // refresh_cur with the row prefetched with the decode operands
+      if (tid < P.SS) P.cur[(uint64_t)tid * P.PH + r.hit] = (uint16_t)e_cur;
+      if (P.SS > NT) refresh_cur(P, r, tid + NT, NT);   // SetSize > workgroup (BIGANN): the rest
+    }
     for (uint32_t w = tid; w < E; w += NT) {
       const uint64_t rvw = w < NT ? e_rv : rv[w], bpw = w < NT ? e_bp : bp[w],
                      ppw = w < NT ? e_pp : pp[w];
@@ -1550,8 +1586,14 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, AnswerL
     const uint64_t* a = P.arena + (uint64_t)r.slot * E;
     for (uint32_t w = tid; w < E; w += NT) row.w[w] = a[w];
   }
+  float* const qf = reinterpret_cast<float*>(red);   // free since the gather's last barrier
+  if (q_lds) {
+    if (tid < S.dim) qf[tid] = qreg0;
+    if (tid + NT < S.dim) qf[tid + NT] = qreg1;
+  }
   __syncthreads();
   STAMP_AT(stamp_wg, 52);
+  AST(4);
   // ---- results: row + header into pinned host memory, arena copy -----------
   if (mode != A_CHAINED) {
     const bool has_row = (mode == A_FINAL || mode == A_CACHED);
@@ -1564,13 +1606,13 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, AnswerL
       for (uint32_t w = tid; w < E; w += NT) ar[w] = row.w[w];
     }
     float d = 0.0f;
-    const float* qq = P.qv ? P.qv : S.q;
-    if (has_row && qq && tid < 8) d = l2_lds(row.f, qq, S.dim);
+    if (has_row && qq && tid < 8) d = l2_lds(row.f, q_lds ? qf : qq, S.dim);
     uint64_t cs = 0;
     if (tid < 64) cs = row_csum(S, row, has_row);
     publish_hdr(S, s, r.status, r.slot, d, cs);
   }
   STAMP_AT(stamp_wg, 53);
+  AST(5);
   // ---- arrival: workgroups of refresh chains count in; the last one decodes
   // the chained sub-queries in order.  Producer side: drain this wave's stores,
   // barrier, one lane releases at agent scope and counts (MI355X_MICROARCH.md
@@ -1593,7 +1635,10 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, AnswerL
 }
 
 template <int W>
-__global__ void __launch_bounds__(kAnsBlock) k_answer(PmStep S) {
+#ifndef PM_ANSWER_WGS
+#define PM_ANSWER_WGS 8   // min waves per SIMD (HIP launch bounds): <= 64 VGPRs, four 512-thread workgroups per CU
+#endif
+__global__ void __launch_bounds__(kAnsBlock, PM_ANSWER_WGS) k_answer(PmStep S) {
   __shared__ AnswerLds<kAnsBlock> L;
   answer_role<W, false, kAnsBlock>(S, blockIdx.x, L);
 }

@@ -1,14 +1,22 @@
-#!/bin/bash
-# Round profile set (run on the GPU box from the repo root):
-#   bench line, kernel stats and the two PMC passes of the same bench command
-#   (SIFT1M sessions + the BIGANN-100M / 1B blocks).
-# usage: tools/profile_round.sh OUTDIR
-set -e
-out=$1; mkdir -p "$out"
+# Profile set of one round on one MI355X (run through gpurun from the repo root),
+# one stage per gpurun call:
+#   bench   bench.json: the bench line (the driver's command)
+#   trace   rocprofv3 --kernel-trace --stats of the same bench (no cpu_baseline)
+#   pmcf    rocprofv3 --pmc FETCH_SIZE   (separate passes of the same command)
+#   pmcw    rocprofv3 --pmc WRITE_SIZE
+# usage: bash tools/profile_round.sh OUTDIR STAGE...
+set -o pipefail
+OUT=$1; shift
+mkdir -p $OUT
 export TMPDIR=/tmp
-cmd="bench.py --steps 30 --warmup 1 --no-cpu-baseline --no-config2 --no-config0 --no-single"
-timeout -k 10 400 python3 -u bench.py --steps 200 --warmup 5 > "$out/bench.json" 2> "$out/bench.err"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/ks" -o run -- python3 $cmd > "$out/ks.log" 2>&1
-timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/pf" -o run -- python3 $cmd > "$out/pf.log" 2>&1
-timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$out/pw" -o run -- python3 $cmd > "$out/pw.log" 2>&1
-echo done
+B="bench.py --steps 20 --warmup 5"
+for st in "$@"; do
+  case $st in
+    bench) timeout -k 10 900 python3 $B > $OUT/bench.json 2> $OUT/bench.err || exit 1 ;;
+    trace) timeout -k 10 1000 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $B --no-cpu-baseline > $OUT/bench_trace.json 2> $OUT/trace.err || exit 1 ;;
+    pmcf) timeout -k 10 1100 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmcf -o run -- python3 $B --no-cpu-baseline > $OUT/bench_pmcf.json 2> $OUT/pmcf.err || exit 1 ;;
+    pmcw) timeout -k 10 1100 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmcw -o run -- python3 $B --no-cpu-baseline > $OUT/bench_pmcw.json 2> $OUT/pmcw.err || exit 1 ;;
+  esac
+done
+find $OUT -name "*.csv" -size +1M -exec gzip -f {} \;
+find $OUT -type f | head -40
