@@ -415,7 +415,7 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
   if (g->E > pmk::step_max_e()) return fail(PM_EINVAL, "DBEntrySize above the step kernel's LDS limit");
   g->shard = shard; g->nshards = nshards;
   uint64_t off_tag = 0, off_pp = 0, off_par = 0, off_ridx = 0, off_rval = 0, off_hist = 0, off_ar = 0,
-           off_tab = 0, off_cur = 0, off_db = 0;
+           off_tab = 0, off_tabT = 0, off_cur = 0, off_db = 0;
   for (uint64_t i = 0; i < g->P; ++i) {
     PartHost& ph = g->parts[i];
     uint64_t start = i * g->PS, end = std::min((i + 1) * g->PS, N);
@@ -448,6 +448,7 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
     ph.d.arena = (uint64_t*)(uintptr_t)off_ar; off_ar += (uint64_t)ph.d.MaxQ * g->E;
     ph.d.tab = (uint16_t*)(uintptr_t)off_tab; off_tab += (uint64_t)ph.d.H * ph.d.SS;
     ph.d.cur = (uint16_t*)(uintptr_t)off_cur; off_cur += (uint64_t)ph.d.PH * ph.d.SS;
+    ph.d.tabT = (uint16_t*)(uintptr_t)off_tabT; off_tabT += tabT_words(ph.d.H, ph.d.SS);
     ph.cache.reserve(ph.d.MaxQ);
   }
   CHK(g->zero16.reserve(64));
@@ -476,7 +477,7 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
   CHK(g->fqn.reserve(g->P * 4));
   CHK(g->arena.reserve(std::max<uint64_t>(8, off_ar * 8)));
   CHK(g->tab.reserve(off_tab * 2));
-  CHK(g->tabT.reserve(off_tab * 2));
+  CHK(g->tabT.reserve(off_tabT * 2));
   CHK(g->cur.reserve(std::max<uint64_t>(2, off_cur * 2)));
   CHK(g->done.reserve(4 * (3 + 16 * 4096)));
   {   // step completion counter (pm_query.hip chain_add): 2^31 in the low half, 0 chained
@@ -504,7 +505,7 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
     d.hist = g->hist.as<uint32_t>() + (uintptr_t)d.hist;
     d.fqn = g->fqn.as<uint32_t>() + i;
     d.arena = g->arena.as<uint64_t>() + (uintptr_t)d.arena;
-    d.tabT = g->tabT.as<uint16_t>() + (uintptr_t)d.tab;
+    d.tabT = g->tabT.as<uint16_t>() + (uintptr_t)d.tabT;
     d.tab = g->tab.as<uint16_t>() + (uintptr_t)d.tab;
     d.cur = g->cur.as<uint16_t>() + (uintptr_t)d.cur;
   }

@@ -67,7 +67,8 @@ struct PmPart {
   // hands over backup tag PH+g*Qpc+j), so this table, built once per
   // preprocessing, holds every PRF value the online phase needs.
   PM_G uint16_t* tab;
-  PM_G uint16_t* tabT;    // the same table hint-major: tabT[t*SS + c] (set expansion reads one row)
+  PM_G uint16_t* tabT;    // the same table tag-major in tiles of 8 chunks (tabT_at): set expansion
+                          // reads one tag's row; k_prep_offsets writes whole 16-B tiles
   // The hint search's row: cur[c*PH + h] = PRF(current tag of primary hint h,
   // chunk c) & (CS-1), i.e. tab[c][tag[h]] kept in hint order, so matching a
   // (chunk, offset) streams PH contiguous u16 instead of gathering through
@@ -79,6 +80,14 @@ struct PmPart {
   // the step's PmStep::q
   const PM_G float* qv;
 };
+
+// tabT layout: chunk c of tag t at tile (c / 8, t), element c % 8 (16-B tiles of
+// 8 chunks; SetSize padded to a multiple of 8 with kSkip), so the writer of 8
+// chunks x consecutive tags stores full lines instead of one 2-B store per line.
+__host__ __device__ inline uint64_t tabT_index(uint32_t H, uint32_t t, uint32_t c) {
+  return ((uint64_t)(c >> 3) * H + t) * 8 + (c & 7);
+}
+__host__ __device__ inline uint64_t tabT_words(uint32_t H, uint32_t SS) { return (uint64_t)((SS + 7) / 8) * 8 * H; }
 
 // Sub-query kinds / statuses for one batched step.
 enum : uint32_t { SUB_NONE = 0, SUB_REAL = 1, SUB_DUMMY = 2, SUB_HOSTCACHE = 3 };

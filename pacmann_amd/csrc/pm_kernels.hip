@@ -54,15 +54,22 @@ __global__ void __launch_bounds__(kOffsBlock) k_prep_offsets(const PmPart* __res
   const uint32_t mask = P.CS - 1;
   const uint32_t own = h >= P.PH ? (h - P.PH) / P.Qpc : 0xffffffffu;
   uint16_t* o = P.tab;
-  uint16_t* oT = P.tabT + (uint64_t)h * SS;
   const R1Lane r1v = r1_lane(A, P.rk, h);   // initial tag of hint h is h
+  static_assert(kOffsChunksPerBlock == 8, "one 16-B tabT tile of 8 chunks per thread");
+  uint16_t tile[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) tile[j] = kSkip;   // chunks past SetSize: padding
   for (uint32_t c = c0; c < c1; ++c) {
     uint16_t v = (uint16_t)(prf_lo32_split(A, P.rk, r1u[c - c0], r1v, c) & mask);
     v = (c == own) ? kSkip : v;
     o[(uint64_t)c * H + h] = v;   // chunk-major: refreshed tags' re-evaluation, fold
-    oT[c] = v;                    // hint-major: set expansion
+    tile[c - c0] = v;
     if (h < P.PH) P.cur[(uint64_t)c * P.PH + h] = v;   // hint search (tags start at h)
   }
+  uint4 t4;   // tag-major tile (set expansion): one 16-B store
+  t4.x = tile[0] | ((uint32_t)tile[1] << 16); t4.y = tile[2] | ((uint32_t)tile[3] << 16);
+  t4.z = tile[4] | ((uint32_t)tile[5] << 16); t4.w = tile[6] | ((uint32_t)tile[7] << 16);
+  *reinterpret_cast<uint4*>(P.tabT + tabT_index(H, h, c0)) = t4;
 }
 
 template <int W>   // 64-bit words per lane segment: 2 (16-B loads) or 1

@@ -1269,8 +1269,7 @@ enum : uint32_t { A_ZERO = 0, A_FINAL = 1, A_CHAINED = 2, A_CACHED = 3, A_DUMMY 
 // clear); read by the next step's hint search, after this launch ends.
 __device__ __forceinline__ void refresh_cur(const PmPart& P, const PmRes& r, uint32_t tid, uint32_t nt) {
   const uint32_t ntag = P.PH + r.chunk * P.Qpc + r.ing;
-  const PM_G uint16_t* src = P.tabT + (uint64_t)ntag * P.SS;
-  for (uint32_t c = tid; c < P.SS; c += nt) P.cur[(uint64_t)c * P.PH + r.hit] = src[c];
+  for (uint32_t c = tid; c < P.SS; c += nt) P.cur[(uint64_t)c * P.PH + r.hit] = P.tabT[tabT_index(P.H, ntag, c)];
 }
 
 // Decode one chained sub-query (its hint was refreshed earlier in this step)
@@ -1382,7 +1381,7 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, AnswerL
     // decode operands: independent of the gather, issued first (pir.go:450-468)
     const uint64_t dslot = (uint64_t)r.chunk * P.Qpc + r.ing;
     if (mode == A_FINAL && !(r.flags & 2u) && tid < P.SS)   // the new tag's PRF row (backup hint (chunk, ing))
-      e_cur = P.tabT[(uint64_t)(P.PH + r.chunk * P.Qpc + r.ing) * P.SS + tid];
+      e_cur = P.tabT[tabT_index(P.H, P.PH + r.chunk * P.Qpc + r.ing, tid)];
     if (mode == A_FINAL && tid < E) {
       e_rv = P.rval[dslot * E + tid];
       e_bp = P.parity[((uint64_t)P.PH + dslot) * E + tid];
@@ -1419,9 +1418,8 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, AnswerL
     // ---- query set (pir.go:363-371 dummy; :424-444 real) -------------------
     if (mode == A_FINAL || mode == A_CHAINED) {
       const uint32_t pchunk = r.pp != kDefaultProgramPoint ? (r.pp >> lg) : kNone;
-      const uint16_t* trow = P.tabT + (uint64_t)r.tag * P.SS;
       for (uint32_t i = tid; i < P.SS; i += NT) {
-        uint32_t o = trow[i];
+        uint32_t o = P.tabT[tabT_index(P.H, r.tag, i)];
         if (i == pchunk) o = r.pp & mask;
         if (i == r.chunk) o = P.ridx[r.chunk * P.Qpc + r.ing] & mask;
         qo[i] = (uint16_t)o;
@@ -1666,7 +1664,7 @@ __global__ void __launch_bounds__(kGatherBlock) k_gather(PmStep S) {
   const uint32_t pchunk = real && r.pp != kDefaultProgramPoint ? (r.pp >> lg) : kNone;
   const uint32_t rchunk = real ? r.chunk : kNone;
   const uint32_t rep = real ? (P.ridx[r.chunk * P.Qpc + r.ing] & mask) : 0;
-  const PM_G uint16_t* trow = P.tabT + (uint64_t)r.tag * P.SS;
+
   const PM_G uint64_t* base = S.db + P.row0 * E;
   PM_G uint64_t* out = S.part_x + ((uint64_t)s * S.nsplit + j) * EX;
   typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
@@ -1685,7 +1683,7 @@ __global__ void __launch_bounds__(kGatherBlock) k_gather(PmStep S) {
           uint32_t o = 0;
           if (i < c1) {
             if (real) {
-              o = trow[i];
+              o = P.tabT[tabT_index(P.H, r.tag, i)];
               if (i == pchunk) o = r.pp & mask;
               if (i == rchunk) o = rep;
             } else {
