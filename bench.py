@@ -55,9 +55,15 @@ GROUPS = 4      # lock-step groups (GPU_MAX_HW_QUEUES = 4 hardware queues per pr
 THREADS = 16    # host worker threads of the batched loop (the box gives a GPU 16 host cores)
 SYMBOLS = {"prep_fold": "void pm::k_prep_fold_pipe<4, 1, 4, 1>(pm::PmPart const*, unsigned long const*, "
                         "unsigned long const*, unsigned int, unsigned int, unsigned int, unsigned int, unsigned int)",
-           "answer": "void pm::k_answer<2>(pm::PmStep)", "step": "void pm::k_step<2>(pm::PmStep)", "resolve": "void pm::k_resolve<true>(pm::PmStep)",
+           "answer": None, "step": "void pm::k_step<2>(pm::PmStep)", "resolve": "void pm::k_resolve<true>(pm::PmStep)",
            "hint_match": "pm::k_match(pm::PmStep)", "prep_offsets": "pm::k_prep_offsets(pm::PmPart const*)",
            "gather": "void pm::k_gather<2>(pm::PmStep)"}
+# the server answer of search-sized shapes: the small-LDS instance with
+# PM_ANSWER_NT threads per workgroup (pm_query.hip step_answer; 0: generic)
+ANSWER_NT = int(os.environ.get("PM_ANSWER_NT", "128"))
+ANSWER_BLOCK = ANSWER_NT or 512
+SYMBOLS["answer"] = (f"void pm::k_answer_s<2, {ANSWER_NT}>(pm::PmStep)" if ANSWER_NT
+                     else "void pm::k_answer<2>(pm::PmStep)")
 HOST = ["host_search_knn", "host_knn_init", "host_knn_final", "host_knn_batch", "host_knn_update",
         "host_gvi_parse", "host_batch_query", "host_step_launch", "host_step_wait", "host_step_post",
         "host_wait_first_token", "host_wait_all_tokens", "host_rows_seen", "host_rows_torn"]
@@ -208,7 +214,7 @@ def batch_pir_msmarco(ctx, with_cpu: bool):
             "alg_bytes_per_launch": by / n,
             "kernel_avg_us": {k: round(v[1] / v[0] * 1e3, 3) for k, v in
                               ((k, clients[0].ctx.timing_get(k)) for k in ("hint_match", "resolve", "answer")) if v[0]}}
-        attach_traffic(out["clients_grouped"]["roofline"], SYMBOLS["answer"], C2_CLIENTS * C2_B * 512)
+        attach_traffic(out["clients_grouped"]["roofline"], SYMBOLS["answer"], C2_CLIENTS * C2_B * ANSWER_BLOCK)
     del grp, clients
     if with_cpu:
         from oracle import oracle as O
@@ -299,7 +305,7 @@ def private_search_msmarco(local, args, with_cpu: bool):
                            "launches": n, "alg_bytes_per_launch": by / n,
                            "aggregate": {"achieved": round(by / wall / 1e9, 1),
                                          "frac": round(by / wall / 1e9 / HBM_PEAK_GBS, 4)}}
-        attach_traffic(out["roofline"], SYMBOLS["answer"], (S2 // MS_GROUPS) * PARALLEL * M * 512)
+        attach_traffic(out["roofline"], SYMBOLS["answer"], (S2 // MS_GROUPS) * PARALLEL * M * ANSWER_BLOCK)
     if with_cpu:   # the oracle replaying session 0's workload, one core
         cb = cpu_baseline(v, g, qs[0], MS_WARMUP, ans[0], ctx, 601, 602, k=MS_K)
         out["cpu_baseline"] = cb
@@ -784,8 +790,8 @@ def main():
             return None
         ach = (by / n) / (ms / n / 1e3) / 1e9
         grid = None
-        if name == "answer" and args.mode == "batched":   # the PMC summary by launch shape: 512-thread WG per sub-query
-            grid = (S // max(1, args.groups)) * PARALLEL * M * 512
+        if name == "answer" and args.mode == "batched":   # the PMC summary by launch shape: one workgroup per sub-query
+            grid = (S // max(1, args.groups)) * PARALLEL * M * ANSWER_BLOCK
         r = {"bound": "hbm", "kernel": name, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
              "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
              "launches": n, "avg_ms": round(ms / n, 5), "alg_bytes_per_launch": by / n}

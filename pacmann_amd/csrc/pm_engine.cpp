@@ -905,7 +905,7 @@ static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
     S.part_x = g->part_x.as<uint64_t>();
     c->timed_ext("gather", ans_bytes, [&](pmk::PmEvents ev) { pmk::step_gather(st, S, ev); }, 2);
   }
-  c->timed_ext("answer", S.nsplit > 1 ? 0 : ans_bytes, [&](pmk::PmEvents ev) { pmk::step_answer(st, S, ev); }, 2);
+  c->timed_ext("answer", S.nsplit > 1 ? 0 : ans_bytes, [&](pmk::PmEvents ev) { pmk::step_answer(st, S, g->maxSS, ev); }, 2);
   HIPCHK(hipGetLastError());
   c->host_add(HT_STEP_LAUNCH, ms_since(t_begin));
   return wait_and_post(g, S, nsub, t_begin);
@@ -2086,7 +2086,7 @@ static int group_step(StepGroup& G, const std::vector<char>& in) {
     S.stamps = G.stamps.as<uint64_t>();
   }
 #endif
-  c->timed_ext("answer", S.nsplit > 1 ? 0 : ans_bytes, [&](pmk::PmEvents ev) { pmk::step_answer(st, S, ev); }, 2);
+  c->timed_ext("answer", S.nsplit > 1 ? 0 : ans_bytes, [&](pmk::PmEvents ev) { pmk::step_answer(st, S, G.maxSS, ev); }, 2);
   HIPCHK(hipGetLastError());
 #ifdef PM_ANSWER_STAMPS
   if (stamp_this) {

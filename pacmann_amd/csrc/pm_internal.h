@@ -199,7 +199,7 @@ void step_resolve(hipStream_t st, const PmStep& S, bool lds, PmEvents ev = {});
 bool step_fused_ok(const PmStep& S, uint32_t maxPH, uint32_t max_sub_per_part);
 void step_fused(hipStream_t st, const PmStep& S, PmEvents ev = {});
 bool step_resolve_lds_ok(uint32_t maxPH, uint32_t max_sub_per_part);
-void step_answer(hipStream_t st, const PmStep& S, PmEvents ev = {});
+void step_answer(hipStream_t st, const PmStep& S, uint32_t maxSS, PmEvents ev = {});
 // Split gather ahead of k_answer for wide query sets (SetSize >= 256, BIGANN
 // scale): how many workgroups per sub-query (1: no split), and the launch.
 uint32_t step_gather_split(uint32_t maxSS, uint32_t nsub);

@@ -1189,15 +1189,18 @@ __device__ __forceinline__ float l2_lds(const float* row, const float* __restric
 
 constexpr uint32_t kMaxSSLds = 4096, kMaxELds = 2048;
 
-union RowBuf {   // one decoded entry; the L2 reads its leading floats
-  uint64_t w[kMaxELds];
-  float f[2 * kMaxELds];
+template <uint32_t ME>
+union RowBufT {   // one decoded entry (up to ME words); the L2 reads its leading floats
+  uint64_t w[ME];
+  float f[2 * ME];
 };
+using RowBuf = RowBufT<kMaxELds>;
 
 // PmOutHdr::csum: the position-keyed hash of the row words [pf_w0, pf_w1)
 // as written (the LDS copy, or zeros), pm_internal.h row_hash_mult.  Wave 0
 // only; every lane returns the result.
-__device__ __forceinline__ uint64_t row_csum(const PmStep& S, const RowBuf& row, bool has_row) {
+template <class RB>
+__device__ __forceinline__ uint64_t row_csum(const PmStep& S, const RB& row, bool has_row) {
   uint64_t x = 0;
   for (uint32_t w = S.pf_w0 + (threadIdx.x & 63); w < S.pf_w1; w += 64)
     x += (has_row ? row.w[w] : 0) * row_hash_mult(w);
@@ -1274,8 +1277,8 @@ __device__ __forceinline__ void refresh_cur(const PmPart& P, const PmRes& r, uin
 
 // Decode one chained sub-query (its hint was refreshed earlier in this step)
 // once every earlier refresh is visible; the whole workgroup participates.
-template <bool GRAN>
-__device__ void decode_chained(const PmStep& S, uint32_t s, RowBuf& row) {
+template <bool GRAN, class RB>
+__device__ void decode_chained(const PmStep& S, uint32_t s, RB& row) {
   const PmSub sub = step_sub(S, s);
   const PmRes r = res_after_acquire<GRAN>(S, s);
   const PmPart& P = S.parts[sub.part];
@@ -1313,19 +1316,21 @@ __device__ void decode_chained(const PmStep& S, uint32_t s, RowBuf& row) {
 
 // The finisher of a step (see resolver_count), after its acquire: decodes the
 // chained sub-queries in list order and re-arms the counters.  Whole workgroup.
-template <bool GRAN>
-__device__ void finish_step(const PmStep& S, RowBuf& row) {
+template <bool GRAN, class RB>
+__device__ void finish_step(const PmStep& S, RB& row) {
   const uint32_t nchain = S.done[2];
   for (uint32_t k = 0; k < nchain; ++k) decode_chained<GRAN>(S, S.done[3 + k], row);
   if (threadIdx.x == 0) chain_rearm(S);
 }
 
-template <int NT>
+// MSS / ME: the largest SetSize / entry words the instance serves (the
+// generic instance: every shape of step_max_ss / step_max_e).
+template <int NT, uint32_t MSS = kMaxSSLds, uint32_t ME = kMaxELds>
 struct AnswerLds {
   uint32_t f[17];   // k_step: granule fields, per-wave first candidates, predicted index
-  uint16_t qo[kMaxSSLds];   // the query set: in-chunk offsets < ChunkSize <= 32768
+  uint16_t qo[MSS];   // the query set: in-chunk offsets < ChunkSize <= 32768
   uint64_t red[NT * 2];
-  __attribute__((aligned(16))) RowBuf row;
+  __attribute__((aligned(16))) RowBufT<ME> row;
   uint32_t s_last;
 };
 
@@ -1346,11 +1351,11 @@ __device__ __forceinline__ uint32_t answer_mode(const PmRes& r) {
 // rows gathered and the decode operands loaded for that guess while the
 // resolver runs; its result then either equals the guess in every field the
 // answer reads (kept) or the work is redone for the actual result.
-template <int W, bool GRAN, int NT>
-__device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, AnswerLds<NT>& L) {
+template <int W, bool GRAN, int NT, class LDS>
+__device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, LDS& L) {
   uint16_t* const qo = L.qo;
   uint64_t* const red = L.red;
-  RowBuf& row = L.row;
+  auto& row = L.row;
   const uint32_t tid = threadIdx.x;
   const uint32_t E = S.E, EX = E & ~3u, NSEG = EX / W;
   const PmSub sub = step_sub(S, s);
@@ -1641,6 +1646,21 @@ __global__ void __launch_bounds__(kAnsBlock, PM_ANSWER_WGS) k_answer(PmStep S) {
   answer_role<W, false, kAnsBlock>(S, blockIdx.x, L);
 }
 
+// The same answer for the search-sized shapes (SetSize <= 1024, entries <= 256
+// words: SIFT1M's 124 x 80, MS-MARCO's 196 x 112) with NT-thread workgroups
+// and a 7-8 KB LDS footprint.  The generic instance's 33 KB of LDS (sets up
+// to 4096 chunks, entries up to 2048 words) holds a CU to four workgroups,
+// i.e. four sub-queries in flight; here registers alone bound it (64 VGPRs:
+// 32 waves per CU), so a CU holds 32 / (NT / 64) sub-queries whose latency-
+// bound phases (resolution, set expansion, decode, publication) overlap the
+// others' row gathers.
+constexpr uint32_t kSmallSS = 1024, kSmallE = 256;
+template <int W, int NT>
+__global__ void __launch_bounds__(NT, PM_ANSWER_WGS) k_answer_s(PmStep S) {
+  __shared__ AnswerLds<NT, kSmallSS, kSmallE> L;
+  answer_role<W, false, NT>(S, blockIdx.x, L);
+}
+
 // ---- k_gather: the server's XOR gather of wide sets, split ----------------
 // (HOT LOOP D + E for SetSize >= 256: BIGANN's 764 / 3,816 chunks.)  One
 // workgroup per (sub-query s, chunk range j of nsplit); it expands its range
@@ -1808,7 +1828,24 @@ bool step_resolve_lds_ok(uint32_t maxPH, uint32_t max_sub_per_part) {
   return max_sub_per_part > kSpecSubs && maxPH <= kLdsPH &&
          max_sub_per_part * ((maxPH + 63) / 64) <= kLdsBitWords;
 }
-void step_answer(hipStream_t st, const PmStep& S, PmEvents ev) {
+void step_answer(hipStream_t st, const PmStep& S, uint32_t maxSS, PmEvents ev) {
+  // search-sized shapes: the small-LDS instance (PM_ANSWER_NT threads per
+  // workgroup, 0 = the generic instance)
+  static const int nt = [] { const char* e = getenv("PM_ANSWER_NT"); return e ? atoi(e) : 128; }();
+  if (nt && S.nsplit <= 1 && maxSS <= kSmallSS && S.E <= kSmallE) {
+    const bool w2 = S.E % 2 == 0;
+    if (nt == 128) {
+      if (w2) PM_LAUNCH(ev, (k_answer_s<2, 128>), dim3(S.nsub), dim3(128), st, S);
+      else PM_LAUNCH(ev, (k_answer_s<1, 128>), dim3(S.nsub), dim3(128), st, S);
+    } else if (nt == 512) {
+      if (w2) PM_LAUNCH(ev, (k_answer_s<2, 512>), dim3(S.nsub), dim3(512), st, S);
+      else PM_LAUNCH(ev, (k_answer_s<1, 512>), dim3(S.nsub), dim3(512), st, S);
+    } else {
+      if (w2) PM_LAUNCH(ev, (k_answer_s<2, 256>), dim3(S.nsub), dim3(256), st, S);
+      else PM_LAUNCH(ev, (k_answer_s<1, 256>), dim3(S.nsub), dim3(256), st, S);
+    }
+    return;
+  }
   if (S.E % 2 == 0) PM_LAUNCH(ev, k_answer<2>, dim3(S.nsub), dim3(kAnsBlock), st, S);
   else PM_LAUNCH(ev, k_answer<1>, dim3(S.nsub), dim3(kAnsBlock), st, S);
 }
