@@ -66,7 +66,7 @@ SYMBOLS["answer"] = (f"void pm::k_answer_s<2, {ANSWER_NT}>(pm::PmStep)" if ANSWE
                      else "void pm::k_answer<2>(pm::PmStep)")
 HOST = ["host_search_knn", "host_knn_init", "host_knn_final", "host_knn_batch", "host_knn_update",
         "host_gvi_parse", "host_batch_query", "host_step_launch", "host_step_wait", "host_step_post",
-        "host_wait_first_token", "host_wait_all_tokens", "host_rows_seen", "host_rows_torn"]
+        "host_wait_first_token", "host_wait_all_tokens", "host_rows_seen", "host_rows_torn", "host_wait_done"]
 
 
 T_START = time.perf_counter()
@@ -869,9 +869,14 @@ def main():
         "kernel_avg_us": {k: round(ktime[k][1] / ktime[k][0] * 1e3, 3) if ktime[k][0] else None for k in KERNELS},
         "host_ms": {k: round(htime[k][1], 3) for k in HOST},
         "steps_in_region": nsteps,
-        # result rows the host read at token time vs those that failed their header
-        # checksum then (the publication ordering audit, pm_query.hip publish_hdr)
-        "rows_check": {"seen": int(htime["host_rows_seen"][0]), "torn": int(htime["host_rows_torn"][0])},
+        # result rows the host read at token time vs those whose bytes did not yet
+        # match their header hash then; results are taken only after the step's
+        # completion event (system-scope release), where a mismatch is an error
+        # (result publication)
+        "rows_check": {"seen": int(htime["host_rows_seen"][0]), "torn_at_token": int(htime["host_rows_torn"][0]),
+                       "completion_waits": int(htime["host_wait_done"][0]),
+                       "completion_wait_ms": round(htime["host_wait_done"][1], 3),
+                       "ordered": os.environ.get("PM_PUBLISH_WAIT", "1") != "0"},
         "dominant_kernel": dom,
     }
     if isolated:

@@ -149,8 +149,8 @@ struct HostBuf {
 };
 
 // Host wall-clock accumulators, read back as "host_*" through pm_timing_get.
-enum HostTimer : int { HT_STEP_LAUNCH, HT_STEP_WAIT, HT_STEP_POST, HT_BATCH_QUERY, HT_GVI_PARSE, HT_SEARCH_KNN, HT_KNN_INIT, HT_KNN_BATCH, HT_KNN_UPDATE, HT_KNN_FINAL, HT_WAIT_FIRST, HT_WAIT_ALL, HT_ROWS_SEEN, HT_ROWS_TORN, HT_COUNT };
-static const char* const kHostTimerName[HT_COUNT] = {"host_step_launch", "host_step_wait", "host_step_post", "host_batch_query", "host_gvi_parse", "host_search_knn", "host_knn_init", "host_knn_batch", "host_knn_update", "host_knn_final", "host_wait_first_token", "host_wait_all_tokens", "host_rows_seen", "host_rows_torn"};
+enum HostTimer : int { HT_STEP_LAUNCH, HT_STEP_WAIT, HT_STEP_POST, HT_BATCH_QUERY, HT_GVI_PARSE, HT_SEARCH_KNN, HT_KNN_INIT, HT_KNN_BATCH, HT_KNN_UPDATE, HT_KNN_FINAL, HT_WAIT_FIRST, HT_WAIT_ALL, HT_ROWS_SEEN, HT_ROWS_TORN, HT_WAIT_DONE, HT_COUNT };
+static const char* const kHostTimerName[HT_COUNT] = {"host_step_launch", "host_step_wait", "host_step_post", "host_batch_query", "host_gvi_parse", "host_search_knn", "host_knn_init", "host_knn_batch", "host_knn_update", "host_knn_final", "host_wait_first_token", "host_wait_all_tokens", "host_rows_seen", "host_rows_torn", "host_wait_done"};
 
 struct TimedLaunch { std::string name; hipEvent_t a, b; double bytes; };
 
@@ -170,6 +170,18 @@ struct pm_ctx {
   // and fail the step, 2 = count it and wait for the row to match (PM_ROWS_CHECK)
   int rows_check = 2;
   std::vector<uint64_t> hash_mult;   // row_hash_mult(w) for every word a row can have
+  // Step completion (result publication): an event recorded
+  // after the step's last kernel, with a system-scope release, so that once
+  // hipEventQuery reports it, every result byte the step wrote into pinned
+  // memory is visible to the host (HIP event semantics; the header tokens
+  // alone give no such order).  done_tok: the last token whose event was seen
+  // complete, so one worker queries the runtime and the others read an atomic.
+  // PM_PUBLISH_WAIT=0: the token + row-hash acceptance alone (diagnostics).
+  bool publish_wait = true;
+  hipEvent_t done_ev = nullptr;
+  std::atomic<uint32_t> done_tok{0};
+  std::mutex done_mu;
+  void record_done(hipStream_t st) { if (publish_wait) (void)hipEventRecord(done_ev, st); }
   std::string last_kernel;
   // host-side wall-clock accumulators ("host_*" names in pm_timing_get)
   uint64_t host_n[HT_COUNT] = {};
@@ -210,6 +222,7 @@ struct pm_ctx {
   ~pm_ctx() {
     for (auto& t : launches) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
     for (auto e : pool) (void)hipEventDestroy(e);
+    if (done_ev) (void)hipEventDestroy(done_ev);
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -242,6 +255,12 @@ extern "C" int pm_ctx_create(int device, pm_ctx** out) {
   if (const char* rc = getenv("PM_ROWS_CHECK")) c->rows_check = atoi(rc);
   c->hash_mult.resize(pmk::step_max_e());
   for (size_t w = 0; w < c->hash_mult.size(); ++w) c->hash_mult[w] = row_hash_mult(w);
+  if (const char* pw = getenv("PM_PUBLISH_WAIT")) c->publish_wait = pw[0] != '0';
+  if (c->publish_wait &&
+      hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming | hipEventReleaseToSystem) != hipSuccess) {
+    delete c;
+    return fail(PM_EHIP, "hipEventCreateWithFlags(step completion) failed");
+  }
   const char* ng = getenv("PM_NO_GUESS");
   c->no_guess = ng && ng[0] == '1';
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
@@ -606,18 +625,61 @@ static inline double ms_since(Clock::time_point t) {
   return std::chrono::duration<double, std::milli>(Clock::now() - t).count();
 }
 
-// Completion of a step: every result header in pinned memory carries this
-// step's token (k_answer writes it after the row has drained), so the host
-// polls the headers instead of waiting for the kernel's completion signal.
+// Completion of a step.  Every result header in pinned memory carries this
+// step's token; the host polls the tokens (and prefetches the bytes [pf_off,
+// pf_off + pf_len) of each published row, so the caller's reads hit the cache).
+// A token says that its sub-query is answered, not that the row's bytes have
+// landed: stores from the GPU to fine-grained host memory reach the host in no
+// guaranteed order.  The results are therefore taken only after the step's
+// completion event (recorded after its last kernel with a system-scope
+// release, pm_ctx::done_ev) is seen complete: from then on every byte the
+// step wrote is visible (HIP event semantics).  Rows are then checked against
+// their header hash (PmOutHdr::csum) as an assertion: a mismatch is an error,
+// never retried.  `torn` counts rows whose bytes did not yet match at token
+// time (rows_check >= 1, diagnostics only).
+// PM_PUBLISH_WAIT=0 drops the completion wait: rows are then accepted on the
+// token and a matching hash, re-read until they match (rows_check 2).
 // Debug runs (PM_DEBUG_SYNC), and a step not published within 5 s (a fault, or
 // a bug), fall back to the stream synchronisation, which reports errors.
-// Timed runs poll like any other: their events ride in the kernels' dispatch
-// packets and are read by pm_timing_get.
-// While polling, the bytes [pf_off, pf_off + pf_len) of each published row are
-// prefetched, so the caller's reads of the results hit the cache.
+// sc: the context whose stream ran the step (its done_ev); c: the one whose
+// counters are charged (a session of a shared step, or sc itself).
+static int wait_done(pm_ctx* sc, uint32_t token) {
+  if (sc->done_tok.load(std::memory_order_acquire) == token) return 0;
+  auto t0 = Clock::now();
+  for (uint64_t spin = 0;; ++spin) {
+    if (sc->done_tok.load(std::memory_order_acquire) == token) return 0;
+    if (sc->done_mu.try_lock()) {   // one waiter asks the runtime; the others read done_tok
+      std::lock_guard<std::mutex> lk(sc->done_mu, std::adopt_lock);
+      if (sc->done_tok.load(std::memory_order_acquire) == token) return 0;
+      for (uint64_t k = 0;; ++k) {
+        const hipError_t e = hipEventQuery(sc->done_ev);
+        if (e == hipSuccess) break;
+        if (e != hipErrorNotReady) return fail(PM_EHIP, std::string("step completion: ") + hipGetErrorString(e));
+        if ((k & 0xfff) == 0xfff && ms_since(t0) > 5000.0) {
+          HIPCHK(hipStreamSynchronize(sc->stream));
+          HIPCHK(hipGetLastError());
+          break;
+        }
+      }
+      sc->done_tok.store(token, std::memory_order_release);
+      return 0;
+    }
+    if ((spin & 0xffff) == 0xffff && ms_since(t0) > 10000.0) return fail(PM_EHIP, "step completion wait timed out");
+  }
+}
+
 static int wait_step(pm_ctx* c, const PmOutHdr* hdr, uint32_t nsub, uint32_t token, const char* rows,
-                     size_t row_bytes, size_t pf_off, size_t pf_len, hipStream_t stream = nullptr) {
-  if (!stream) stream = c->stream;   // the stream the step runs on (c: timing and diagnostics)
+                     size_t row_bytes, size_t pf_off, size_t pf_len, pm_ctx* sc = nullptr) {
+  if (!sc) sc = c;
+  hipStream_t stream = sc->stream;
+  const bool ordered = sc->publish_wait && sc->done_ev;
+  const size_t w0 = pf_off / 8, w1 = (pf_off + pf_len + 7) / 8;
+  auto row_hash = [&](uint32_t s) {
+    const volatile uint64_t* rw = (const volatile uint64_t*)(rows + s * row_bytes);
+    uint64_t x = token * kCsumMix;
+    for (size_t w = w0; w < w1; ++w) x += rw[w] * c->hash_mult[w];
+    return x;
+  };
   if (c->debug_sync) {
     HIPCHK(hipStreamSynchronize(stream));
   } else {
@@ -625,22 +687,18 @@ static int wait_step(pm_ctx* c, const PmOutHdr* hdr, uint32_t nsub, uint32_t tok
     const size_t stride = sizeof(PmOutHdr) / sizeof(uint32_t);
     auto t0 = Clock::now();
     uint32_t s = 0;
-    const size_t w0 = pf_off / 8, w1 = (pf_off + pf_len + 7) / 8;
     bool first_look = true;   // the first read of sub-query s's row after its token appeared
     for (uint64_t spin = 0; s < nsub; ++spin) {
       if (tok[s * stride] == token) {
         if (c->timing && s == 0 && first_look) c->host_add(HT_WAIT_FIRST, ms_since(t0));
         std::atomic_thread_fence(std::memory_order_acquire);
         if (c->rows_check) {
-          // the device published the token after a system-scope release of the
-          // row (pm_query.hip publish_hdr); the checksum asserts it
-          const volatile uint64_t* rw = (const volatile uint64_t*)(rows + s * row_bytes);
-          const volatile uint64_t* cs = &hdr[s].csum;
-          uint64_t x = token * kCsumMix;
-          for (size_t w = w0; w < w1; ++w) x += rw[w] * c->hash_mult[w];
-          if (first_look) c->host_add(HT_ROWS_SEEN, 0);
-          if (x != *cs) {
-            if (first_look) c->host_add(HT_ROWS_TORN, 0);
+          const bool match = row_hash(s) == *(const volatile uint64_t*)&hdr[s].csum;
+          if (first_look) {
+            c->host_add(HT_ROWS_SEEN, 0);
+            if (!match) c->host_add(HT_ROWS_TORN, 0);
+          }
+          if (!match && !ordered) {   // token-time acceptance: wait for the bytes to match
             first_look = false;
             if (c->rows_check == 1)
               return fail(PM_EHIP, "step result row " + std::to_string(s) + " does not match its header checksum");
@@ -660,10 +718,19 @@ static int wait_step(pm_ctx* c, const PmOutHdr* hdr, uint32_t nsub, uint32_t tok
         break;
       }
     }
+    if (ordered) {
+      auto td = Clock::now();
+      CHK(wait_done(sc, token));
+      if (c->timing) c->host_add(HT_WAIT_DONE, ms_since(td));
+    }
     std::atomic_thread_fence(std::memory_order_acquire);
   }
   for (uint32_t s = 0; s < nsub; ++s)
     if (hdr[s].token != token) return fail(PM_EHIP, "step results not published (sub-query " + std::to_string(s) + ")");
+  if (ordered && c->rows_check)   // assertion: the completed step's bytes are the ones its headers describe
+    for (uint32_t s = 0; s < nsub; ++s)
+      if (row_hash(s) != hdr[s].csum)
+        return fail(PM_EHIP, "step result row " + std::to_string(s) + " does not match its header after completion");
   return 0;
 }
 
@@ -860,6 +927,7 @@ static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
     S.stamps = g->stamps.as<uint64_t>();
 #endif
     c->timed_ext("step", ans_bytes, [&](pmk::PmEvents ev) { pmk::step_fused(st, S, ev); }, 2);
+    c->record_done(st);
     HIPCHK(hipGetLastError());
     c->host_add(HT_STEP_LAUNCH, ms_since(t_begin));
     CHK(wait_and_post(g, S, nsub, t_begin));
@@ -906,6 +974,7 @@ static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
     c->timed_ext("gather", ans_bytes, [&](pmk::PmEvents ev) { pmk::step_gather(st, S, ev); }, 2);
   }
   c->timed_ext("answer", S.nsplit > 1 ? 0 : ans_bytes, [&](pmk::PmEvents ev) { pmk::step_answer(st, S, g->maxSS, ev); }, 2);
+  c->record_done(st);
   HIPCHK(hipGetLastError());
   c->host_add(HT_STEP_LAUNCH, ms_since(t_begin));
   return wait_and_post(g, S, nsub, t_begin);
@@ -2087,6 +2156,7 @@ static int group_step(StepGroup& G, const std::vector<char>& in) {
   }
 #endif
   c->timed_ext("answer", S.nsplit > 1 ? 0 : ans_bytes, [&](pmk::PmEvents ev) { pmk::step_answer(st, S, G.maxSS, ev); }, 2);
+  c->record_done(st);
   HIPCHK(hipGetLastError());
 #ifdef PM_ANSWER_STAMPS
   if (stamp_this) {
@@ -2118,7 +2188,7 @@ static int group_collect(StepGroup& G, uint32_t s) {
   uint64_t* rows = (uint64_t*)(G.out_h.as<char>() + G.subs.size() * sizeof(PmOutHdr));
   auto t_wait = Clock::now();
   CHK(wait_step(e->ctx, hdr + G.base[s], n, G.token, (const char*)(rows + (uint64_t)G.base[s] * G.E),
-                (size_t)G.E * 8, (size_t)G.pf_w0 * 8, (size_t)(G.pf_w1 - G.pf_w0) * 8, G.c->stream));
+                (size_t)G.E * 8, (size_t)G.pf_w0 * 8, (size_t)(G.pf_w1 - G.pf_w0) * 8, G.c));
   e->ctx->host_add(HT_STEP_WAIT, ms_since(t_wait));
   auto tp = Clock::now();
   post_results(e, hdr, rows, n, G.base[s], G.token);

@@ -108,17 +108,19 @@ struct PmRes {
                                       // bit 1: a later sub-query in this step re-hits this hint
 };
 // Per-sub-query result header, written by the GPU into pinned host memory
-// after the sub-query's row.  Write-combined stores to fine-grained host
-// memory reach the host in no guaranteed order (measured: 2.6e-4 of rows are
-// torn when the token is first seen), and ordering them costs 2.8-4.4x the
-// answer kernel's time (a system-scope L2 write-back per workgroup, or
-// write-through stores).  So the header carries a multilinear
-// hash of the row words the host reads ([pf_w0, pf_w1) of PmStep):
+// after the sub-query's row.  Stores to fine-grained host memory reach the
+// host in no guaranteed order (measured: ~3e-5 of rows not yet complete when
+// their token is first seen), and ordering them inside the kernel costs
+// 2.8-4.4x the answer kernel's time (a system-scope L2 write-back per
+// workgroup, or write-through stores).  So the token only says "answered";
+// the host takes a step's results after the step's completion event, recorded
+// with a system-scope release after the last kernel (pm_engine.cpp
+// wait_step), which orders every byte.  The header also carries a
+// multilinear hash of the row words the host reads ([pf_w0, pf_w1) of PmStep):
 //   csum = token * kCsumMix + sum_w row[w] * row_hash_mult(w)   (mod 2^64)
-// with odd multipliers, and the host accepts a row only when its bytes hash
-// to it, else re-reads.  One stale word changes the sum by (new - old) * odd
-// != 0: always detected; several cancel only if their weighted differences
-// sum to 0 mod 2^64.  A stale header (previous step's token) never matches.
+// with odd multipliers, checked after completion as an assertion (and, with
+// PM_PUBLISH_WAIT=0, as the token-time acceptance test: one stale word changes
+// the sum by (new - old) * odd != 0; a stale header never matches).
 constexpr uint64_t kCsumMix = 0x9E3779B97F4A7C15ull;
 __host__ __device__ inline uint64_t row_hash_mult(uint64_t w) { return sm64(w ^ 0x5851F42D4C957F2Dull) | 1ull; }
 struct alignas(16) PmOutHdr {

@@ -1210,13 +1210,15 @@ __device__ __forceinline__ uint64_t row_csum(const PmStep& S, const RB& row, boo
 }
 
 // Result publication into pinned (fine-grained) host memory.  The default
-// (PM_PUBLISH 0) leaves ordering to the row hash the host verifies
-// (pm_internal.h PmOutHdr): lane 0 stores the header as soon as the row is
-// final in LDS, and no wave waits for its write-combined row stores to be
-// acknowledged (4: they are, before a workgroup barrier and the header, as in
-// round 1 — which still tears, measured).  Two ordered forms, both
-// measured with 0 torn rows in 49M but 2.8x / 4.4x the kernel time, are kept
-// as build options:
+// (PM_PUBLISH 0): lane 0 stores the header as soon as the row is final in
+// LDS, and no wave waits for its row stores to be acknowledged.  The token is
+// a progress mark only: the host takes the step's results after the step's
+// completion event (system-scope release after the last kernel, pm_engine.cpp
+// wait_step), and checks the row hash there as an assertion (pm_internal.h
+// PmOutHdr).  (4: row stores acknowledged before a workgroup barrier and the
+// header, as in round 1 — rows still arrive after the token, measured.)  Two
+// in-kernel ordered forms, both measured with 0 torn rows in 49M but 2.8x /
+// 4.4x the kernel time, are kept as build options:
 //   1: lane 0 stores the other header fields, then a SYSTEM-scope release
 //      (buffer_wbl2 sc0 sc1: the XCD L2's dirty lines, every wave's included,
 //      are written back) and an explicit s_waitcnt vmcnt(0) — inline asm, so
