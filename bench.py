@@ -47,7 +47,7 @@ N, DIM, M, K_TOP, STEP, PARALLEL, F = 1_000_000, 128, 32, 10, 20, 3, 8
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 METRIC = "private queries/sec + PIR-scan HBM GB/s, SIFT1M d=128 at 1/2/4/8 GPUs"
 PREP_KERNELS = ["prep_offsets", "prep_fold", "prep_repl", "l2_rows"]
-STEP_KERNELS = ["step", "hint_match", "resolve", "gather", "answer"]   # timed in the measured region too
+STEP_KERNELS = ["step", "hint_match", "resolve", "match_resolve", "gather", "answer"]   # timed in the measured region too
 KERNELS = PREP_KERNELS + STEP_KERNELS
 PROFILE_QUERIES = 8
 SESSIONS = 256  # client sessions per GPU (128: 9.9K q/s, 256: 11.0K, 384: 11.5K, 512: 11.3K)
@@ -57,7 +57,8 @@ SYMBOLS = {"prep_fold": "void pm::k_prep_fold_pipe<4, 1, 4, 1>(pm::PmPart const*
                         "unsigned long const*, unsigned int, unsigned int, unsigned int, unsigned int, unsigned int)",
            "answer": None, "step": "void pm::k_step<2>(pm::PmStep)", "resolve": "void pm::k_resolve<true>(pm::PmStep)",
            "hint_match": "pm::k_match(pm::PmStep)", "prep_offsets": "pm::k_prep_offsets(pm::PmPart const*)",
-           "gather": "void pm::k_gather<2>(pm::PmStep)"}
+           "gather": "void pm::k_gather<2>(pm::PmStep)",
+           "match_resolve": "void pm::k_match_resolve<4>(pm::PmStep)"}
 # the server answer of search-sized shapes: the small-LDS instance with
 # PM_ANSWER_NT threads per workgroup (pm_query.hip step_answer; 0: generic)
 ANSWER_NT = int(os.environ.get("PM_ANSWER_NT", "128"))
@@ -213,7 +214,7 @@ def batch_pir_msmarco(ctx, with_cpu: bool):
             "frac": round(ach / HBM_PEAK_GBS, 4), "avg_ms": round(ms / n, 5), "launches": n,
             "alg_bytes_per_launch": by / n,
             "kernel_avg_us": {k: round(v[1] / v[0] * 1e3, 3) for k, v in
-                              ((k, clients[0].ctx.timing_get(k)) for k in ("hint_match", "resolve", "answer")) if v[0]}}
+                              ((k, clients[0].ctx.timing_get(k)) for k in ("hint_match", "resolve", "match_resolve", "answer")) if v[0]}}
         attach_traffic(out["clients_grouped"]["roofline"], SYMBOLS["answer"], C2_CLIENTS * C2_B * ANSWER_BLOCK)
     del grp, clients
     if with_cpu:
@@ -281,7 +282,8 @@ def private_search_msmarco(local, args, with_cpu: bool):
     def tsum(name):
         r = [c.timing_get(name) for c in ctxs]
         return tuple(sum(x[i] for x in r) for i in range(3))
-    kt = {k: tsum(k) for k in ("prep_offsets", "prep_fold", "prep_repl", "hint_match", "resolve", "answer")}
+    kt = {k: tsum(k) for k in ("prep_offsets", "prep_fold", "prep_repl", "hint_match", "resolve", "match_resolve",
+                                "answer")}
     preps = [s_.PIR.stats()["PrepCount"] for s_ in sess]
     tq = qs[:, MS_WARMUP:].reshape(-1, MS_DIM)
     gt = pm.knn(v, tq, K_TOP, ctx)
@@ -745,7 +747,7 @@ def main():
         one.PIR.Preprocessing()
         one.ctx.timing(False)
         isolated = {"sessions": gsz, "queries_each": PROFILE_QUERIES, "kernel_avg_us": {}}
-        for k in ("hint_match", "resolve", "answer"):
+        for k in ("hint_match", "resolve", "match_resolve", "answer"):
             n, ms, by = grp[0].ctx.timing_get(k)
             if n:
                 isolated["kernel_avg_us"][k] = round(ms / n * 1e3, 3)

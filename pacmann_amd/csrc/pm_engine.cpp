@@ -174,14 +174,23 @@ struct pm_ctx {
   // after the step's last kernel, with a system-scope release, so that once
   // hipEventQuery reports it, every result byte the step wrote into pinned
   // memory is visible to the host (HIP event semantics; the header tokens
-  // alone give no such order).  done_tok: the last token whose event was seen
-  // complete, so one worker queries the runtime and the others read an atomic.
+  // alone give no such order).  One worker queries the runtime, the others read
+  // an atomic.
+  // Steps of several engines (or a session's own steps beside its group's)
+  // can share one context, so completions are counted per context: record_done
+  // returns the step's sequence number (counted after the record), done_seen
+  // is the highest one known complete.  A later record of the event covers
+  // the earlier steps of the stream.
   // PM_PUBLISH_WAIT=0: the token + row-hash acceptance alone (diagnostics).
   bool publish_wait = true;
   hipEvent_t done_ev = nullptr;
-  std::atomic<uint32_t> done_tok{0};
+  std::atomic<uint64_t> done_rec{0}, done_seen{0};
   std::mutex done_mu;
-  void record_done(hipStream_t st) { if (publish_wait) (void)hipEventRecord(done_ev, st); }
+  uint64_t record_done(hipStream_t st) {
+    if (!publish_wait) return 0;
+    (void)hipEventRecord(done_ev, st);
+    return done_rec.fetch_add(1) + 1;
+  }
   std::string last_kernel;
   // host-side wall-clock accumulators ("host_*" names in pm_timing_get)
   uint64_t host_n[HT_COUNT] = {};
@@ -326,6 +335,7 @@ struct Engine {
   double prepTime = 0, storage = 0, commOn = 0, commOff = 0;
 
   std::shared_ptr<DevBuf> db = std::make_shared<DevBuf>();   // server DB; shared by the clients of pm_batchpir_create_client
+  std::shared_ptr<DevBuf> img = std::make_shared<DevBuf>();  // the DB's fold image (pmk::fold_image), shared likewise
   DevBuf zero16, parts_d, owned_d, tag, pp, parity, ridx, rval, hist, fqn, arena, tab, tabT, cur, done, gran;
   uint32_t gran_words = 0;
   std::vector<uint32_t> owned_list;   // owned partitions in order (owned_d holds their PmPart)
@@ -334,6 +344,7 @@ struct Engine {
   std::vector<double> stamp_sum;   // PM_STAMPS builds: accumulated phase deltas
   uint64_t stamp_n = 0;
   uint32_t step_token = 0;         // PmStep::token of the last step
+  uint64_t step_seq = 0;           // its completion sequence number (pm_ctx::record_done)
   size_t pf_off = 0, pf_len = ~size_t(0);   // bytes of each result row the caller reads next
   bool rows_partial = false;   // this call's caller reads ONLY those bytes (GetVertexInfo): the rest is not sent
   HostBuf desc_h, out_h, err_h, src_h;   // src_h: pm_batchpir_query_dev's row pointers
@@ -487,6 +498,28 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(ctx->stream));
   }
+  // the fold image: a second copy of the owned partitions' rows, laid out for
+  // k_prep_fold_rot (CS 512 shapes only)
+  uint64_t off_img = 0;
+  if (!g->owned_list.empty() && pmk::fold_image_ok(g->minCS, g->maxCS, (uint32_t)g->E)) {
+    for (uint32_t i : g->owned_list) {
+      PmPart& d = g->parts[i].d;
+      d.img = (const uint64_t*)(uintptr_t)off_img;
+      off_img += pmk::fold_image_words(d.SS, (uint32_t)g->E);
+    }
+    if (server) {
+      g->img = server->img;
+    } else {
+      CHK(g->img->reserve(off_img * 8));
+      for (uint32_t i : g->owned_list) {
+        const PmPart& d = g->parts[i].d;
+        pmk::fold_image(ctx->stream, g->img->as<uint64_t>() + (uintptr_t)d.img, g->db->as<uint64_t>() + d.row0 * g->E,
+                        d.N, d.SS, (uint32_t)g->E);
+      }
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipStreamSynchronize(ctx->stream));
+    }
+  }
   CHK(g->tag.reserve(off_tag * 4));
   CHK(g->pp.reserve(off_pp * 4));
   CHK(g->parity.reserve(off_par * 8));
@@ -527,6 +560,7 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
     d.tabT = g->tabT.as<uint16_t>() + (uintptr_t)d.tabT;
     d.tab = g->tab.as<uint16_t>() + (uintptr_t)d.tab;
     d.cur = g->cur.as<uint16_t>() + (uintptr_t)d.cur;
+    d.img = off_img ? g->img->as<uint64_t>() + (uintptr_t)d.img : nullptr;
   }
   HIPCHK(hipMemsetAsync(g->fqn.p, 0, g->P * 4, ctx->stream));
   HIPCHK(hipMemsetAsync(g->hist.p, 0, off_hist * 4, ctx->stream));
@@ -598,7 +632,7 @@ static int engine_prep_launch(pm_ctx* c, const Engine* g, const PmPart* dp, int 
     }
   } else {
     c->timed("prep_fold", fold, [&] { pmk::prep_fold(st, dp, np, g->maxH, g->db->as<uint64_t>(), (uint32_t)g->E, g->minCS, g->maxCS,
-                                               g->zero16.as<uint64_t>(), clients); });
+                                               g->zero16.as<uint64_t>(), clients, g->img->p != nullptr); });
     c->timed("prep_repl", repl, [&] { pmk::prep_repl(st, dp, np, g->maxRepl, g->db->as<uint64_t>(), (uint32_t)g->E); });
   }
   HIPCHK(hipGetLastError());
@@ -643,14 +677,16 @@ static inline double ms_since(Clock::time_point t) {
 // a bug), fall back to the stream synchronisation, which reports errors.
 // sc: the context whose stream ran the step (its done_ev); c: the one whose
 // counters are charged (a session of a shared step, or sc itself).
-static int wait_done(pm_ctx* sc, uint32_t token) {
-  if (sc->done_tok.load(std::memory_order_acquire) == token) return 0;
+static int wait_done(pm_ctx* sc, uint64_t seq) {
+  if (sc->done_seen.load(std::memory_order_acquire) >= seq) return 0;
   auto t0 = Clock::now();
   for (uint64_t spin = 0;; ++spin) {
-    if (sc->done_tok.load(std::memory_order_acquire) == token) return 0;
-    if (sc->done_mu.try_lock()) {   // one waiter asks the runtime; the others read done_tok
+    if (sc->done_seen.load(std::memory_order_acquire) >= seq) return 0;
+    if (sc->done_mu.try_lock()) {   // one waiter asks the runtime; the others read done_seen
       std::lock_guard<std::mutex> lk(sc->done_mu, std::adopt_lock);
-      if (sc->done_tok.load(std::memory_order_acquire) == token) return 0;
+      if (sc->done_seen.load(std::memory_order_acquire) >= seq) return 0;
+      // every step counted so far was recorded before this query
+      const uint64_t rec = sc->done_rec.load(std::memory_order_acquire);
       for (uint64_t k = 0;; ++k) {
         const hipError_t e = hipEventQuery(sc->done_ev);
         if (e == hipSuccess) break;
@@ -661,7 +697,9 @@ static int wait_done(pm_ctx* sc, uint32_t token) {
           break;
         }
       }
-      sc->done_tok.store(token, std::memory_order_release);
+      uint64_t prev = sc->done_seen.load(std::memory_order_relaxed);
+      while (prev < rec && !sc->done_seen.compare_exchange_weak(prev, rec, std::memory_order_release)) {}
+      if (rec < seq) return fail(PM_EHIP, "step completion: waited for a step that was not recorded");
       return 0;
     }
     if ((spin & 0xffff) == 0xffff && ms_since(t0) > 10000.0) return fail(PM_EHIP, "step completion wait timed out");
@@ -669,10 +707,10 @@ static int wait_done(pm_ctx* sc, uint32_t token) {
 }
 
 static int wait_step(pm_ctx* c, const PmOutHdr* hdr, uint32_t nsub, uint32_t token, const char* rows,
-                     size_t row_bytes, size_t pf_off, size_t pf_len, pm_ctx* sc = nullptr) {
+                     size_t row_bytes, size_t pf_off, size_t pf_len, uint64_t seq, pm_ctx* sc = nullptr) {
   if (!sc) sc = c;
   hipStream_t stream = sc->stream;
-  const bool ordered = sc->publish_wait && sc->done_ev;
+  const bool ordered = sc->publish_wait && sc->done_ev && seq;
   const size_t w0 = pf_off / 8, w1 = (pf_off + pf_len + 7) / 8;
   auto row_hash = [&](uint32_t s) {
     const volatile uint64_t* rw = (const volatile uint64_t*)(rows + s * row_bytes);
@@ -720,7 +758,7 @@ static int wait_step(pm_ctx* c, const PmOutHdr* hdr, uint32_t nsub, uint32_t tok
     }
     if (ordered) {
       auto td = Clock::now();
-      CHK(wait_done(sc, token));
+      CHK(wait_done(sc, seq));
       if (c->timing) c->host_add(HT_WAIT_DONE, ms_since(td));
     }
     std::atomic_thread_fence(std::memory_order_acquire);
@@ -743,7 +781,7 @@ static int wait_and_post(Engine* g, const PmStep& S, uint32_t nsub, Clock::time_
   const uint64_t E = g->E;
   auto t_wait = Clock::now();
   CHK(wait_step(c, S.hdr_h, nsub, S.token, (const char*)S.rows_h, E * 8, (size_t)S.pf_w0 * 8,
-                (size_t)(S.pf_w1 - S.pf_w0) * 8));
+                (size_t)(S.pf_w1 - S.pf_w0) * 8, g->step_seq));
   c->host_add(HT_STEP_WAIT, ms_since(t_wait));
 
   if (c->verify_rows) {   // diagnostics: what the host saw at token time vs after the stream drains
@@ -927,7 +965,7 @@ static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
     S.stamps = g->stamps.as<uint64_t>();
 #endif
     c->timed_ext("step", ans_bytes, [&](pmk::PmEvents ev) { pmk::step_fused(st, S, ev); }, 2);
-    c->record_done(st);
+    g->step_seq = c->record_done(st);
     HIPCHK(hipGetLastError());
     c->host_add(HT_STEP_LAUNCH, ms_since(t_begin));
     CHK(wait_and_post(g, S, nsub, t_begin));
@@ -974,7 +1012,7 @@ static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
     c->timed_ext("gather", ans_bytes, [&](pmk::PmEvents ev) { pmk::step_gather(st, S, ev); }, 2);
   }
   c->timed_ext("answer", S.nsplit > 1 ? 0 : ans_bytes, [&](pmk::PmEvents ev) { pmk::step_answer(st, S, g->maxSS, ev); }, 2);
-  c->record_done(st);
+  g->step_seq = c->record_done(st);
   HIPCHK(hipGetLastError());
   c->host_add(HT_STEP_LAUNCH, ms_since(t_begin));
   return wait_and_post(g, S, nsub, t_begin);
@@ -1998,6 +2036,7 @@ struct StepGroup {
   DevBuf parts_d, subs_d, sb_d, bits, cand, meta, spec, res_d, ans, part_x, done, prep_parts, desc_d, stamps;
   HostBuf desc_h, out_h;
   uint32_t token = 0, pf_w0 = 0, pf_w1 = 0;
+  uint64_t seq = 0;   // the last shared step's completion sequence number (pm_ctx::record_done)
   std::vector<PmSub> subs;
   std::vector<uint32_t> sb, base;
   std::vector<uint64_t> gen;   // each session's Engine::prep_gen at the last upload of its parts
@@ -2104,6 +2143,10 @@ static int group_step(StepGroup& G, const std::vector<char>& in) {
   }
   S.subs = G.subs_d.as<PmSub>();
   S.sb = G.sb_d.as<uint32_t>();
+  if (!(nsub <= kArgSubs && np <= kArgParts)) {   // the DMA'd descriptor is the device copy
+    S.subs = const_cast<PmSub*>(S.subs_h);
+    S.sb = const_cast<uint32_t*>(S.sb_h);
+  }
   S.bits = G.bits.as<uint64_t>();
   S.cand = G.cand.as<uint32_t>();
   S.meta = G.meta.as<uint32_t>();
@@ -2136,9 +2179,13 @@ static int group_step(StepGroup& G, const std::vector<char>& in) {
   auto t0 = Clock::now();
   uint32_t nreal = 0;
   for (auto& x : G.subs) nreal += x.kind == SUB_REAL;
-  c->timed_ext("hint_match", (double)nreal * G.maxPH, [&](pmk::PmEvents ev) { pmk::step_match(st, S, G.maxPH, ev); }, 2);
   const bool lds = pmk::step_resolve_lds_ok(G.maxPH, max_per_part);
-  c->timed_ext("resolve", 0, [&](pmk::PmEvents ev) { pmk::step_resolve(st, S, lds, ev); }, 2);
+  if (pmk::step_match_resolve_ok(S, lds)) {   // one launch: match + resolve per partition
+    c->timed_ext("match_resolve", (double)nreal * G.maxPH, [&](pmk::PmEvents ev) { pmk::step_match_resolve(st, S, ev); }, 2);
+  } else {
+    c->timed_ext("hint_match", (double)nreal * G.maxPH, [&](pmk::PmEvents ev) { pmk::step_match(st, S, G.maxPH, ev); }, 2);
+    c->timed_ext("resolve", 0, [&](pmk::PmEvents ev) { pmk::step_resolve(st, S, lds, ev); }, 2);
+  }
   S.nsplit = c->no_split ? 1 : pmk::step_gather_split(G.maxSS, nsub);
   if (S.nsplit > 1) {
     CHK(G.part_x.reserve((uint64_t)nsub * S.nsplit * (G.E & ~3u) * 8));
@@ -2156,7 +2203,7 @@ static int group_step(StepGroup& G, const std::vector<char>& in) {
   }
 #endif
   c->timed_ext("answer", S.nsplit > 1 ? 0 : ans_bytes, [&](pmk::PmEvents ev) { pmk::step_answer(st, S, G.maxSS, ev); }, 2);
-  c->record_done(st);
+  G.seq = c->record_done(st);
   HIPCHK(hipGetLastError());
 #ifdef PM_ANSWER_STAMPS
   if (stamp_this) {
@@ -2188,7 +2235,7 @@ static int group_collect(StepGroup& G, uint32_t s) {
   uint64_t* rows = (uint64_t*)(G.out_h.as<char>() + G.subs.size() * sizeof(PmOutHdr));
   auto t_wait = Clock::now();
   CHK(wait_step(e->ctx, hdr + G.base[s], n, G.token, (const char*)(rows + (uint64_t)G.base[s] * G.E),
-                (size_t)G.E * 8, (size_t)G.pf_w0 * 8, (size_t)(G.pf_w1 - G.pf_w0) * 8, G.c));
+                (size_t)G.E * 8, (size_t)G.pf_w0 * 8, (size_t)(G.pf_w1 - G.pf_w0) * 8, G.seq, G.c));
   e->ctx->host_add(HT_STEP_WAIT, ms_since(t_wait));
   auto tp = Clock::now();
   post_results(e, hdr, rows, n, G.base[s], G.token);

@@ -79,6 +79,11 @@ struct PmPart {
   // several clients' steps share one launch (pm_search_loop_batched); null:
   // the step's PmStep::q
   const PM_G float* qv;
+  // The partition's fold image (server-side, built once with the DB; null
+  // where k_prep_fold_rot does not apply): per 32-B column slice s and group
+  // of 4 chunks b, the 64 KB LDS image k_prep_fold_rot stages, line k =
+  // row k of chunks 4b..4b+3 (rows past N zero).  pmk::fold_image_words.
+  const PM_G uint64_t* img;
 };
 
 // tabT layout: chunk c of tag t at tile (c / 8, t), element c % 8 (16-B tiles of
@@ -188,14 +193,23 @@ void prep_init(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxH, 
 void prep_offsets(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxH, uint32_t maxSS);
 // dparts: `clients` clients of each partition, partition-major (nparts = partitions x clients)
 void prep_fold(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxH, const uint64_t* db,
-               uint32_t E, uint32_t minCS, uint32_t maxCS, const uint64_t* zero16, uint32_t clients = 1);
+               uint32_t E, uint32_t minCS, uint32_t maxCS, const uint64_t* zero16, uint32_t clients = 1,
+               bool have_img = false);
 void prep_repl(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxRepl,
                const uint64_t* db, uint32_t E);
+// The bank-rotated fold's DB image (CS 512, even E, E >= 4): whether it applies,
+// its size per partition (words) and the build of one partition's image.
+bool fold_image_ok(uint32_t minCS, uint32_t maxCS, uint32_t E);
+uint64_t fold_image_words(uint32_t SS, uint32_t E);
+void fold_image(hipStream_t st, uint64_t* img, const uint64_t* part_rows, uint64_t N, uint32_t SS, uint32_t E);
 // Timing events carried by a launch's own dispatch packet (null: untimed)
 struct PmEvents { hipEvent_t a = nullptr, b = nullptr; };
 void step_match(hipStream_t st, const PmStep& S, uint32_t maxPH, PmEvents ev = {});
 uint32_t step_match_blocks(uint32_t maxPH);   // k_match workgroups per sub-query
 void step_resolve(hipStream_t st, const PmStep& S, bool lds, PmEvents ev = {});
+// k_match_part + k_resolve fused (batched serving; descriptor already in device memory)
+bool step_match_resolve_ok(const PmStep& S, bool lds);
+void step_match_resolve(hipStream_t st, const PmStep& S, PmEvents ev = {});
 // k_step: match, resolve and answer in one launch (descriptor in the kernel
 // arguments, <= 64 sub-queries and <= 8192 hints per partition, <= 256 workgroups)
 bool step_fused_ok(const PmStep& S, uint32_t maxPH, uint32_t max_sub_per_part);

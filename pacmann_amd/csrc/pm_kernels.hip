@@ -6,6 +6,9 @@
 namespace pm {
 
 
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
 __device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
   return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
 }
@@ -365,6 +368,157 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_pipe(const PmPart* _
   }
 }
 
+// Bank-rotated fold for CS = 512 (same result as k_prep_fold): a workgroup
+// owns (partition, 32-B column slice, group of <= 5,120 hints), one hint per
+// lane slot (5 per lane), and folds the slice of every chunk into its hints'
+// parities, like k_prep_fold_pipe.  What differs is how a chunk reaches LDS
+// and is read there.  k_prep_fold_pipe has each lane read its hint's 32-B row
+// with ds_read_b128: random rows land on random bank slots, ~3 rows pile up
+// per slot in a 16-lane group, and the LDS array bounds the fold.  Here four
+// chunks are staged side by side: LDS line k (128 B = the 32 banks of
+// ds_read_b32) holds row k of chunks 4b..4b+3, one 32-B slot each.  In a
+// 32-lane group, lane 8s + j reads chunk slot (s + phase) & 3 and, at step t,
+// word (j + t) & 7 of its row: the 32 lanes touch 32 distinct banks whatever
+// rows their hints select, so every ds_read_b32 takes its minimum 2 LDS
+// cycles.  Accumulator t of a lane always holds word (j + t) & 7 of its slice
+// (XOR order does not matter) and is stored there at the end.
+// The staged bytes come from the partition's fold image (PmPart::img: the
+// same 64 KB LDS image per (slice, 4 chunks), contiguous, rows past N zero),
+// a second, server-side copy of the DB laid out for this kernel (640 MB for
+// SIFT1M: HBM capacity traded for whole-line sequential staging instead of
+// 32-B pieces at 640-B stride).  Hint offsets come from the tag-major table
+// (tabT: 8 chunks in 16 B per tag; hint h's initial tag is h).
+// Two buffers of (CS + 1) lines (line CS is zero: kSkip), 128.3 KB.
+#ifndef PM_ROT_HPL
+#define PM_ROT_HPL 5
+#endif
+#ifndef PM_ROT_ABL
+#define PM_ROT_ABL 0   // diagnostic builds: 1 = no LDS reads, 2 = no staging in the loop
+#endif
+constexpr int kRotHPL = PM_ROT_HPL;   // hints per lane (SIFT1M's 12,512 hints: 3 groups of 4,171)
+constexpr uint32_t kRotCS = 512, kRotBufBytes = kRotCS * 128;   // one image block per (slice, 4 chunks)
+template <int CS>
+__global__ void __launch_bounds__(kFoldThreads) k_prep_fold_rot(const PmPart* __restrict__ parts, uint32_t E,
+                                                                uint32_t ngmax, uint32_t nsl, uint32_t npg,
+                                                                uint32_t K) {
+  constexpr uint32_t LINE = 32, BUFW = (CS + 1) * LINE;
+  // static (not extern) LDS: its address is a constant the reads fold into
+  // their offsets
+  __shared__ __attribute__((aligned(16))) uint32_t rot_lds[2 * BUFW];
+  constexpr uint32_t ITEMS = CS * 8;   // 16-B staging items per buffer (4 chunks x CS rows x 2)
+  static_assert(ITEMS % kFoldThreads == 0, "whole staging items per thread");
+  constexpr uint32_t G = ITEMS / kFoldThreads;
+  // XCD-aware order of k_prep_fold_pipe (workgroups b and b + 8 share an
+  // XCD): pg = (partition, hint group) runs on XCD pg % 8; there, groups of 4
+  // slices of the K clients follow each other.  (Client-major order, all
+  // clients of one slice back to back, measured 10-15 % slower in 64-client
+  // launches.)
+  constexpr uint32_t LW = 4;
+  const uint32_t ngl = (nsl + LW - 1) / LW, per_pg = K * ngl * LW;
+  const uint32_t xcd = blockIdx.x % 8, kq = blockIdx.x / 8;
+  const uint32_t pg = xcd + 8 * (kq / per_pg), r = kq % per_pg;
+  const uint32_t client = (r / LW) % K, slice = (r / (K * LW)) * LW + r % LW;
+  if (pg >= npg || slice >= nsl) return;   // block-uniform
+  const PmPart& P = parts[(pg / ngmax) * K + client];
+  const uint32_t H = P.H, SS = P.SS, tid = threadIdx.x;
+  const uint32_t ng = (H + kFoldThreads * kRotHPL - 1) / (kFoldThreads * kRotHPL);
+  const uint32_t grp = pg % ngmax;
+  if (grp >= ng) return;   // block-uniform
+  const uint32_t hb = (H + ng - 1) / ng, h0 = grp * hb, h1 = min(H, h0 + hb);
+  const uint32_t w = slice * 4, nbuf = SS / 4;   // SetSize is a multiple of 4 (pir.go:497)
+  const PM_G char* img = (const PM_G char*)P.img + (uint64_t)slice * nbuf * kRotBufBytes;
+  const PM_G uint16_t* tabT = P.tabT;
+  const uint32_t lane = tid & 63, j = lane & 7, ks = (lane >> 3) & 3;
+  const uint32_t hl = h0 + tid;   // hint of lane slot k: hl + k * kFoldThreads
+  uint32_t acc[kRotHPL][8];
+#pragma unroll
+  for (int k = 0; k < kRotHPL; ++k)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc[k][t] = 0;
+  const uint32_t wave_item0 = tid & ~63u;
+  auto stage = [&](uint32_t b, uint32_t buf) {   // one contiguous 64 KB block of the image
+    uint32_t* L = rot_lds + buf * BUFW;
+    const PM_G char* src = img + (uint64_t)b * kRotBufBytes;
+#pragma unroll
+    for (uint32_t i = 0; i < G; ++i)
+      __builtin_amdgcn_global_load_lds((g_cvoid_t*)(src + (tid + i * kFoldThreads) * 16u),
+                                       (lds_void_t*)(L + (i * kFoldThreads + wave_item0) * 4), 16, 0, 0);
+  };
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  auto load_tab = [&](uint32_t b, u32x2* out) {   // chunks 4b .. 4b+3 of each hint: 8 B of its tabT tile
+#pragma unroll
+    for (int k = 0; k < kRotHPL; ++k)
+      out[k] = *reinterpret_cast<const PM_G u32x2*>(
+          (const PM_G char*)tabT + (uint32_t)tabT_index(H, min(hl + k * kFoldThreads, H - 1), 4 * b) * 2u);
+  };
+  for (uint32_t x = tid; x < 2 * LINE; x += kFoldThreads) rot_lds[(x / LINE) * BUFW + CS * LINE + x % LINE] = 0;
+  u32x2 tv[kRotHPL], tn[kRotHPL];
+  stage(0, 0);
+  load_tab(0, tv);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const char* lds0 = reinterpret_cast<const char*>(rot_lds);
+  for (uint32_t b = 0; b < nbuf; ++b) {
+    if (b + 1 < nbuf) { if (PM_ROT_ABL != 2) stage(b + 1, (b + 1) & 1); load_tab(b + 1, tn); }
+    const uint32_t lb = (b & 1) * BUFW * 4;   // byte offset of this buffer
+    // per phase: this lane's chunk slot and its word base in the line
+    uint32_t cso[4];
+#pragma unroll
+    for (uint32_t ph = 0; ph < 4; ++ph) cso[ph] = lb + ((ks + ph) & 3) * 32 + 4 * j;
+#pragma unroll
+    for (int k = 0; k < (PM_ROT_ABL == 1 ? 0 : kRotHPL); ++k) {
+      const bool hv = hl + k * kFoldThreads < h1;   // lane slots past the group: zero line
+      // the 4 offsets in phase order: rotate the 64-bit tile right by 16 ks
+      const uint64_t t64 = ((uint64_t)tv[k].y << 32) | tv[k].x;
+      const uint32_t sh = 16 * ks;
+      const uint64_t rot = sh ? ((t64 >> sh) | (t64 << (64 - sh))) : t64;
+      uint32_t v[4][8];
+#pragma unroll
+      for (uint32_t ph = 0; ph < 4; ++ph) {
+        uint32_t o = (uint32_t)(rot >> (16 * ph)) & 0xffffu;
+        o = hv ? min(o, (uint32_t)CS) : (uint32_t)CS;   // kSkip -> the zero line
+        // word (j + t) & 7 of the slot: base + 4t, or base + 4t - 32 where
+        // j + t >= 8 (a per-lane select; 4t is the instruction's offset)
+        const uint32_t a = o * (LINE * 4) + cso[ph], a2 = a - 32;
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+          v[ph][t] = *reinterpret_cast<const uint32_t*>(lds0 + ((j < 8u - t) ? a : a2) + 4 * t);
+      }
+#pragma unroll
+      for (int t = 0; t < 8; ++t)   // v_bitop3_b32 0x96 = a ^ b ^ c (gfx950): two XORs per instruction
+        acc[k][t] = xor3(xor3(acc[k][t], v[0][t], v[1][t]), v[2][t], v[3][t]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kRotHPL; ++k) tv[k] = tn[k];
+  }
+#pragma unroll
+  for (int k = 0; k < kRotHPL; ++k) {
+    if ((hl + k * kFoldThreads) >= h1) continue;
+    PM_G uint32_t* dst = reinterpret_cast<PM_G uint32_t*>(P.parity + (uint64_t)(hl + k * kFoldThreads) * E + w);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) dst[(j + t) & 7] = acc[k][t];
+    if (w == 0)   // xorSlices leaves the words past len&~3 zero
+      for (uint32_t t = E & ~3u; t < E; ++t) P.parity[(uint64_t)(hl + k * kFoldThreads) * E + t] = 0;
+  }
+}
+
+// One partition's fold image: 16-B item it of block (slice s, chunks 4b..) =
+// line it / 8, chunk slot (it / 2) % 4, half it % 2 of row (4b + slot)*512 + line.
+__global__ void __launch_bounds__(kBlock) k_fold_image(uint4* __restrict__ img, const uint64_t* __restrict__ rows,
+                                                      uint64_t N, uint32_t nbuf, uint32_t E, uint64_t nitems) {
+  for (uint64_t x = (uint64_t)blockIdx.x * kBlock + threadIdx.x; x < nitems; x += (uint64_t)gridDim.x * kBlock) {
+    const uint32_t it = (uint32_t)(x % (kRotCS * 8));
+    const uint64_t blk = x / (kRotCS * 8);
+    const uint32_t b = (uint32_t)(blk % nbuf), s = (uint32_t)(blk / nbuf);
+    const uint64_t r = (uint64_t)(4 * b + ((it >> 1) & 3)) * kRotCS + (it >> 3);
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (r < N) v = *reinterpret_cast<const uint4*>(rows + r * E + 4 * s + (it & 1) * 2);
+    img[x] = v;
+  }
+}
+
 // Replacement rows (pir.go:345-350): Qpc random offsets per chunk, idx + copy.
 __global__ void __launch_bounds__(kBlock) k_prep_repl(const PmPart* __restrict__ parts,
                                                       const uint64_t* __restrict__ db, uint32_t E) {
@@ -611,8 +765,19 @@ void prep_offsets(hipStream_t st, const PmPart* d, int np, uint32_t maxH, uint32
   hipLaunchKernelGGL(k_prep_offsets, dim3(cdiv(maxH, kOffsBlock), cdiv(maxSS, kOffsChunksPerBlock), np),
                      dim3(kOffsBlock), 0, st, d);
 }
+bool fold_image_ok(uint32_t minCS, uint32_t maxCS, uint32_t E) {
+  static const bool rot = [] { const char* e = getenv("PM_FOLD_ROT"); return !e || e[0] != '0'; }();
+  return rot && minCS == kRotCS && maxCS == kRotCS && E % 2 == 0 && E >= 4;
+}
+uint64_t fold_image_words(uint32_t SS, uint32_t E) { return (uint64_t)(E / 4) * (SS / 4) * (kRotBufBytes / 8); }
+void fold_image(hipStream_t st, uint64_t* img, const uint64_t* rows, uint64_t N, uint32_t SS, uint32_t E) {
+  const uint64_t nitems = fold_image_words(SS, E) / 2;
+  unsigned grid = cdiv(nitems, kBlock);
+  if (grid > 256 * 32) grid = 256 * 32;
+  hipLaunchKernelGGL(k_fold_image, dim3(grid), dim3(kBlock), 0, st, (uint4*)img, rows, N, SS / 4, E, nitems);
+}
 void prep_fold(hipStream_t st, const PmPart* d, int np, uint32_t maxH, const uint64_t* db, uint32_t E,
-               uint32_t minCS, uint32_t maxCS, const uint64_t* zero16, uint32_t clients) {
+               uint32_t minCS, uint32_t maxCS, const uint64_t* zero16, uint32_t clients, bool have_img) {
   const uint32_t EX = E & ~3u;
   if (EX == 0) {
     hipLaunchKernelGGL(k_prep_fold<2>, dim3(cdiv((uint64_t)maxH * E, kBlock), np), dim3(kBlock), 0,
@@ -645,6 +810,12 @@ void prep_fold(hipStream_t st, const PmPart* d, int np, uint32_t maxH, const uin
 #ifndef PM_FOLD_D512
 #define PM_FOLD_D512 1
 #endif
+    if (have_img && fold_image_ok(minCS, maxCS, E)) {   // the bank-rotated fold (same slices and block order)
+      const uint32_t ngr = cdiv(maxH, (uint64_t)kFoldThreads * kRotHPL), npgr = (np / K) * ngr;
+      hipLaunchKernelGGL(k_prep_fold_rot<512>, dim3(cdiv(npgr, 8) * 8 * per_pg), dim3(kFoldThreads), 0, st, d, E,
+                         ngr, nsl, npgr, K);
+      return;
+    }
     const uint32_t nb = maxCS == 512 ? PM_FOLD_NB512 : 3;   // LDS buffers: <= 150 KB
     const size_t lds = (size_t)nb * ((maxCS + 1) * psw + kPipeTabWords) * 8;
     const dim3 grid(cdiv(npg, 8) * 8 * per_pg), blk(kFoldThreads);

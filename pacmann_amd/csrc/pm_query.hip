@@ -367,9 +367,9 @@ __global__ void __launch_bounds__(kBlock) k_match(PmStep S) {
     __shared__ PmSub s_sub;
     if (threadIdx.x == 0) {
       s_sub = S.subs_h[s];
-      if (blockIdx.x == 0) S.subs[s] = s_sub;
+      if (blockIdx.x == 0 && S.subs != S.subs_h) S.subs[s] = s_sub;
     }
-    if (blockIdx.x == 0 && s == 0)
+    if (blockIdx.x == 0 && s == 0 && S.sb != S.sb_h)
       for (uint32_t i = threadIdx.x; i <= S.np; i += kBlock) S.sb[i] = S.sb_h[i];
     __syncthreads();
     sub = s_sub;
@@ -396,48 +396,49 @@ __global__ void __launch_bounds__(kBlock) k_match(PmStep S) {
 #ifndef PM_MATCHPART_G
 #define PM_MATCHPART_G 6
 #endif
-template <int HPT>
-__global__ void __launch_bounds__(kBlock, PM_MATCHPART_WAVES) k_match_part(PmStep S) {
-  constexpr int NT = kBlock, G = PM_MATCHPART_G;
-  __shared__ uint32_t s_cand[G][NT / 64][6];
-  const uint32_t p = blockIdx.y, blk = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint32_t pb0 = desc_sb(S, p), pn = desc_sb(S, p + 1) - pb0;
-  if (!S.args_valid && blk == 0) {   // stage the descriptor for the later kernels
-    for (uint32_t i = tid; i < pn; i += NT) S.subs[pb0 + i] = S.subs_h[pb0 + i];
-    if (p == 0)
-      for (uint32_t i = tid; i <= S.np; i += NT) S.sb[i] = S.sb_h[i];
+// k_resolve's predictions for sub-queries k = k0, k0 + kstep, ... of a
+// partition (one wave each): the chunk's QueryHistogram, the predicted
+// in-chunk index and the PRF values the refreshed hints would need.
+__device__ __forceinline__ void match_part_predict(const PmStep& S, const PmPart& P, uint32_t pb0, uint32_t pn,
+                                                   uint32_t k0, uint32_t kstep) {
+  if (pn > kSpecSubs) return;
+  const uint32_t lane = threadIdx.x & 63, lg = P.log2CS;
+  for (uint32_t k = k0; k < pn; k += kstep) {
+    PmSub sub = desc_sub(S, pb0 + k);
+    sub.kind = __builtin_amdgcn_readfirstlane(sub.kind);
+    if (sub.kind != SUB_REAL) continue;
+    const bool live = sub.idx < P.N;
+    const uint32_t chunk = (uint32_t)(sub.idx >> lg);
+    const uint32_t h0k = live ? P.hist[chunk] : 0;
+    PmSub st;
+    bool validt;
+    const uint32_t sing = predict_ing(S, P, pb0, pn, k, chunk, h0k, st, validt);
+    const uint32_t cht = (uint32_t)(st.idx >> lg);
+    const uint32_t pred = (live && sing < P.Qpc && chunk < P.SS) ? P.PH + chunk * P.Qpc + sing : kNone;
+    uint32_t v = kSkip;
+    if (lane < pn && lane > k && validt && cht < P.SS && pred != kNone) v = P.tab[(uint64_t)cht * P.H + pred];
+    const uint64_t s = pb0 + k;
+    if (lane < pn) S.spec[s * kSpecSubs + lane] = v;
+    if (lane == 0) { S.meta[2 * s] = h0k; S.meta[2 * s + 1] = sing; }
   }
-  if (pn == 0) return;
-  const PmPart P = S.parts[p];
+}
+
+// Hints [blk * NT * HPT, +NT * HPT) of partition p against each of its pn
+// sub-queries: the match bits and each sub-query's first two matches with
+// their tag and program point (the block's record in S.cand).  `tid` is the
+// thread's index in its team of NT threads; a workgroup may run several
+// teams side by side on different blocks (k_match_resolve), so every barrier
+// here is reached by the whole workgroup: a team whose block lies past PH
+// (`act` false) runs the same loop and barriers without loads or stores.
+template <int HPT, int NT, int G>
+__device__ __forceinline__ void match_part_block(const PmStep& S, const PmPart& P, uint32_t pb0, uint32_t pn,
+                                                 uint32_t blk, uint32_t tid, uint32_t (&s_cand)[G][NT / 64][6]) {
+  const uint32_t lane = tid & 63, wave = tid >> 6;
   const uint32_t base = blk * NT * HPT;
-  if (base >= P.PH) return;
+  const bool act = base < P.PH;   // team-uniform
   const uint32_t mask = P.CS - 1, lg = P.log2CS;
-  // k_resolve's predictions for every real sub-query, one wave each, spread
-  // over the partition's hint blocks (sub-query k: block k % nb, wave k / nb)
-  const uint32_t nb = (P.PH + NT * HPT - 1) / (NT * HPT);
-  if (pn <= kSpecSubs) {
-    for (uint32_t k = blk + nb * wave; k < pn; k += nb * (NT / 64)) {
-      PmSub sub = desc_sub(S, pb0 + k);
-      sub.kind = __builtin_amdgcn_readfirstlane(sub.kind);
-      if (sub.kind != SUB_REAL) continue;
-      const bool live = sub.idx < P.N;
-      const uint32_t chunk = (uint32_t)(sub.idx >> lg);
-      const uint32_t h0k = live ? P.hist[chunk] : 0;
-      PmSub st;
-      bool validt;
-      const uint32_t sing = predict_ing(S, P, pb0, pn, k, chunk, h0k, st, validt);
-      const uint32_t cht = (uint32_t)(st.idx >> lg);
-      const uint32_t pred = (live && sing < P.Qpc && chunk < P.SS) ? P.PH + chunk * P.Qpc + sing : kNone;
-      uint32_t v = kSkip;
-      if (lane < pn && lane > k && validt && cht < P.SS && pred != kNone) v = P.tab[(uint64_t)cht * P.H + pred];
-      const uint64_t s = pb0 + k;
-      if (lane < pn) S.spec[s * kSpecSubs + lane] = v;
-      if (lane == 0) { S.meta[2 * s] = h0k; S.meta[2 * s + 1] = sing; }
-    }
-  }
   for (uint32_t j0 = 0; j0 < pn; j0 += G) {
-    uint32_t kind[G], chk[G], off[G];
-    bool lv[G];
+    uint32_t kind[G], off[G];
     uint16_t rv[G][HPT];
     // each sub-query's search-row values of this block's hints (contiguous
     // u16: 2 B per hint; a hint matches iff its value is the offset, see
@@ -449,19 +450,19 @@ __global__ void __launch_bounds__(kBlock, PM_MATCHPART_WAVES) k_match_part(PmSte
       kind[g] = __builtin_amdgcn_readfirstlane(sub.kind);
       const uint64_t idx = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(sub.idx >> 32)) << 32) |
                            __builtin_amdgcn_readfirstlane((uint32_t)sub.idx);
-      lv[g] = kind[g] == SUB_REAL && idx < P.N;
-      chk[g] = (uint32_t)(idx >> lg);
+      const bool lv = act && kind[g] == SUB_REAL && idx < P.N;
+      const uint32_t chk = (uint32_t)(idx >> lg);
       off[g] = (uint32_t)(idx & mask);
-      const PM_G uint16_t* crow = P.cur + (uint64_t)chk[g] * P.PH;
+      const PM_G uint16_t* crow = P.cur + (uint64_t)chk * P.PH;
 #pragma unroll
       for (int u = 0; u < HPT; ++u) {
         const uint32_t h = base + u * NT + tid;
-        rv[g][u] = (lv[g] && h < P.PH) ? crow[h] : kSkip;
+        rv[g][u] = (lv && h < P.PH) ? crow[h] : kSkip;
       }
     }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      if (j0 + g >= pn || kind[g] != SUB_REAL) continue;   // uniform
+      if (!act || j0 + g >= pn || kind[g] != SUB_REAL) continue;   // team-uniform
       const uint64_t s = pb0 + j0 + g;
       uint32_t h0 = kNone, t0 = 0, p0 = 0, h1 = kNone, t1 = 0, p1 = 0;   // wave-uniform
 #pragma unroll
@@ -489,7 +490,7 @@ __global__ void __launch_bounds__(kBlock, PM_MATCHPART_WAVES) k_match_part(PmSte
       }
     }
     __syncthreads();
-    if (tid < (uint32_t)G && j0 + tid < pn) {   // merge each sub-query's wave pairs
+    if (act && tid < (uint32_t)G && j0 + tid < pn) {   // merge each sub-query's wave pairs
       const uint32_t g = tid;
       const PmSub sub = desc_sub(S, pb0 + j0 + g);
       if (sub.kind == SUB_REAL) {
@@ -510,6 +511,27 @@ __global__ void __launch_bounds__(kBlock, PM_MATCHPART_WAVES) k_match_part(PmSte
     }
     if (j0 + G < pn) __syncthreads();
   }
+}
+
+template <int HPT>
+__global__ void __launch_bounds__(kBlock, PM_MATCHPART_WAVES) k_match_part(PmStep S) {
+  constexpr int NT = kBlock, G = PM_MATCHPART_G;
+  __shared__ uint32_t s_cand[G][NT / 64][6];
+  const uint32_t p = blockIdx.y, blk = blockIdx.x, tid = threadIdx.x, wave = tid >> 6;
+  const uint32_t pb0 = desc_sb(S, p), pn = desc_sb(S, p + 1) - pb0;
+  if (!S.args_valid && blk == 0 && S.subs != S.subs_h) {   // stage the descriptor for the later kernels
+    for (uint32_t i = tid; i < pn; i += NT) S.subs[pb0 + i] = S.subs_h[pb0 + i];
+    if (p == 0)
+      for (uint32_t i = tid; i <= S.np; i += NT) S.sb[i] = S.sb_h[i];
+  }
+  if (pn == 0) return;
+  const PmPart P = S.parts[p];
+  if (blk * NT * HPT >= P.PH) return;
+  // predictions spread over the partition's hint blocks (sub-query k: block
+  // k % nb, wave k / nb)
+  const uint32_t nb = (P.PH + NT * HPT - 1) / (NT * HPT);
+  match_part_predict(S, P, pb0, pn, blk + nb * wave, nb * (NT / 64));
+  match_part_block<HPT, NT, G>(S, P, pb0, pn, blk, tid, s_cand);
 }
 
 // First set bit at position >= start in a sub-query's match bitmask (one wave).
@@ -1165,6 +1187,37 @@ __global__ void __launch_bounds__(LDS ? kBlock : kResolveBlockG) k_resolve(PmSte
   if (L.fin && threadIdx.x == 0) chain_rearm(S);
 }
 
+// k_match_part + k_resolve in one launch, one 512-thread workgroup per
+// partition (batched serving: the resolver's MODE-0 fast prologue, <= 64
+// sub-queries per partition).  The match writes exactly what k_match_part
+// writes (bits, per-block records, predictions) to global memory, two 1,024-
+// hint blocks at a time (two teams of 256 threads), and after a workgroup
+// barrier the same workgroup resolves the partition from them, out of L2.
+// Saves the match kernel's launch and its ~4 workgroups per partition.  The
+// descriptor must already be in device memory (S.subs == S.subs_h): nothing
+// here stages it, as every resolver reads the whole step's sb.
+template <int HPT>
+__global__ void __launch_bounds__(kResolveBlockG) k_match_resolve(PmStep S) {
+  constexpr int NT = kBlock, G = PM_MATCHPART_G, TEAMS = kResolveBlockG / kBlock;
+  __shared__ ResolveLds<0> L;
+  __shared__ uint32_t s_cand[TEAMS][G][NT / 64][6];
+  const uint32_t p = blockIdx.x, tid = threadIdx.x;
+  const uint32_t pb0 = step_sb(S, p), pn = step_sb(S, p + 1) - pb0;
+  if (pn == 0) return;
+  {
+    const PmPart P = S.parts[p];
+    const uint32_t team = tid / NT, ttid = tid % NT;
+    match_part_predict(S, P, pb0, pn, tid >> 6, kResolveBlockG / 64);
+    const uint32_t nb = (P.PH + NT * HPT - 1) / (NT * HPT);
+    for (uint32_t b = 0; b < nb; b += TEAMS)
+      match_part_block<HPT, NT, G>(S, P, pb0, pn, b + team, ttid, s_cand[team]);
+  }
+  __syncthreads();   // the match's global stores, visible to this workgroup's resolver
+  resolve_role<0, kResolveBlockG, false>(S, p, L);
+  __syncthreads();
+  if (L.fin && threadIdx.x == 0) chain_rearm(S);
+}
+
 // L2Dist of the first `dim` floats of an LDS row against q (device), one
 // 8-lane group; bit-exact (see k_l2_rows).  Call with lanes 0..7 of a wave.
 __device__ __forceinline__ float l2_lds(const float* row, const float* __restrict__ q, uint32_t dim) {
@@ -1817,6 +1870,14 @@ void step_match(hipStream_t st, const PmStep& S, uint32_t maxPH, PmEvents ev) {
     PM_LAUNCH(ev, k_match_part<kMatchHints / kBlock>, dim3(step_match_blocks(maxPH), S.np), dim3(kBlock), st, S);
   else
     PM_LAUNCH(ev, k_match, dim3(step_match_blocks(maxPH), S.nsub), dim3(kBlock), st, S);
+}
+bool step_match_resolve_ok(const PmStep& S, bool lds) {
+  static const int mode = [] { const char* e = getenv("PM_MATCH_RESOLVE"); return e ? atoi(e) : 1; }();
+  return mode && !lds && !S.args_valid && S.subs == S.subs_h && S.sb == S.sb_h && S.np >= 128 &&
+         S.nsub >= 4 * S.np;
+}
+void step_match_resolve(hipStream_t st, const PmStep& S, PmEvents ev) {
+  PM_LAUNCH(ev, k_match_resolve<kMatchHints / kBlock>, dim3(S.np), dim3(kResolveBlockG), st, S);
 }
 void step_resolve(hipStream_t st, const PmStep& S, bool lds, PmEvents ev) {
   if (lds) PM_LAUNCH(ev, k_resolve<true>, dim3(S.np), dim3(kBlock), st, S);
