@@ -378,10 +378,11 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_pipe(const PmPart* _
 // chunks are staged side by side: LDS line k (128 B = the 32 banks of
 // ds_read_b32) holds row k of chunks 4b..4b+3, one 32-B slot each.  In a
 // 32-lane group, lane 8s + j reads chunk slot (s + phase) & 3 and, at step t,
-// word (j + t) & 7 of its row: the 32 lanes touch 32 distinct banks whatever
-// rows their hints select, so every ds_read_b32 takes its minimum 2 LDS
-// cycles.  Accumulator t of a lane always holds word (j + t) & 7 of its slice
-// (XOR order does not matter) and is stored there at the end.
+// word (j + t) & 7 of its row (PM_ROT_B64 0): the 32 lanes touch 32 distinct
+// banks whatever rows their hints select, so every ds_read_b32 takes its
+// minimum 2 LDS cycles.  The default reads 8-B pairs ((j & 3) + t) & 3
+// instead (PM_ROT_B64 below).  Accumulator t of a lane always holds the same
+// word of its slice (XOR order does not matter) and is stored there at the end.
 // The staged bytes come from the partition's fold image (PmPart::img: the
 // same 64 KB LDS image per (slice, 4 chunks), contiguous, rows past N zero),
 // a second, server-side copy of the DB laid out for this kernel (640 MB for
@@ -391,6 +392,12 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_pipe(const PmPart* _
 // Two buffers of (CS + 1) lines (line CS is zero: kSkip), 128.3 KB.
 #ifndef PM_ROT_HPL
 #define PM_ROT_HPL 5
+#endif
+#ifndef PM_ROT_B64
+#define PM_ROT_B64 1   // 8-B LDS reads: half the reads and address selects of the 4-B form, at the
+                       // same LDS rate (lanes j and j + 4 share a bank pair when their rows have the
+                       // same parity: 2 cycles per 32-lane group, like ds_read_b32's 2 x 128 B);
+                       // 0.56-0.58 vs 0.68-0.69 ms per SIFT1M client, the fold being VALU-bound
 #endif
 #ifndef PM_ROT_ABL
 #define PM_ROT_ABL 0   // diagnostic builds: 1 = no LDS reads, 2 = no staging in the loop
@@ -464,7 +471,7 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_rot(const PmPart* __
     // per phase: this lane's chunk slot and its word base in the line
     uint32_t cso[4];
 #pragma unroll
-    for (uint32_t ph = 0; ph < 4; ++ph) cso[ph] = lb + ((ks + ph) & 3) * 32 + 4 * j;
+    for (uint32_t ph = 0; ph < 4; ++ph) cso[ph] = lb + ((ks + ph) & 3) * 32 + (PM_ROT_B64 ? 8 * (j & 3) : 4 * j);
 #pragma unroll
     for (int k = 0; k < (PM_ROT_ABL == 1 ? 0 : kRotHPL); ++k) {
       const bool hv = hl + k * kFoldThreads < h1;   // lane slots past the group: zero line
@@ -480,9 +487,18 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_rot(const PmPart* __
         // word (j + t) & 7 of the slot: base + 4t, or base + 4t - 32 where
         // j + t >= 8 (a per-lane select; 4t is the instruction's offset)
         const uint32_t a = o * (LINE * 4) + cso[ph], a2 = a - 32;
+        if (PM_ROT_B64) {   // word pair ((j & 3) + t) & 3: 8-B reads, lanes j and j + 4 2-way on a bank pair
 #pragma unroll
-        for (int t = 0; t < 8; ++t)
-          v[ph][t] = *reinterpret_cast<const uint32_t*>(lds0 + ((j < 8u - t) ? a : a2) + 4 * t);
+          for (int t = 0; t < 4; ++t) {
+            const uint64_t x = *reinterpret_cast<const uint64_t*>(lds0 + (((j & 3) < 4u - t) ? a : a2) + 8 * t);
+            v[ph][2 * t] = (uint32_t)x;
+            v[ph][2 * t + 1] = (uint32_t)(x >> 32);
+          }
+        } else {
+#pragma unroll
+          for (int t = 0; t < 8; ++t)
+            v[ph][t] = *reinterpret_cast<const uint32_t*>(lds0 + ((j < 8u - t) ? a : a2) + 4 * t);
+        }
       }
 #pragma unroll
       for (int t = 0; t < 8; ++t)   // v_bitop3_b32 0x96 = a ^ b ^ c (gfx950): two XORs per instruction
@@ -498,7 +514,8 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_rot(const PmPart* __
     if ((hl + k * kFoldThreads) >= h1) continue;
     PM_G uint32_t* dst = reinterpret_cast<PM_G uint32_t*>(P.parity + (uint64_t)(hl + k * kFoldThreads) * E + w);
 #pragma unroll
-    for (int t = 0; t < 8; ++t) dst[(j + t) & 7] = acc[k][t];
+    for (int t = 0; t < 8; ++t)
+      dst[PM_ROT_B64 ? 2 * (((j & 3) + t / 2) & 3) + (t & 1) : (j + t) & 7] = acc[k][t];
     if (w == 0)   // xorSlices leaves the words past len&~3 zero
       for (uint32_t t = E & ~3u; t < E; ++t) P.parity[(uint64_t)(hl + k * kFoldThreads) * E + t] = 0;
   }
