@@ -64,6 +64,9 @@ static constexpr AesTables kAesTablesHost{};
 static __device__ const AesTables g_aes = kAesTablesHost;
 
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+__device__ __forceinline__ uint32_t aes_x3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
 
 // Fill the replicated table.  Call with the whole block, then __syncthreads().
 __device__ __forceinline__ void aes_lds_init(uint32_t* te, const uint32_t* __restrict__ g_te0) {
@@ -99,10 +102,11 @@ __device__ __forceinline__ void aes_rounds(const AesLane& A, const uint32_t* __r
   for (int r = R0; r < 10; ++r) {
     // Te0[a] ^ rotl8(Te0[b]) ^ rotl16(Te0[c]) ^ rotl24(Te0[d]) ^ rk
     //   = Te0[a] ^ Te2[c] ^ rotl8(Te0[b] ^ Te2[d]) ^ rk
-    uint32_t t0 = A.Tk<0>(s0) ^ A.T2k<2>(s2) ^ rotl32(A.Tk<1>(s1) ^ A.T2k<3>(s3), 8) ^ rk[4 * r + 0];
-    uint32_t t1 = A.Tk<0>(s1) ^ A.T2k<2>(s3) ^ rotl32(A.Tk<1>(s2) ^ A.T2k<3>(s0), 8) ^ rk[4 * r + 1];
-    uint32_t t2 = A.Tk<0>(s2) ^ A.T2k<2>(s0) ^ rotl32(A.Tk<1>(s3) ^ A.T2k<3>(s1), 8) ^ rk[4 * r + 2];
-    uint32_t t3 = A.Tk<0>(s3) ^ A.T2k<2>(s1) ^ rotl32(A.Tk<1>(s0) ^ A.T2k<3>(s2), 8) ^ rk[4 * r + 3];
+    // (v_bitop3_b32 0x96 = three-input XOR on gfx950: 4 VALU per column instead of 5)
+    uint32_t t0 = aes_x3(aes_x3(A.Tk<0>(s0), A.T2k<2>(s2), rk[4 * r + 0]), rotl32(A.Tk<1>(s1) ^ A.T2k<3>(s3), 8), 0u);
+    uint32_t t1 = aes_x3(aes_x3(A.Tk<0>(s1), A.T2k<2>(s3), rk[4 * r + 1]), rotl32(A.Tk<1>(s2) ^ A.T2k<3>(s0), 8), 0u);
+    uint32_t t2 = aes_x3(aes_x3(A.Tk<0>(s2), A.T2k<2>(s0), rk[4 * r + 2]), rotl32(A.Tk<1>(s3) ^ A.T2k<3>(s1), 8), 0u);
+    uint32_t t3 = aes_x3(aes_x3(A.Tk<0>(s3), A.T2k<2>(s1), rk[4 * r + 3]), rotl32(A.Tk<1>(s0) ^ A.T2k<3>(s2), 8), 0u);
     s0 = t0; s1 = t1; s2 = t2; s3 = t3;
   }
 }
