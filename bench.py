@@ -53,8 +53,8 @@ PROFILE_QUERIES = 8
 SESSIONS = 256  # client sessions per GPU (128: 9.9K q/s, 256: 11.0K, 384: 11.5K, 512: 11.3K)
 GROUPS = 4      # lock-step groups (GPU_MAX_HW_QUEUES = 4 hardware queues per process)
 THREADS = 16    # host worker threads of the batched loop (the box gives a GPU 16 host cores)
-SYMBOLS = {"prep_fold": "void pm::k_prep_fold_pipe<4, 1, 4, 1>(pm::PmPart const*, unsigned long const*, "
-                        "unsigned long const*, unsigned int, unsigned int, unsigned int, unsigned int, unsigned int)",
+SYMBOLS = {"prep_fold": "void pm::k_prep_fold_rot<512>(pm::PmPart const*, unsigned int, unsigned int, unsigned int, "
+                        "unsigned int, unsigned int)",
            "answer": None, "step": "void pm::k_step<2>(pm::PmStep)", "resolve": "void pm::k_resolve<true>(pm::PmStep)",
            "hint_match": "pm::k_match(pm::PmStep)", "prep_offsets": "pm::k_prep_offsets(pm::PmPart const*)",
            "gather": "void pm::k_gather<2>(pm::PmStep)",
@@ -519,7 +519,8 @@ def bigann_shard(name, n_entries, layout, shard, rank, ws, local, dist, nccl_gro
 # (graphann_test.go:221-284): N = 1e8 rows of D = 128 uint32, v[i*D+j] = i+j,
 # q[j] = j, the sum of all row products mod 2^32 (closed form 1,178,525,696).
 C0_N, C0_D, C0_SUM, C0_CPU_ROWS = 100_000_000, 128, 1_178_525_696, 1 << 23
-IP_SCAN_SYMBOL = "pm::k_ip_scan(uint4 const*, unsigned long, unsigned int const*, unsigned int, unsigned int*)"
+IP_SCAN_SYMBOL = ("pm::k_ip_scan(HIP_vector_type<unsigned int, 4u> const*, unsigned long, unsigned int const*, "
+                  "unsigned int, unsigned int*)")   # as rocprofv3 names it
 IP_SCAN_GRID = 2048 * 256   # pmk::ip_rows' scan launch: 2,048 workgroups of 256 threads (pm_kernels.hip)
 
 
@@ -821,9 +822,9 @@ def main():
         ach_c = comp / (fold["avg_ms"] / 1e3) / 1e9
         fold["clients_per_launch"] = k
         fold["compulsory"] = {"bytes": comp, "achieved": round(ach_c, 1), "frac": round(ach_c / HBM_PEAK_GBS, 4)}
-        # PMC bytes of launches of this shape (k_prep_fold_pipe<4,1,4>: 2 hint groups x 20 column slices
-        # per partition, 1,024 threads per workgroup)
-        units = 16 * k * -(-(c0["PrimaryHintNum"] + c0["SetSize"] * c0["MaxQueryPerChunk"]) // 7168)
+        # PMC bytes of launches of this shape (k_prep_fold_rot<512>: 3 hint groups of <= 5,120 x 20
+        # column slices per partition, 1,024 threads per workgroup)
+        units = 16 * k * -(-(c0["PrimaryHintNum"] + c0["SetSize"] * c0["MaxQueryPerChunk"]) // 5120)
         attach_traffic(fold, SYMBOLS["prep_fold"], -(-units // 8) * 8 * (E // 4) * 1024)
         fold["note"] = ("fold bytes (hint x chunk entry reads, SURVEY.md §8d) exceed HBM peak because the "
                         "kernel serves them from LDS; 'compulsory' is the DB read once plus the parity writes "
