@@ -7,7 +7,8 @@ d = 128, degree m = 32 graph, k = 10, step = 20, parallel = 3, batch PIR with
 BatchSize = m = 32 (16 partitions) and FailureProbLog2 = 8, exactly the
 private-search.go harness (run-private-search.sh flags).  Data are synthetic
 (no dataset in the image): a clustered SIFT-like mixture with integer values in
-[0,255] and a uniform random degree-32 graph (private-search.go:54-69).
+[0,255] and a degree-32 graph built on the GPU (exact kNN + robustPrune; --graph
+random: the reference's genRandomGraph, private-search.go:54-69).
 
 Serving: one GPU serves S client sessions at once (--sessions, default 256).
 Every session is a full PianoPIR client (own keys, hint state, cache,
