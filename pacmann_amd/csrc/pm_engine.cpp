@@ -353,6 +353,7 @@ struct Engine {
   ~Engine() { if (dev_ev) (void)hipEventDestroy(dev_ev); }
   std::vector<PartHost> parts;
   uint32_t maxH = 0, maxPH = 0, maxSS = 0, maxRepl = 0, maxCS = 0, minCS = ~0u;
+  bool ph8 = true;   // every owned partition's PH is a multiple of 8 (16-B hint search rows)
 
   // per-step host view
   std::vector<PmSub> subs;
@@ -466,6 +467,7 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
     g->maxCS = std::max(g->maxCS, ph.d.CS);
     g->minCS = std::min(g->minCS, ph.d.CS);
     g->maxPH = std::max(g->maxPH, ph.d.PH);
+    g->ph8 = g->ph8 && ph.d.PH % 8 == 0;
     g->maxSS = std::max(g->maxSS, ph.d.SS);
     g->maxRepl = std::max(g->maxRepl, ph.d.SS * ph.d.Qpc);
     // carve offsets (elements)
@@ -2033,6 +2035,7 @@ struct SpinBarrier {
 struct StepGroup {
   pm_ctx* c = nullptr;   // the shared steps' stream
   uint32_t S = 0, P = 0, maxPH = 0, maxSS = 0, E = 0, dim = 0;
+  bool ph8 = false;
   DevBuf parts_d, subs_d, sb_d, bits, cand, meta, spec, res_d, ans, part_x, done, prep_parts, desc_d, stamps;
   HostBuf desc_h, out_h;
   uint32_t token = 0, pf_w0 = 0, pf_w1 = 0;
@@ -2073,7 +2076,7 @@ static int group_init(StepGroup& G, pm_ctx* c) {
   G.c = c;
   G.S = (uint32_t)G.es.size();
   const Engine& e = *G.es[0];
-  G.P = (uint32_t)e.P; G.maxPH = e.maxPH; G.maxSS = e.maxSS; G.E = (uint32_t)e.E;
+  G.P = (uint32_t)e.P; G.maxPH = e.maxPH; G.ph8 = e.ph8; G.maxSS = e.maxSS; G.E = (uint32_t)e.E;
   HIPCHK(hipSetDevice(c->device));
   CHK(G.parts_d.reserve((size_t)G.S * G.P * sizeof(PmPart)));
   CHK(G.done.reserve(4 * (3 + 65536)));
@@ -2181,7 +2184,7 @@ static int group_step(StepGroup& G, const std::vector<char>& in) {
   for (auto& x : G.subs) nreal += x.kind == SUB_REAL;
   const bool lds = pmk::step_resolve_lds_ok(G.maxPH, max_per_part);
   if (pmk::step_match_resolve_ok(S, lds)) {   // one launch: match + resolve per partition
-    c->timed_ext("match_resolve", (double)nreal * G.maxPH, [&](pmk::PmEvents ev) { pmk::step_match_resolve(st, S, ev); }, 2);
+    c->timed_ext("match_resolve", (double)nreal * G.maxPH, [&](pmk::PmEvents ev) { pmk::step_match_resolve(st, S, G.ph8, G.maxPH, max_per_part, ev); }, 2);
   } else {
     c->timed_ext("hint_match", (double)nreal * G.maxPH, [&](pmk::PmEvents ev) { pmk::step_match(st, S, G.maxPH, ev); }, 2);
     c->timed_ext("resolve", 0, [&](pmk::PmEvents ev) { pmk::step_resolve(st, S, lds, ev); }, 2);

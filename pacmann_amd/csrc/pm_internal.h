@@ -209,7 +209,9 @@ uint32_t step_match_blocks(uint32_t maxPH);   // k_match workgroups per sub-quer
 void step_resolve(hipStream_t st, const PmStep& S, bool lds, PmEvents ev = {});
 // k_match_part + k_resolve fused (batched serving; descriptor already in device memory)
 bool step_match_resolve_ok(const PmStep& S, bool lds);
-void step_match_resolve(hipStream_t st, const PmStep& S, PmEvents ev = {});
+// ph8: every partition's PH is a multiple of 8
+void step_match_resolve(hipStream_t st, const PmStep& S, bool ph8, uint32_t maxPH, uint32_t max_sub_per_part,
+                        PmEvents ev = {});
 // k_step: match, resolve and answer in one launch (descriptor in the kernel
 // arguments, <= 64 sub-queries and <= 8192 hints per partition, <= 256 workgroups)
 bool step_fused_ok(const PmStep& S, uint32_t maxPH, uint32_t max_sub_per_part);

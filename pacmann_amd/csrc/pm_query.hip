@@ -577,6 +577,31 @@ __device__ __forceinline__ uint32_t find_next_g(const PmStep& S, uint64_t sub, u
   return kNone;
 }
 
+// The same from the hint search rows (k_match_resolve_s, which keeps no match
+// bits): the first primary hint h >= start whose search-row value in `chunk`
+// is `off`, against the state at the start of the step (nothing writes cur
+// before the step's k_answer).  One wave, 8 hints per lane (PH % 8 == 0).
+__device__ __forceinline__ uint32_t find_cur(const PmPart& P, uint32_t chunk, uint32_t off, uint32_t start) {
+  const uint32_t lane = threadIdx.x & 63;
+  const PM_G uint16_t* row = P.cur + (uint64_t)chunk * P.PH;
+  for (uint32_t h0 = start & ~7u; h0 < P.PH; h0 += 512) {
+    const uint32_t h = h0 + lane * 8;
+    uint32_t f = kNone;
+    if (h < P.PH) {
+      const uint4 v = *reinterpret_cast<const PM_G uint4*>(row + h);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int e = 7; e >= 0; --e) {
+        const uint32_t val = (w[e >> 1] >> (16 * (e & 1))) & 0xffffu;
+        if (val == off && h + e >= start) f = h + e;
+      }
+    }
+    const uint64_t m = __ballot(f != kNone);
+    if (m) return __builtin_amdgcn_readlane(f, (uint32_t)__builtin_ctzll(m));
+  }
+  return kNone;
+}
+
 // Minimum over the wave of a per-lane candidate.
 __device__ __forceinline__ uint32_t wave_min(uint32_t x) {
 #pragma unroll
@@ -593,7 +618,7 @@ constexpr int kMaxSubPerPart = 256;
 // nw <= 128 match words, one match record per sub-query).
 template <int MODE>
 struct ResolveLds {
-  static constexpr int NS = MODE == 2 ? kSpecSubs : kMaxSubPerPart;
+  static constexpr int NS = MODE >= 2 ? kSpecSubs : kMaxSubPerPart;
   static constexpr bool STG = MODE == 1;
   static constexpr uint32_t NB = kLdsBitWords;
   uint64_t s_idx[NS];
@@ -660,17 +685,20 @@ __device__ __forceinline__ void resolve_role(const PmStep& S, uint32_t p, Resolv
   // program points or match bits; two independent chains of two round trips
   // (MODE 0, partitions too large to stage: the same from global memory,
   // the match records read ten blocks at a time)
-  const bool fast = MODE == 2 || (MODE == 1 && n <= kSpecSubs && nw <= 128) || (MODE == 0 && n <= kSpecSubs);
+  // (MODE 3: k_match_resolve_s filled the fast prologue's LDS itself)
+  const bool fast = MODE >= 2 || (MODE == 1 && n <= kSpecSubs && nw <= 128) || (MODE == 0 && n <= kSpecSubs);
   // match bits, tags and program points: LDS-staged by the staged prologue,
   // read from global memory on the (rare) paths of the fast one that need them
   const bool staged = MODE == 1 && !fast;
   auto find_bits = [&](uint32_t j, uint32_t start) -> uint32_t {
+    if constexpr (MODE == 3) return find_cur(P, s_chunk[j], (uint32_t)(s_idx[j] & mask), start);
     if (staged) return find_next(bits_l + (uint64_t)j * nw, nw, start);
     return find_next_g<GRAN>(S, b0 + j, nw, start);
   };
   auto tag_of = [&](uint32_t h) -> uint32_t { return staged ? tag_l[h] : P.tag[h]; };
   auto pp_of = [&](uint32_t h) -> uint32_t { return staged ? pp_l[h] : P.pp[h]; };
-  if (fast) {
+  if (MODE == 3) {
+  } else if (fast) {
     constexpr uint32_t NFW = NT / 64 - 1;   // candidate waves; the last wave predicts
     if (wave < NFW) {
       // first two stale candidates of each real sub-query, with their tag and
@@ -751,7 +779,7 @@ __device__ __forceinline__ void resolve_role(const PmStep& S, uint32_t p, Resolv
       }
       if (lane == 0) s_fqn = fq;
     }
-  } else if constexpr (MODE != 2) {
+  } else if constexpr (MODE < 2) {
     // --- phase 0: prefetch sub-queries, counters, match bits, tags ------------
     // Every global load of the staging is issued before the first LDS store:
     // the kernel is latency-bound, so one round trip instead of one per item.
@@ -1037,7 +1065,7 @@ __device__ __forceinline__ void resolve_role(const PmStep& S, uint32_t p, Resolv
     STAMP(40);
     return;
   }
-  if constexpr (MODE != 2) {
+  if constexpr (MODE < 2) {
   // --- phase 2 (n > 64): the sequential chain of Client.Query calls, on wave 0
   // The chain state lives in plain LDS arrays: lane 0 writes, every lane of the
   // same wave reads in a later iteration (LDS instructions of one wave complete
@@ -1214,6 +1242,141 @@ __global__ void __launch_bounds__(kResolveBlockG) k_match_resolve(PmStep S) {
   }
   __syncthreads();   // the match's global stores, visible to this workgroup's resolver
   resolve_role<0, kResolveBlockG, false>(S, p, L);
+  __syncthreads();
+  if (L.fin && threadIdx.x == 0) chain_rearm(S);
+}
+
+// k_match_resolve for the search-sized shapes (<= 64 sub-queries per
+// partition, PH % 8 == 0 and PH <= 8 * 512 * NU: SIFT1M's 3,584 and MS-MARCO's
+// 7,168 hints): one 512-thread workgroup per partition, and the match in ONE
+// round trip.  Every thread loads the 8 * NU contiguous search-row values
+// (PmPart::cur, 16-B loads) of its hints for every sub-query of a group of G,
+// all in flight together; each wave's first two matches (hint order = lane
+// order) come out of a ballot, and the resolver's fast prologue is filled in
+// LDS directly: no match bits, records or predictions pass through global
+// memory (the rare third candidate is re-read from cur, find_cur).  The last
+// wave reads the requests, QueryHistogram and FinishedQueryNum and makes the
+// predictions of resolve_role's staged prologue (in-chunk index, re-evaluation
+// values) meanwhile.  Results are identical to k_match_resolve's.
+template <int NU>
+__global__ void __launch_bounds__(kResolveBlockG) k_match_resolve_s(PmStep S) {
+  constexpr int NT = kResolveBlockG, NW = NT / 64, G = 8 / NU;
+  __shared__ ResolveLds<3> L;
+  __shared__ uint32_t s_m[kSpecSubs][NU][NW][2];   // each (sub-query, row block, wave): first two matches
+  const uint32_t p = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t b0 = step_sb(S, p), n = step_sb(S, p + 1) - b0;
+  if (n == 0) return;
+  const PmPart P = S.parts[p];
+  const uint32_t lg = P.log2CS, mask = P.CS - 1;
+  if (wave == NW - 1) {
+    // requests, counters and predictions (resolve_role's staged prologue, from global memory)
+    const uint32_t k = lane;
+    PmSub sub{0, SUB_NONE, 0};
+    if (k < n) sub = step_sub(S, b0 + k);
+    const bool real = k < n && sub.kind == SUB_REAL;
+    const uint64_t idx = k < n ? sub.idx : ~0ull;
+    const uint32_t ch = k < n ? (uint32_t)(sub.idx >> lg) : kNone;
+    const uint32_t h0 = (real && sub.idx < P.N) ? P.hist[ch] : 0;
+    const uint32_t fq = lane == 0 ? *P.fqn : 0;
+    bool first = real;   // not a repeat of an earlier real sub-query
+    for (uint32_t t = 0; t + 1 < n; ++t) {
+      const uint64_t it = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(idx >> 32), t) << 32) |
+                          __builtin_amdgcn_readlane((uint32_t)idx, t);
+      const bool rt = __builtin_amdgcn_readlane(real ? 1u : 0u, t) != 0;
+      if (k > t && rt && it == idx) first = false;
+    }
+    uint32_t ing = h0;
+    for (uint32_t q = 0; q + 1 < n; ++q) {
+      const bool fq2 = __builtin_amdgcn_readlane(first ? 1u : 0u, q) != 0;
+      const uint32_t cq = __builtin_amdgcn_readlane(ch, q);
+      if (k > q && fq2 && cq == ch) ++ing;
+    }
+    for (uint32_t e0 = 0; e0 < n * n; e0 += 64) {   // uniform: every lane joins the shuffles
+      const uint32_t e = e0 + lane, kk = (e / n) & 63, j = e % n;
+      const uint32_t sk = __shfl(ing, kk), ck = __shfl(ch, kk), cj = __shfl(ch, j);
+      const bool rk = __shfl(real ? 1u : 0u, kk) != 0, rj = __shfl(real ? 1u : 0u, j) != 0;
+      if (e < n * n && kk < j && rk && rj && ck < P.SS && cj < P.SS && sk < P.Qpc)
+        L.spec_v[kk * kSpecSubs + j] = P.tab[(uint64_t)cj * P.H + P.PH + ck * P.Qpc + sk];
+    }
+    if (k < n) {
+      L.s_kind[k] = sub.kind; L.s_idx[k] = sub.idx; L.s_chunk[k] = ch; L.s_st[k] = kNone;
+      L.s_hist0[k] = h0; L.s_sing[k] = ing;
+    }
+    if (lane == 0) L.s_fqn = fq;
+  }
+  // the match: sub-queries j0 .. j0 + G - 1 at a time
+  for (uint32_t j0 = 0; j0 < n; j0 += G) {
+    uint32_t off[G];
+    uint4 v[G][NU];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      PmSub sub{0, SUB_NONE, 0};
+      if (j0 + g < n) sub = step_sub(S, b0 + j0 + g);
+      const uint32_t kind = __builtin_amdgcn_readfirstlane(sub.kind);
+      const uint64_t idx = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(sub.idx >> 32)) << 32) |
+                           __builtin_amdgcn_readfirstlane((uint32_t)sub.idx);
+      const bool lv = kind == SUB_REAL && idx < P.N;
+      off[g] = lv ? (uint32_t)(idx & mask) : kNone;
+      const PM_G uint16_t* crow = P.cur + (uint64_t)(lv ? (uint32_t)(idx >> lg) : 0u) * P.PH;
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const uint32_t h = (u * NT + tid) * 8;
+        v[g][u] = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);   // kSkip x 8
+        if (lv && h < P.PH) v[g][u] = *reinterpret_cast<const PM_G uint4*>(crow + h);
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (j0 + g >= n) break;   // uniform
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const uint32_t w[4] = {v[g][u].x, v[g][u].y, v[g][u].z, v[g][u].w};
+        uint32_t bm = 0;   // this lane's 8 hints that match, bit e = hint (u * NT + tid) * 8 + e
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          bm |= (((w[e >> 1] >> (16 * (e & 1))) & 0xffffu) == off[g] ? 1u : 0u) << e;
+        uint64_t b = __ballot(bm != 0);
+        uint32_t a0 = kNone, a1 = kNone;
+        if (b) {
+          const uint32_t l0 = (uint32_t)__builtin_ctzll(b);
+          const uint32_t hb = (u * NT + wave * 64) * 8;
+          uint32_t m0 = __builtin_amdgcn_readlane(bm, l0);
+          a0 = hb + l0 * 8 + (uint32_t)__builtin_ctz(m0);
+          m0 &= m0 - 1;
+          if (m0) {
+            a1 = hb + l0 * 8 + (uint32_t)__builtin_ctz(m0);
+          } else {
+            b &= b - 1;
+            if (b) {
+              const uint32_t l1 = (uint32_t)__builtin_ctzll(b);
+              a1 = hb + l1 * 8 + (uint32_t)__builtin_ctz(__builtin_amdgcn_readlane(bm, l1));
+            }
+          }
+        }
+        if (lane == 0) { s_m[j0 + g][u][wave][0] = a0; s_m[j0 + g][u][wave][1] = a1; }
+      }
+    }
+  }
+  __syncthreads();
+  if (wave == 0 && lane < n) {
+    // each sub-query's first two matches in hint order, with their tag and program point
+    const uint32_t j = lane;
+    uint32_t c1 = kNone, c2 = kNone, t1 = 0, p1 = 0, t2 = 0, p2 = 0;
+    if (L.s_kind[j] == SUB_REAL) {
+      for (int u = 0; u < NU && c2 == kNone; ++u)
+        for (int w = 0; w < NW && c2 == kNone; ++w)
+          for (int i = 0; i < 2; ++i) {
+            const uint32_t h = s_m[j][u][w][i];
+            if (h == kNone || c2 != kNone) continue;
+            if (c1 == kNone) c1 = h; else c2 = h;
+          }
+      if (c1 != kNone) { t1 = P.tag[c1]; p1 = P.pp[c1]; }
+      if (c2 != kNone) { t2 = P.tag[c2]; p2 = P.pp[c2]; }
+    }
+    L.s_c1[j] = c1; L.s_c2[j] = c2; L.s_t1[j] = t1; L.s_p1[j] = p1; L.s_t2[j] = t2; L.s_p2[j] = p2;
+  }
+  __syncthreads();
+  resolve_role<3, kResolveBlockG, false>(S, p, L);
   __syncthreads();
   if (L.fin && threadIdx.x == 0) chain_rearm(S);
 }
@@ -1876,8 +2039,17 @@ bool step_match_resolve_ok(const PmStep& S, bool lds) {
   return mode && !lds && !S.args_valid && S.subs == S.subs_h && S.sb == S.sb_h && S.np >= 128 &&
          S.nsub >= 4 * S.np;
 }
-void step_match_resolve(hipStream_t st, const PmStep& S, PmEvents ev) {
-  PM_LAUNCH(ev, k_match_resolve<kMatchHints / kBlock>, dim3(S.np), dim3(kResolveBlockG), st, S);
+void step_match_resolve(hipStream_t st, const PmStep& S, bool ph8, uint32_t maxPH, uint32_t max_sub_per_part,
+                        PmEvents ev) {
+  // the one-round-trip form where its shapes hold (PM_MATCH_RESOLVE=2: always the general one)
+  static const int mode = [] { const char* e = getenv("PM_MATCH_RESOLVE"); return e ? atoi(e) : 1; }();
+  const bool small = mode == 1 && max_sub_per_part <= kSpecSubs && ph8;
+  if (small && maxPH <= 8u * kResolveBlockG)
+    PM_LAUNCH(ev, k_match_resolve_s<1>, dim3(S.np), dim3(kResolveBlockG), st, S);
+  else if (small && maxPH <= 16u * kResolveBlockG)
+    PM_LAUNCH(ev, k_match_resolve_s<2>, dim3(S.np), dim3(kResolveBlockG), st, S);
+  else
+    PM_LAUNCH(ev, k_match_resolve<kMatchHints / kBlock>, dim3(S.np), dim3(kResolveBlockG), st, S);
 }
 void step_resolve(hipStream_t st, const PmStep& S, bool lds, PmEvents ev) {
   if (lds) PM_LAUNCH(ev, k_resolve<true>, dim3(S.np), dim3(kBlock), st, S);
