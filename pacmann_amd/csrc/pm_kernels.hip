@@ -399,8 +399,14 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_pipe(const PmPart* _
                        // same parity: 2 cycles per 32-lane group, like ds_read_b32's 2 x 128 B);
                        // 0.56-0.58 vs 0.68-0.69 ms per SIFT1M client, the fold being VALU-bound
 #endif
+#ifndef PM_ROT_B128
+#define PM_ROT_B128 1   // 16-B reads of the two halves of a row's 32-B slot: half the reads of the 8-B form
+                        // and one v_perm per (hint, chunk) for its offset instead of a 64-bit rotation
+#endif
 #ifndef PM_ROT_ABL
-#define PM_ROT_ABL 0   // diagnostic builds: 1 = no LDS reads, 2 = no staging in the loop
+#define PM_ROT_ABL 0   // diagnostic builds: 1 = no LDS reads, 2 = no staging in the loop, 3 = one row per
+                       // wave (no bank conflicts), 4 = 2 and 3, 5 = no fold work at all (B128 form), 6 = 4 without
+                       // the tabT loads in the loop
 #endif
 constexpr int kRotHPL = PM_ROT_HPL;   // hints per lane (SIFT1M's 12,512 hints: 3 groups of 4,171)
 constexpr uint32_t kRotCS = 512, kRotBufBytes = kRotCS * 128;   // one image block per (slice, 4 chunks)
@@ -435,7 +441,14 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_rot(const PmPart* __
   const uint32_t w = slice * 4, nbuf = SS / 4;   // SetSize is a multiple of 4 (pir.go:497)
   const PM_G char* img = (const PM_G char*)P.img + (uint64_t)slice * nbuf * kRotBufBytes;
   const PM_G uint16_t* tabT = P.tabT;
+#if PM_ROT_B128
+  // 16-B reads: lane l reads chunk slot (s + phase) & 3, halves f then f ^ 1
+  // (s = l & 3, f = (l >> 2) & 1: every ds_read_b128 lane group of 16 holds
+  // each (slot, half) twice, MI355X_MICROARCH.md §LDS)
+  const uint32_t lane = tid & 63, j = (lane >> 2) & 1, ks = lane & 3;
+#else
   const uint32_t lane = tid & 63, j = lane & 7, ks = (lane >> 3) & 3;
+#endif
   const uint32_t hl = h0 + tid;   // hint of lane slot k: hl + k * kFoldThreads
   uint32_t acc[kRotHPL][8];
 #pragma unroll
@@ -454,9 +467,11 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_rot(const PmPart* __
   typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
   auto load_tab = [&](uint32_t b, u32x2* out) {   // chunks 4b .. 4b+3 of each hint: 8 B of its tabT tile
 #pragma unroll
-    for (int k = 0; k < kRotHPL; ++k)
+    for (int k = 0; k < kRotHPL; ++k) {
       out[k] = *reinterpret_cast<const PM_G u32x2*>(
           (const PM_G char*)tabT + (uint32_t)tabT_index(H, min(hl + k * kFoldThreads, H - 1), 4 * b) * 2u);
+      if (PM_ROT_B128 && hl + k * kFoldThreads >= h1) out[k] = u32x2{0xffffffffu, 0xffffffffu};   // kSkip: zero line
+    }
   };
   for (uint32_t x = tid; x < 2 * LINE; x += kFoldThreads) rot_lds[(x / LINE) * BUFW + CS * LINE + x % LINE] = 0;
   u32x2 tv[kRotHPL], tn[kRotHPL];
@@ -466,8 +481,37 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_rot(const PmPart* __
   __syncthreads();
   const char* lds0 = reinterpret_cast<const char*>(rot_lds);
   for (uint32_t b = 0; b < nbuf; ++b) {
-    if (b + 1 < nbuf) { if (PM_ROT_ABL != 2) stage(b + 1, (b + 1) & 1); load_tab(b + 1, tn); }
+    if (b + 1 < nbuf) { if (PM_ROT_ABL != 2 && PM_ROT_ABL < 4) stage(b + 1, (b + 1) & 1); if (PM_ROT_ABL != 6) load_tab(b + 1, tn); }
     const uint32_t lb = (b & 1) * BUFW * 4;   // byte offset of this buffer
+#if PM_ROT_B128
+    {
+      uint32_t cso[4], psel[4];
+#pragma unroll
+      for (uint32_t ph = 0; ph < 4; ++ph) {
+        const uint32_t sl = (ks + ph) & 3;
+        cso[ph] = lb + sl * 32 + 16 * j;
+        psel[ph] = 0x0c0c0000u | ((2 * sl + 1) << 8) | (2 * sl);   // v_perm: tile word sl, zero-extended
+      }
+#pragma unroll
+      for (int k = 0; k < (PM_ROT_ABL == 5 ? 0 : kRotHPL); ++k) {
+        uint32_t v[4][8];
+#pragma unroll
+        for (uint32_t ph = 0; ph < 4; ++ph) {
+          uint32_t o = min(__builtin_amdgcn_perm(tv[k].y, tv[k].x, psel[ph]), (uint32_t)CS);   // kSkip -> zero line
+          if (PM_ROT_ABL == 3 || PM_ROT_ABL == 4 || PM_ROT_ABL == 6) o = __builtin_amdgcn_readfirstlane(o);   // one row per wave: no conflicts
+          const uint32_t a = o * (LINE * 4) + cso[ph];
+          const uint4 x0 = *reinterpret_cast<const uint4*>(lds0 + a);
+          const uint4 x1 = *reinterpret_cast<const uint4*>(lds0 + (a ^ 16u));
+          v[ph][0] = x0.x; v[ph][1] = x0.y; v[ph][2] = x0.z; v[ph][3] = x0.w;
+          v[ph][4] = x1.x; v[ph][5] = x1.y; v[ph][6] = x1.z; v[ph][7] = x1.w;
+        }
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc[k][t] = xor3(xor3(acc[k][t], v[0][t], v[1][t]), v[2][t], v[3][t]);
+      }
+    }
+    if (false)
+#endif
+    {
     // per phase: this lane's chunk slot and its word base in the line
     uint32_t cso[4];
 #pragma unroll
@@ -504,10 +548,11 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_rot(const PmPart* __
       for (int t = 0; t < 8; ++t)   // v_bitop3_b32 0x96 = a ^ b ^ c (gfx950): two XORs per instruction
         acc[k][t] = xor3(xor3(acc[k][t], v[0][t], v[1][t]), v[2][t], v[3][t]);
     }
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < kRotHPL; ++k) tv[k] = tn[k];
+    for (int k = 0; k < kRotHPL; ++k) tv[k] = PM_ROT_ABL == 6 ? tv[k] + u32x2{1u, 3u} : tn[k];
   }
 #pragma unroll
   for (int k = 0; k < kRotHPL; ++k) {
@@ -515,7 +560,8 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_rot(const PmPart* __
     PM_G uint32_t* dst = reinterpret_cast<PM_G uint32_t*>(P.parity + (uint64_t)(hl + k * kFoldThreads) * E + w);
 #pragma unroll
     for (int t = 0; t < 8; ++t)
-      dst[PM_ROT_B64 ? 2 * (((j & 3) + t / 2) & 3) + (t & 1) : (j + t) & 7] = acc[k][t];
+      dst[PM_ROT_B128 ? 4 * (j ^ (t >> 2)) + (t & 3)
+                      : PM_ROT_B64 ? 2 * (((j & 3) + t / 2) & 3) + (t & 1) : (j + t) & 7] = acc[k][t];
     if (w == 0)   // xorSlices leaves the words past len&~3 zero
       for (uint32_t t = E & ~3u; t < E; ++t) P.parity[(uint64_t)(hl + k * kFoldThreads) * E + t] = 0;
   }
