@@ -2036,7 +2036,7 @@ struct StepGroup {
   pm_ctx* c = nullptr;   // the shared steps' stream
   uint32_t S = 0, P = 0, maxPH = 0, maxSS = 0, E = 0, dim = 0;
   bool ph8 = false;
-  DevBuf parts_d, subs_d, sb_d, bits, cand, meta, spec, res_d, ans, part_x, done, prep_parts, desc_d, stamps;
+  DevBuf parts_d, subs_d, sb_d, bits, cand, meta, spec, res_d, ans, part_x, done, prep_parts, desc_d, stamps, qset;
   HostBuf desc_h, out_h;
   uint32_t token = 0, pf_w0 = 0, pf_w1 = 0;
   uint64_t seq = 0;   // the last shared step's completion sequence number (pm_ctx::record_done)
@@ -2183,13 +2183,18 @@ static int group_step(StepGroup& G, const std::vector<char>& in) {
   uint32_t nreal = 0;
   for (auto& x : G.subs) nreal += x.kind == SUB_REAL;
   const bool lds = pmk::step_resolve_lds_ok(G.maxPH, max_per_part);
+  S.nsplit = c->no_split ? 1 : pmk::step_gather_split(G.maxSS, nsub);
+  if (pmk::step_qset_ok(S, lds, G.ph8, G.maxPH, max_per_part, G.maxSS)) {
+    S.qw = (G.maxSS + 7) & ~7u;
+    CHK(G.qset.reserve((uint64_t)nsub * S.qw * 2));
+    S.qset = G.qset.as<uint16_t>();
+  }
   if (pmk::step_match_resolve_ok(S, lds)) {   // one launch: match + resolve per partition
     c->timed_ext("match_resolve", (double)nreal * G.maxPH, [&](pmk::PmEvents ev) { pmk::step_match_resolve(st, S, G.ph8, G.maxPH, max_per_part, ev); }, 2);
   } else {
     c->timed_ext("hint_match", (double)nreal * G.maxPH, [&](pmk::PmEvents ev) { pmk::step_match(st, S, G.maxPH, ev); }, 2);
     c->timed_ext("resolve", 0, [&](pmk::PmEvents ev) { pmk::step_resolve(st, S, lds, ev); }, 2);
   }
-  S.nsplit = c->no_split ? 1 : pmk::step_gather_split(G.maxSS, nsub);
   if (S.nsplit > 1) {
     CHK(G.part_x.reserve((uint64_t)nsub * S.nsplit * (G.E & ~3u) * 8));
     S.part_x = G.part_x.as<uint64_t>();

@@ -175,6 +175,11 @@ struct PmStep {
   // XORs of each sub-query's set, [nsub][nsplit][E&~3]; k_answer folds them.
   uint32_t nsplit;             // 0/1: k_answer gathers its set itself
   PM_G uint64_t* part_x;
+  // Query sets expanded by k_match_resolve_s ([nsub][qw] u16 offsets; qw = SetSize
+  // rounded up to 8), read by k_answer with the resolution record; null: the
+  // answer expands its set from tabT itself.
+  PM_G uint16_t* qset;
+  uint32_t qw;
   // Small steps ship the descriptor inside the kernel arguments (no PCIe
   // round trip); larger ones use subs_h / sb_h.
   uint32_t args_valid;
@@ -217,6 +222,9 @@ void step_match_resolve(hipStream_t st, const PmStep& S, bool ph8, uint32_t maxP
 bool step_fused_ok(const PmStep& S, uint32_t maxPH, uint32_t max_sub_per_part);
 void step_fused(hipStream_t st, const PmStep& S, PmEvents ev = {});
 bool step_resolve_lds_ok(uint32_t maxPH, uint32_t max_sub_per_part);
+// k_match_resolve_s writes the query sets for the answer (PmStep::qset); S.nsplit set
+bool step_qset_ok(const PmStep& S, bool lds, bool ph8, uint32_t maxPH, uint32_t max_sub_per_part,
+                  uint32_t maxSS);
 void step_answer(hipStream_t st, const PmStep& S, uint32_t maxSS, PmEvents ev = {});
 // Split gather ahead of k_answer for wide query sets (SetSize >= 256, BIGANN
 // scale): how many workgroups per sub-query (1: no split), and the launch.

@@ -1046,8 +1046,10 @@ __device__ __forceinline__ void resolve_role(const PmStep& S, uint32_t p, Resolv
     // --- flush (one writer per result / hint / chunk) -----------------------
     if (in) {
       const bool ok = st == ST_OK;
-      put_res<GRAN>(S, b0 + k, PmRes{st, ok ? rhit : 0u, ok ? ch : 0u, ok ? ring : 0u, ok ? rtag : 0u,
-                            ok ? rpp : 0u, (ok || st == ST_DUP || st == ST_CACHED) ? rslot : 0u, ok ? rfl : 0u});
+      const PmRes rr{st, ok ? rhit : 0u, ok ? ch : 0u, ok ? ring : 0u, ok ? rtag : 0u,
+                     ok ? rpp : 0u, (ok || st == ST_DUP || st == ST_CACHED) ? rslot : 0u, ok ? rfl : 0u};
+      put_res<GRAN>(S, b0 + k, rr);
+      if constexpr (MODE == 3) s_res[k] = rr;   // k_match_resolve_s expands the query sets from LDS
     }
     if (k < nmod) { P.tag[mh] = mt; P.pp[mh] = mp; }
     bool last = in && st == ST_OK;   // QueryHistogram: the last success per chunk writes
@@ -1379,6 +1381,31 @@ __global__ void __launch_bounds__(kResolveBlockG) k_match_resolve_s(PmStep S) {
   resolve_role<3, kResolveBlockG, false>(S, p, L);
   __syncthreads();
   if (L.fin && threadIdx.x == 0) chain_rearm(S);
+  if (S.qset) {
+    // The query set of every successful sub-query (pir.go:424-444: the hit
+    // hint's offsets, its program point, the chunk's replacement), expanded
+    // here so that k_answer_s reads it with its resolution record in one round
+    // trip instead of gathering the tag's PRF row after the record arrives.
+    // One 16-B tabT tile (8 chunks) per thread; S.qw words per sub-query.
+    const uint32_t nt8 = S.qw / 8;
+    for (uint32_t x = tid; x < n * nt8; x += NT) {
+      const uint32_t j = x / nt8, t = x % nt8;
+      const PmRes r = L.s_res[j];
+      if (r.status != ST_OK) continue;
+      const uint32_t c0 = 8 * t;
+      const bool rc = r.chunk - c0 < 8u;
+      const uint32_t ro = rc ? P.ridx[r.chunk * P.Qpc + r.ing] & mask : 0u;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (c0 < P.SS) v = *reinterpret_cast<const PM_G uint4*>(P.tabT + tabT_index(P.H, r.tag, c0));
+      uint32_t w[4] = {v.x, v.y, v.z, v.w};
+      auto put = [&](uint32_t e, uint32_t o) {
+        w[e >> 1] = (w[e >> 1] & ~(0xffffu << (16 * (e & 1)))) | ((o & 0xffffu) << (16 * (e & 1)));
+      };
+      if (r.pp != kDefaultProgramPoint && (r.pp >> lg) - c0 < 8u) put((r.pp >> lg) - c0, r.pp & mask);
+      if (rc) put(r.chunk - c0, ro);
+      *reinterpret_cast<PM_G uint4*>(S.qset + (uint64_t)(b0 + j) * S.qw + c0) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  }
 }
 
 // L2Dist of the first `dim` floats of an LDS row against q (device), one
@@ -1546,7 +1573,7 @@ __device__ void finish_step(const PmStep& S, RB& row) {
 template <int NT, uint32_t MSS = kMaxSSLds, uint32_t ME = kMaxELds>
 struct AnswerLds {
   uint32_t f[17];   // k_step: granule fields, per-wave first candidates, predicted index
-  uint16_t qo[MSS];   // the query set: in-chunk offsets < ChunkSize <= 32768
+  __attribute__((aligned(16))) uint16_t qo[MSS];   // the query set: in-chunk offsets < ChunkSize <= 32768
   uint64_t red[NT * 2];
   __attribute__((aligned(16))) RowBufT<ME> row;
   uint32_t s_last;
@@ -1597,6 +1624,11 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, LDS& L)
     if (tid < S.dim) qreg0 = qq[tid];
     if (tid + NT < S.dim) qreg1 = qq[tid + NT];
   }
+  // the pre-expanded query set (S.qset, three-kernel path after k_match_resolve_s),
+  // loaded now, in flight with the resolution record
+  const bool qpre = !GRAN && S.qset != nullptr;
+  uint4 qpv = make_uint4(0, 0, 0, 0);
+  if (qpre && tid < S.qw / 8) qpv = *reinterpret_cast<const PM_G uint4*>(S.qset + (uint64_t)s * S.qw + 8 * tid);
   uint64_t e_rv = 0, e_bp = 0, e_pp = 0;
   uint32_t e_cur = kSkip;   // the refreshed hint's new search-row value at chunk tid (refresh_cur)
   // set expansion + gather into row.w[0..EX) and the decode operands for (r, mode)
@@ -1639,7 +1671,10 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, LDS& L)
       return;
     }
     // ---- query set (pir.go:363-371 dummy; :424-444 real) -------------------
-    if (mode == A_FINAL || mode == A_CHAINED) {
+    if (qpre && (mode == A_FINAL || mode == A_CHAINED)) {
+      // expanded by k_match_resolve_s, loaded with the resolution record
+      if (tid < S.qw / 8) *reinterpret_cast<uint4*>(qo + 8 * tid) = qpv;
+    } else if (mode == A_FINAL || mode == A_CHAINED) {
       const uint32_t pchunk = r.pp != kDefaultProgramPoint ? (r.pp >> lg) : kNone;
       for (uint32_t i = tid; i < P.SS; i += NT) {
         uint32_t o = P.tabT[tabT_index(P.H, r.tag, i)];
@@ -2050,6 +2085,13 @@ void step_match_resolve(hipStream_t st, const PmStep& S, bool ph8, uint32_t maxP
     PM_LAUNCH(ev, k_match_resolve_s<2>, dim3(S.np), dim3(kResolveBlockG), st, S);
   else
     PM_LAUNCH(ev, k_match_resolve<kMatchHints / kBlock>, dim3(S.np), dim3(kResolveBlockG), st, S);
+}
+bool step_qset_ok(const PmStep& S, bool lds, bool ph8, uint32_t maxPH, uint32_t max_sub_per_part,
+                  uint32_t maxSS) {
+  static const int mode = [] { const char* e = getenv("PM_MATCH_RESOLVE"); return e ? atoi(e) : 1; }();
+  static const int qs = [] { const char* e = getenv("PM_QSET"); return e ? atoi(e) : 1; }();
+  return qs && mode == 1 && step_match_resolve_ok(S, lds) && max_sub_per_part <= kSpecSubs && ph8 &&
+         maxPH <= 16u * kResolveBlockG && maxSS <= kSmallSS && S.nsplit <= 1;
 }
 void step_resolve(hipStream_t st, const PmStep& S, bool lds, PmEvents ev) {
   if (lds) PM_LAUNCH(ev, k_resolve<true>, dim3(S.np), dim3(kBlock), st, S);
