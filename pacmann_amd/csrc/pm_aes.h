@@ -94,12 +94,12 @@ struct AesLane {
   template <int K> __device__ __forceinline__ uint32_t Sk(uint32_t s) const { return (Tk<K>(s) >> 8) & 0xffu; }
 };
 
-// Full rounds R0..9 on state (s0..s3) with round keys rk[4*R0..39].
-template <int R0 = 1>
+// Full rounds R0..R1-1 on state (s0..s3) with round keys rk[4*R0..4*R1-1].
+template <int R0 = 1, int R1 = 10>
 __device__ __forceinline__ void aes_rounds(const AesLane& A, const uint32_t* __restrict__ rk,
                                            uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3) {
 #pragma unroll
-  for (int r = R0; r < 10; ++r) {
+  for (int r = R0; r < R1; ++r) {
     // Te0[a] ^ rotl8(Te0[b]) ^ rotl16(Te0[c]) ^ rotl24(Te0[d]) ^ rk
     //   = Te0[a] ^ Te2[c] ^ rotl8(Te0[b] ^ Te2[d]) ^ rk
     // (v_bitop3_b32 0x96 = three-input XOR on gfx950: 4 VALU per column instead of 5)
@@ -163,4 +163,16 @@ __device__ __forceinline__ uint32_t prf_lo32_split(const AesLane& A, const uint3
   return c0 ^ x;
 }
 
+// The low 16 bits of the same PRF (the hint tables keep PRF & (ChunkSize - 1),
+// ChunkSize <= 2^15).  Output bytes 0 and 1 of the last round are S[s0 byte 0]
+// and S[s1 byte 1], so round 9 computes only columns 0 and 1 and round 10 two
+// S-box bytes: 122 lookups per PRF instead of 132.
+__device__ __forceinline__ uint32_t prf_lo16_split(const AesLane& A, const uint32_t* __restrict__ rk,
+                                                   const R1Uniform& u, const R1Lane& v, uint32_t x) {
+  uint32_t s0 = u.u0 ^ v.v0, s1 = u.u1 ^ v.v1, s2 = u.u2 ^ v.v2, s3 = u.u3 ^ v.v3;
+  aes_rounds<2, 9>(A, rk, s0, s1, s2, s3);
+  const uint32_t t0 = aes_x3(aes_x3(A.Tk<0>(s0), A.T2k<2>(s2), rk[36]), rotl32(A.Tk<1>(s1) ^ A.T2k<3>(s3), 8), 0u);
+  const uint32_t t1 = aes_x3(aes_x3(A.Tk<0>(s1), A.T2k<2>(s3), rk[37]), rotl32(A.Tk<1>(s2) ^ A.T2k<3>(s0), 8), 0u);
+  return ((A.Sk<0>(t0) | (A.Sk<1>(t1) << 8)) ^ rk[40] ^ x) & 0xffffu;
+}
 }  // namespace pm

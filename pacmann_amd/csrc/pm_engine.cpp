@@ -617,8 +617,10 @@ static int engine_prep_launch(pm_ctx* c, const Engine* g, const PmPart* dp, int 
   hipStream_t st = c->stream;
   c->timed("prep_init", 0, [&] { pmk::prep_init(st, dp, np, g->maxH, g->maxRepl, (uint32_t)g->E, g->skipPrep); });
   double aes = 0, fold = 0, repl = 0;
+  uint32_t minH = ~0u;
   for (int i = 0; i < np; ++i) {
     const PmPart& d = host_parts[i];
+    minH = std::min(minH, d.H);
     aes += (double)d.H * d.SS;
     // algorithmic fold bytes: hpc * SS (hint, chunk) pairs of one E-word entry
     fold += ((double)d.PH + (double)(d.SS - 1) * d.Qpc) * d.SS * (double)g->E * 8;
@@ -634,7 +636,7 @@ static int engine_prep_launch(pm_ctx* c, const Engine* g, const PmPart* dp, int 
     }
   } else {
     c->timed("prep_fold", fold, [&] { pmk::prep_fold(st, dp, np, g->maxH, g->db->as<uint64_t>(), (uint32_t)g->E, g->minCS, g->maxCS,
-                                               g->zero16.as<uint64_t>(), clients, g->img->p != nullptr); });
+                                               g->zero16.as<uint64_t>(), clients, g->img->p != nullptr, minH); });
     c->timed("prep_repl", repl, [&] { pmk::prep_repl(st, dp, np, g->maxRepl, g->db->as<uint64_t>(), (uint32_t)g->E); });
   }
   HIPCHK(hipGetLastError());

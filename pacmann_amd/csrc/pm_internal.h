@@ -199,7 +199,7 @@ void prep_offsets(hipStream_t st, const PmPart* dparts, int nparts, uint32_t max
 // dparts: `clients` clients of each partition, partition-major (nparts = partitions x clients)
 void prep_fold(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxH, const uint64_t* db,
                uint32_t E, uint32_t minCS, uint32_t maxCS, const uint64_t* zero16, uint32_t clients = 1,
-               bool have_img = false);
+               bool have_img = false, uint32_t minH = 0);
 void prep_repl(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxRepl,
                const uint64_t* db, uint32_t E);
 // The bank-rotated fold's DB image (CS 512, even E, E >= 4): whether it applies,

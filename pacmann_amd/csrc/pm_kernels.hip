@@ -63,7 +63,7 @@ __global__ void __launch_bounds__(kOffsBlock) k_prep_offsets(const PmPart* __res
 #pragma unroll
   for (int j = 0; j < 8; ++j) tile[j] = kSkip;   // chunks past SetSize: padding
   for (uint32_t c = c0; c < c1; ++c) {
-    uint16_t v = (uint16_t)(prf_lo32_split(A, P.rk, r1u[c - c0], r1v, c) & mask);
+    uint16_t v = (uint16_t)(prf_lo16_split(A, P.rk, r1u[c - c0], r1v, c) & mask);
     v = (c == own) ? kSkip : v;
     o[(uint64_t)c * H + h] = v;   // chunk-major: refreshed tags' re-evaluation, fold
     tile[c - c0] = v;
@@ -412,8 +412,8 @@ constexpr int kRotHPL = PM_ROT_HPL;   // hints per lane (SIFT1M's 12,512 hints: 
 constexpr uint32_t kRotCS = 512, kRotBufBytes = kRotCS * 128;   // one image block per (slice, 4 chunks)
 template <int CS>
 __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_rot(const PmPart* __restrict__ parts, uint32_t E,
-                                                                uint32_t ngmax, uint32_t nsl, uint32_t npg,
-                                                                uint32_t K) {
+                                                                uint32_t nvg, uint32_t nsl, uint32_t npv,
+                                                                uint32_t M, uint32_t K, uint32_t ngc) {
   constexpr uint32_t LINE = 32, BUFW = (CS + 1) * LINE;
   // static (not extern) LDS: its address is a constant the reads fold into
   // their offsets
@@ -421,26 +421,47 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_rot(const PmPart* __
   constexpr uint32_t ITEMS = CS * 8;   // 16-B staging items per buffer (4 chunks x CS rows x 2)
   static_assert(ITEMS % kFoldThreads == 0, "whole staging items per thread");
   constexpr uint32_t G = ITEMS / kFoldThreads;
-  // XCD-aware order of k_prep_fold_pipe (workgroups b and b + 8 share an
-  // XCD): pg = (partition, hint group) runs on XCD pg % 8; there, groups of 4
-  // slices of the K clients follow each other.  (Client-major order, all
-  // clients of one slice back to back, measured 10-15 % slower in 64-client
-  // launches.)
-  constexpr uint32_t LW = 4;
-  const uint32_t ngl = (nsl + LW - 1) / LW, per_pg = K * ngl * LW;
+  // Virtual hint groups: the K clients' hint lists of a partition, concatenated
+  // (client c's hint h is virtual hint c * H + h), cut into groups of HB =
+  // 1,024 x kRotHPL lane slots.  A group spans at most two clients (HB <= H),
+  // and only the partition's last group has idle slots: 157 workgroups per
+  // (partition, slice) for 64 SIFT1M clients instead of 3 per client (192),
+  // each staging the slice's image once.  Order: XCD x takes the (partition,
+  // group) pairs [x M, (x + 1) M); there, groups of 4 slices of consecutive
+  // pairs follow each other (the pairs of one partition read the same image
+  // blocks out of the XCD's L2).  (Round 1's order, (partition, group) on XCD
+  // pg % 8 with groups of 4 slices of its K clients in turn, was measured
+  // 10-15 % faster than all clients of one slice back to back.)  ngc != 0:
+  // partitions with fewer than HB hints (small configs) keep ngc groups per
+  // client instead (no mixing).
+  constexpr uint32_t LW = 4, HB = kFoldThreads * kRotHPL;
   const uint32_t xcd = blockIdx.x % 8, kq = blockIdx.x / 8;
-  const uint32_t pg = xcd + 8 * (kq / per_pg), r = kq % per_pg;
-  const uint32_t client = (r / LW) % K, slice = (r / (K * LW)) * LW + r % LW;
-  if (pg >= npg || slice >= nsl) return;   // block-uniform
-  const PmPart& P = parts[(pg / ngmax) * K + client];
+  const uint32_t loc = (kq / LW) % M, slice = (kq / (LW * M)) * LW + kq % LW;
+  const uint32_t pgv = xcd * M + loc;
+  if (pgv >= npv || slice >= nsl) return;   // block-uniform
+  const uint32_t part = pgv / nvg, vg = pgv % nvg;
+  const PmPart& P = parts[part * K];   // H, SS and the fold image are the same for every client
   const uint32_t H = P.H, SS = P.SS, tid = threadIdx.x;
-  const uint32_t ng = (H + kFoldThreads * kRotHPL - 1) / (kFoldThreads * kRotHPL);
-  const uint32_t grp = pg % ngmax;
-  if (grp >= ng) return;   // block-uniform
-  const uint32_t hb = (H + ng - 1) / ng, h0 = grp * hb, h1 = min(H, h0 + hb);
+  const uint32_t vend = K * H;
+  uint32_t v0, v1;
+  if (ngc == 0) {
+    v0 = vg * HB;
+    if (v0 >= vend) return;   // block-uniform (a partition with fewer hints than maxH)
+    v1 = min(v0 + HB, vend);
+  } else {
+    const uint32_t c = vg / ngc, g = vg % ngc;
+    if (c >= K || g * HB >= H) return;   // block-uniform
+    v0 = c * H + g * HB;
+    v1 = min(v0 + HB, (c + 1) * H);
+  }
+  const uint32_t cA = v0 / H, cB = min(cA + 1, K - 1), vb = (cA + 1) * H;
+  const PmPart& PA = parts[part * K + cA];
+  const PmPart& PB = parts[part * K + cB];
+  const PM_G uint16_t* const tabA = PA.tabT;
+  const PM_G uint16_t* const tabB = PB.tabT;
+  const uint32_t hA = cA * H;
   const uint32_t w = slice * 4, nbuf = SS / 4;   // SetSize is a multiple of 4 (pir.go:497)
   const PM_G char* img = (const PM_G char*)P.img + (uint64_t)slice * nbuf * kRotBufBytes;
-  const PM_G uint16_t* tabT = P.tabT;
 #if PM_ROT_B128
   // 16-B reads: lane l reads chunk slot (s + phase) & 3, halves f then f ^ 1
   // (s = l & 3, f = (l >> 2) & 1: every ds_read_b128 lane group of 16 holds
@@ -449,7 +470,7 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_rot(const PmPart* __
 #else
   const uint32_t lane = tid & 63, j = lane & 7, ks = (lane >> 3) & 3;
 #endif
-  const uint32_t hl = h0 + tid;   // hint of lane slot k: hl + k * kFoldThreads
+  const uint32_t vl = v0 + tid;   // virtual hint of lane slot k: vl + k * kFoldThreads
   uint32_t acc[kRotHPL][8];
 #pragma unroll
   for (int k = 0; k < kRotHPL; ++k)
@@ -468,9 +489,11 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_rot(const PmPart* __
   auto load_tab = [&](uint32_t b, u32x2* out) {   // chunks 4b .. 4b+3 of each hint: 8 B of its tabT tile
 #pragma unroll
     for (int k = 0; k < kRotHPL; ++k) {
+      const uint32_t v = min(vl + k * kFoldThreads, vend - 1);
+      const bool inB = v >= vb;
       out[k] = *reinterpret_cast<const PM_G u32x2*>(
-          (const PM_G char*)tabT + (uint32_t)tabT_index(H, min(hl + k * kFoldThreads, H - 1), 4 * b) * 2u);
-      if (PM_ROT_B128 && hl + k * kFoldThreads >= h1) out[k] = u32x2{0xffffffffu, 0xffffffffu};   // kSkip: zero line
+          (const PM_G char*)(inB ? tabB : tabA) + (uint32_t)tabT_index(H, v - (inB ? vb : hA), 4 * b) * 2u);
+      if (PM_ROT_B128 && vl + k * kFoldThreads >= v1) out[k] = u32x2{0xffffffffu, 0xffffffffu};   // kSkip: zero line
     }
   };
   for (uint32_t x = tid; x < 2 * LINE; x += kFoldThreads) rot_lds[(x / LINE) * BUFW + CS * LINE + x % LINE] = 0;
@@ -518,7 +541,7 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_rot(const PmPart* __
     for (uint32_t ph = 0; ph < 4; ++ph) cso[ph] = lb + ((ks + ph) & 3) * 32 + (PM_ROT_B64 ? 8 * (j & 3) : 4 * j);
 #pragma unroll
     for (int k = 0; k < (PM_ROT_ABL == 1 ? 0 : kRotHPL); ++k) {
-      const bool hv = hl + k * kFoldThreads < h1;   // lane slots past the group: zero line
+      const bool hv = vl + k * kFoldThreads < v1;   // lane slots past the group: zero line
       // the 4 offsets in phase order: rotate the 64-bit tile right by 16 ks
       const uint64_t t64 = ((uint64_t)tv[k].y << 32) | tv[k].x;
       const uint32_t sh = 16 * ks;
@@ -556,14 +579,17 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_rot(const PmPart* __
   }
 #pragma unroll
   for (int k = 0; k < kRotHPL; ++k) {
-    if ((hl + k * kFoldThreads) >= h1) continue;
-    PM_G uint32_t* dst = reinterpret_cast<PM_G uint32_t*>(P.parity + (uint64_t)(hl + k * kFoldThreads) * E + w);
+    const uint32_t v = vl + k * kFoldThreads;
+    if (v >= v1) continue;
+    const bool inB = v >= vb;
+    PM_G uint64_t* const par = (inB ? PB.parity : PA.parity) + (uint64_t)(v - (inB ? vb : hA)) * E;
+    PM_G uint32_t* dst = reinterpret_cast<PM_G uint32_t*>(par + w);
 #pragma unroll
     for (int t = 0; t < 8; ++t)
       dst[PM_ROT_B128 ? 4 * (j ^ (t >> 2)) + (t & 3)
                       : PM_ROT_B64 ? 2 * (((j & 3) + t / 2) & 3) + (t & 1) : (j + t) & 7] = acc[k][t];
     if (w == 0)   // xorSlices leaves the words past len&~3 zero
-      for (uint32_t t = E & ~3u; t < E; ++t) P.parity[(uint64_t)(hl + k * kFoldThreads) * E + t] = 0;
+      for (uint32_t t = E & ~3u; t < E; ++t) par[t] = 0;
   }
 }
 
@@ -840,7 +866,8 @@ void fold_image(hipStream_t st, uint64_t* img, const uint64_t* rows, uint64_t N,
   hipLaunchKernelGGL(k_fold_image, dim3(grid), dim3(kBlock), 0, st, (uint4*)img, rows, N, SS / 4, E, nitems);
 }
 void prep_fold(hipStream_t st, const PmPart* d, int np, uint32_t maxH, const uint64_t* db, uint32_t E,
-               uint32_t minCS, uint32_t maxCS, const uint64_t* zero16, uint32_t clients, bool have_img) {
+               uint32_t minCS, uint32_t maxCS, const uint64_t* zero16, uint32_t clients, bool have_img,
+               uint32_t minH) {
   const uint32_t EX = E & ~3u;
   if (EX == 0) {
     hipLaunchKernelGGL(k_prep_fold<2>, dim3(cdiv((uint64_t)maxH * E, kBlock), np), dim3(kBlock), 0,
@@ -874,9 +901,13 @@ void prep_fold(hipStream_t st, const PmPart* d, int np, uint32_t maxH, const uin
 #define PM_FOLD_D512 1
 #endif
     if (have_img && fold_image_ok(minCS, maxCS, E)) {   // the bank-rotated fold (same slices and block order)
-      const uint32_t ngr = cdiv(maxH, (uint64_t)kFoldThreads * kRotHPL), npgr = (np / K) * ngr;
-      hipLaunchKernelGGL(k_prep_fold_rot<512>, dim3(cdiv(npgr, 8) * 8 * per_pg), dim3(kFoldThreads), 0, st, d, E,
-                         ngr, nsl, npgr, K);
+      // virtual hint groups over the K clients of each partition (see the kernel)
+      const uint64_t HB = (uint64_t)kFoldThreads * kRotHPL;
+      const uint32_t ngc = minH >= HB ? 0u : (uint32_t)cdiv(maxH, HB);
+      const uint32_t nvg = ngc ? K * ngc : (uint32_t)cdiv((uint64_t)K * maxH, HB), npv = (np / K) * nvg;
+      const uint32_t M = cdiv(npv, 8);
+      hipLaunchKernelGGL(k_prep_fold_rot<512>, dim3(8 * M * cdiv(nsl, 4) * 4), dim3(kFoldThreads), 0, st, d, E,
+                         nvg, nsl, npv, M, K, ngc);
       return;
     }
     const uint32_t nb = maxCS == 512 ? PM_FOLD_NB512 : 3;   // LDS buffers: <= 150 KB
