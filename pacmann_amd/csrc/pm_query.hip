@@ -1260,9 +1260,9 @@ __global__ void __launch_bounds__(kResolveBlockG) k_match_resolve(PmStep S) {
 // wave reads the requests, QueryHistogram and FinishedQueryNum and makes the
 // predictions of resolve_role's staged prologue (in-chunk index, re-evaluation
 // values) meanwhile.  Results are identical to k_match_resolve's.
-template <int NU>
-__global__ void __launch_bounds__(kResolveBlockG) k_match_resolve_s(PmStep S) {
-  constexpr int NT = kResolveBlockG, NW = NT / 64, G = 8 / NU;
+template <int NU, int NT>
+__global__ void __launch_bounds__(NT) k_match_resolve_s(PmStep S) {
+  constexpr int NW = NT / 64, G = 8 / NU;
   __shared__ ResolveLds<3> L;
   __shared__ uint32_t s_m[kSpecSubs][NU][NW][2];   // each (sub-query, row block, wave): first two matches
   const uint32_t p = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1378,7 +1378,7 @@ __global__ void __launch_bounds__(kResolveBlockG) k_match_resolve_s(PmStep S) {
     L.s_c1[j] = c1; L.s_c2[j] = c2; L.s_t1[j] = t1; L.s_p1[j] = p1; L.s_t2[j] = t2; L.s_p2[j] = p2;
   }
   __syncthreads();
-  resolve_role<3, kResolveBlockG, false>(S, p, L);
+  resolve_role<3, NT, false>(S, p, L);
   __syncthreads();
   if (L.fin && threadIdx.x == 0) chain_rearm(S);
   if (S.qset) {
@@ -1633,6 +1633,10 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, LDS& L)
   uint32_t e_cur = kSkip;   // the refreshed hint's new search-row value at chunk tid (refresh_cur)
   // set expansion + gather into row.w[0..EX) and the decode operands for (r, mode)
   auto gather = [&](const PmRes& r, uint32_t mode) {
+    // a pre-expanded set goes to LDS before any later load is issued (its wait
+    // then covers only the loads issued with the record)
+    if (qpre && (mode == A_FINAL || mode == A_CHAINED) && tid < S.qw / 8)
+      *reinterpret_cast<uint4*>(qo + 8 * tid) = qpv;
     // decode operands: independent of the gather, issued first (pir.go:450-468)
     const uint64_t dslot = (uint64_t)r.chunk * P.Qpc + r.ing;
     if (mode == A_FINAL && !(r.flags & 2u) && tid < P.SS)   // the new tag's PRF row (backup hint (chunk, ing))
@@ -1672,8 +1676,7 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, LDS& L)
     }
     // ---- query set (pir.go:363-371 dummy; :424-444 real) -------------------
     if (qpre && (mode == A_FINAL || mode == A_CHAINED)) {
-      // expanded by k_match_resolve_s, loaded with the resolution record
-      if (tid < S.qw / 8) *reinterpret_cast<uint4*>(qo + 8 * tid) = qpv;
+      // expanded by k_match_resolve_s: in LDS already (above)
     } else if (mode == A_FINAL || mode == A_CHAINED) {
       const uint32_t pchunk = r.pp != kDefaultProgramPoint ? (r.pp >> lg) : kNone;
       for (uint32_t i = tid; i < P.SS; i += NT) {
@@ -2079,10 +2082,21 @@ void step_match_resolve(hipStream_t st, const PmStep& S, bool ph8, uint32_t maxP
   // the one-round-trip form where its shapes hold (PM_MATCH_RESOLVE=2: always the general one)
   static const int mode = [] { const char* e = getenv("PM_MATCH_RESOLVE"); return e ? atoi(e) : 1; }();
   const bool small = mode == 1 && max_sub_per_part <= kSpecSubs && ph8;
-  if (small && maxPH <= 8u * kResolveBlockG)
-    PM_LAUNCH(ev, k_match_resolve_s<1>, dim3(S.np), dim3(kResolveBlockG), st, S);
+  // workgroup size (PM_MR_NT): 256 leaves the GPU's wave slots to the other
+  // groups' kernels while wave 0 runs the chain
+  static const int nt = [] { const char* e = getenv("PM_MR_NT"); return e ? atoi(e) : 256; }();
+  if (small && nt == 128 && maxPH <= 8u * 128 * 4)
+    PM_LAUNCH(ev, (k_match_resolve_s<4, 128>), dim3(S.np), dim3(128), st, S);
+  else if (small && nt == 128 && maxPH <= 8u * 128 * 8)
+    PM_LAUNCH(ev, (k_match_resolve_s<8, 128>), dim3(S.np), dim3(128), st, S);
+  else if (small && nt == 256 && maxPH <= 8u * 256 * 2)
+    PM_LAUNCH(ev, (k_match_resolve_s<2, 256>), dim3(S.np), dim3(256), st, S);
+  else if (small && nt == 256 && maxPH <= 8u * 256 * 4)
+    PM_LAUNCH(ev, (k_match_resolve_s<4, 256>), dim3(S.np), dim3(256), st, S);
+  else if (small && maxPH <= 8u * kResolveBlockG)
+    PM_LAUNCH(ev, (k_match_resolve_s<1, kResolveBlockG>), dim3(S.np), dim3(kResolveBlockG), st, S);
   else if (small && maxPH <= 16u * kResolveBlockG)
-    PM_LAUNCH(ev, k_match_resolve_s<2>, dim3(S.np), dim3(kResolveBlockG), st, S);
+    PM_LAUNCH(ev, (k_match_resolve_s<2, kResolveBlockG>), dim3(S.np), dim3(kResolveBlockG), st, S);
   else
     PM_LAUNCH(ev, k_match_resolve<kMatchHints / kBlock>, dim3(S.np), dim3(kResolveBlockG), st, S);
 }

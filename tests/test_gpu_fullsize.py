@@ -165,10 +165,18 @@ def _sessions_vs_oracle(ctx, oracle, v, graph, qs_per_session, k, seeds, ngroups
         s.Preprocess()
     ans, wall, on, mt = pm.search_loop_batched(sess, qs_per_session, k, 20, 3, ngroups, nthreads)
     assert wall > 0 and (mt > 0).all()
-    for i, (p, s) in enumerate(seeds):
+
+    def run_oracle(i):   # one C call per phase: the oracle sessions run on host threads side by side
+        p, s = seeds[i]
         o = oracle.Graph(v, graph, pir_seed=p, search_seed=s)
         o.Preprocess()
         oa, _, _ = o.SearchLoop(qs_per_session[i], k, 20, 3)
+        return o, oa
+
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=min(8, len(seeds))) as ex:
+        runs = list(ex.map(run_oracle, range(len(seeds))))
+    for i, (o, oa) in enumerate(runs):
         bad = np.where((ans[i] != oa).any(axis=1))[0]
         assert len(bad) == 0, (i, bad[:5].tolist())
         assert sess[i].counts() == o.counts(), i
@@ -214,3 +222,37 @@ def test_search_msmarco_full_sessions(ctx, oracle):
     qs = np.stack([(v[rng.integers(0, N, 47)] + rng.normal(0, 0.1, (47, 192))).astype(np.float32)
                    for _ in seeds])
     _sessions_vs_oracle(ctx, oracle, v, graph, qs, 100, seeds, ngroups=1, nthreads=2)
+
+
+def test_search_sift1m_full_shared_step(ctx, oracle):
+    """The bench's serving kernels at full SIFT1M size: eight sessions in ONE
+    lock-step group, so every round is one shared step over 8 x 16 = 128
+    partitions -- the shapes that select k_match_resolve_s (match + resolve
+    with the query sets expanded for k_answer_s) -- and the sessions'
+    simultaneous re-preprocessing folds 8 clients per launch over mixed hint
+    groups (k_prep_fold_rot).  Every session equals an independent oracle run."""
+    from pacmann_amd.synth import random_graph, sift_like_vectors
+    N = 1_000_000
+    v = sift_like_vectors(N, 128, seed=101)
+    graph = random_graph(N, 32, seed=201)
+    rng = np.random.default_rng(13)
+    seeds = [(110 + i, 210 + i) for i in range(8)]
+    qs = np.stack([np.clip(np.rint(v[rng.integers(0, N, 26)] + rng.normal(0, 8, (26, 128))), 0, 255)
+                   .astype(np.float32) for _ in seeds])
+    _sessions_vs_oracle(ctx, oracle, v, graph, qs, 10, seeds, ngroups=1, nthreads=8)
+
+
+def test_search_msmarco_full_shared_step(ctx, oracle):
+    """MS-MARCO d=192 at full size through the shared step of eight sessions
+    (128 partitions of CS 1,024 / SS 196 / E 112: k_match_resolve_s over 7,168
+    hints, pre-expanded query sets, 8-client k_prep_fold_pipe), 47 queries each
+    (every session re-preprocesses), k = 100.  Equal to independent oracle runs."""
+    from pacmann_amd.synth import msmarco_like_vectors, random_graph
+    N = 3_201_821
+    v = msmarco_like_vectors(N, 192, seed=15)
+    graph = random_graph(N, 32, seed=16)
+    rng = np.random.default_rng(18)
+    seeds = [(150 + i, 250 + i) for i in range(8)]
+    qs = np.stack([(v[rng.integers(0, N, 47)] + rng.normal(0, 0.1, (47, 192))).astype(np.float32)
+                   for _ in seeds])
+    _sessions_vs_oracle(ctx, oracle, v, graph, qs, 100, seeds, ngroups=1, nthreads=8)
