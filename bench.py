@@ -650,6 +650,13 @@ def cpu_baseline_all_cores(v, g, out):
 
 
 def main():
+    # The contract is ONE JSON line on rank 0's stdout; native libraries write
+    # banners there (gloo prints its peer-connection lines at rendezvous), so
+    # file descriptor 1 points at stderr for the whole run and the line goes
+    # to the saved descriptor.
+    sys.stdout.flush()
+    line_fd = os.dup(1)
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
@@ -934,7 +941,8 @@ def main():
             except Exception as e:   # recorded, never fatal to the headline line
                 out[key] = {"error": f"{type(e).__name__}: {e}"}
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        sys.stdout.flush()
+        os.write(line_fd, (json.dumps(out) + "\n").encode())
     if dist:
         dist.destroy_process_group()
 
