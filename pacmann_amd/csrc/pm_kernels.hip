@@ -38,19 +38,24 @@ constexpr int kOffsBlock = 1024;   // 64 KiB of replicated table per workgroup: 
 // them the kernel is only 2 % faster).  1,024-thread workgroups share one 64 KiB
 // table copy (the LDS init is 4 B per PRF, not 16) and keep 16 waves per CU
 // for the lookups' latency: 0.370 -> 0.335 ms at SIFT1M shape.
+#ifndef PM_OFFS_TILES
+#define PM_OFFS_TILES 1   // 8-chunk tiles per workgroup sharing one 64 KiB table fill (2 and 4 measured no faster: 244 / 268 vs 240 us per client alone)
+#endif
+constexpr int kOffsTiles = PM_OFFS_TILES;
 __global__ void __launch_bounds__(kOffsBlock) k_prep_offsets(const PmPart* __restrict__ parts) {
   __shared__ uint32_t te[kTeLdsWords];
-  __shared__ R1Uniform r1u[kOffsChunksPerBlock];
+  __shared__ R1Uniform r1u[kOffsTiles][kOffsChunksPerBlock];
   const PmPart& P = parts[blockIdx.z];
   const uint32_t H = P.H, SS = P.SS;
-  const uint32_t c0 = blockIdx.y * kOffsChunksPerBlock;
-  if (blockIdx.x * kOffsBlock >= H || c0 >= SS) return;   // block-uniform
+  const uint32_t cb = blockIdx.y * kOffsChunksPerBlock * kOffsTiles;
+  if (blockIdx.x * kOffsBlock >= H || cb >= SS) return;   // block-uniform
   aes_lds_init(te, g_aes.te0);
   __syncthreads();
   const AesLane A(te, threadIdx.x);
-  const uint32_t c1 = min(SS, c0 + kOffsChunksPerBlock);
+  const uint32_t cend = min(SS, cb + kOffsChunksPerBlock * kOffsTiles);
   // round 1's chunk-dependent half, once per chunk for the workgroup (pm_aes.h)
-  if (threadIdx.x < c1 - c0) r1u[threadIdx.x] = r1_uniform(A, P.rk, c0 + threadIdx.x);
+  if (threadIdx.x < cend - cb)
+    r1u[threadIdx.x / kOffsChunksPerBlock][threadIdx.x % kOffsChunksPerBlock] = r1_uniform(A, P.rk, cb + threadIdx.x);
   __syncthreads();
   const uint32_t h = blockIdx.x * kOffsBlock + threadIdx.x;
   if (h >= H) return;
@@ -59,20 +64,25 @@ __global__ void __launch_bounds__(kOffsBlock) k_prep_offsets(const PmPart* __res
   uint16_t* o = P.tab;
   const R1Lane r1v = r1_lane(A, P.rk, h);   // initial tag of hint h is h
   static_assert(kOffsChunksPerBlock == 8, "one 16-B tabT tile of 8 chunks per thread");
-  uint16_t tile[8];
+  for (int tl = 0; tl < kOffsTiles; ++tl) {
+    const uint32_t c0 = cb + tl * kOffsChunksPerBlock;
+    if (c0 >= SS) break;
+    const uint32_t c1 = min(SS, c0 + kOffsChunksPerBlock);
+    uint16_t tile[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) tile[j] = kSkip;   // chunks past SetSize: padding
-  for (uint32_t c = c0; c < c1; ++c) {
-    uint16_t v = (uint16_t)(prf_lo16_split(A, P.rk, r1u[c - c0], r1v, c) & mask);
-    v = (c == own) ? kSkip : v;
-    o[(uint64_t)c * H + h] = v;   // chunk-major: refreshed tags' re-evaluation, fold
-    tile[c - c0] = v;
-    if (h < P.PH) P.cur[(uint64_t)c * P.PH + h] = v;   // hint search (tags start at h)
+    for (int j = 0; j < 8; ++j) tile[j] = kSkip;   // chunks past SetSize: padding
+    for (uint32_t c = c0; c < c1; ++c) {
+      uint16_t v = (uint16_t)(prf_lo16_split(A, P.rk, r1u[tl][c - c0], r1v, c) & mask);
+      v = (c == own) ? kSkip : v;
+      o[(uint64_t)c * H + h] = v;   // chunk-major: refreshed tags' re-evaluation, fold
+      tile[c - c0] = v;
+      if (h < P.PH) P.cur[(uint64_t)c * P.PH + h] = v;   // hint search (tags start at h)
+    }
+    uint4 t4;   // tag-major tile (set expansion): one 16-B store
+    t4.x = tile[0] | ((uint32_t)tile[1] << 16); t4.y = tile[2] | ((uint32_t)tile[3] << 16);
+    t4.z = tile[4] | ((uint32_t)tile[5] << 16); t4.w = tile[6] | ((uint32_t)tile[7] << 16);
+    *reinterpret_cast<uint4*>(P.tabT + tabT_index(H, h, c0)) = t4;
   }
-  uint4 t4;   // tag-major tile (set expansion): one 16-B store
-  t4.x = tile[0] | ((uint32_t)tile[1] << 16); t4.y = tile[2] | ((uint32_t)tile[3] << 16);
-  t4.z = tile[4] | ((uint32_t)tile[5] << 16); t4.w = tile[6] | ((uint32_t)tile[7] << 16);
-  *reinterpret_cast<uint4*>(P.tabT + tabT_index(H, h, c0)) = t4;
 }
 
 template <int W>   // 64-bit words per lane segment: 2 (16-B loads) or 1
@@ -851,7 +861,7 @@ void prep_init(hipStream_t st, const PmPart* d, int np, uint32_t maxH, uint32_t 
   hipLaunchKernelGGL(k_prep_init, dim3(cdiv(n, kBlock), np), dim3(kBlock), 0, st, d);
 }
 void prep_offsets(hipStream_t st, const PmPart* d, int np, uint32_t maxH, uint32_t maxSS) {
-  hipLaunchKernelGGL(k_prep_offsets, dim3(cdiv(maxH, kOffsBlock), cdiv(maxSS, kOffsChunksPerBlock), np),
+  hipLaunchKernelGGL(k_prep_offsets, dim3(cdiv(maxH, kOffsBlock), cdiv(maxSS, kOffsChunksPerBlock * kOffsTiles), np),
                      dim3(kOffsBlock), 0, st, d);
 }
 bool fold_image_ok(uint32_t minCS, uint32_t maxCS, uint32_t E) {
