@@ -55,11 +55,11 @@ SESSIONS = 256  # client sessions per GPU (128: 9.9K q/s, 256: 11.0K, 384: 11.5K
 GROUPS = 4      # lock-step groups (GPU_MAX_HW_QUEUES = 4 hardware queues per process)
 THREADS = 16    # host worker threads of the batched loop (the box gives a GPU 16 host cores)
 SYMBOLS = {"prep_fold": "void pm::k_prep_fold_rot<512>(pm::PmPart const*, unsigned int, unsigned int, unsigned int, "
-                        "unsigned int, unsigned int)",
+                        "unsigned int, unsigned int, unsigned int, unsigned int)",
            "answer": None, "step": "void pm::k_step<2>(pm::PmStep)", "resolve": "void pm::k_resolve<true>(pm::PmStep)",
            "hint_match": "pm::k_match(pm::PmStep)", "prep_offsets": "pm::k_prep_offsets(pm::PmPart const*)",
            "gather": "void pm::k_gather<2>(pm::PmStep)",
-           "match_resolve": "void pm::k_match_resolve<4>(pm::PmStep)"}
+           "match_resolve": "void pm::k_match_resolve_s<2, 256>(pm::PmStep)"}
 # the server answer of search-sized shapes: the small-LDS instance with
 # PM_ANSWER_NT threads per workgroup (pm_query.hip step_answer; 0: generic)
 ANSWER_NT = int(os.environ.get("PM_ANSWER_NT", "128"))
@@ -830,10 +830,12 @@ def main():
         ach_c = comp / (fold["avg_ms"] / 1e3) / 1e9
         fold["clients_per_launch"] = k
         fold["compulsory"] = {"bytes": comp, "achieved": round(ach_c, 1), "frac": round(ach_c / HBM_PEAK_GBS, 4)}
-        # PMC bytes of launches of this shape (k_prep_fold_rot<512>: 3 hint groups of <= 5,120 x 20
-        # column slices per partition, 1,024 threads per workgroup)
-        units = 16 * k * -(-(c0["PrimaryHintNum"] + c0["SetSize"] * c0["MaxQueryPerChunk"]) // 5120)
-        attach_traffic(fold, SYMBOLS["prep_fold"], -(-units // 8) * 8 * (E // 4) * 1024)
+        # PMC bytes of launches of this shape (k_prep_fold_rot<512>: the k clients' hints of a
+        # partition in virtual groups of 5,120, (partition, group) pairs spread over 8 XCDs, 20
+        # column slices in groups of 4, 1,024 threads per workgroup; pm_kernels.hip prep_fold)
+        H0 = c0["PrimaryHintNum"] + c0["SetSize"] * c0["MaxQueryPerChunk"]
+        npv = stats["PartitionNum"] * -(-(k * H0) // 5120)
+        attach_traffic(fold, SYMBOLS["prep_fold"], 8 * -(-npv // 8) * -(-(E // 4) // 4) * 4 * 1024)
         fold["note"] = ("fold bytes (hint x chunk entry reads, SURVEY.md §8d) exceed HBM peak because the "
                         "kernel serves them from LDS; 'compulsory' is the DB read once plus the parity writes "
                         "of the clients folded in one launch")
