@@ -619,19 +619,49 @@ __global__ void __launch_bounds__(kBlock) k_fold_image(uint4* __restrict__ img, 
 }
 
 // Replacement rows (pir.go:345-350): Qpc random offsets per chunk, idx + copy.
+// One workgroup per kReplRows slots: their offsets are hashed once per row
+// (not once per word) into LDS, then the rows are copied in 16-B pieces with
+// every piece of a thread in flight together (32-bit index math throughout).
+constexpr uint32_t kReplRows = 32, kReplIt = (kReplRows * 1024 / 16 + kBlock - 1) / kBlock;   // E <= 128 words
+template <int W>
 __global__ void __launch_bounds__(kBlock) k_prep_repl(const PmPart* __restrict__ parts,
                                                       const uint64_t* __restrict__ db, uint32_t E) {
+  typedef uint64_t vec __attribute__((ext_vector_type(W)));
+  __shared__ uint32_t rrow[kReplRows];   // partition row of each slot, ~0u past the partition's end
   const PmPart& P = parts[blockIdx.y];
-  const uint64_t e = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  const uint64_t nslot = (uint64_t)P.SS * P.Qpc;
-  if (e >= nslot * E) return;
-  const uint64_t slot = e / E;
-  const uint32_t w = (uint32_t)(e % E);
-  const uint32_t c = (uint32_t)(slot / P.Qpc);
-  const uint64_t off = hash4(P.seed, DOM_REPL, P.idx, P.epoch, slot) & (P.CS - 1);
-  const uint64_t r = (uint64_t)c * P.CS + off;
-  if (w == 0) P.ridx[slot] = (uint32_t)r;
-  P.rval[e] = r < P.N ? db[(P.row0 + r) * E + w] : 0;
+  const uint32_t nslot = P.SS * P.Qpc;
+  const uint32_t s0 = blockIdx.x * kReplRows;
+  if (s0 >= nslot) return;   // block-uniform
+  const uint32_t ns = min(kReplRows, nslot - s0);
+  if (threadIdx.x < ns) {
+    const uint32_t slot = s0 + threadIdx.x, c = slot / P.Qpc;
+    const uint64_t off = hash4(P.seed, DOM_REPL, P.idx, P.epoch, slot) & (P.CS - 1);
+    const uint64_t r = (uint64_t)c * P.CS + off;
+    P.ridx[slot] = (uint32_t)r;
+    rrow[threadIdx.x] = r < P.N ? (uint32_t)r : ~0u;
+  }
+  __syncthreads();
+  const uint32_t nseg = E / W, tot = ns * nseg;
+  const uint64_t* const src = db + P.row0 * E;
+  uint64_t* const dst = P.rval + (uint64_t)s0 * E;
+  for (uint32_t x0 = 0; x0 < tot; x0 += kReplIt * kBlock) {
+    vec v[kReplIt];
+    uint32_t at[kReplIt];
+#pragma unroll
+    for (uint32_t u = 0; u < kReplIt; ++u) {
+      const uint32_t x = x0 + u * kBlock + threadIdx.x;
+      at[u] = ~0u;
+      v[u] = vec{};
+      if (x < tot) {
+        const uint32_t i = x / nseg, sg = x - i * nseg, r = rrow[i];
+        at[u] = i * E + sg * W;
+        if (r != ~0u) v[u] = *reinterpret_cast<const vec*>(src + (uint64_t)r * E + sg * W);
+      }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kReplIt; ++u)
+      if (at[u] != ~0u) *reinterpret_cast<vec*>(dst + at[u]) = v[u];
+  }
 }
 
 // Initialization (pir.go:203-255): tags 0..H-1, program points, histogram.
@@ -949,8 +979,10 @@ void prep_fold(hipStream_t st, const PmPart* d, int np, uint32_t maxH, const uin
 }
 void prep_repl(hipStream_t st, const PmPart* d, int np, uint32_t maxRepl, const uint64_t* db,
                uint32_t E) {
-  hipLaunchKernelGGL(k_prep_repl, dim3(cdiv((uint64_t)maxRepl * E, kBlock), np), dim3(kBlock), 0, st,
-                     d, db, E);
+  if (E % 2 == 0)
+    hipLaunchKernelGGL(k_prep_repl<2>, dim3(cdiv(maxRepl, kReplRows), np), dim3(kBlock), 0, st, d, db, E);
+  else
+    hipLaunchKernelGGL(k_prep_repl<1>, dim3(cdiv(maxRepl, kReplRows), np), dim3(kBlock), 0, st, d, db, E);
 }
 void server_answer(hipStream_t st, const PmPart* d, const uint32_t* offs, uint32_t nq, uint32_t SS,
                    const uint64_t* db, uint32_t E, uint64_t* out) {
