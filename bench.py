@@ -832,10 +832,10 @@ def main():
         fold["compulsory"] = {"bytes": comp, "achieved": round(ach_c, 1), "frac": round(ach_c / HBM_PEAK_GBS, 4)}
         # PMC bytes of launches of this shape (k_prep_fold_rot<512>: the k clients' hints of a
         # partition in virtual groups of 5,120, (partition, group) pairs spread over 8 XCDs, 20
-        # column slices in groups of 4, 1,024 threads per workgroup; pm_kernels.hip prep_fold)
+        # column slices in groups of 2 (PM_ROT_LW), 1,024 threads per workgroup; pm_kernels.hip prep_fold)
         H0 = c0["PrimaryHintNum"] + c0["SetSize"] * c0["MaxQueryPerChunk"]
         npv = stats["PartitionNum"] * -(-(k * H0) // 5120)
-        attach_traffic(fold, SYMBOLS["prep_fold"], 8 * -(-npv // 8) * -(-(E // 4) // 4) * 4 * 1024)
+        attach_traffic(fold, SYMBOLS["prep_fold"], 8 * -(-npv // 8) * -(-(E // 4) // 2) * 2 * 1024)
         fold["note"] = ("fold bytes (hint x chunk entry reads, SURVEY.md §8d) exceed HBM peak because the "
                         "kernel serves them from LDS; 'compulsory' is the DB read once plus the parity writes "
                         "of the clients folded in one launch")

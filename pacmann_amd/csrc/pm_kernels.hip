@@ -413,6 +413,10 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_pipe(const PmPart* _
 #define PM_ROT_B128 1   // 16-B reads of the two halves of a row's 32-B slot: half the reads of the 8-B form
                         // and one v_perm per (hint, chunk) for its offset instead of a 64-bit rotation
 #endif
+#ifndef PM_ROT_LW
+#define PM_ROT_LW 2   // column slices of one (partition, group) pair dealt to an XCD back to back
+                      // (64-client fold: 1 -> 31.5-31.7 ms, 2 -> 28.0-28.1, 4 -> 31.4-40.3, 5 -> 27.4-45.5)
+#endif
 #ifndef PM_ROT_ABL
 #define PM_ROT_ABL 0   // diagnostic builds: 1 = no LDS reads, 2 = no staging in the loop, 3 = one row per
                        // wave (no bank conflicts), 4 = 2 and 3, 5 = no fold work at all (B128 form), 6 = 4 without
@@ -437,14 +441,14 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_rot(const PmPart* __
   // and only the partition's last group has idle slots: 157 workgroups per
   // (partition, slice) for 64 SIFT1M clients instead of 3 per client (192),
   // each staging the slice's image once.  Order: XCD x takes the (partition,
-  // group) pairs [x M, (x + 1) M); there, groups of 4 slices of consecutive
+  // group) pairs [x M, (x + 1) M); there, groups of PM_ROT_LW slices of consecutive
   // pairs follow each other (the pairs of one partition read the same image
   // blocks out of the XCD's L2).  (Round 1's order, (partition, group) on XCD
   // pg % 8 with groups of 4 slices of its K clients in turn, was measured
   // 10-15 % faster than all clients of one slice back to back.)  ngc != 0:
   // partitions with fewer than HB hints (small configs) keep ngc groups per
   // client instead (no mixing).
-  constexpr uint32_t LW = 4, HB = kFoldThreads * kRotHPL;
+  constexpr uint32_t LW = PM_ROT_LW, HB = kFoldThreads * kRotHPL;
   const uint32_t xcd = blockIdx.x % 8, kq = blockIdx.x / 8;
   const uint32_t loc = (kq / LW) % M, slice = (kq / (LW * M)) * LW + kq % LW;
   const uint32_t pgv = xcd * M + loc;
@@ -946,7 +950,7 @@ void prep_fold(hipStream_t st, const PmPart* d, int np, uint32_t maxH, const uin
       const uint32_t ngc = minH >= HB ? 0u : (uint32_t)cdiv(maxH, HB);
       const uint32_t nvg = ngc ? K * ngc : (uint32_t)cdiv((uint64_t)K * maxH, HB), npv = (np / K) * nvg;
       const uint32_t M = cdiv(npv, 8);
-      hipLaunchKernelGGL(k_prep_fold_rot<512>, dim3(8 * M * cdiv(nsl, 4) * 4), dim3(kFoldThreads), 0, st, d, E,
+      hipLaunchKernelGGL(k_prep_fold_rot<512>, dim3(8 * M * cdiv(nsl, PM_ROT_LW) * PM_ROT_LW), dim3(kFoldThreads), 0, st, d, E,
                          nvg, nsl, npv, M, K, ngc);
       return;
     }
