@@ -417,6 +417,10 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_pipe(const PmPart* _
 #define PM_ROT_LW 2   // column slices of one (partition, group) pair dealt to an XCD back to back
                       // (64-client fold: 1 -> 31.5-31.7 ms, 2 -> 28.0-28.1, 4 -> 31.4-40.3, 5 -> 27.4-45.5)
 #endif
+#ifndef PM_ROT_PF
+#define PM_ROT_PF 0   // L2 prefetch of the image block two buffers ahead (measured no gain once the
+                      // staging overlaps the fold: 24.2-25.4 vs 24.8-25.0 ms per 64-client launch)
+#endif
 #ifndef PM_ROT_ABL
 #define PM_ROT_ABL 0   // diagnostic builds: 1 = no LDS reads, 2 = no staging in the loop, 3 = one row per
                        // wave (no bank conflicts), 4 = 2 and 3, 5 = no fold work at all (B128 form), 6 = 4 without
@@ -432,6 +436,7 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_rot(const PmPart* __
   // static (not extern) LDS: its address is a constant the reads fold into
   // their offsets
   __shared__ __attribute__((aligned(16))) uint32_t rot_lds[2 * BUFW];
+  __shared__ uint32_t pf_lds[PM_ROT_PF ? kFoldThreads : 1];   // landing area of the L2 prefetch (never read)
   constexpr uint32_t ITEMS = CS * 8;   // 16-B staging items per buffer (4 chunks x CS rows x 2)
   static_assert(ITEMS % kFoldThreads == 0, "whole staging items per thread");
   constexpr uint32_t G = ITEMS / kFoldThreads;
@@ -507,18 +512,39 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_rot(const PmPart* __
       const bool inB = v >= vb;
       out[k] = *reinterpret_cast<const PM_G u32x2*>(
           (const PM_G char*)(inB ? tabB : tabA) + (uint32_t)tabT_index(H, v - (inB ? vb : hA), 4 * b) * 2u);
-      if (PM_ROT_B128 && vl + k * kFoldThreads >= v1) out[k] = u32x2{0xffffffffu, 0xffffffffu};   // kSkip: zero line
     }
   };
   for (uint32_t x = tid; x < 2 * LINE; x += kFoldThreads) rot_lds[(x / LINE) * BUFW + CS * LINE + x % LINE] = 0;
   u32x2 tv[kRotHPL], tn[kRotHPL];
   stage(0, 0);
+  // lane slots past the group read the zero line (kSkip).  Applied when a tile
+  // is taken into use, not at its load: a select on the loaded value right
+  // after the load made every iteration wait for its prefetched staging and
+  // tabT loads before folding the current buffer (the double buffer's
+  // overlap lost)
+  auto skip_idle = [&](u32x2* t) {
+#pragma unroll
+    for (int k = 0; k < kRotHPL; ++k)
+      if (PM_ROT_B128 && vl + k * kFoldThreads >= v1) t[k] = u32x2{0xffffffffu, 0xffffffffu};
+  };
   load_tab(0, tv);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  skip_idle(tv);
   const char* lds0 = reinterpret_cast<const char*>(rot_lds);
   for (uint32_t b = 0; b < nbuf; ++b) {
     if (b + 1 < nbuf) { if (PM_ROT_ABL != 2 && PM_ROT_ABL < 4) stage(b + 1, (b + 1) & 1); if (PM_ROT_ABL != 6) load_tab(b + 1, tn); }
+    // L2 prefetch of block b + 2 (no third LDS buffer fits): one 4-B LDS-DMA load
+    // per 128-B line by waves 0-7, issued after this iteration's staging and
+    // tabT loads, so the counted wait below leaves only it in flight
+    // (LDS-DMA intrinsics keep their order, so every staging load precedes it;
+    // a tabT load the compiler places after it is covered by its own wait)
+    // (issued by every thread, branch-free: two threads per line; past the last
+    // block it re-reads the last one)
+    if (PM_ROT_PF)
+      __builtin_amdgcn_global_load_lds(
+          (g_cvoid_t*)(img + (uint64_t)min(b + 2, nbuf - 1) * kRotBufBytes + (tid & (kFoldThreads / 2 - 1)) * 128u),
+          (lds_void_t*)(pf_lds + (tid & ~63u)), 4, 0, 0);
     const uint32_t lb = (b & 1) * BUFW * 4;   // byte offset of this buffer
 #if PM_ROT_B128
     {
@@ -586,10 +612,19 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_rot(const PmPart* __
         acc[k][t] = xor3(xor3(acc[k][t], v[0][t], v[1][t]), v[2][t], v[3][t]);
     }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if (PM_ROT_PF) {
+      // the prefetch may stay in flight: counted wait, then a raw barrier
+      // (__syncthreads' fence would wait for every load, the prefetch included)
+      asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
 #pragma unroll
     for (int k = 0; k < kRotHPL; ++k) tv[k] = PM_ROT_ABL == 6 ? tv[k] + u32x2{1u, 3u} : tn[k];
+    skip_idle(tv);
   }
 #pragma unroll
   for (int k = 0; k < kRotHPL; ++k) {
