@@ -1266,7 +1266,7 @@ __global__ void __launch_bounds__(NT) k_match_resolve_s(PmStep S) {
   __shared__ ResolveLds<3> L;
   __shared__ uint32_t s_m[kSpecSubs][NU][NW][2];   // each (sub-query, row block, wave): first two matches
   const uint32_t p = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint32_t b0 = step_sb(S, p), n = step_sb(S, p + 1) - b0;
+  const uint32_t b0 = S.sb[p], n = S.sb[p + 1] - b0;   // device descriptor (never in the arguments here)
   if (n == 0) return;
   const PmPart P = S.parts[p];
   const uint32_t lg = P.log2CS, mask = P.CS - 1;
@@ -1306,17 +1306,23 @@ __global__ void __launch_bounds__(NT) k_match_resolve_s(PmStep S) {
     }
     if (lane == 0) L.s_fqn = fq;
   }
+  // every request of the partition at once, lane k of each wave holding
+  // sub-query k (n <= 64): one round trip, then the search-row loads of G
+  // sub-queries at a time.  (Loaded per sub-query inside the batch, each
+  // descriptor load's wait also drained the previous sub-query's row loads:
+  // the batch's loads were serialised.)
+  PmSub mine{0, SUB_NONE, 0};
+  if (lane < n) mine = step_sub(S, b0 + lane);
   // the match: sub-queries j0 .. j0 + G - 1 at a time
   for (uint32_t j0 = 0; j0 < n; j0 += G) {
     uint32_t off[G];
     uint4 v[G][NU];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      PmSub sub{0, SUB_NONE, 0};
-      if (j0 + g < n) sub = step_sub(S, b0 + j0 + g);
-      const uint32_t kind = __builtin_amdgcn_readfirstlane(sub.kind);
-      const uint64_t idx = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(sub.idx >> 32)) << 32) |
-                           __builtin_amdgcn_readfirstlane((uint32_t)sub.idx);
+      const uint32_t jj = min(j0 + g, n - 1);   // uniform
+      const uint32_t kind = j0 + g < n ? (uint32_t)__builtin_amdgcn_readlane(mine.kind, jj) : (uint32_t)SUB_NONE;
+      const uint64_t idx = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(mine.idx >> 32), jj) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane((uint32_t)mine.idx, jj);
       const bool lv = kind == SUB_REAL && idx < P.N;
       off[g] = lv ? (uint32_t)(idx & mask) : kNone;
       const PM_G uint16_t* crow = P.cur + (uint64_t)(lv ? (uint32_t)(idx >> lg) : 0u) * P.PH;
