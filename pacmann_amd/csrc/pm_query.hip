@@ -1715,10 +1715,15 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, LDS& L)
           typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
           for (uint32_t i0 = sl; i0 < P.SS; i0 += kG * nsl) {
             uint32_t rr[kG];   // partition rows (< 2^32): 32-bit, so the batch fits 64 VGPRs
+            // the batch's set offsets: unconditional LDS reads (clamped index),
+            // all in flight before one wait (a read inside each bounds branch
+            // waited for its own result before the next was issued)
+#pragma unroll
+            for (int u = 0; u < kG; ++u) rr[u] = qo[min(i0 + u * nsl, P.SS - 1)];
 #pragma unroll
             for (int u = 0; u < kG; ++u) {
               const uint32_t i = i0 + u * nsl;
-              rr[u] = i < P.SS ? i * P.CS + qo[i] : ~0u;
+              rr[u] = i < P.SS ? i * P.CS + rr[u] : ~0u;
             }
             u64x2 x[kG];
 #pragma unroll
