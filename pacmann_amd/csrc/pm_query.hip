@@ -1385,24 +1385,43 @@ __global__ void __launch_bounds__(NT) k_match_resolve_s(PmStep S) {
   }
   __syncthreads();
   resolve_role<3, NT, false>(S, p, L);
+  // The query set of every successful sub-query (pir.go:424-444: the hit
+  // hint's offsets, its program point, the chunk's replacement), expanded
+  // here so that k_answer_s reads it with its resolution record in one round
+  // trip instead of gathering the tag's PRF row after the record arrives.
+  // One 16-B tabT tile (8 chunks) per thread; S.qw words per sub-query.
+  // Thread tid takes tile x = (tid - 64) mod NT first: waves 1.. get here
+  // while wave 0 still runs the chain, and load that tile (and the chunk's
+  // replacement row) for the usual outcome -- hit = the first candidate (tag
+  // s_t1), in-chunk index = the prediction (s_sing) -- so that after the chain
+  // the expansion only checks the guess.
+  const uint32_t nt8 = S.qset ? S.qw / 8 : 0;
+  const uint32_t x0 = (tid + NT - 64) % NT;
+  uint4 gv = make_uint4(0, 0, 0, 0);
+  uint32_t gr = 0, gtag = kNone, ging = kNone;
+  if (tid >= 64 && x0 < n * nt8) {
+    const uint32_t j = x0 / nt8, c0 = 8 * (x0 % nt8);
+    if (L.s_kind[j] == SUB_REAL && L.s_c1[j] != kNone) {
+      gtag = L.s_t1[j];
+      if (c0 < P.SS) gv = *reinterpret_cast<const PM_G uint4*>(P.tabT + tabT_index(P.H, gtag, c0));
+      const uint32_t ch = L.s_chunk[j], sg = L.s_sing[j];
+      if (ch - c0 < 8u && sg < P.Qpc) { ging = sg; gr = P.ridx[ch * P.Qpc + sg]; }
+    }
+  }
   __syncthreads();
   if (L.fin && threadIdx.x == 0) chain_rearm(S);
   if (S.qset) {
-    // The query set of every successful sub-query (pir.go:424-444: the hit
-    // hint's offsets, its program point, the chunk's replacement), expanded
-    // here so that k_answer_s reads it with its resolution record in one round
-    // trip instead of gathering the tag's PRF row after the record arrives.
-    // One 16-B tabT tile (8 chunks) per thread; S.qw words per sub-query.
-    const uint32_t nt8 = S.qw / 8;
-    for (uint32_t x = tid; x < n * nt8; x += NT) {
+    for (uint32_t x = x0; x < n * nt8; x += NT) {
       const uint32_t j = x / nt8, t = x % nt8;
       const PmRes r = L.s_res[j];
       if (r.status != ST_OK) continue;
       const uint32_t c0 = 8 * t;
       const bool rc = r.chunk - c0 < 8u;
-      const uint32_t ro = rc ? P.ridx[r.chunk * P.Qpc + r.ing] & mask : 0u;
+      const bool first = x == x0 && tid >= 64;   // this thread's guessed tile
+      const uint32_t ro = rc ? (first && r.ing == ging ? gr : P.ridx[r.chunk * P.Qpc + r.ing]) & mask : 0u;
       uint4 v = make_uint4(0, 0, 0, 0);
-      if (c0 < P.SS) v = *reinterpret_cast<const PM_G uint4*>(P.tabT + tabT_index(P.H, r.tag, c0));
+      if (first && r.tag == gtag) v = gv;
+      else if (c0 < P.SS) v = *reinterpret_cast<const PM_G uint4*>(P.tabT + tabT_index(P.H, r.tag, c0));
       uint32_t w[4] = {v.x, v.y, v.z, v.w};
       auto put = [&](uint32_t e, uint32_t o) {
         w[e >> 1] = (w[e >> 1] & ~(0xffffu << (16 * (e & 1)))) | ((o & 0xffffu) << (16 * (e & 1)));
