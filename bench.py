@@ -931,8 +931,12 @@ def main():
             import datetime
 
             import torch
-            torch.cuda.set_device(local)
-            nccl_group = dist.new_group(backend="nccl", timeout=datetime.timedelta(seconds=180))
+            try:
+                torch.cuda.set_device(local)
+                nccl_group = dist.new_group(backend="nccl", timeout=datetime.timedelta(seconds=180))
+            except Exception as e:   # recorded; the shards then combine over the gloo group
+                nccl_group = None
+                out["rccl_group_error"] = f"{type(e).__name__}: {e}"
         for key, nm, n_entries, layout in (("config3_bigann_100m", "BIGANN-100M-shaped (configs[3])",
                                             100_000_000, ws),
                                            ("config4_bigann_1b", "BIGANN-1B-shaped (configs[4]), 8-way layout",
