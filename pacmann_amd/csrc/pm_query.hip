@@ -36,7 +36,8 @@ namespace pm {
 
 constexpr int kAnsBlock = 512;
 #ifndef PM_ANSWER_KG
-#define PM_ANSWER_KG 8   // k_answer gather: rows per thread in flight together (12: 27 VGPRs spill at 8 waves)
+#define PM_ANSWER_KG 6   // k_answer gather: rows per thread in flight together (no VGPR spill at 8 waves;
+                         // alone 76.0-76.7 us vs 77.3 at 8 and 81-82 at 10, which spills 9 VGPRs)
 #endif
 constexpr uint32_t kNone = 0xffffffffu;
 
