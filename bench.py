@@ -578,6 +578,36 @@ def dist_init():
     return dist, dist.get_rank(), ws, local % max(ndev, 1)
 
 
+def rccl_group(dist, local, out):
+    """An RCCL (nccl backend) group over all ranks for the sharded blocks'
+    combine, or None (the shards then combine over the gloo group).  RCCL
+    creates its communicator at the first collective, so a one-element
+    all-reduce runs inside the attempt; the ranks then agree over gloo (MIN of
+    their success flags), so either every rank uses RCCL or none does."""
+    import datetime
+
+    import torch
+    grp, ok = None, 1
+    try:
+        torch.cuda.set_device(local)
+        grp = dist.new_group(backend="nccl", timeout=datetime.timedelta(seconds=180))
+        t = torch.ones(1, device=f"cuda:{local}")
+        dist.all_reduce(t, group=grp)
+        torch.cuda.synchronize(local)
+        ok = int(t.item() == dist.get_world_size())
+        if not ok:
+            out["rccl_group_error"] = f"probe all-reduce gave {t.item()}"
+    except Exception as e:   # recorded; the shards then combine over the gloo group
+        ok = 0
+        out["rccl_group_error"] = f"{type(e).__name__}: {e}"
+    flag = torch.tensor([ok], dtype=torch.int32)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)   # default (gloo) group: every rank decides alike
+    if int(flag.item()) != 1:
+        out.setdefault("rccl_group_error", "another rank could not use RCCL")
+        return None
+    return grp
+
+
 def cpu_baseline(v, g, q0, warmup, answers0, ctx, pir_seed, search_seed, k=K_TOP):
     """The oracle (single-thread C++ restatement of the Go/AVX path; its hint
     fold on one thread like the reference's ThreadNum = 1) replaying session
@@ -928,15 +958,7 @@ def main():
     if not args.no_bigann:
         nccl_group = None
         if dist and args.combine == "rccl":
-            import datetime
-
-            import torch
-            try:
-                torch.cuda.set_device(local)
-                nccl_group = dist.new_group(backend="nccl", timeout=datetime.timedelta(seconds=180))
-            except Exception as e:   # recorded; the shards then combine over the gloo group
-                nccl_group = None
-                out["rccl_group_error"] = f"{type(e).__name__}: {e}"
+            nccl_group = rccl_group(dist, local, out)
         for key, nm, n_entries, layout in (("config3_bigann_100m", "BIGANN-100M-shaped (configs[3])",
                                             100_000_000, ws),
                                            ("config4_bigann_1b", "BIGANN-1B-shaped (configs[4]), 8-way layout",

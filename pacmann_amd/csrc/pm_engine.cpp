@@ -348,7 +348,7 @@ struct Engine {
   size_t pf_off = 0, pf_len = ~size_t(0);   // bytes of each result row the caller reads next
   bool rows_partial = false;   // this call's caller reads ONLY those bytes (GetVertexInfo): the rest is not sent
   HostBuf desc_h, out_h, err_h, src_h;   // src_h: pm_batchpir_query_dev's row pointers
-  DevBuf stage_d;                        // ... and its rows of a multi-step query
+  HostBuf stage_h;                       // ... and its rows of a multi-step query (pinned staging)
   hipEvent_t dev_ev = nullptr;           // ... its completion, for the consumer's stream
   ~Engine() { if (dev_ev) (void)hipEventDestroy(dev_ev); }
   std::vector<PartHost> parts;
@@ -501,7 +501,9 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
     HIPCHK(hipStreamSynchronize(ctx->stream));
   }
   // the fold image: a second copy of the owned partitions' rows, laid out for
-  // k_prep_fold_rot (CS 512 shapes only)
+  // k_prep_fold_rot (CS 512 shapes only; PM_FOLD_ROT=0 disables it).  It is
+  // skipped, and the fold reads the rows themselves (k_prep_fold_pipe), when
+  // it would take more than a quarter of the device memory still free.
   uint64_t off_img = 0;
   if (!g->owned_list.empty() && pmk::fold_image_ok(g->minCS, g->maxCS, (uint32_t)g->E)) {
     for (uint32_t i : g->owned_list) {
@@ -509,6 +511,16 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
       d.img = (const uint64_t*)(uintptr_t)off_img;
       off_img += pmk::fold_image_words(d.SS, (uint32_t)g->E);
     }
+    size_t free_b = 0, total_b = 0;
+    if (!server && hipMemGetInfo(&free_b, &total_b) == hipSuccess && off_img * 8 > free_b / 4) {
+      for (uint32_t i : g->owned_list) g->parts[i].d.img = nullptr;
+      off_img = 0;
+    } else if (server && !server->img->p) {   // the server went without one
+      for (uint32_t i : g->owned_list) g->parts[i].d.img = nullptr;
+      off_img = 0;
+    }
+  }
+  if (off_img) {
     if (server) {
       g->img = server->img;
     } else {
@@ -1400,13 +1412,28 @@ extern "C" int pm_batchpir_query_ok(pm_batchpir* h, const uint64_t* ids, uint64_
 // copied HBM to HBM by one k_gather_rows launch; only the row pointers come
 // from the host.  A query that needed several steps (a partition at its budget
 // mid-batch, pir.go:527-530) has its rows in host memory and uploads them.
+static int query_dev_impl(Engine* g, const uint64_t* ids, uint64_t n, uint64_t* dev_out, hipStream_t cs);
 extern "C" int pm_batchpir_query_dev(pm_batchpir* h, const uint64_t* ids, uint64_t n, uint64_t* dev_out,
                                      void* stream) {
   Engine* g = &h->e;
   if (n && (!ids || !dev_out)) return fail(PM_EINVAL, "NULL argument");
+  auto t = Clock::now();
+  const int r = query_dev_impl(g, ids, n, dev_out, (hipStream_t)stream);
+  g->ctx->host_add(HT_BATCH_QUERY, ms_since(t));
+  return r;
+}
+static int query_dev_impl(Engine* g, const uint64_t* ids, uint64_t n, uint64_t* dev_out, hipStream_t cs) {
   const uint64_t E = g->E;
   hipStream_t st = g->ctx->stream;
   HIPCHK(hipSetDevice(g->ctx->device));
+  if (!g->dev_ev) HIPCHK(hipEventCreateWithFlags(&g->dev_ev, hipEventDisableTiming));
+  // dev_out may still be read by work the consumer queued before this call
+  // (its last collective, a kernel on the previous rows): the engine's writes
+  // into it wait for that work (stream order, no host synchronisation)
+  if (cs) {
+    HIPCHK(hipEventRecord(g->dev_ev, cs));
+    HIPCHK(hipStreamWaitEvent(st, g->dev_ev, 0));
+  }
   bool fast = false;
   CHK(bq_prepare(g, ids, n, &fast));
   if (fast) {
@@ -1429,27 +1456,29 @@ extern "C" int pm_batchpir_query_dev(pm_batchpir* h, const uint64_t* ids, uint64
     }
     pmk::gather_rows(st, src, n, (uint32_t)E, dev_out);
     HIPCHK(hipGetLastError());
-  } else {   // rows collected on the host by the multi-step path
-    std::vector<uint64_t> rows(n * (E + 1), 0);
+  } else {   // rows collected on the host by the multi-step path (a partition at its budget mid-batch)
     std::vector<uint8_t> ok(n);
     std::vector<const uint64_t*> rp(n);
-    CHK(batch_query_impl_rows(g, ids, n, rp.data(), ok.data()));
+    CHK(batch_query_impl_rows(g, ids, n, rp.data(), ok.data()));   // runs the re-preprocessing trigger itself
+    // staged in pinned memory: the copy is asynchronous, so the staging buffer
+    // must outlive this call (it is the engine's; the next call's copy is
+    // ordered after this one on the same stream)
+    HIPCHK(hipStreamSynchronize(st));   // the previous call's copy out of stage_h is done
+    CHK(g->stage_h.reserve(std::max<uint64_t>(1, n) * (E + 1) * 8));
+    uint64_t* rows = g->stage_h.as<uint64_t>();
     for (uint64_t i = 0; i < n; ++i) {
       memcpy(&rows[i * (E + 1)], rp[i], E * 8);
       rows[i * (E + 1) + E] = ok[i];
     }
-    HIPCHK(hipMemcpyAsync(dev_out, rows.data(), rows.size() * 8, hipMemcpyHostToDevice, st));
-    HIPCHK(hipStreamSynchronize(st));
-    return 0;   // batch_query_impl_rows ran the re-preprocessing trigger itself
+    HIPCHK(hipMemcpyAsync(dev_out, rows, n * (E + 1) * 8, hipMemcpyHostToDevice, st));
   }
-  if (stream) {   // the consumer's stream waits for the rows; no host synchronisation
-    if (!g->dev_ev) HIPCHK(hipEventCreateWithFlags(&g->dev_ev, hipEventDisableTiming));
+  if (cs) {   // the consumer's stream waits for the rows; no host synchronisation
     HIPCHK(hipEventRecord(g->dev_ev, st));
-    HIPCHK(hipStreamWaitEvent((hipStream_t)stream, g->dev_ev, 0));
+    HIPCHK(hipStreamWaitEvent(cs, g->dev_ev, 0));
   } else {
     HIPCHK(hipStreamSynchronize(st));
   }
-  return bq_tail(g, n);   // stream-ordered after the copy
+  return fast ? bq_tail(g, n) : 0;   // stream-ordered after the copy
 }
 extern "C" int pm_batchpir_stats_get(pm_batchpir* h, pm_batchpir_stats* s) {
   const Engine& g = h->e;

@@ -74,7 +74,6 @@ class ShardedBatchPIR:
             if len(hip_runtimes()) > 1:
                 raise RuntimeError("two HIP runtimes are mapped (libpacmann.so was loaded before torch): "
                                    "import torch before creating any pacmann_amd context")
-        self._buf = None
 
     def Preprocessing(self):
         self.pir.Preprocessing()
@@ -82,20 +81,17 @@ class ShardedBatchPIR:
     def DummyPreprocessing(self):
         self.pir.DummyPreprocessing()
 
-    def _rows(self, n: int):
-        import torch
-        if self._buf is None or self._buf.shape[0] < n:
-            self._buf = torch.empty((max(n, 1), self.E + 1), dtype=torch.int64, device=f"cuda:{self.device}")
-        return self._buf[:n]
-
     def QueryDevice(self, idx):
-        """The combined responses as one device tensor [len(idx), E + 1] (int64
-        view of the uint64 words; column E = success flag), every rank holding
-        the same values after the in-place all-reduce."""
+        """The combined responses as a fresh device tensor [len(idx), E + 1]
+        (int64 view of the uint64 words; column E = success flag), every rank
+        holding the same values after the in-place all-reduce.  The tensor
+        comes from torch's caching allocator on the current stream, and the
+        engine's writes into it wait for that stream's earlier work
+        (pm_batchpir_query_dev), so a caller may keep using earlier results."""
         import torch
         ids = np.ascontiguousarray(idx, dtype=np.uint64).ravel()
         with torch.cuda.device(self.device):
-            rows = self._rows(len(ids))
+            rows = torch.empty((len(ids), self.E + 1), dtype=torch.int64, device=f"cuda:{self.device}")
             stream = torch.cuda.current_stream()
             self.pir.QueryDevice(ids, rows.data_ptr(), stream.cuda_stream)
             if self.nccl:

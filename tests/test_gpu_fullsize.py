@@ -156,35 +156,52 @@ def test_batch_pir_msmarco_full_vs_oracle(ctx, oracle):
 # ---------------------------------------------------------------------------
 # private search at full size: SIFT1M (configs[1]) and MS-MARCO d=192
 # ---------------------------------------------------------------------------
-def _sessions_vs_oracle(ctx, oracle, v, graph, qs_per_session, k, seeds, ngroups, nthreads):
+def _sessions_vs_oracle(ctx, oracle, v, graph, qs_per_session, k, seeds, ngroups, nthreads, check=None,
+                        oracle_workers=8, timing=False):
+    """Serve the sessions through pm_search_loop_batched, then replay each
+    checked session (`check`: indices, default all) as an independent oracle
+    client with the same seeds and queries.  Answers, counts and batch-PIR
+    counters must be equal.  Each oracle client is freed as soon as it has
+    been compared (a SIFT1M client holds 0.85 GB, an MS-MARCO one 3.4 GB).
+    timing: kernel timings of the shared steps are returned too."""
     import pacmann_amd as pm
     base = pm.PIRGraphInfo(v, graph, pir_seed=seeds[0][0], search_seed=seeds[0][1], ctx=ctx)
     base.Preprocess()
     sess = [base] + [base.Session(p, s) for p, s in seeds[1:]]
     for s in sess[1:]:
         s.Preprocess()
+    if timing:
+        sess[0].ctx.timing_reset()
+        sess[0].ctx.timing(2)
     ans, wall, on, mt = pm.search_loop_batched(sess, qs_per_session, k, 20, 3, ngroups, nthreads)
+    kt = None
+    if timing:
+        sess[0].ctx.timing(False)
+        kt = {n: sess[0].ctx.timing_get(n) for n in ("match_resolve", "answer", "prep_fold", "prep_offsets")}
     assert wall > 0 and (mt > 0).all()
+    got = [(sess[i].counts(), sess[i].PIR.stats()) for i in range(len(seeds))]
 
     def run_oracle(i):   # one C call per phase: the oracle sessions run on host threads side by side
         p, s = seeds[i]
         o = oracle.Graph(v, graph, pir_seed=p, search_seed=s)
         o.Preprocess()
         oa, _, _ = o.SearchLoop(qs_per_session[i], k, 20, 3)
-        return o, oa
+        res = (oa, o.counts(), o.pir().stats())
+        del o
+        return res
 
     from concurrent.futures import ThreadPoolExecutor
-    with ThreadPoolExecutor(max_workers=min(8, len(seeds))) as ex:
-        runs = list(ex.map(run_oracle, range(len(seeds))))
-    for i, (o, oa) in enumerate(runs):
-        bad = np.where((ans[i] != oa).any(axis=1))[0]
-        assert len(bad) == 0, (i, bad[:5].tolist())
-        assert sess[i].counts() == o.counts(), i
-        ps, po = sess[i].PIR.stats(), o.pir().stats()
-        for key in ("FinishedBatchNum", "QueriesMadeInPartition", "PrepCount"):
-            assert ps[key] == po[key], (i, key)
-        assert ps["PrepCount"] >= 2, i
-    return ans
+    idx = list(range(len(seeds))) if check is None else list(check)
+    with ThreadPoolExecutor(max_workers=min(oracle_workers, len(idx))) as ex:
+        for i, (oa, oc, po) in zip(idx, ex.map(run_oracle, idx)):
+            bad = np.where((ans[i] != oa).any(axis=1))[0]
+            assert len(bad) == 0, (i, bad[:5].tolist())
+            assert got[i][0] == oc, i
+            ps = got[i][1]
+            for key in ("FinishedBatchNum", "QueriesMadeInPartition", "PrepCount"):
+                assert ps[key] == po[key], (i, key)
+            assert ps["PrepCount"] >= 2, i
+    return (ans, kt) if timing else ans
 
 
 def test_search_sift1m_full_sessions(ctx, oracle):
@@ -256,3 +273,57 @@ def test_search_msmarco_full_shared_step(ctx, oracle):
     qs = np.stack([(v[rng.integers(0, N, 47)] + rng.normal(0, 0.1, (47, 192))).astype(np.float32)
                    for _ in seeds])
     _sessions_vs_oracle(ctx, oracle, v, graph, qs, 100, seeds, ngroups=1, nthreads=8)
+
+
+# ---------------------------------------------------------------------------
+# the bench's exact serving shapes (bench.py: SIFT1M 256 sessions in 4
+# lock-step groups of 64; MS-MARCO 64 sessions in 2 groups of 32)
+# ---------------------------------------------------------------------------
+def test_search_sift1m_bench_group_shape(ctx, oracle):
+    """configs[1] at the bench's launch shapes: 64 sessions in ONE lock-step
+    group over the full SIFT1M DB (1e6 x 640 B, 16 partitions each), so every
+    round is one shared step over 64 x 16 = 1,024 partitions and 6,144
+    sub-queries (k_match_resolve_s, k_answer_s with a grid of 6,144
+    workgroups = 786,432 threads), and the 64 sessions' simultaneous
+    maintenance after query 22 (window 23) folds all 64 clients in one
+    k_prep_fold_rot launch (virtual hint groups mixing the clients).  24
+    queries each, so every session re-preprocesses; all 64 sessions are
+    replayed by independent oracle clients (pir.go:303-352, 354-471) and must
+    equal them answer for answer, with equal counters."""
+    from pacmann_amd.synth import random_graph, sift_like_vectors
+    N, S = 1_000_000, 64
+    v = sift_like_vectors(N, 128, seed=103)
+    graph = random_graph(N, 32, seed=203)
+    rng = np.random.default_rng(23)
+    seeds = [(300 + i, 400 + i) for i in range(S)]
+    qs = np.clip(np.rint(v[rng.integers(0, N, S * 24)] + rng.normal(0, 8, (S * 24, 128))), 0, 255)
+    qs = qs.astype(np.float32).reshape(S, 24, 128)
+    _, kt = _sessions_vs_oracle(ctx, oracle, v, graph, qs, 10, seeds, ngroups=1, nthreads=16, oracle_workers=16,
+                                timing=True)
+    # the launch shapes the bench measures actually ran
+    n_ans, _, by = kt["answer"]
+    assert n_ans == 24 * 20, n_ans             # one answer launch per shared step
+    assert kt["match_resolve"][0] == n_ans     # the fused match + resolve each step
+    assert by / n_ans > 300e6                  # 6,144 sub-queries x ~80.5 KB of answer bytes
+    n_fold, _, fby = kt["prep_fold"]
+    assert n_fold == 1 and fby > 60 * 15.8e9, (n_fold, fby)   # 64 clients' folds in one launch
+
+
+def test_search_msmarco_bench_group_shape(ctx, oracle):
+    """The MS-MARCO private-search block's launch shape: 32 sessions in ONE
+    lock-step group (a shared step of 32 x 16 partitions of CS 1,024 / SS 196 /
+    E 112, 3,072 sub-queries) over the full 3,201,821 x d = 192 DB, 47 queries
+    each (window 45: every session re-preprocesses, the 32 clients folded in
+    one launch), k = 100; every session equals an independent oracle run."""
+    from pacmann_amd.synth import msmarco_like_vectors, random_graph
+    N, S = 3_201_821, 32
+    v = msmarco_like_vectors(N, 192, seed=25)
+    graph = random_graph(N, 32, seed=26)
+    rng = np.random.default_rng(28)
+    seeds = [(500 + i, 600 + i) for i in range(S)]
+    qs = (v[rng.integers(0, N, S * 47)] + rng.normal(0, 0.1, (S * 47, 192))).astype(np.float32).reshape(S, 47, 192)
+    _, kt = _sessions_vs_oracle(ctx, oracle, v, graph, qs, 100, seeds, ngroups=1, nthreads=16, oracle_workers=8,
+                                timing=True)
+    n_ans, _, by = kt["answer"]
+    assert n_ans == 47 * 20 and kt["match_resolve"][0] == n_ans
+    assert kt["prep_fold"][0] == 1

@@ -29,18 +29,28 @@ def _db():
     return np.random.default_rng(13).integers(0, 2**64, size=N * E, dtype=np.uint64)
 
 
-def _batches(n):
+def _batches(n, wide=False):
+    """3B ids per batch (6 sub-queries per partition), or with wide=True 6B
+    (12 per partition) whose first 16 ids are new ids of partition 0: that
+    partition's FinishedQueryNum then tracks QueriesMadeInPartition, so late
+    in the window a batch would take it past MaxQueryNum and the engine serves
+    it by the multi-step path (one sub-query at a time, pir.go:527-530)."""
     rng = np.random.default_rng(14)
-    for _ in range(n):
-        q = rng.integers(0, N, size=3 * B, dtype=np.uint64)
-        q[4] = q[1]
+    PS = N // (B // 2)
+    for b in range(n):
+        if wide:   # partition 0: 16 ids never asked before (no local-cache hits); the rest elsewhere
+            q = rng.integers(PS, N, size=6 * B, dtype=np.uint64)
+            q[:16] = np.arange(b * 16, b * 16 + 16, dtype=np.uint64) % np.uint64(PS)
+        else:
+            q = rng.integers(0, N, size=3 * B, dtype=np.uint64)
+            q[4] = q[1]
         yield q
 
 
-def _nbatches():
+def _nbatches(wide=False):
     from oracle import oracle as O
     o = O.PianoPIR(N // (B // 2), E * 8, np.zeros(N // (B // 2) * E, np.uint64), F)
-    return int(o.Config()["MaxQueryNum"] // 3) + 6   # past the re-preprocessing trigger
+    return int(o.Config()["MaxQueryNum"] // (6 if wide else 3)) + 6   # past the re-preprocessing trigger
 
 
 def _free_port():
@@ -49,7 +59,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _rank(rank, world, port, out_dir, backend, nb):
+def _rank(rank, world, port, out_dir, backend, nb, wide):
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -62,7 +72,7 @@ def _rank(rank, world, port, out_dir, backend, nb):
         assert pir.device_path and pir.pir.nshards == world and pir.pir.shard == rank
         pir.Preprocessing()
         rows, oks = [], []
-        for q in _batches(nb):
+        for q in _batches(nb, wide):
             dev = pir.QueryDevice(q)
             assert dev.is_cuda and dev.shape == (len(q), E + 1)
             h = dev.cpu().numpy().view(np.uint64)
@@ -70,26 +80,28 @@ def _rank(rank, world, port, out_dir, backend, nb):
             oks.append(h[:, E].copy())
         np.save(os.path.join(out_dir, f"rows{rank}.npy"), np.stack(rows))
         np.save(os.path.join(out_dir, f"ok{rank}.npy"), np.stack(oks))
-        np.save(os.path.join(out_dir, f"prep{rank}.npy"), np.array([pir.stats()["PrepCount"]]))
+        steps = pir.pir.ctx.timing_get("host_step_launch")[0]   # steps run (a multi-step batch runs several)
+        np.save(os.path.join(out_dir, f"prep{rank}.npy"), np.array([pir.stats()["PrepCount"], steps]))
     finally:
         dist.destroy_process_group()
 
 
-def _run(world, backend, oracle):
+def _run(world, backend, oracle, wide=False):
     import torch.multiprocessing as mp
-    nb = _nbatches()
+    nb = _nbatches(wide)
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_rank, args=(world, _free_port(), d, backend, nb), nprocs=world, join=True)
+        mp.spawn(_rank, args=(world, _free_port(), d, backend, nb, wide), nprocs=world, join=True)
         rows = [np.load(os.path.join(d, f"rows{r}.npy")) for r in range(world)]
         oks = [np.load(os.path.join(d, f"ok{r}.npy")) for r in range(world)]
         preps = [int(np.load(os.path.join(d, f"prep{r}.npy"))[0]) for r in range(world)]
+        steps = [int(np.load(os.path.join(d, f"prep{r}.npy"))[1]) for r in range(world)]
     for r in range(1, world):   # every rank holds the combined answer
         assert np.array_equal(rows[r], rows[0]) and np.array_equal(oks[r], oks[0])
     db = _db()
     o = oracle.SimpleBatchPianoPIR(N, E * 8, B, db, F, seed=SEED)
     o.Preprocessing()
     full = db.reshape(N, E)
-    for i, q in enumerate(_batches(nb)):
+    for i, q in enumerate(_batches(nb, wide)):
         want, _ = o.Query(q)
         assert np.array_equal(rows[0][i], want), i
         ok = oks[0][i].astype(bool)
@@ -97,6 +109,8 @@ def _run(world, backend, oracle):
         assert np.array_equal(rows[0][i][ok], full[q.astype(np.int64)][ok]), i
         assert not rows[0][i][~ok].any(), i
     assert preps[0] == o.stats()["PrepCount"] > 1
+    if wide:   # rank 0 holds partition 0: some batch took the multi-step path there
+        assert steps[0] > nb, (steps[0], nb)
 
 
 def test_sharded_device_combine_gloo_world2(oracle):
@@ -105,3 +119,10 @@ def test_sharded_device_combine_gloo_world2(oracle):
 
 def test_sharded_device_combine_rccl_world1(oracle):
     _run(1, "nccl", oracle)
+
+
+def test_sharded_device_combine_multistep_gloo_world2(oracle):
+    """The same combine when a batch takes partition 0 past its query budget
+    mid-batch: the owning rank's rows come from the multi-step path (staged on
+    the host, copied to the device tensor in stream order)."""
+    _run(2, "gloo", oracle, wide=True)
