@@ -249,6 +249,61 @@ int  pm_search_loop_batched(pm_graph** sessions, uint32_t S, const float* querie
                             double* online_s, double* maintenance_s);
 pm_batchpir* pm_graph_pir(pm_graph* g);
 
+/* ---- private search over a SHARDED graph DB (multi-GPU) --
+ * The reference's PIRGraphInfo (private-search.go:336-531) fetches every
+ * vertex record through SimpleBatchPianoPIR.Query (batch-pir.go:170-248),
+ * whose 16 partitions are independent sub-PIRs (batch-pir.go:62-85): the
+ * sharding axis.  Rank `shard` of `nshards` holds the partitions
+ * p % nshards == shard (DB rows, keys, hint state) and runs the SAME sessions
+ * (same seeds, same queries) as every other rank; each shared step's answers
+ * are combined across the ranks so every rank continues identical searches.
+ *
+ * pm_graph_create_shard: host vectors (n x dim f32) and graph (n x m u32) as
+ * pm_graph_create; only this shard's partitions are uploaded.
+ * pm_graph_create_synth: the synthetic graph of the reference's
+ * `-input synthetic` mode (private-search.go:42-69,114-117,168-170: uniform
+ * [0,1) f32 vectors, uniform neighbour ids without self loops) as a pure
+ * function of data_seed (pm_internal.h graph_synth_elem), generated on the
+ * device: graph DBs of 10^8-10^9 entries that cannot be built or shipped.
+ * pm_graph_synth_rows: the host restatement of those rows (vec / nb NULLable).
+ * Sessions: pm_graph_create_session on a preprocessed base, as unsharded. */
+int pm_graph_create_shard(pm_ctx* ctx, uint64_t n, uint64_t dim, uint64_t m, const float* vectors,
+                          const uint32_t* graph, uint32_t shard, uint32_t nshards, uint64_t pir_seed,
+                          uint64_t search_seed, pm_graph** out);
+int pm_graph_create_synth(pm_ctx* ctx, uint64_t n, uint64_t dim, uint64_t m, uint64_t data_seed, uint32_t shard,
+                          uint32_t nshards, uint64_t pir_seed, uint64_t search_seed, pm_graph** out);
+int pm_graph_synth_rows(uint64_t n, uint64_t dim, uint64_t m, uint64_t data_seed, const uint64_t* ids, uint64_t k,
+                        float* vec, uint32_t* nb);
+/* The combine of one team's shared step: SUM-all-reduce (uint64, wrapping)
+ * the nwords device words at dev_words in place across the ranks, ordered on
+ * `stream` (a hipStream_t: the reduction waits for the stream's work and the
+ * stream's later work waits for the reduction).  Every rank calls it for the
+ * same (round, team) sequence.  0 = success. */
+typedef int (*pm_combine_fn)(void* user, uint32_t team, uint64_t* dev_words, uint64_t nwords, void* stream);
+/* Words of one team's records: sessions x parallel x m x W (W = the entry
+ * words holding the neighbour list, + 1 for {dist, ok}). */
+uint64_t pm_sharded_record_words(pm_graph* g, uint32_t sessions, int parallel);
+/* pm_search_loop_batched over a sharded graph DB: S sessions (clients of one
+ * shard's server DB) in ngroups lock-step teams; every round of a team is one
+ * shared step over this shard's partitions followed by ONE combine of the
+ * team's per-id records {neighbour list, L2 distance to the session's query,
+ * success flag} (zero where this shard holds no answer: exactly one shard
+ * answers an id, so the sum is the unsharded answer bit for bit).  Teams issue
+ * their combines in one global (round, team) order on every rank.
+ * team_bufs: NULL (library buffers) or one device buffer per team of
+ * pm_sharded_record_words(sessions of that team) words (the tensors a
+ * torch.distributed combine reduces in place); team g = sessions
+ * [S*g/ngroups, S*(g+1)/ngroups).  combine NULL: no exchange, valid when this
+ * shard holds every partition, or with model_peers = 1 (synthetic graphs
+ * only): the other shards' partitions are answered from the graph's spec on
+ * the device (a wider shard layout measured one shard per GPU; modelled).
+ * Outputs as pm_search_loop_batched; the answers are identical on every rank
+ * and equal to the unsharded search's. */
+int pm_search_loop_sharded(pm_graph** sessions, uint32_t S, const float* queries, uint64_t q, int k, int step,
+                           int parallel, uint32_t ngroups, uint32_t nthreads, pm_combine_fn combine, void* user,
+                           uint64_t* const* team_bufs, int model_peers, int64_t* answers, double* wall_s,
+                           double* online_s, double* maintenance_s);
+
 /* ---- graph construction + ground truth (graphann/build_graph.go) ------- */
 /* Exact k nearest base rows of each query by (L2Dist, id), k <= 64: the
  * ground truth ComputeRecall (build_graph.go:821-863) scores against.  ids:

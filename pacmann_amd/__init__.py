@@ -59,6 +59,9 @@ class BatchStats(C.Structure):
         return {n: getattr(self, n) for n, _ in self._fields_}
 
 
+# pm_combine_fn (include/pacmann.h): (user, team, dev_words, nwords, stream) -> 0 on success
+COMBINE_FN = C.CFUNCTYPE(C.c_int, vp, C.c_uint32, vp, u64, vp)
+
 # name -> (restype, argtypes) ; every exported symbol of include/pacmann.h
 SIGNATURES = {
     "pm_ctx_create": (C.c_int, [C.c_int, C.POINTER(vp)]),
@@ -114,6 +117,14 @@ SIGNATURES = {
     "pm_batchpir_group_destroy": (None, [vp]),
     "pm_search_loop_batched": (C.c_int, [C.POINTER(vp), C.c_uint32, f32p, u64, C.c_int, C.c_int, C.c_int, C.c_uint32,
                                          C.c_uint32, i64p, C.POINTER(dbl), C.POINTER(dbl), C.POINTER(dbl)]),
+    "pm_graph_create_shard": (C.c_int, [vp, u64, u64, u64, f32p, u32p, C.c_uint32, C.c_uint32, u64, u64,
+                                        C.POINTER(vp)]),
+    "pm_graph_create_synth": (C.c_int, [vp, u64, u64, u64, u64, C.c_uint32, C.c_uint32, u64, u64, C.POINTER(vp)]),
+    "pm_graph_synth_rows": (C.c_int, [u64, u64, u64, u64, u64p, u64, f32p, u32p]),
+    "pm_sharded_record_words": (u64, [vp, C.c_uint32, C.c_int]),
+    "pm_search_loop_sharded": (C.c_int, [C.POINTER(vp), C.c_uint32, f32p, u64, C.c_int, C.c_int, C.c_int, C.c_uint32,
+                                         C.c_uint32, COMBINE_FN, vp, C.POINTER(vp), C.c_int, i64p, C.POINTER(dbl),
+                                         C.POINTER(dbl), C.POINTER(dbl)]),
 }
 
 Q_OK, Q_EBUDGET, Q_ECHUNK, Q_ENOHIT, Q_ERANGE = range(5)
@@ -591,6 +602,42 @@ class PIRGraphInfo:
         return ans, on.value, mt.value
 
 
+    @classmethod
+    def Shard(cls, vectors, graph, shard: int, nshards: int, pir_seed: int = 1, search_seed: int = 1,
+              ctx: Context | None = None) -> "PIRGraphInfo":
+        """PIRGraphInfo over shard `shard` of `nshards` of the graph DB
+        (pm_graph_create_shard): this handle holds and serves the batch-PIR
+        partitions p % nshards == shard only; search with search_loop_sharded."""
+        s = cls.__new__(cls)
+        s.ctx = ctx or default_context()
+        v = np.ascontiguousarray(vectors, dtype=np.float32)
+        g = np.ascontiguousarray(graph, dtype=np.uint32)
+        s.N, s.Dim = v.shape
+        s.M = g.shape[1]
+        s.shard, s.nshards, s.synthetic = shard, nshards, None
+        h = vp()
+        _check(lib().pm_graph_create_shard(s.ctx.h, s.N, s.Dim, s.M, _p(v, f32p), _p(g, u32p), shard, nshards,
+                                           pir_seed, search_seed, C.byref(h)))
+        s.h = h
+        return s
+
+    @classmethod
+    def Synthetic(cls, n: int, dim: int, m: int, data_seed: int, shard: int = 0, nshards: int = 1,
+                  pir_seed: int = 1, search_seed: int = 1, ctx: Context | None = None) -> "PIRGraphInfo":
+        """PIRGraphInfo over the synthetic graph of the reference's
+        `-input synthetic` mode (uniform [0,1) vectors, uniform neighbours)
+        generated on the device from data_seed (pm_graph_create_synth); rows
+        are graph_synth_rows(n, dim, m, data_seed, ids)."""
+        s = cls.__new__(cls)
+        s.ctx = ctx or default_context()
+        s.N, s.Dim, s.M = n, dim, m
+        s.shard, s.nshards, s.synthetic = shard, nshards, data_seed
+        h = vp()
+        _check(lib().pm_graph_create_synth(s.ctx.h, n, dim, m, data_seed, shard, nshards, pir_seed, search_seed,
+                                           C.byref(h)))
+        s.h = h
+        return s
+
     def Session(self, pir_seed: int, search_seed: int, ctx: Context | None = None) -> "PIRGraphInfo":
         """Another client session over this (preprocessed) graph and its server
         DB (pm_graph_create_session): own context, keys, hint state, start set
@@ -598,6 +645,8 @@ class PIRGraphInfo:
         s = PIRGraphInfo.__new__(PIRGraphInfo)
         s.ctx = ctx or Context(self.ctx.device)
         s.N, s.Dim, s.M = self.N, self.Dim, self.M
+        s.shard, s.nshards = getattr(self, "shard", 0), getattr(self, "nshards", 1)
+        s.synthetic = getattr(self, "synthetic", None)
         s._base = self   # the base keeps the shared server alive until the session's preprocessing
         h = vp()
         _check(lib().pm_graph_create_session(s.ctx.h, self.h, pir_seed, search_seed, C.byref(h)))
@@ -642,6 +691,56 @@ def search_loop_batched(sessions, queries, k: int, step: int, parallel: int, ngr
                                         C.byref(wall), on.ctypes.data_as(C.POINTER(dbl)),
                                         mt.ctypes.data_as(C.POINTER(dbl))))
     return ans, wall.value, on, mt
+
+
+def team_sizes(S: int, ngroups: int) -> list[int]:
+    """Sessions per lock-step team, as the serving loops split them."""
+    NG = max(1, min(ngroups or 1, S))
+    return [S * (g + 1) // NG - S * g // NG for g in range(NG)]
+
+
+def search_loop_sharded(sessions, queries, k: int, step: int, parallel: int, ngroups: int = 1, nthreads: int = 0,
+                        combiner=None, model_peers: bool = False):
+    """The batched serving loop over a sharded graph DB (pm_search_loop_sharded):
+    every rank calls it with its own shard's sessions and the same queries
+    [S, q, dim]; each shared step's per-id records are summed over the ranks by
+    `combiner` (pacmann_amd.shard.RecordCombiner: an in-place all-reduce over a
+    torch.distributed group), or, with model_peers (synthetic graphs), the
+    other shards' answers come from the graph's spec.  Returns (answers
+    [S, q, k], wall_s, online_s[S], maint_s[S])."""
+    S = len(sessions)
+    qs = np.ascontiguousarray(queries, dtype=np.float32)
+    if qs.ndim != 3 or qs.shape[0] != S or qs.shape[2] != sessions[0].Dim:
+        raise ValueError("queries must be [len(sessions), q, dim]")
+    q = qs.shape[1]
+    ans = np.zeros((S, q, k), dtype=np.int64)
+    hs = (vp * S)(*[s.h for s in sessions])
+    wall = C.c_double()
+    on = np.zeros(S, dtype=np.float64)
+    mt = np.zeros(S, dtype=np.float64)
+    fn, bufs = COMBINE_FN(), None
+    if combiner is not None:
+        words = [int(lib().pm_sharded_record_words(sessions[0].h, n, parallel)) for n in team_sizes(S, ngroups)]
+        ptrs = combiner.prepare(words)
+        bufs = (vp * len(ptrs))(*ptrs)
+        fn = COMBINE_FN(combiner.callback)
+    rc = lib().pm_search_loop_sharded(hs, S, _p(qs, f32p), q, k, step, parallel, ngroups, nthreads, fn, None, bufs,
+                                      int(model_peers), _p(ans, i64p), C.byref(wall),
+                                      on.ctypes.data_as(C.POINTER(dbl)), mt.ctypes.data_as(C.POINTER(dbl)))
+    if combiner is not None:
+        combiner.finish()   # raises the combine's own exception first
+    _check(rc)
+    return ans, wall.value, on, mt
+
+
+def graph_synth_rows(n: int, dim: int, m: int, data_seed: int, ids):
+    """Rows of the synthetic graph (pm_graph_synth_rows): (vectors [k, dim] f32,
+    neighbours [k, m] u32) of vertices `ids`."""
+    i = _u64(ids).ravel()
+    vec = np.zeros((len(i), dim), dtype=np.float32)
+    nb = np.zeros((len(i), m), dtype=np.uint32)
+    _check(lib().pm_graph_synth_rows(n, dim, m, data_seed, _p(i, u64p), len(i), _p(vec, f32p), _p(nb, u32p)))
+    return vec, nb
 
 
 def knn(base, queries, k: int, ctx: Context | None = None, with_dist: bool = False):

@@ -149,8 +149,8 @@ struct HostBuf {
 };
 
 // Host wall-clock accumulators, read back as "host_*" through pm_timing_get.
-enum HostTimer : int { HT_STEP_LAUNCH, HT_STEP_WAIT, HT_STEP_POST, HT_BATCH_QUERY, HT_GVI_PARSE, HT_SEARCH_KNN, HT_KNN_INIT, HT_KNN_BATCH, HT_KNN_UPDATE, HT_KNN_FINAL, HT_WAIT_FIRST, HT_WAIT_ALL, HT_ROWS_SEEN, HT_ROWS_TORN, HT_WAIT_DONE, HT_COUNT };
-static const char* const kHostTimerName[HT_COUNT] = {"host_step_launch", "host_step_wait", "host_step_post", "host_batch_query", "host_gvi_parse", "host_search_knn", "host_knn_init", "host_knn_batch", "host_knn_update", "host_knn_final", "host_wait_first_token", "host_wait_all_tokens", "host_rows_seen", "host_rows_torn", "host_wait_done"};
+enum HostTimer : int { HT_STEP_LAUNCH, HT_STEP_WAIT, HT_STEP_POST, HT_BATCH_QUERY, HT_GVI_PARSE, HT_SEARCH_KNN, HT_KNN_INIT, HT_KNN_BATCH, HT_KNN_UPDATE, HT_KNN_FINAL, HT_WAIT_FIRST, HT_WAIT_ALL, HT_ROWS_SEEN, HT_ROWS_TORN, HT_WAIT_DONE, HT_COMBINE, HT_COMBINE_TURN, HT_COUNT };
+static const char* const kHostTimerName[HT_COUNT] = {"host_step_launch", "host_step_wait", "host_step_post", "host_batch_query", "host_gvi_parse", "host_search_knn", "host_knn_init", "host_knn_batch", "host_knn_update", "host_knn_final", "host_wait_first_token", "host_wait_all_tokens", "host_rows_seen", "host_rows_torn", "host_wait_done", "host_combine", "host_combine_turn"};
 
 struct TimedLaunch { std::string name; hipEvent_t a, b; double bytes; };
 
@@ -421,13 +421,19 @@ static inline double answer_bytes(const PmPart& d, uint64_t E) {
   return rows * (double)E * 8 + 4.0 * d.SS + 8.0 * E;
 }
 
+// A DB generated on the device instead of uploaded: kind 0 = uniform words
+// (pm_batchpir_create_synth), kind 1 = the synthetic graph's PIRGraphInfo
+// entries (pm_graph_create_synth, graph_synth_elem).
+struct DbGen { int kind; uint64_t seed; uint32_t dim, m; };
 static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, uint64_t B,
                          const uint64_t* rawDB, uint64_t F, uint64_t seed, bool batch,
                          uint32_t shard = 0, uint32_t nshards = 1, const Engine* server = nullptr,
-                         const uint64_t* synth_seed = nullptr) {
+                         const DbGen* gen = nullptr) {
   if (nshards == 0 || shard >= nshards) return fail(PM_EINVAL, "shard must be < nshards");
   if (!ctx) return fail(PM_EINVAL, "ctx is NULL");
-  if (!rawDB && N && !server && !synth_seed) return fail(PM_EINVAL, "rawDB is NULL");
+  if (!rawDB && N && !server && !gen) return fail(PM_EINVAL, "rawDB is NULL");
+  if (gen && gen->kind == 1 && (uint64_t)(gen->dim + gen->m) * 4 != Ebytes)
+    return fail(PM_EINVAL, "graph entry size must be 4 * (dim + m)");
   if (server && server->ctx->device != ctx->device) return fail(PM_EINVAL, "a client shares the server DB of its own device only");
   if (N == 0) return fail(PM_EINVAL, "DBSize must be > 0");
   if (Ebytes < 8) return fail(PM_EINVAL, "DBEntryByteNum must be >= 8");
@@ -489,14 +495,15 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
   else CHK(g->db->reserve(std::max<uint64_t>(8, off_db * g->E * 8)));
   for (uint32_t i : server ? std::vector<uint32_t>{} : g->owned_list) {
     const uint64_t start = (uint64_t)i * g->PS, rows = g->parts[i].d.N;
-    if (synth_seed)
-      pmk::db_synth(ctx->stream, g->db->as<uint64_t>() + g->parts[i].d.row0 * g->E, start, rows, (uint32_t)g->E,
-                    *synth_seed);
+    uint64_t* dst = g->db->as<uint64_t>() + g->parts[i].d.row0 * g->E;
+    if (gen && gen->kind == 0)
+      pmk::db_synth(ctx->stream, dst, start, rows, (uint32_t)g->E, gen->seed);
+    else if (gen)
+      pmk::graph_synth(ctx->stream, dst, start, rows, N, gen->dim, gen->m, gen->seed);
     else
-      HIPCHK(hipMemcpy(g->db->as<uint64_t>() + g->parts[i].d.row0 * g->E, rawDB + start * g->E, rows * g->E * 8,
-                       hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(dst, rawDB + start * g->E, rows * g->E * 8, hipMemcpyHostToDevice));
   }
-  if (synth_seed) {
+  if (gen) {
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(ctx->stream));
   }
@@ -1206,8 +1213,9 @@ extern "C" int pm_batchpir_create_synth(pm_ctx* ctx, uint64_t DBSize, uint64_t D
                                         uint64_t db_seed, uint32_t shard, uint32_t nshards, pm_batchpir** out) {
   if (!out) return fail(PM_EINVAL, "out is NULL");
   pm_batchpir* h = new pm_batchpir();
+  const DbGen gen{0, db_seed, 0, 0};
   int r = engine_create(ctx, &h->e, DBSize, DBEntryByteNum, BatchSize, nullptr, FailureProbLog2, seed, true, shard,
-                        nshards, nullptr, &db_seed);
+                        nshards, nullptr, &gen);
   if (r) { delete h; return r; }
   *out = h;
   return 0;
@@ -1614,6 +1622,23 @@ struct pm_graph {
   const float* vectors = nullptr;
   const uint32_t* graph = nullptr;
   std::shared_ptr<DevBuf> dvec = std::make_shared<DevBuf>();
+  // Sharded / synthetic graphs (pm_graph_create_shard / _synth): the batch
+  // PIR holds the partitions p % nshards == shard only, and there is no device
+  // copy of all vectors (dvec stays empty): the start set's vectors, fetched
+  // non-privately like GetStartVertex (private-search.go:508-531), live in
+  // dstartvec.  A synthetic graph has no host arrays either: its rows are
+  // graph_synth_elem of data_seed.
+  uint32_t shard = 0, nshards = 1;
+  bool synth = false;
+  uint64_t data_seed = 0;
+  DevBuf dstartvec;
+  std::vector<uint8_t> okv;            // sharded loop: success flags of a multi-step batch
+  const uint32_t* true_nb(uint64_t id, uint32_t* tmp) const {   // the graph's neighbour list of id
+    if (!synth) return graph + id * m;
+    const uint64_t kg = sm64(data_seed + DOM_SYNTH_NB);
+    for (uint32_t k = 0; k < m; ++k) tmp[k] = graph_synth_nb(kg, n, id, (uint32_t)m, k);
+    return tmp;
+  }
   pm_batchpir* server = nullptr;   // sessions: the base's batch PIR whose server DB they share
   DevBuf dq, dids, ddist;
   float* q_shared = nullptr;   // batched serving: this session's query slot in its group's buffer
@@ -1638,6 +1663,64 @@ struct pm_graph {
   Clock::time_point t_init;
   ~pm_graph() { delete pir; }
 };
+
+// PIRGraphInfo over one shard of the graph DB (multi-GPU private search,
+// SURVEY.md §8e): host vectors and graph as pm_graph_create, but only the
+// partitions p % nshards == shard are uploaded and served by this handle.
+extern "C" int pm_graph_create_shard(pm_ctx* ctx, uint64_t n, uint64_t dim, uint64_t m, const float* vectors,
+                                     const uint32_t* graph, uint32_t shard, uint32_t nshards, uint64_t pir_seed,
+                                     uint64_t search_seed, pm_graph** out) {
+  if (!ctx || !out || !vectors || !graph) return fail(PM_EINVAL, "NULL argument");
+  if (n == 0 || dim == 0 || m == 0) return fail(PM_EINVAL, "n, dim, m must be > 0");
+  if ((dim * 4 + m * 4) % 8) return fail(PM_EINVAL, "(4*dim + 4*m) must be a multiple of 8");
+  if (nshards == 0 || shard >= nshards) return fail(PM_EINVAL, "shard must be < nshards");
+  HIPCHK(hipSetDevice(ctx->device));
+  pm_graph* g = new pm_graph();
+  g->ctx = ctx; g->n = n; g->dim = dim; g->m = m;
+  g->pir_seed = pir_seed; g->rng.s = search_seed;
+  g->shard = shard; g->nshards = nshards;
+  g->vec_own = std::make_shared<const std::vector<float>>(vectors, vectors + n * dim);
+  g->graph_own = std::make_shared<const std::vector<uint32_t>>(graph, graph + n * m);
+  g->vectors = g->vec_own->data();
+  g->graph = g->graph_own->data();
+  if (int r = g->dq.reserve(dim * 4)) { delete g; return r; }
+  *out = g;
+  return 0;
+}
+// The same over the synthetic graph (graph_synth_elem of data_seed, the
+// reference's -input synthetic mode) generated on the device: BIGANN-scale
+// graph DBs that cannot be built or shipped (BASELINE.json configs[3]/[4]).
+extern "C" int pm_graph_create_synth(pm_ctx* ctx, uint64_t n, uint64_t dim, uint64_t m, uint64_t data_seed,
+                                     uint32_t shard, uint32_t nshards, uint64_t pir_seed, uint64_t search_seed,
+                                     pm_graph** out) {
+  if (!ctx || !out) return fail(PM_EINVAL, "NULL argument");
+  if (n <= 1 || dim == 0 || m == 0 || m > 64 || n > 0xffffffffull)
+    return fail(PM_EINVAL, "need 1 < n < 2^32, dim > 0, 0 < m <= 64");
+  if ((dim + m) % 2) return fail(PM_EINVAL, "(4*dim + 4*m) must be a multiple of 8");
+  if (nshards == 0 || shard >= nshards) return fail(PM_EINVAL, "shard must be < nshards");
+  HIPCHK(hipSetDevice(ctx->device));
+  pm_graph* g = new pm_graph();
+  g->ctx = ctx; g->n = n; g->dim = dim; g->m = m;
+  g->pir_seed = pir_seed; g->rng.s = search_seed;
+  g->shard = shard; g->nshards = nshards;
+  g->synth = true; g->data_seed = data_seed;
+  if (int r = g->dq.reserve(dim * 4)) { delete g; return r; }
+  *out = g;
+  return 0;
+}
+// Host restatement of the synthetic graph's rows (tests, checks): vec[i*dim..]
+// and nb[i*m..] of vertex ids[i]; either output may be NULL.
+extern "C" int pm_graph_synth_rows(uint64_t n, uint64_t dim, uint64_t m, uint64_t data_seed, const uint64_t* ids,
+                                   uint64_t k, float* vec, uint32_t* nb) {
+  if (k && !ids) return fail(PM_EINVAL, "NULL argument");
+  const uint64_t kv = sm64(data_seed + DOM_SYNTH_VEC), kg = sm64(data_seed + DOM_SYNTH_NB);
+  for (uint64_t i = 0; i < k; ++i) {
+    if (ids[i] >= n) return fail(PM_EINVAL, "id out of range");
+    if (vec) for (uint64_t j = 0; j < dim; ++j) vec[i * dim + j] = graph_synth_vec(kv, ids[i], (uint32_t)dim, (uint32_t)j);
+    if (nb) for (uint64_t j = 0; j < m; ++j) nb[i * m + j] = graph_synth_nb(kg, n, ids[i], (uint32_t)m, (uint32_t)j);
+  }
+  return 0;
+}
 
 extern "C" int pm_graph_create(pm_ctx* ctx, uint64_t n, uint64_t dim, uint64_t m, const float* vectors,
                                const uint32_t* graph, int nonprivate, int skip_prep, uint64_t pir_seed,
@@ -1678,6 +1761,8 @@ extern "C" int pm_graph_create_session(pm_ctx* ctx, pm_graph* base, uint64_t pir
   g->vec_own = base->vec_own; g->graph_own = base->graph_own;
   g->vectors = base->vectors; g->graph = base->graph;
   g->dvec = base->dvec;
+  g->shard = base->shard; g->nshards = base->nshards;
+  g->synth = base->synth; g->data_seed = base->data_seed;
   g->server = base->pir;
   if (int r = g->dq.reserve(g->dim * 4)) { delete g; return r; }
   *out = g;
@@ -1694,6 +1779,18 @@ extern "C" int pm_graph_preprocess(pm_graph* g) {
     CHK(pm_batchpir_create_client(g->ctx, g->server, g->pir_seed, &g->pir));
     if (g->skipPrep) CHK(pm_batchpir_dummy_preprocessing(g->pir));
     else CHK(pm_batchpir_preprocessing(g->pir));
+  } else if (g->synth) {   // the synthetic graph's entries generated on the device, this shard's partitions
+    const uint64_t ebytes = g->dim * 4 + g->m * 4;
+    delete g->pir; g->pir = nullptr;
+    pm_batchpir* h = new pm_batchpir();
+    const DbGen gen{1, g->data_seed, (uint32_t)g->dim, (uint32_t)g->m};
+    if (int r = engine_create(g->ctx, &h->e, g->n, ebytes, g->m, nullptr, 8, g->pir_seed, true, g->shard, g->nshards,
+                              nullptr, &gen)) { delete h; return r; }
+    g->pir = h;
+    g->pir->e.pf_off = g->dim * 4;
+    g->pir->e.pf_len = g->m * 4;
+    if (g->skipPrep) CHK(pm_batchpir_dummy_preprocessing(g->pir));
+    else CHK(pm_batchpir_preprocessing(g->pir));
   } else {   // the PIR is built in non-private mode too (private-search.go:405)
     const uint64_t ebytes = g->dim * 4 + g->m * 4, E = ebytes / 8;
     std::vector<uint64_t> raw(g->n * E);
@@ -1703,7 +1800,8 @@ extern "C" int pm_graph_preprocess(pm_graph* g) {
       memcpy(e + g->dim * 4, &g->graph[i * g->m], g->m * 4);
     }
     delete g->pir; g->pir = nullptr;
-    CHK(pm_batchpir_create(g->ctx, g->n, ebytes, g->m, raw.data(), 8, g->pir_seed, &g->pir));
+    CHK(pm_batchpir_create_shard(g->ctx, g->n, ebytes, g->m, raw.data(), 8, g->pir_seed, g->shard, g->nshards,
+                                 &g->pir));
     g->pir->e.pf_off = g->dim * 4;   // the search reads the neighbour lists of the rows
     g->pir->e.pf_len = g->m * 4;
     if (g->skipPrep) CHK(pm_batchpir_dummy_preprocessing(g->pir));
@@ -1721,6 +1819,23 @@ extern "C" int pm_graph_preprocess(pm_graph* g) {
   std::vector<uint32_t> ids(g->start.begin(), g->start.end());
   CHK(g->dstart.reserve(std::max<size_t>(4, ids.size() * 4)));
   if (!ids.empty()) HIPCHK(hipMemcpy(g->dstart.p, ids.data(), ids.size() * 4, hipMemcpyHostToDevice));
+  if (!g->dvec->p && !g->nonprivate) {   // the start set's vectors themselves (GetStartVertex, non-private)
+    const uint64_t ns = g->start.size();
+    CHK(g->dstartvec.reserve(std::max<uint64_t>(4, ns * g->dim * 4)));
+    if (g->synth) {
+      DevBuf did;
+      CHK(did.reserve(std::max<uint64_t>(8, ns * 8)));
+      HIPCHK(hipMemcpy(did.p, g->start.data(), ns * 8, hipMemcpyHostToDevice));
+      pmk::graph_synth_vecs(g->ctx->stream, did.as<uint64_t>(), ns, (uint32_t)g->dim, g->data_seed,
+                            g->dstartvec.as<float>());
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipStreamSynchronize(g->ctx->stream));
+    } else {
+      std::vector<float> sv(ns * g->dim);
+      for (uint64_t i = 0; i < ns; ++i) memcpy(&sv[i * g->dim], g->vectors + g->start[i] * g->dim, g->dim * 4);
+      if (ns) HIPCHK(hipMemcpy(g->dstartvec.p, sv.data(), sv.size() * 4, hipMemcpyHostToDevice));
+    }
+  }
   return 0;
 }
 
@@ -1779,7 +1894,7 @@ static int gvi_pre(pm_graph* g, bool with_q, bool* fast) {
   Engine* e = &g->pir->e;
   // the ground-truth rows of the success check (private-search.go:483-497) are
   // pulled into the cache while the GPU answers
-  for (uint64_t i = 0; i < n; ++i) {
+  for (uint64_t i = 0; g->graph && i < n; ++i) {
     const char* gr = (const char*)&g->graph[(uint64_t)g->batch[i] * m];
     for (uint64_t b = 0; b < m * 4; b += 64) __builtin_prefetch(gr + b);
     __builtin_prefetch(gr + m * 4 - 1);
@@ -1811,16 +1926,18 @@ static int gvi_post(pm_graph* g, bool with_q, bool fast) {
     const char* r = (const char*)g->rowp[i] + nb_off;
     for (uint64_t b = 0; b < m * 4; b += 64) __builtin_prefetch(r + b);
   }
+  uint32_t tmp[64];
   for (uint64_t i = 0; i < n; ++i) {
     uint32_t* nbi = &g->nb[i * m];
     memcpy(nbi, (const char*)g->rowp[i] + nb_off, m * 4);
-    if (memcmp(nbi, &g->graph[(uint64_t)g->batch[i] * m], m * 4) == 0) g->succ++;
+    if (memcmp(nbi, g->true_nb((uint64_t)g->batch[i], tmp), m * 4) == 0) g->succ++;
   }
   e->rows_partial = false;
   g->ctx->host_add(HT_GVI_PARSE, ms_since(t_parse));
   return 0;
 }
 static int get_vertex_info(pm_graph* g, bool with_q) {
+  if (g->nshards > 1) return fail(PM_EINVAL, "a sharded graph searches through pm_search_loop_sharded (the shards' combine)");
   bool fast = false;
   CHK(gvi_pre(g, with_q, &fast));
   if (fast) {
@@ -1881,8 +1998,10 @@ static int knn_begin_enqueue(pm_graph* g, const float* query, int benchmarking) 
   HIPCHK(hipMemcpyAsync(g->dq.p, qh, g->dim * 4, hipMemcpyHostToDevice, st));
   if (ns) {
     CHK(g->ddist.reserve(ns * 4));
+    const bool ids = g->dvec->p != nullptr;   // all vectors on the device, or the start set's own (sharded / synthetic)
     g->ctx->timed("l2_rows", (double)ns * g->dim * 4, [&] {
-      pmk::l2_rows(st, g->dvec->as<float>(), g->dim, ns, g->dstart.as<uint32_t>(), g->dq.as<float>(), (uint32_t)g->dim, g->ddist.as<float>());
+      pmk::l2_rows(st, ids ? g->dvec->as<float>() : g->dstartvec.as<float>(), g->dim, ns,
+                   ids ? g->dstart.as<uint32_t>() : nullptr, g->dq.as<float>(), (uint32_t)g->dim, g->ddist.as<float>());
     });
     HIPCHK(hipMemcpyAsync(qh + g->dim, g->ddist.p, ns * 4, hipMemcpyDeviceToHost, st));
   }
@@ -1905,7 +2024,8 @@ static void knn_begin_finish(pm_graph* g, int parallel, int benchmarking, const 
   for (size_t i = 0; (int64_t)g->heap.size() < parallel && i < g->fs.size(); ++i) {
     const int64_t id = g->fs[i].first.id;
     if (g->known.find((uint64_t)id)) continue;
-    knn_add_known(g, id, &g->graph[(uint64_t)id * m], g->fs[i].first.dist, 0);
+    uint32_t tmp[64];   // GetStartVertex returns the start vertices' neighbour lists (non-private)
+    knn_add_known(g, id, g->true_nb((uint64_t)id, tmp), g->fs[i].first.dist, 0);
     heap_push(g->heap, g->fs[i].first);
   }
 }
@@ -2063,9 +2183,14 @@ struct SpinBarrier {
   }
 };
 
+struct ShardComb;
 struct StepGroup {
   pm_ctx* c = nullptr;   // the shared steps' stream
   uint32_t S = 0, P = 0, maxPH = 0, maxSS = 0, E = 0, dim = 0;
+  // the partitions the clients hold (all P, or a shard's p % nshards == shard);
+  // client s's partition lp[i] is the shared step's partition s * Pl + i
+  std::vector<uint32_t> lp;
+  uint32_t Pl = 0;
   bool ph8 = false;
   DevBuf parts_d, subs_d, sb_d, bits, cand, meta, spec, res_d, ans, part_x, done, prep_parts, desc_d, stamps, qset;
   HostBuf desc_h, out_h;
@@ -2079,8 +2204,37 @@ struct StepGroup {
   bool rows_partial = false;   // graph search: only the neighbour words of each row go to the host
   // the sessions' queries and start sets, scored in ONE k_l2_rows launch per query
   uint32_t ns = 0;
-  DevBuf qbuf, start_ids, start_dist;
+  DevBuf qbuf, start_ids, start_dist, start_vec;   // start_vec: [S][ns][dim] (sharded / synthetic graphs)
   HostBuf qstage;   // [S][dim] queries, then [S][ns] start-set distances
+  // ---- sharded private search (pm_search_loop_sharded): this rank's share of
+  // every shared step becomes per-id records [S][npos][W] (group_exchange),
+  // summed over the ranks by the combine, then read back by every rank
+  ShardComb* comb = nullptr;
+  uint32_t team = 0;
+  uint64_t round = 0;
+  std::vector<pm_graph*> gs;
+  uint32_t npos = 0, W = 0, w0 = 0, nb_off = 0;   // ids per session per round, record words, first row word
+  DevBuf out_d, map_d, ids_d, rec_own;            // step outputs (device), map, ids; the records if not the caller's
+  uint64_t* rec_d = nullptr;                      // [S*npos*W] records (all-reduced) then [nsub] {status, ref}
+  DevBuf st_d;                                    // ... the status words when the records are the caller's buffer
+  HostBuf map_h, ids_h, slow_h, rec_h;
+  std::vector<char> slow;                         // sessions served by the multi-step path this round
+};
+
+// The sharded loop's exchange: the caller's combine (an in-place SUM
+// all-reduce of a team's records over the ranks, ordered on the given stream),
+// issued in one global order (round-major, then team) on every rank so the
+// ranks' collectives match; or model_peers: the partitions this rank does not
+// hold are answered from the synthetic graph's spec on the device (a shard
+// layout wider than the job, measured one shard per GPU).
+struct ShardComb {
+  pm_combine_fn fn = nullptr;   // include/pacmann.h
+  void* user = nullptr;
+  bool model_peers = false;
+  uint32_t NG = 1;
+  uint64_t* const* bufs = nullptr;   // the caller's device buffers, one per team (null: the library's)
+  std::atomic<uint64_t> ticket{0};
+  std::atomic<bool> abort{false};
 };
 
 static int group_upload_parts(StepGroup& G) {
@@ -2088,7 +2242,7 @@ static int group_upload_parts(StepGroup& G) {
   v.reserve((size_t)G.S * G.P);
   for (uint32_t s = 0; s < G.S; ++s) {
     Engine* e = G.es[s];
-    for (uint32_t p = 0; p < G.P; ++p) {
+    for (uint32_t p : G.lp) {
       PmPart d = e->parts[p].d;
       d.qv = G.qv.empty() ? nullptr : G.qv[s];
       v.push_back(d);
@@ -2108,8 +2262,10 @@ static int group_init(StepGroup& G, pm_ctx* c) {
   G.S = (uint32_t)G.es.size();
   const Engine& e = *G.es[0];
   G.P = (uint32_t)e.P; G.maxPH = e.maxPH; G.ph8 = e.ph8; G.maxSS = e.maxSS; G.E = (uint32_t)e.E;
+  G.lp = e.owned_list;
+  G.Pl = (uint32_t)G.lp.size();
   HIPCHK(hipSetDevice(c->device));
-  CHK(G.parts_d.reserve((size_t)G.S * G.P * sizeof(PmPart)));
+  CHK(G.parts_d.reserve(std::max<size_t>(1, (size_t)G.S * G.Pl) * sizeof(PmPart)));
   CHK(G.done.reserve(4 * (3 + 65536)));
   const uint32_t init[3] = {1u << 31, 0, 0};
   HIPCHK(hipMemcpy(G.done.p, init, sizeof init, hipMemcpyHostToDevice));
@@ -2131,11 +2287,12 @@ static int group_step(StepGroup& G, const std::vector<char>& in) {
   for (uint32_t s = 0; s < G.S; ++s) {
     Engine* e = G.es[s];
     G.base[s] = (uint32_t)G.subs.size();
-    for (uint32_t p = 0; p < G.P; ++p) {
+    for (uint32_t li = 0; li < G.Pl; ++li) {
+      const uint32_t p = G.lp[li];
       if (in[s]) {
         for (uint32_t j = e->sb[p]; j < e->sb[p + 1]; ++j) {
           PmSub x = e->subs[j];
-          x.part += s * G.P;
+          x.part = s * G.Pl + li;
           G.subs.push_back(x);
           if (x.kind == SUB_REAL || x.kind == SUB_DUMMY) ans_bytes += answer_bytes(e->parts[p].d, G.E);
         }
@@ -2146,7 +2303,7 @@ static int group_step(StepGroup& G, const std::vector<char>& in) {
       G.sb.push_back((uint32_t)G.subs.size());
     }
   }
-  const uint32_t nsub = (uint32_t)G.subs.size(), np = G.S * G.P;
+  const uint32_t nsub = (uint32_t)G.subs.size(), np = G.S * G.Pl;
   if (nsub == 0) return 0;
   const uint32_t words = (G.maxPH + 63) / 64, cblk = pmk::step_match_blocks(G.maxPH);
   CHK(G.subs_d.reserve(nsub * sizeof(PmSub)));
@@ -2159,7 +2316,7 @@ static int group_step(StepGroup& G, const std::vector<char>& in) {
   CHK(G.ans.reserve((uint64_t)nsub * G.E * 8));
   const size_t dsub = nsub * sizeof(PmSub);
   CHK(G.desc_h.reserve(dsub + (np + 1) * 4));
-  CHK(G.out_h.reserve(nsub * sizeof(PmOutHdr) + (size_t)nsub * G.E * 8));
+  if (!G.comb) CHK(G.out_h.reserve(nsub * sizeof(PmOutHdr) + (size_t)nsub * G.E * 8));
   char* dh = G.desc_h.as<char>();
   memcpy(dh, G.subs.data(), dsub);
   memcpy(dh + dsub, G.sb.data(), (np + 1) * 4);
@@ -2192,8 +2349,14 @@ static int group_step(StepGroup& G, const std::vector<char>& in) {
   Engine* e0 = G.es[0];
   S.db = e0->db->as<uint64_t>();
   S.q = nullptr;   // each partition's PmPart::qv
-  S.hdr_h = G.out_h.as<PmOutHdr>();
-  S.rows_h = (uint64_t*)(G.out_h.as<char>() + nsub * sizeof(PmOutHdr));
+  if (G.comb) {   // sharded: results stay on the device for group_exchange's records
+    CHK(G.out_d.reserve(nsub * sizeof(PmOutHdr) + (size_t)nsub * G.E * 8));
+    S.hdr_h = G.out_d.as<PmOutHdr>();
+    S.rows_h = (uint64_t*)(G.out_d.as<char>() + nsub * sizeof(PmOutHdr));
+  } else {
+    S.hdr_h = G.out_h.as<PmOutHdr>();
+    S.rows_h = (uint64_t*)(G.out_h.as<char>() + nsub * sizeof(PmOutHdr));
+  }
   S.words = words; S.E = G.E; S.dim = G.dim; S.nsub = nsub; S.np = np;
   S.np_live = np_live;
   S.args_valid = (nsub <= kArgSubs && np <= kArgParts) ? 1u : 0u;
@@ -2242,7 +2405,7 @@ static int group_step(StepGroup& G, const std::vector<char>& in) {
   }
 #endif
   c->timed_ext("answer", S.nsplit > 1 ? 0 : ans_bytes, [&](pmk::PmEvents ev) { pmk::step_answer(st, S, G.maxSS, ev); }, 2);
-  G.seq = c->record_done(st);
+  if (!G.comb) G.seq = c->record_done(st);   // sharded: group_exchange publishes the records
   HIPCHK(hipGetLastError());
 #ifdef PM_ANSWER_STAMPS
   if (stamp_this) {
@@ -2283,16 +2446,20 @@ static int group_collect(StepGroup& G, uint32_t s) {
 }
 
 // The team's queries (staged in G.qstage) to the device and every session's
-// start-set distances (search.go:130-146) in one k_l2_rows launch.
+// start-set distances (search.go:130-146) in one k_l2_rows launch: over the
+// device copy of all vectors by start id, or (sharded / synthetic graphs)
+// over the sessions' start vectors themselves.
 static int group_start_dist(StepGroup& G, pm_graph** gs) {
   hipStream_t st = G.c->stream;
   float* qst = G.qstage.as<float>();
   HIPCHK(hipMemcpyAsync(G.qbuf.p, qst, (uint64_t)G.S * G.dim * 4, hipMemcpyHostToDevice, st));
   const uint64_t nrows = (uint64_t)G.S * G.ns;
   if (nrows) {
+    const bool ids = gs[0]->dvec->p != nullptr;
     G.c->timed("l2_rows", (double)nrows * G.dim * 4, [&] {
-      pmk::l2_rows(st, gs[0]->dvec->as<float>(), G.dim, nrows, G.start_ids.as<uint32_t>(), G.qbuf.as<float>(),
-                   G.dim, G.start_dist.as<float>(), G.ns);
+      pmk::l2_rows(st, ids ? gs[0]->dvec->as<float>() : G.start_vec.as<float>(), G.dim, nrows,
+                   ids ? G.start_ids.as<uint32_t>() : nullptr, G.qbuf.as<float>(), G.dim, G.start_dist.as<float>(),
+                   G.ns);
     });
     HIPCHK(hipMemcpyAsync(qst + (uint64_t)G.S * G.dim, G.start_dist.p, nrows * 4, hipMemcpyDeviceToHost, st));
   }
@@ -2319,7 +2486,7 @@ static int group_prep(StepGroup& G, pm_graph** gs, const std::vector<char>& need
   }
   // partition-major: the clients' folds of one partition run side by side and
   // share its DB rows through the caches instead of re-reading them per client
-  for (uint32_t p = 0; p < G.P; ++p)
+  for (uint32_t p : G.lp)
     for (uint32_t s : who) hp.push_back(gs[s]->pir->e.parts[p].d);
   const Engine* e0 = &gs[who[0]]->pir->e;
   bool skip = false;
@@ -2338,10 +2505,218 @@ static int group_prep(StepGroup& G, pm_graph** gs, const std::vector<char>& need
   return 0;
 }
 
+// ---- sharded private search (pm_search_loop_sharded) --------------------
+// Every rank runs the same sessions (same seeds, same queries) over its shard
+// of the graph DB.  A round: each session's GetVertexInfo batch is bucketed
+// (bq_prepare: the global decisions, identical on every rank) and its
+// sub-queries on this rank's partitions join the team's shared step; the step's
+// answers become per-id records [session][position] = {neighbour words, dist |
+// ok << 32}, zero where this rank holds no answer; ONE combine per shared step
+// sums the records over the ranks; every rank then reads all records back and
+// continues the identical searches.  Host mirrors (FinishedQueryNum, the local
+// cache, counters, the maintenance trigger) are per rank and per partition, as
+// in the single-rank engine, so each rank's partitions evolve exactly as the
+// unsharded engine's do.
+
+// Bucket session s's batch (rank-local sub-queries) and fill its rows of the
+// record map: the answering sub-query (client-local index) of each position,
+// -1 (no local answer) or -2 (answered by a modelled peer).  A batch that
+// needs several steps here (a partition at its query budget) is served now on
+// the session's own stream and its records packed on the host.
+static int gvi_pre_sharded(pm_graph* g, StepGroup& G, uint32_t s, bool* fast) {
+  const uint64_t n = g->batch.size(), m = g->m;
+  if (n != G.npos) return fail(PM_EINVAL, "sharded search: every round must fetch parallel * m ids");
+  g->total += n;
+  g->nb.resize(n * m);
+  g->dist.assign(n, 0.0f);
+  Engine* e = &g->pir->e;
+  g->qids.assign(g->batch.begin(), g->batch.end());
+  auto t = Clock::now();
+  e->rows_partial = true;
+  CHK(bq_prepare(e, g->qids.data(), n, fast));
+  int32_t* map = G.map_h.as<int32_t>() + (uint64_t)s * G.npos;
+  if (*fast) {
+    e->resp_map.clear();
+    for (size_t j = 0; j < e->subs.size(); ++j) {
+      const uint32_t k = e->subs[j].kind;
+      if (k == SUB_REAL || k == SUB_HOSTCACHE) e->resp_map.put(e->sub_gid[j], (uint32_t)j);   // last wins
+    }
+  } else {
+    g->rowp.resize(n);
+    g->okv.assign(n, 0);
+    CHK(batch_query_impl(e, g->qids.data(), n, nullptr, g->qdev(), (uint32_t)g->dim, g->dist.data(), g->rowp.data(),
+                         g->okv.data()));
+    uint64_t* rec = G.slow_h.as<uint64_t>() + (uint64_t)s * G.npos * G.W;
+    for (uint64_t i = 0; i < n; ++i) {
+      uint64_t* r = rec + i * G.W;
+      const bool own = e->parts[g->qids[i] / e->PS].owned;
+      for (uint32_t w = 0; w + 1 < G.W; ++w) r[w] = own && g->okv[i] ? g->rowp[i][G.w0 + w] : 0;
+      uint32_t db;
+      memcpy(&db, &g->dist[i], 4);
+      r[G.W - 1] = own && g->okv[i] ? (1ull << 32) | db : 0;
+    }
+  }
+  uint64_t* ids = G.ids_h.as<uint64_t>() + (uint64_t)s * G.npos;
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint64_t id = g->qids[i], p = id / e->PS;
+    int32_t v = -1;
+    if (e->parts[p].owned) {
+      if (*fast)
+        if (const uint32_t* j = e->resp_map.find(id)) v = (int32_t)*j;
+    } else if (G.comb->model_peers) {   // answered by its partition's holder unless dropped (batch-pir.go:195-200)
+      for (uint64_t j = 0; j < e->qn && j < e->pq[p].size(); ++j)
+        if (e->pq[p][j] == id) { v = -2; break; }
+    }
+    map[i] = v;
+    ids[i] = id;
+  }
+  G.slow[s] = !*fast;
+  e->ctx->host_add(HT_BATCH_QUERY, ms_since(t));
+  return 0;
+}
+
+// After the shared step (group_step): the records of this rank's answers, the
+// multi-step sessions' host-packed records, the modelled peers' records, the
+// combine, and one copy of all records (and the step's statuses) to the host.
+static int group_exchange(StepGroup& G, const std::vector<char>& in) {
+  pm_ctx* c = G.c;
+  hipStream_t st = c->stream;
+  const uint32_t nrec = G.S * G.npos, nsub = (uint32_t)G.subs.size();
+  const uint64_t nw = (uint64_t)nrec * G.W;
+  int32_t* map = G.map_h.as<int32_t>();
+  for (uint32_t s = 0; s < G.S; ++s)   // client-local sub-query indices -> the shared step's
+    for (uint32_t i = 0; i < G.npos; ++i) {
+      int32_t& v = map[(uint64_t)s * G.npos + i];
+      if (v >= 0) v = in[s] ? v + (int32_t)G.base[s] : -1;
+    }
+  HIPCHK(hipMemcpyAsync(G.map_d.p, map, (uint64_t)nrec * 4, hipMemcpyHostToDevice, st));
+  uint32_t* st2 = G.st_d.as<uint32_t>();
+  const PmOutHdr* hdr = G.out_d.as<PmOutHdr>();
+  const uint64_t* rows = (const uint64_t*)(G.out_d.as<char>() + nsub * sizeof(PmOutHdr));
+  c->timed("pack_records", (double)nw * 8, [&] {
+    pmk::pack_records(st, G.map_d.as<int32_t>(), nrec, hdr, rows, G.E, G.w0, G.W, G.rec_d, nsub, st2); });
+  for (uint32_t s = 0; s < G.S; ++s)
+    if (G.slow[s])
+      HIPCHK(hipMemcpyAsync(G.rec_d + (uint64_t)s * G.npos * G.W, G.slow_h.as<uint64_t>() + (uint64_t)s * G.npos * G.W,
+                            (uint64_t)G.npos * G.W * 8, hipMemcpyHostToDevice, st));
+  if (G.comb->model_peers) {
+    HIPCHK(hipMemcpyAsync(G.ids_d.p, G.ids_h.p, (uint64_t)nrec * 8, hipMemcpyHostToDevice, st));
+    const pm_graph* g0 = G.gs[0];
+    c->timed("synth_records", 0, [&] {
+      pmk::synth_records(st, G.map_d.as<int32_t>(), G.ids_d.as<uint64_t>(), nrec, G.npos, G.qbuf.as<float>(), G.dim,
+                         (uint32_t)g0->m, g0->n, g0->data_seed, G.w0, G.W, G.rec_d); });
+  }
+  HIPCHK(hipGetLastError());
+  if (G.comb->fn) {   // the collective, in the global (round, team) order on every rank
+    ShardComb* cb = G.comb;
+    const uint64_t turn = G.round * cb->NG + G.team;
+    auto tw = Clock::now();
+    while (cb->ticket.load(std::memory_order_acquire) != turn) {
+      if (cb->abort.load()) return fail(PM_EHIP, "sharded search: another team failed");
+      std::this_thread::yield();
+    }
+    c->host_add(HT_COMBINE_TURN, ms_since(tw));
+    auto t0 = Clock::now();
+    int rc = 0;
+    c->timed("combine", (double)nw * 8, [&] { rc = cb->fn(cb->user, G.team, G.rec_d, nw, (void*)st); });
+    c->host_add(HT_COMBINE, ms_since(t0));
+    cb->ticket.fetch_add(1, std::memory_order_acq_rel);
+    if (rc) return fail(PM_EHIP, "sharded search: the combine callback failed (" + std::to_string(rc) + ")");
+  }
+  HIPCHK(hipMemcpyAsync(G.rec_h.p, G.rec_d, nw * 8, hipMemcpyDeviceToHost, st));
+  if (nsub) HIPCHK(hipMemcpyAsync(G.rec_h.as<uint64_t>() + nw, st2, (uint64_t)nsub * 8, hipMemcpyDeviceToHost, st));
+  G.seq = c->record_done(st);
+  G.round++;
+  return 0;
+}
+
+// Session s's share of the exchanged records: host mirrors of its sub-queries
+// on this rank (post_results), the batch's counters and trigger (bq_tail), and
+// the neighbour lists and distances of all its ids (Entry2VectorAndNeighbors,
+// private-search.go:418-439, with the success check :483-497).
+static int group_collect_sharded(StepGroup& G, uint32_t s, bool fast) {
+  pm_graph* g = G.gs[s];
+  Engine* e = G.es[s];
+  auto t_wait = Clock::now();
+  if (G.c->publish_wait) CHK(wait_done(G.c, G.seq));
+  else HIPCHK(hipStreamSynchronize(G.c->stream));
+  e->ctx->host_add(HT_STEP_WAIT, ms_since(t_wait));
+  const uint64_t nw = (uint64_t)G.S * G.npos * G.W, m = g->m;
+  const uint64_t* rec = G.rec_h.as<uint64_t>();
+  const uint32_t* st2 = (const uint32_t*)(rec + nw);
+  if (fast) {
+    auto tp = Clock::now();
+    for (size_t j = 0; j < e->subs.size(); ++j) {
+      const uint64_t k = G.base[s] + j;
+      if (st2[2 * k] == ST_OK) {
+        PartHost& ph = e->parts[e->subs[j].part];
+        ph.fqn++;
+        ph.cache.put(e->subs[j].idx, st2[2 * k + 1]);
+      }
+    }
+    e->ctx->host_add(HT_STEP_POST, ms_since(tp));
+    CHK(bq_tail(e, G.npos));
+  }
+  auto t_parse = Clock::now();
+  uint32_t tmp[64];
+  for (uint64_t i = 0; i < G.npos; ++i) {
+    const uint64_t* r = rec + ((uint64_t)s * G.npos + i) * G.W;
+    uint32_t* nbi = &g->nb[i * m];
+    memcpy(nbi, (const char*)r + G.nb_off, m * 4);
+    const uint32_t db = (uint32_t)r[G.W - 1];
+    memcpy(&g->dist[i], &db, 4);
+    if (memcmp(nbi, g->true_nb((uint64_t)g->batch[i], tmp), m * 4) == 0) g->succ++;
+  }
+  e->rows_partial = false;
+  g->ctx->host_add(HT_GVI_PARSE, ms_since(t_parse));
+  return 0;
+}
+
+// Buffers of a sharded team (after group_init).
+static int group_shard_init(StepGroup& G, pm_graph** gs, uint32_t S, int parallel, ShardComb* comb, uint32_t team) {
+  G.comb = comb;
+  G.team = team;
+  G.round = 0;
+  G.gs.assign(gs, gs + S);
+  const Engine& e = gs[0]->pir->e;
+  G.npos = (uint32_t)(parallel * gs[0]->m);
+  G.w0 = (uint32_t)(gs[0]->dim * 4 / 8);
+  const uint32_t w1 = (uint32_t)((gs[0]->dim * 4 + gs[0]->m * 4 + 7) / 8);
+  G.W = w1 - G.w0 + 1;
+  G.nb_off = (uint32_t)(gs[0]->dim * 4 - (uint64_t)G.w0 * 8);
+  if (e.pf_off != (size_t)gs[0]->dim * 4) return fail(PM_EINVAL, "sharded search: entries are not PIRGraphInfo's");
+  const uint64_t nrec = (uint64_t)S * G.npos, nw = nrec * G.W;
+  if (comb->bufs) {
+    G.rec_d = comb->bufs[team];
+    if (!G.rec_d) return fail(PM_EINVAL, "sharded search: NULL team buffer");
+  } else {
+    CHK(G.rec_own.reserve(nw * 8));
+    G.rec_d = G.rec_own.as<uint64_t>();
+  }
+  CHK(G.st_d.reserve(std::max<uint64_t>(8, nrec * 8)));   // at most one sub-query per position
+  CHK(G.map_d.reserve(nrec * 4));
+  CHK(G.ids_d.reserve(nrec * 8));
+  CHK(G.map_h.reserve(nrec * 4));
+  CHK(G.ids_h.reserve(nrec * 8));
+  CHK(G.slow_h.reserve(nw * 8));
+  CHK(G.rec_h.reserve(nw * 8 + nrec * 8));
+  G.slow.assign(S, 0);
+  if (!gs[0]->dvec->p) {   // the sessions' start vectors side by side for the team's one k_l2_rows launch
+    const uint64_t per = (uint64_t)G.ns * G.dim;
+    CHK(G.start_vec.reserve(std::max<uint64_t>(4, S * per * 4)));
+    for (uint32_t i = 0; i < S; ++i)
+      if (per) HIPCHK(hipMemcpyAsync(G.start_vec.as<float>() + i * per, gs[i]->dstartvec.p, per * 4,
+                                     hipMemcpyDeviceToDevice, G.c->stream));
+    HIPCHK(hipStreamSynchronize(G.c->stream));
+  }
+  return 0;
+}
+
 // One lock-step team: sessions gs[0..S) share one step stream (gs[0]'s) and T
 // worker threads; maintenance seconds into mt[0..S).  Runs on the calling thread.
 static int run_batched_team(pm_graph** gs, uint32_t S, const float* queries, uint64_t q, int k, int step,
-                            int parallel, uint32_t T, int64_t* answers, double* mt_out) {
+                            int parallel, uint32_t T, int64_t* answers, double* mt_out, ShardComb* comb = nullptr,
+                            uint32_t team = 0) {
   StepGroup G;
   G.dim = (uint32_t)gs[0]->dim;
   G.rows_partial = true;   // GetVertexInfo reads the neighbour lists only
@@ -2369,6 +2744,7 @@ static int run_batched_team(pm_graph** gs, uint32_t S, const float* queries, uin
     G.qv.push_back(gs[i]->qdev());
   }
   CHK(group_init(G, gs[0]->ctx));
+  if (comb) CHK(group_shard_init(G, gs, S, parallel, comb, team));
   T = std::max(1u, std::min(T, S));
   std::vector<char> fast(S, 0), need_prep(S, 0);
   std::vector<double> mt(S, 0.0);
@@ -2380,6 +2756,7 @@ static int run_batched_team(pm_graph** gs, uint32_t S, const float* queries, uin
   auto set_err = [&](int rc, uint32_t s) {
     int z = 0;
     if (rc && err.compare_exchange_strong(z, rc)) err_msg = "session " + std::to_string(s) + ": " + pm_last_error();
+    if (rc && comb) comb->abort.store(true);   // the other teams stop waiting for this one's turns
   };
   std::vector<int64_t> steps_buf((size_t)T * std::max(k, 1));
   // worker w serves sessions s = w, w + T, ...; worker 0 (this thread) also launches the shared steps
@@ -2409,14 +2786,15 @@ static int run_batched_team(pm_graph** gs, uint32_t S, const float* queries, uin
           pm_graph* g = gs[s];
           knn_batch(g, parallel, 0);
           bool f = false;
-          const int rc = gvi_pre(g, true, &f);
+          const int rc = comb ? gvi_pre_sharded(g, G, s, &f) : gvi_pre(g, true, &f);
           fast[s] = f;
           if (rc) set_err(rc, s);
         }
         bar.wait();
         if (w == 0) {
           if (!err.load()) {
-            const int rc = group_step(G, fast);
+            int rc = group_step(G, fast);
+            if (!rc && comb) rc = group_exchange(G, fast);   // records, combine, read-back
             if (rc) set_err(rc, 0);
           }
           stop.store(err.load() != 0);
@@ -2425,12 +2803,17 @@ static int run_batched_team(pm_graph** gs, uint32_t S, const float* queries, uin
         if (stop.load()) return;
         for (uint32_t s = w; s < S && !err.load(); s += T) {   // rows -> neighbours, known set
           pm_graph* g = gs[s];
-          if (fast[s]) {   // this client's share of the shared step's results
-            const int rw = group_collect(G, s);
+          if (comb) {   // every id's record, combined over the shards
+            const int rw = group_collect_sharded(G, s, fast[s]);
             if (rw) { set_err(rw, s); break; }
+          } else {
+            if (fast[s]) {   // this client's share of the shared step's results
+              const int rw = group_collect(G, s);
+              if (rw) { set_err(rw, s); break; }
+            }
+            const int rc = gvi_post(g, true, fast[s]);
+            if (rc) { set_err(rc, s); break; }
           }
-          const int rc = gvi_post(g, true, fast[s]);
-          if (rc) { set_err(rc, s); break; }
           knn_update(g, st);
         }
       }
@@ -2553,6 +2936,77 @@ extern "C" int pm_search_loop_batched(pm_graph** gs, uint32_t S, const float* qu
       rc[g] = run_batched_team(gs + s0, s1 - s0, qbase + (uint64_t)s0 * q * gs[0]->dim, q, k, step, parallel, Tg,
                                answers + (uint64_t)s0 * q * (uint64_t)k, mt.data() + s0);
       if (rc[g]) msg[g] = pm_last_error();
+    });
+  }
+  for (auto& t : teams) t.join();
+  const double wall = std::chrono::duration<double>(Clock::now() - t0).count();
+  for (uint32_t g = 0; g < NG; ++g)
+    if (rc[g]) return fail(rc[g], "group " + std::to_string(g) + ": " + msg[g]);
+  if (wall_s) *wall_s = wall;
+  for (uint32_t s = 0; s < S; ++s) {
+    if (online_s) online_s[s] = wall - mt[s];
+    if (maint_s) maint_s[s] = mt[s];
+  }
+  return 0;
+}
+
+// Words of one team's records in pm_search_loop_sharded: sessions x (parallel
+// x m) ids x W, W = the row words holding the neighbour list + 1.
+extern "C" uint64_t pm_sharded_record_words(pm_graph* g, uint32_t sessions, int parallel) {
+  if (!g || parallel <= 0) return 0;
+  const uint64_t w0 = g->dim * 4 / 8, w1 = (g->dim * 4 + g->m * 4 + 7) / 8;
+  return (uint64_t)sessions * (uint64_t)parallel * g->m * (w1 - w0 + 1);
+}
+
+// The batched serving loop over a sharded graph DB (every rank calls it with
+// its own shard's sessions, the same seeds and queries).  Teams are
+// pm_search_loop_batched's; each shared step ends in ONE combine of the team's
+// records (see group_exchange).  combine NULL: no exchange (one shard holds
+// every partition), or model_peers (synthetic graphs): the partitions of the
+// other shards are answered from the graph's spec.  team_bufs (NULL: the
+// library allocates): one device buffer per team of pm_sharded_record_words
+// words, the tensors a torch.distributed combine all-reduces in place.
+extern "C" int pm_search_loop_sharded(pm_graph** gs, uint32_t S, const float* queries, uint64_t q, int k, int step,
+                                      int parallel, uint32_t ngroups, uint32_t nthreads, pm_combine_fn combine,
+                                      void* user, uint64_t* const* team_bufs, int model_peers, int64_t* answers,
+                                      double* wall_s, double* online_s, double* maint_s) {
+  if (!gs || !S || (!queries && q) || (!answers && q)) return fail(PM_EINVAL, "NULL argument");
+  for (uint32_t i = 0; i < S; ++i) {
+    if (!gs[i] || !gs[i]->pir || gs[i]->nonprivate) return fail(PM_EINVAL, "sessions must be preprocessed private graphs");
+    const Engine& a = gs[0]->pir->e;
+    const Engine& b = gs[i]->pir->e;
+    if (a.db.get() != b.db.get() || a.P != b.P || a.E != b.E || gs[i]->dim != gs[0]->dim || gs[i]->m != gs[0]->m ||
+        b.shard != a.shard || b.nshards != a.nshards || gs[i]->ctx->device != gs[0]->ctx->device)
+      return fail(PM_EINVAL, "sharded sessions must be clients of one shard's server DB on one device");
+    for (uint32_t j = 0; j < i; ++j)
+      if (gs[j] == gs[i] || gs[j]->ctx == gs[i]->ctx) return fail(PM_EINVAL, "sessions need distinct graphs and contexts");
+  }
+  if (model_peers && !gs[0]->synth) return fail(PM_EINVAL, "modelled peers need the synthetic graph (its rows are computable)");
+  if (model_peers && combine) return fail(PM_EINVAL, "pass a combine or model_peers, not both");
+  if (gs[0]->pir->e.nshards > 1 && !combine && !model_peers)
+    return fail(PM_EINVAL, "a sharded graph needs a combine (or model_peers)");
+  if (gs[0]->m > 64) return fail(PM_EINVAL, "sharded search: m <= 64");
+  const uint32_t NG = std::max(1u, std::min(ngroups ? ngroups : 1u, S));
+  const uint32_t TT = std::max(NG, nthreads ? nthreads : std::min<uint32_t>(S, 16u));
+  ShardComb comb;
+  comb.fn = combine;
+  comb.user = user;
+  comb.model_peers = model_peers != 0;
+  comb.NG = NG;
+  comb.bufs = team_bufs;
+  std::vector<double> mt(S, 0.0);
+  std::vector<int> rc(NG, 0);
+  std::vector<std::string> msg(NG);
+  std::vector<std::thread> teams;
+  auto t0 = Clock::now();
+  for (uint32_t g = 0; g < NG; ++g) {
+    const uint32_t s0 = (uint32_t)((uint64_t)S * g / NG), s1 = (uint32_t)((uint64_t)S * (g + 1) / NG);
+    const uint32_t Tg = std::max(1u, std::min(s1 - s0, (uint32_t)((uint64_t)TT * (g + 1) / NG - (uint64_t)TT * g / NG)));
+    teams.emplace_back([&, g, s0, s1, Tg] {
+      if (hipSetDevice(gs[0]->ctx->device) != hipSuccess) { rc[g] = PM_EHIP; msg[g] = "hipSetDevice"; return; }
+      rc[g] = run_batched_team(gs + s0, s1 - s0, queries + (uint64_t)s0 * q * gs[0]->dim, q, k, step, parallel, Tg,
+                               answers + (uint64_t)s0 * q * (uint64_t)k, mt.data() + s0, &comb, g);
+      if (rc[g]) { msg[g] = pm_last_error(); comb.abort.store(true); }
     });
   }
   for (auto& t : teams) t.join();

@@ -25,7 +25,7 @@ constexpr uint16_t kSkip = 0xffffu;                      // prep offset sentinel
 constexpr int kBlock = 256;
 
 // Randomness streams; identical spec to oracle/pm_oracle.cpp.
-enum : uint64_t { DOM_KEY = 1, DOM_REPL = 2, DOM_DUMMY = 3, DOM_SYNTH_DB = 9 };
+enum : uint64_t { DOM_KEY = 1, DOM_REPL = 2, DOM_DUMMY = 3, DOM_SYNTH_DB = 9, DOM_SYNTH_VEC = 10, DOM_SYNTH_NB = 11 };
 __host__ __device__ inline uint64_t sm64(uint64_t x) {
   uint64_t z = x + 0x9e3779b97f4a7c15ULL;
   z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
@@ -38,6 +38,30 @@ __host__ __device__ inline uint64_t hash4(uint64_t seed, uint64_t dom, uint64_t 
   h = sm64(h ^ a);
   h = sm64(h ^ b);
   return sm64(h ^ c);
+}
+
+// The synthetic graph DB (pm_graph_create_synth; BIGANN-scale configs[3]/[4],
+// where no graph can be built or shipped): the reference's synthetic mode
+// (private-search.go:114-117,168-170: genRandomMatrix's uniform [0,1) f32
+// vectors, genRandomGraph's uniform neighbour ids without self loops,
+// :42-69) as a pure function of (seed, vertex), so a shard generates only its
+// own rows and anyone can recompute any row.  u32 element e of vertex v's
+// PIRGraphInfo entry (private-search.go:363-397: f32[dim] || u32[m]):
+//   e <  dim: float((sm64(kv ^ (v*dim + e)) >> 40) * 2^-24)        (24 random bits, rand.Float32)
+//   e >= dim: x = sm64(kg ^ (v*m + e - dim)) % n, x + 1 (mod n) if x == v
+// with kv = sm64(seed + DOM_SYNTH_VEC), kg = sm64(seed + DOM_SYNTH_NB).
+__host__ __device__ inline float graph_synth_vec(uint64_t kv, uint64_t v, uint32_t dim, uint32_t j) {
+  return (float)(sm64(kv ^ (v * dim + j)) >> 40) * 0x1.0p-24f;
+}
+__host__ __device__ inline uint32_t graph_synth_nb(uint64_t kg, uint64_t n, uint64_t v, uint32_t m, uint32_t k) {
+  uint64_t x = sm64(kg ^ (v * m + k)) % n;
+  if (x == v) x = (x + 1) % n;
+  return (uint32_t)x;
+}
+__host__ __device__ inline uint32_t graph_synth_elem(uint64_t kv, uint64_t kg, uint64_t n, uint32_t dim, uint32_t m,
+                                                     uint64_t v, uint32_t e) {
+  if (e < dim) return __builtin_bit_cast(uint32_t, graph_synth_vec(kv, v, dim, e));
+  return graph_synth_nb(kg, n, v, m, e - dim);
 }
 
 // One PianoPIR instance ("partition") as the device sees it.  Parameters
@@ -245,6 +269,28 @@ void ip_fill(hipStream_t st, uint32_t* rows, uint64_t N, uint32_t D);
 void db_synth(hipStream_t st, uint64_t* dst, uint64_t r0, uint64_t rows, uint32_t E, uint64_t db_seed);
 // out[i] = {E words at src[i] (or zeros when null), success flag}, src in pinned host memory
 void gather_rows(hipStream_t st, const uint64_t* const* src, uint64_t n, uint32_t E, uint64_t* out);
+// ---- sharded private search (pm_shard.hip) ----
+// Synthetic graph DB rows (graph_synth_elem): dst row i = global vertex r0 + i,
+// E = (dim + m) / 2 words per row.
+void graph_synth(hipStream_t st, uint64_t* dst, uint64_t r0, uint64_t rows, uint64_t n, uint32_t dim, uint32_t m,
+                 uint64_t seed);
+// out[i*dim + j] = vector of vertex ids[i] (the start set, GetStartVertex)
+void graph_synth_vecs(hipStream_t st, const uint64_t* ids, uint64_t nids, uint32_t dim, uint64_t seed, float* out);
+// Per-id records of a shared step for the shards' combine.  Record r (session
+// s = r / npos, position r % npos of its GetVertexInfo batch) = the W - 1 row
+// words [w0, w0 + W - 1) of its answer (the neighbour list) and one word
+// {dist f32 bits | ok << 32}; map[r] = the answering sub-query of the step
+// (a DUP followed to its source) or < 0 (no local answer: zeros).  Also
+// st2[j] = {status, ref} of every sub-query j < nsub (the host's mirrors).
+void pack_records(hipStream_t st, const int32_t* map, uint32_t nrec, const PmOutHdr* hdr, const uint64_t* rows,
+                  uint32_t E, uint32_t w0, uint32_t W, uint64_t* rec, uint32_t nsub, uint32_t* st2);
+// Modelled peers (a shard layout wider than the job): records with map[r] ==
+// -2 are those another shard of the layout answers; they are filled from the
+// synthetic graph's spec, the distance to session r / npos's query (qbuf) in
+// the reference's L2 order (l2_distance_amd64.s:4-36).
+void synth_records(hipStream_t st, const int32_t* map, const uint64_t* ids, uint32_t nrec, uint32_t npos,
+                   const float* qbuf, uint32_t dim, uint32_t m, uint64_t n, uint64_t seed, uint32_t w0, uint32_t W,
+                   uint64_t* rec);
 void prf_batch(hipStream_t st, const uint32_t* rk, const uint64_t* tags, const uint64_t* xs,
                uint64_t n, uint64_t* out);
 // graph construction and ground truth (pm_graph.hip)

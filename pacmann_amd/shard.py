@@ -121,3 +121,73 @@ class ShardedBatchPIR:
 
     def stats(self) -> dict:
         return self.pir.stats()
+
+
+class RecordCombiner:
+    """The combine of pm_search_loop_sharded (private graph search over the
+    sharded DB) over a torch.distributed group.
+
+    Each lock-step team of the loop owns one device tensor of int64 words (its
+    sessions' per-id records: neighbour words, {dist, ok}), allocated here and
+    handed to the library.  After every shared step the library calls back
+    with the team index and the HIP stream the records were written on; the
+    callback sums the tensor over the group IN PLACE, ordered on that stream:
+    nccl (RCCL over xGMI) reduces on the device with the stream made current
+    (torch's ProcessGroupNCCL waits for it and makes it wait for the
+    collective: no host synchronisation); gloo copies to the host, reduces
+    and copies back.  Exactly one rank contributes a non-zero record per id,
+    so the integer sum is the unsharded answer.  The library issues the
+    callbacks of all teams in one (round, team) order on every rank, so the
+    collectives match across ranks."""
+
+    def __init__(self, group=None, device: int | None = None):
+        import torch
+        import torch.distributed as dist
+        self._dist, self._torch = dist, torch
+        self.group = group
+        self.nccl = dist.get_backend(group) == "nccl"
+        if device is None:
+            device = int(os.environ.get("LOCAL_RANK", "-1"))
+            if device < 0:
+                device = torch.cuda.current_device()
+        self.device = device
+        self.bufs = []
+        self.error = None
+        self.calls = 0
+
+    def prepare(self, words_per_team):
+        """Allocate the teams' record tensors; returns their device addresses."""
+        torch = self._torch
+        self.bufs = [torch.zeros(max(1, int(w)), dtype=torch.int64, device=f"cuda:{self.device}")
+                     for w in words_per_team]
+        torch.cuda.synchronize(self.device)
+        self.error = None
+        return [b.data_ptr() for b in self.bufs]
+
+    def callback(self, user, team, ptr, nwords, stream):
+        """pm_combine_fn: returns 0, or 1 after recording the exception."""
+        torch, dist = self._torch, self._dist
+        try:
+            t = self.bufs[team]
+            if ptr != t.data_ptr() or nwords > t.numel():
+                raise RuntimeError(f"team {team}: unexpected record buffer")
+            view = t[:nwords]
+            with torch.cuda.device(self.device):
+                ext = torch.cuda.ExternalStream(stream, device=torch.device("cuda", self.device))
+                with torch.cuda.stream(ext):
+                    if self.nccl:
+                        dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group)
+                    else:
+                        host = view.cpu()   # on the records' stream: after they are written
+                        dist.all_reduce(host, op=dist.ReduceOp.SUM, group=self.group)
+                        view.copy_(host)
+            self.calls += 1
+            return 0
+        except Exception as e:   # the library fails the loop with this status
+            self.error = e
+            return 1
+
+    def finish(self):
+        self._torch.cuda.synchronize(self.device)
+        if self.error is not None:
+            raise self.error

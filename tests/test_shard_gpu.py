@@ -31,7 +31,8 @@ def _db():
 
 def _batches(n, wide=False):
     """3B ids per batch (6 sub-queries per partition), or with wide=True 6B
-    (12 per partition) whose first 16 ids are new ids of partition 0: that
+    (12 per partition) whose first 16 ids are new ids of partition 0 spread
+    over its chunks (no per-chunk limit, pir.go:396-400): that
     partition's FinishedQueryNum then tracks QueriesMadeInPartition, so late
     in the window a batch would take it past MaxQueryNum and the engine serves
     it by the multi-step path (one sub-query at a time, pir.go:527-530)."""
@@ -40,7 +41,7 @@ def _batches(n, wide=False):
     for b in range(n):
         if wide:   # partition 0: 16 ids never asked before (no local-cache hits); the rest elsewhere
             q = rng.integers(PS, N, size=6 * B, dtype=np.uint64)
-            q[:16] = np.arange(b * 16, b * 16 + 16, dtype=np.uint64) % np.uint64(PS)
+            q[:16] = (np.arange(b * 16, b * 16 + 16, dtype=np.uint64) * np.uint64(263)) % np.uint64(PS)   # spread over chunks
         else:
             q = rng.integers(0, N, size=3 * B, dtype=np.uint64)
             q[4] = q[1]

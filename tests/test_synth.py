@@ -22,3 +22,20 @@ def test_synth_rows_spec():
         want = [sm64(k ^ (r * E + w)) for w in range(E)]
         assert got[i].tolist() == want
     assert got.dtype == np.uint64 and got.shape == (4, E)
+
+
+def test_synthetic_graph_rows():
+    """pm_graph_synth_rows (host code, no device) follows the synthetic graph
+    spec (pm_internal.h graph_synth_elem, the reference's -input synthetic
+    mode): vectors in [0, 1) with 24 random bits, neighbours in range and
+    never the vertex itself, rows a pure function of (seed, vertex)."""
+    import numpy as np
+    import pacmann_amd as pm
+    v, nb = pm.graph_synth_rows(1000, 16, 8, 5, np.arange(1000))
+    assert v.dtype == np.float32 and (v >= 0).all() and (v < 1).all()
+    assert np.array_equal(v * np.float32(2 ** 24), np.rint(v * np.float32(2 ** 24)))
+    assert (nb < 1000).all() and not (nb == np.arange(1000)[:, None]).any()
+    v2, nb2 = pm.graph_synth_rows(1000, 16, 8, 5, [999, 3])
+    assert np.array_equal(v2, v[[999, 3]]) and np.array_equal(nb2, nb[[999, 3]])
+    v3, _ = pm.graph_synth_rows(1000, 16, 8, 6, [3])
+    assert not np.array_equal(v3, v[[3]])
