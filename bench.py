@@ -317,150 +317,120 @@ def private_search_msmarco(local, args, with_cpu: bool):
     return out
 
 
-# BASELINE.json configs[3] / configs[4]: BIGANN-shaped batch PIR.  Entries are
-# PIRGraphInfo's wire format for d = 128, m = 32 (private-search.go:418-439):
-# (128 + 32) * 4 B = 640 B = 80 words.  The DB is generated on the device
-# (pm_batchpir_create_synth), uniform like TestBatchPIRPerf's.  A private query
-# of the harness is STEP rounds of PARALLEL * M = 96 ids; the rounds here draw
-# uniform ids (the 100M / 1B graphs cannot be built offline in bench time).
-BIG_E, BIG_ROUNDS, BIG_PROFILE_ROUNDS = 80, 400, 40
+# BASELINE.json configs[3] / configs[4]: private graph search over a sharded
+# BIGANN-scale graph DB.  No 10^8 / 10^9-vector dataset or graph can be built
+# or shipped here, so the graph is the reference's synthetic mode
+# (private-search.go:42-69,114-117,168-170: uniform [0,1) f32 vectors, uniform
+# neighbour ids, uniform [0,1) queries) generated on the device from a seed
+# (pm_graph_create_synth); entries are PIRGraphInfo's d = 128, m = 32 wire
+# format, (128 + 32) * 4 B = 640 B = 80 words.  S client sessions per GPU run
+# the full private-search.go loop (SearchKNN over PIRGraphInfo, 20 rounds of
+# 96 ids, maintenance trigger) in lock-step teams over this rank's shard of the
+# batch PIR (partitions p % layout == shard); every shared step ends in ONE
+# combine of the team's per-id records (RCCL all-reduce over xGMI when the
+# layout is spread over the job's ranks).  A layout wider than the job (the
+# 1B DB on fewer than 8 GPUs: 640 GB does not fit one GPU's 288 GB) runs one
+# shard per GPU with the other shards' answers generated from the graph's
+# spec on the device (modelled peers: their PIR work is not measured).
+BIG_DIM, BIG_E, BIG_SEARCH_Q, BIG_SEARCH_WARMUP, BIG_GROUPS = 128, 80, 12, 2, 2
+BIG_SESSIONS = {"config3_bigann_100m": 32, "config4_bigann_1b": 16}   # caps; memory decides below
 
 
-def bigann_pir(name, n_entries, layout, rank, ws, local, dist, nccl_group, rounds=BIG_ROUNDS):
-    """One BIGANN block on every rank.  `layout` = shards the 16 partitions are
-    split into.  layout == ws: rank r holds shard r, the whole DB over the
-    node, combined by an RCCL all-reduce per round.  layout > ws (the 1B DB
-    on fewer than 8 GPUs: 640 GB does not fit one GPU's 288 GB): each rank
-    measures the shards r, r + ws, ... one after another, and the block
-    reports the layout's round time as the slowest shard's (modelled: the
-    shards of a real 8-GPU run answer concurrently; its all-reduce is not
-    included)."""
-    if layout <= ws:
-        return bigann_shard(name, n_entries, layout, rank, rank, ws, local, dist, nccl_group, rounds)
-    per = [bigann_shard(name, n_entries, layout, sh, rank, ws, local, dist, nccl_group, rounds, reduce=False)
-           for sh in range(rank, layout, ws)]
-    out = dict(per[0])
-    if dist:   # every rank's shards, on rank 0
-        import torch
-        t = torch.zeros((layout, 4), dtype=torch.float64)
-        for sh, r in zip(range(rank, layout, ws), per):
-            t[sh] = torch.tensor([r["ms_per_round"], r["preprocessing_s"], r["check"]["mismatches"],
-                                  r["check"]["ids_answered"]], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        rows = t.tolist()
-    else:
-        rows = [[r["ms_per_round"], r["preprocessing_s"], r["check"]["mismatches"], r["check"]["ids_answered"]]
-                for r in per]
-    ms_round = max(r[0] for r in rows)
-    prep = max(r[1] for r in rows)
-    support = per[0]["support_batch_num"]
-    online_q = ms_round * STEP / 1e3
-    maint_q = prep / support * STEP * PARALLEL
-    out["shards_measured"] = layout
-    out["per_shard"] = [{"shard": i, "ms_per_round": round(r[0], 4), "preprocessing_s": round(r[1], 4)}
-                        for i, r in enumerate(rows)]
-    out["check"] = {"ids_answered": int(sum(r[3] for r in rows)), "mismatches": int(sum(r[2] for r in rows))}
-    out["modelled_layout"] = {
-        "ms_per_round": round(ms_round, 4), "preprocessing_s": round(prep, 4),
-        "online_s_per_query": round(online_q, 6), "maintenance_s_per_query": round(maint_q, 6),
-        "private_queries_per_s": round(1.0 / (online_q + maint_q), 2),
-        "note": f"all {layout} shards measured one after another on {ws} GPU(s); a {layout}-GPU node answers "
-                "a round in the slowest shard's time (taken here) plus one RCCL all-reduce of the round's "
-                "96 x 81 words (not included: unmeasured on one GPU)"}
-    out["combine"] = (f"none measured: the {layout} shards ran one after another on this GPU; at {layout} GPUs "
-                      "the rounds combine through ShardedBatchPIR's device-resident RCCL all-reduce")
-    return out
+def client_bytes(sub: dict, E: int) -> int:
+    """Device bytes of one client's state for one partition (engine_create's
+    arrays: tags, program points, parities, replacement rows, histogram,
+    local cache arena, the PRF tables tab + tabT and the search row cur)."""
+    PH, SS, Q, MQ = sub["PrimaryHintNum"], sub["SetSize"], sub["MaxQueryPerChunk"], sub["MaxQueryNum"]
+    H = PH + SS * Q
+    return (H * 4 + PH * 4 + H * E * 8 + SS * Q * (4 + E * 8) + SS * 4 + MQ * E * 8 + H * SS * 2
+            + (SS + 7) // 8 * 8 * H * 2 + PH * SS * 2)
 
 
-def bigann_shard(name, n_entries, layout, shard, rank, ws, local, dist, nccl_group, rounds=BIG_ROUNDS,
-                 reduce=True):
-    """Shard `shard` of the layout on this rank (see bigann_pir); reduce: the
-    times are the max and the checks the sum over the ranks (one shard each)."""
-    progress(f"  {name}: shard {shard} of {layout}")
+def bigann_search(key, name, n_entries, layout, rank, ws, local, dist, comb_group, args):
     import gc
 
+    import torch
+
     import pacmann_amd as pm
-    ctx = pm.Context(local)
+    from pacmann_amd.shard import RecordCombiner
+    shard = rank % layout
+    modelled = layout > ws
     combine = layout == ws and ws > 1
+    progress(f"  {key}: shard {shard} of {layout}" + (" (other shards modelled)" if modelled else ""))
+    ctx = pm.Context(local)
+    ctx.timing(1)
     t0 = time.perf_counter()
-    if combine:   # the whole DB over the job: each rank one shard, entries all-reduced per round
-        from pacmann_amd.shard import ShardedBatchPIR
-        sp = ShardedBatchPIR(n_entries, BIG_E * 8, M, None, F, seed=31, group=nccl_group, ctx=ctx, db_seed=41,
-                             device=local)
-        g = sp.pir
-    else:
-        g = pm.SimpleBatchPianoPIR(n_entries, BIG_E * 8, M, None, F, seed=31, ctx=ctx, shard=shard,
-                                   nshards=layout, db_seed=41)
+    base = pm.PIRGraphInfo.Synthetic(n_entries, BIG_DIM, M, data_seed=51, shard=shard, nshards=layout,
+                                     pir_seed=61, search_seed=62, ctx=ctx)
+    base.Preprocess()   # the DB generated on the device, then the first client's preprocessing
     ctx.sync()
-    t_create = time.perf_counter() - t0
-    ctx.timing_reset()
-    ctx.timing(True)
-    if dist:
-        dist.barrier()
-    t0 = time.perf_counter()
-    g.Preprocessing()
-    ctx.sync()
-    prep = time.perf_counter() - t0
+    t_base = time.perf_counter() - t0
     ctx.timing(False)
     kprep = {k: ctx.timing_get(k) for k in ("prep_offsets", "prep_fold", "prep_repl")}
-    stats = g.stats()
-    PS = stats["PartitionSize"]
-    sub = g.SubConfig(shard)
-    rng = np.random.default_rng(4242)
-    ids = rng.integers(0, n_entries, size=(rounds + BIG_PROFILE_ROUNDS + 10, PARALLEL * M)).astype(np.uint64)
-    def one(q):
-        return sp.QueryWithMask(q) if combine else g.QueryWithMask(q)
-
-    for q in ids[:10]:
-        one(q)
-    keep = []
+    pir = base.PIR
+    stats = pir.stats()
+    own = [p for p in range(stats["PartitionNum"]) if p % layout == shard]
+    subs = [pir.SubConfig(p) for p in own]
+    per_client = sum(client_bytes(c, BIG_E) for c in subs)
+    free, _ = ctx.mem_info()
+    S = int(max(1, min(BIG_SESSIONS[key], 1 + (free * 0.8) // per_client)))
+    if args.big_sessions:
+        S = min(S, args.big_sessions)
+    if dist:   # the same sessions on every rank
+        t = torch.tensor([S], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        S = int(t.item())
+    sess = [base] + [base.Session(61 + i, 62 + i, pm.Context(local)) for i in range(1, S)]
+    for x in sess[1:]:
+        x.Preprocess()
+    ctxs = [x.ctx for x in sess]
+    nq = BIG_SEARCH_WARMUP + BIG_SEARCH_Q
+    qs = np.random.default_rng(63).random((S, nq, BIG_DIM), dtype=np.float32)   # genRandomMatrix queries
+    comb = RecordCombiner(group=comb_group, device=local) if combine else None
+    groups = min(BIG_GROUPS, S)
+    pm.search_loop_sharded(sess, qs[:, :BIG_SEARCH_WARMUP], K_TOP, STEP, PARALLEL, groups, args.threads,
+                           combiner=comb, model_peers=modelled)
+    for c in ctxs:
+        c.sync()
+        c.timing_reset()
+        c.timing(2)
     if dist:
         dist.barrier()
-    ctx.sync()
     t0 = time.perf_counter()
-    for q in ids[10:10 + rounds]:
-        keep.append(one(q))
-    ctx.sync()
+    ans, wall, online, maint = pm.search_loop_sharded(sess, qs[:, BIG_SEARCH_WARMUP:], K_TOP, STEP, PARALLEL, groups,
+                                                      args.threads, combiner=comb, model_peers=modelled)
+    for c in ctxs:
+        c.sync()
     if dist:
         dist.barrier()
-    online = time.perf_counter() - t0
-    # profile window: per-launch device time of the step kernels
-    ctx.timing_reset()
-    ctx.timing(2)
-    for q in ids[10 + rounds:]:
-        one(q)
-    ctx.timing(False)
-    kstep = {k: ctx.timing_get(k) for k in ("hint_match", "resolve", "gather", "answer", "step")}
-    # the reference's property (pir_test.go:45-49): each successful entry is its row
-    bad = nok = 0
-    for q, (out, ok) in zip(ids[10:10 + rounds], keep):
-        if combine:
-            mine = np.ones(len(q), bool)
-        else:
-            mine = (q // np.uint64(PS)) % np.uint64(layout) == np.uint64(shard)
-        bad += int((ok & ~mine).sum())
-        sel = np.where(ok)[0]
-        nok += len(sel)
-        if len(sel):
-            bad += int((out[sel] != pm.synth_rows(41, q[sel], BIG_E)).any(axis=1).sum())
-        bad += int(out[~ok].any(axis=1).sum())
-    if combine:
-        del sp
-    del g, keep
-    gc.collect()
-    ctx.close()
-    if dist and reduce:
-        import torch
-        t = torch.tensor([prep, online, t_create], dtype=torch.float64)
+    elapsed = time.perf_counter() - t0
+    for c in ctxs:
+        c.timing(False)
+
+    def tsum(name):
+        r = [c.timing_get(name) for c in ctxs]
+        return tuple(sum(x[i] for x in r) for i in range(3))
+    kt = {k: tsum(k) for k in ("hint_match", "resolve", "match_resolve", "gather", "answer", "pack_records",
+                                "synth_records", "combine", "prep_offsets", "prep_fold", "prep_repl", "l2_rows")}
+    ht = {k: tsum(k) for k in ("host_combine", "host_combine_turn", "host_step_wait", "host_batch_query",
+                                "host_gvi_parse")}
+    rounds = BIG_SEARCH_Q * STEP * groups   # shared steps in the timed region (every team)
+    same = 1
+    if dist:   # every rank holds the same answers (the combined records drive identical searches)
+        h = torch.tensor([int(np.bitwise_xor.reduce(ans.ravel().astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15)))
+                          & ((1 << 62) - 1)], dtype=torch.int64)
+        hmax, hmin = h.clone(), h.clone()
+        dist.all_reduce(hmax, op=dist.ReduceOp.MAX)
+        dist.all_reduce(hmin, op=dist.ReduceOp.MIN)
+        same = int(hmax.item() == hmin.item())
+        t = torch.tensor([elapsed, t_base], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        prep, online, t_create = (float(x) for x in t)
-        c = torch.tensor([bad, nok], dtype=torch.int64)
-        dist.all_reduce(c, op=dist.ReduceOp.SUM)
-        bad, nok = (int(x) for x in c)
-    ms_round = online / rounds * 1e3
-    online_q = ms_round * STEP / 1e3
-    # amortised maintenance per query, the harness's accounting (private-search.go:298)
-    maint_q = prep / stats["SupportBatchNum"] * STEP * PARALLEL
+        elapsed, t_base = (float(x) for x in t)
+    tot, succ = 0, 0
+    for x in sess:
+        a, b = x.counts()
+        tot, succ = tot + a, succ + b
+    prep_client = kprep["prep_offsets"][1] + kprep["prep_fold"][1] + kprep["prep_repl"][1]   # one client, ms
 
     def roof(entry, nbytes=None):
         n, ms, by = entry
@@ -468,52 +438,59 @@ def bigann_shard(name, n_entries, layout, shard, rank, ws, local, dist, nccl_gro
         if not n or not ms or not by:
             return None
         ach = (by / n) / (ms / n / 1e3) / 1e9
-        return {"avg_ms": round(ms / n, 5), "alg_bytes_per_launch": by / n, "achieved": round(ach, 1),
+        return {"avg_ms": round(ms / n, 5), "launches": n, "alg_bytes_per_launch": by / n, "achieved": round(ach, 1),
                 "unit": "GB/s", "peak": HBM_PEAK_GBS, "frac": round(ach / HBM_PEAK_GBS, 4)}
-
-    n_part = sum(1 for p in range(16) if p % layout == shard)
-    rows_local = sum(min(PS, n_entries - p * PS) for p in range(16) if p % layout == shard)
     fold = roof(kprep["prep_fold"])
     if fold:
+        rows_local = sum(c["DBSize"] for c in subs)
         comp = rows_local * BIG_E * 8
         fold["compulsory"] = {"bytes": comp, "achieved": round(comp / (fold["avg_ms"] / 1e3) / 1e9, 1),
                               "frac": round(comp / (fold["avg_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
-    gather_key = "gather" if kstep["gather"][0] else "answer"
-    # PMC HBM bytes of the same launches (profiles/r*/pmc_summary.json, by launch shape)
-    H = sub["PrimaryHintNum"] + sub["SetSize"] * sub["MaxQueryPerChunk"]
-    fold_grid = -(-H * (BIG_E // 2) // 256) * 256 * n_part
-    nsub = PARALLEL * M // 16 * n_part
-    nsplit = max(1, min(-(-sub["SetSize"] // 48), -(-2048 // nsub), 64)) if sub["SetSize"] >= 256 else 1
-    gather_grid = nsplit * nsub * 256
-    if fold:
-        attach_traffic(fold, "void pm::k_prep_fold<2>(pm::PmPart const*, unsigned long const*, unsigned int)",
-                       fold_grid)
-    ans_roof = roof(kstep[gather_key])
-    if ans_roof and gather_key == "gather":
-        ans_roof["kernel"] = "gather"
-        attach_traffic(ans_roof, "void pm::k_gather<2>(pm::PmStep)", gather_grid)
-    return {
-        "workload": f"{name}: {n_entries:,} x 640 B entries (d=128 f32 + m=32 u32 ids), BatchSize 32 "
-                    f"(16 partitions), FailureProbLog2 8, device-generated uniform DB; rounds of "
-                    f"{PARALLEL * M} uniform ids, {STEP} rounds per private query",
-        "n_ranks": ws, "layout_shards": layout, "shards_measured": min(ws, layout), "shard": shard,
-        "support_batch_num": stats["SupportBatchNum"],
-        "partitions_per_rank": n_part, "rank_db_gb": round(rows_local * BIG_E * 8 / 1e9, 2),
-        "subconfig": {k: sub[k] for k in ("ChunkSize", "SetSize", "PrimaryHintNum", "MaxQueryPerChunk",
-                                          "MaxQueryNum")},
-        "combine": (("RCCL" if nccl_group is not None else "gloo (--combine gloo)")
-                    + " all-reduce of the shards' disjoint entries per round (sum == xor)" if combine
-                    else "none (one rank holds every partition)" if layout == 1
-                    else f"none: each rank runs one shard of the {layout}-way layout; the combine is not run"),
-        "db_create_s": round(t_create, 3), "preprocessing_s": round(prep, 4),
-        "rounds": rounds, "ms_per_round": round(ms_round, 4),
-        "online_s_per_query": round(online_q, 6), "maintenance_s_per_query": round(maint_q, 6),
-        "private_queries_per_s": round(1.0 / (online_q + maint_q), 2),
-        "kernel_avg_us": {k: round(v[1] / v[0] * 1e3, 3) for k, v in {**kprep, **kstep}.items() if v[0]},
-        "pir_scan_fold": fold,
-        "pir_scan_answer": ans_roof,
-        "check": {"ids_answered": nok, "mismatches": bad},
+    gkey = "gather" if kt["gather"][0] else "answer"
+    ans_roof = roof(kt[gkey])
+    if ans_roof:
+        ans_roof["kernel"] = gkey
+    support = stats["SupportBatchNum"]
+    maint_model = prep_client / 1e3 / support * STEP * PARALLEL   # one client's amortised maintenance (:298)
+    n_comb, ms_comb, by_comb = kt["combine"]
+    out = {
+        "workload": f"{name}: private graph search (SearchKNN over PIRGraphInfo, k = {K_TOP}, step {STEP}, "
+                    f"parallel {PARALLEL}) over a {n_entries:,}-vertex synthetic graph (the reference's -input "
+                    f"synthetic mode: uniform [0,1) d = {BIG_DIM} vectors, uniform degree-{M} neighbours, uniform "
+                    f"queries) generated on the device; 640-B entries, BatchSize 32 (16 partitions), "
+                    f"FailureProbLog2 8",
+        "n_ranks": ws, "layout_shards": layout, "shard": shard,
+        "peers": ("modelled: the other shards' answers generated from the graph's spec on the device "
+                  f"({layout} shards, {ws} GPU(s); their PIR work is not measured)" if modelled else
+                  "RCCL all-reduce of the team's records per shared step" if combine and comb_group is not None else
+                  "gloo all-reduce of the team's records per shared step" if combine else
+                  "none (one rank holds every partition)"),
+        "sessions": S, "lockstep_groups": groups, "queries_per_session": BIG_SEARCH_Q,
+        "private_queries_per_s": round(S * BIG_SEARCH_Q / elapsed, 2), "wall_s": round(elapsed, 4),
+        "ms_per_round": round(elapsed / (BIG_SEARCH_Q * STEP) * 1e3, 4),
+        "online_s_per_query": round(float(np.mean(online)) / BIG_SEARCH_Q, 6),
+        "maintenance_s_per_query_in_region": round(float(np.mean(maint)) / BIG_SEARCH_Q, 6),
+        "maintenance_s_per_query_amortised": round(maint_model, 6),
+        "support_batch_num": support, "partitions_per_rank": len(own),
+        "rank_db_gb": round(sum(c["DBSize"] for c in subs) * BIG_E * 8 / 1e9, 2),
+        "client_state_gb": round(per_client / 1e9, 2),
+        "subconfig": {k: subs[0][k] for k in ("ChunkSize", "SetSize", "PrimaryHintNum", "MaxQueryPerChunk",
+                                              "MaxQueryNum")},
+        "db_and_first_client_s": round(t_base, 3), "preprocessing_ms_one_client": round(prep_client, 3),
+        "kernel_avg_us": {k: round(v[1] / v[0] * 1e3, 3) for k, v in {**kt, **kprep}.items() if v[0]},
+        "combine": {"launches": n_comb, "ms_per_round": round(ms_comb / n_comb, 5) if n_comb else None,
+                    "bytes_per_round": by_comb / n_comb if n_comb else 0,
+                    "host_ms_per_round": round(ht["host_combine"][1] / max(1, ht["host_combine"][0]), 5),
+                    "turn_wait_ms_per_round": round(ht["host_combine_turn"][1] / max(1, ht["host_combine_turn"][0]), 5),
+                    "note": "device time of the in-place all-reduce on the team stream (events around the "
+                            "combine), per shared step; host_ms is the callback's wall time"},
+        "pir_scan_fold": fold, "pir_scan_answer": ans_roof,
+        "check": {"ids_fetched": tot, "ids_answered": succ, "ranks_identical": bool(same)},
     }
+    del sess, base, ctxs, pir
+    gc.collect()
+    ctx.close()
+    return out
 
 
 # BASELINE.json configs[0]: graphann_test.go's InnerProduct benchmark
@@ -702,6 +679,7 @@ def main():
     ap.add_argument("--no-single", action="store_true", help="skip the one-client latency block")
     ap.add_argument("--no-bigann", action="store_true", help="skip the BIGANN-100M / 1B batch-PIR blocks")
     ap.add_argument("--no-config0", action="store_true", help="skip the InnerProduct scan block")
+    ap.add_argument("--big-sessions", type=int, default=0, help="cap on the BIGANN blocks' sessions per GPU")
     ap.add_argument("--combine", choices=["rccl", "gloo"], default="rccl",
                     help="collective of the sharded BIGANN rounds (gloo: host tensors, e.g. ranks sharing one GPU)")
     ap.add_argument("--no-kernel-timing", action="store_true",
@@ -965,7 +943,8 @@ def main():
                                             1_000_000_000, 8)):
             try:
                 progress(key)
-                out[key] = bigann_pir(nm, n_entries, layout, rank, ws, local, dist, nccl_group)
+                out[key] = bigann_search(key, nm, n_entries, layout, rank, ws, local, dist,
+                                         nccl_group if nccl_group is not None else None, args)
             except Exception as e:   # recorded, never fatal to the headline line
                 out[key] = {"error": f"{type(e).__name__}: {e}"}
     if rank == 0:

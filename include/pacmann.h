@@ -52,6 +52,9 @@ int         pm_ctx_create(int device, pm_ctx** out);
 void        pm_ctx_destroy(pm_ctx* ctx);
 const char* pm_last_error(void);
 int         pm_ctx_sync(pm_ctx* ctx);
+/* Free and total device memory of the context's GPU (bytes; sizing how many
+ * client sessions a GPU holds next to its DB). */
+int         pm_ctx_mem_info(pm_ctx* ctx, uint64_t* free_bytes, uint64_t* total_bytes);
 /* Per-kernel timing.  Level 1: HIP events around the preprocessing and leaf
  * kernels on the stream they run on ("prep_offsets", "prep_fold",
  * "prep_repl", "l2_rows", "ip_scan", "prf", server "answer").  Level 2 also

@@ -68,6 +68,7 @@ SIGNATURES = {
     "pm_ctx_destroy": (None, [vp]),
     "pm_last_error": (C.c_char_p, []),
     "pm_ctx_sync": (C.c_int, [vp]),
+    "pm_ctx_mem_info": (C.c_int, [vp, u64p, u64p]),
     "pm_timing_enable": (C.c_int, [vp, C.c_int]),
     "pm_timing_reset": (C.c_int, [vp]),
     "pm_timing_get": (C.c_int, [vp, C.c_char_p, u64p, C.POINTER(dbl), C.POINTER(dbl)]),
@@ -205,6 +206,12 @@ class Context:
 
     def sync(self):
         _check(lib().pm_ctx_sync(self.h))
+
+    def mem_info(self):
+        """(free, total) device memory in bytes."""
+        f, t = C.c_uint64(), C.c_uint64()
+        _check(lib().pm_ctx_mem_info(self.h, C.byref(f), C.byref(t)))
+        return f.value, t.value
 
     def timing(self, on):
         """0 off, 1 (True) preprocessing and leaf kernels, 2 also the step kernels."""

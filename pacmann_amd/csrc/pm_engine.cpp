@@ -279,6 +279,15 @@ extern "C" int pm_ctx_create(int device, pm_ctx** out) {
 }
 extern "C" void pm_ctx_destroy(pm_ctx* c) { if (c) { (void)hipSetDevice(c->device); delete c; } }
 extern "C" int pm_ctx_sync(pm_ctx* c) { HIPCHK(hipStreamSynchronize(c->stream)); HIPCHK(hipGetLastError()); return 0; }
+extern "C" int pm_ctx_mem_info(pm_ctx* c, uint64_t* free_b, uint64_t* total_b) {
+  if (!c) return fail(PM_EINVAL, "ctx is NULL");
+  HIPCHK(hipSetDevice(c->device));
+  size_t f = 0, t = 0;
+  HIPCHK(hipMemGetInfo(&f, &t));
+  if (free_b) *free_b = f;
+  if (total_b) *total_b = t;
+  return 0;
+}
 extern "C" int pm_timing_enable(pm_ctx* c, int on) { c->timing = on; return 0; }
 extern "C" int pm_timing_reset(pm_ctx* c) {
   HIPCHK(hipStreamSynchronize(c->stream));
@@ -2010,7 +2019,7 @@ static int knn_begin_enqueue(pm_graph* g, const float* query, int benchmarking) 
 // sdh: the start set's distances (null: where knn_begin_enqueue put them)
 static void knn_begin_finish(pm_graph* g, int parallel, int benchmarking, const float* sdh = nullptr) {
   if (benchmarking) return;
-  const uint64_t ns = g->start.size(), m = g->m;
+  const uint64_t ns = g->start.size();
   if (!sdh) sdh = g->stage_h.as<float>() + g->dim;
   // the first `parallel` start vertices in stable distance order (search.go:130-146):
   // a partial sort on (dist, position) selects exactly those

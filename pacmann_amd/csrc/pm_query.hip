@@ -2105,8 +2105,11 @@ void step_match(hipStream_t st, const PmStep& S, uint32_t maxPH, PmEvents ev) {
 }
 bool step_match_resolve_ok(const PmStep& S, bool lds) {
   static const int mode = [] { const char* e = getenv("PM_MATCH_RESOLVE"); return e ? atoi(e) : 1; }();
+  // one workgroup per partition matches every hint of it: search-sized hint
+  // counts only (PH <= 16,384; BIGANN's 57,344 / 114,688 hints per partition
+  // go to k_match_part's workgroup per (partition, hint block) instead)
   return mode && !lds && !S.args_valid && S.subs == S.subs_h && S.sb == S.sb_h && S.np >= 128 &&
-         S.nsub >= 4 * S.np;
+         S.nsub >= 4 * S.np && S.words <= 256;
 }
 void step_match_resolve(hipStream_t st, const PmStep& S, bool ph8, uint32_t maxPH, uint32_t max_sub_per_part,
                         PmEvents ev) {
