@@ -415,14 +415,15 @@ def bigann_search(key, name, n_entries, layout, rank, ws, local, dist, comb_grou
     ht = {k: tsum(k) for k in ("host_combine", "host_combine_turn", "host_step_wait", "host_batch_query",
                                 "host_gvi_parse")}
     rounds = BIG_SEARCH_Q * STEP * groups   # shared steps in the timed region (every team)
-    same = 1
-    if dist:   # every rank holds the same answers (the combined records drive identical searches)
+    same = None if modelled else 1   # modelled layouts: each rank serves another shard (its own failures)
+    if dist and not modelled:   # every rank holds the same answers (the combined records drive identical searches)
         h = torch.tensor([int(np.bitwise_xor.reduce(ans.ravel().astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15)))
                           & ((1 << 62) - 1)], dtype=torch.int64)
         hmax, hmin = h.clone(), h.clone()
         dist.all_reduce(hmax, op=dist.ReduceOp.MAX)
         dist.all_reduce(hmin, op=dist.ReduceOp.MIN)
         same = int(hmax.item() == hmin.item())
+    if dist:
         t = torch.tensor([elapsed, t_base], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, t_base = (float(x) for x in t)
@@ -485,7 +486,7 @@ def bigann_search(key, name, n_entries, layout, rank, ws, local, dist, comb_grou
                     "note": "device time of the in-place all-reduce on the team stream (events around the "
                             "combine), per shared step; host_ms is the callback's wall time"},
         "pir_scan_fold": fold, "pir_scan_answer": ans_roof,
-        "check": {"ids_fetched": tot, "ids_answered": succ, "ranks_identical": bool(same)},
+        "check": {"ids_fetched": tot, "ids_answered": succ, "ranks_identical": None if same is None else bool(same)},
     }
     del sess, base, ctxs, pir
     gc.collect()
