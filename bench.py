@@ -46,6 +46,17 @@ sys.path.insert(0, str(ROOT))
 
 N, DIM, M, K_TOP, STEP, PARALLEL, F = 1_000_000, 128, 32, 10, 20, 3, 8
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# LDS ceilings (MI355X_MICROARCH.md §LDS: 64 x 4-B banks; every CU streaming at
+# ~2.4 GHz): ds_read_b64 / b128 ~150 TB/s (256 B/clk/CU), ds_read_b32 ~75 TB/s
+# (128 B/clk/CU, 32 lookups/clk/CU when conflict-free)
+LDS_B128_PEAK_GBS, LDS_B32_PEAK_GBS = 150_000.0, 75_000.0
+# k_prep_offsets' AES (pm_aes.h prf_lo16_split): rounds 2-8 16 T-table lookups
+# each, round 9 two columns (8), round 10 two S-box bytes (2), round 1's
+# per-hint half (4 per 8 chunks) = 122.5 conflict-free ds_read_b32 per PRF
+# (the tables are 32x bank-replicated), and ~2 VALU per lookup (v_perm address,
+# v_bitop3 XORs, one rotation per column)
+AES_LOOKUPS_PER_PRF = 122.5
+PRF_PEAK_G = LDS_B32_PEAK_GBS * 1e9 / 4 / AES_LOOKUPS_PER_PRF / 1e9   # ~153 G PRF/s: the lookup ceiling
 METRIC = "private queries/sec + PIR-scan HBM GB/s, SIFT1M d=128 at 1/2/4/8 GPUs"
 PREP_KERNELS = ["prep_offsets", "prep_fold", "prep_repl", "l2_rows"]
 STEP_KERNELS = ["step", "hint_match", "resolve", "match_resolve", "gather", "answer"]   # timed in the measured region too
@@ -339,10 +350,12 @@ BIG_SESSIONS = {"config3_bigann_100m": 32, "config4_bigann_1b": 16}   # caps; me
 def client_bytes(sub: dict, E: int) -> int:
     """Device bytes of one client's state for one partition (engine_create's
     arrays: tags, program points, parities, replacement rows, histogram,
-    local cache arena, the PRF tables tab + tabT and the search row cur)."""
+    local cache arena, the tag-major PRF table tabT and the search row cur;
+    the chunk-major table tab is not allocated for the BIGANN shapes, whose
+    fold reads tabT: pmk::fold_needs_tab)."""
     PH, SS, Q, MQ = sub["PrimaryHintNum"], sub["SetSize"], sub["MaxQueryPerChunk"], sub["MaxQueryNum"]
     H = PH + SS * Q
-    return (H * 4 + PH * 4 + H * E * 8 + SS * Q * (4 + E * 8) + SS * 4 + MQ * E * 8 + H * SS * 2
+    return (H * 4 + PH * 4 + H * E * 8 + SS * Q * (4 + E * 8) + SS * 4 + MQ * E * 8
             + (SS + 7) // 8 * 8 * H * 2 + PH * SS * 2)
 
 
@@ -486,6 +499,7 @@ def bigann_search(key, name, n_entries, layout, rank, ws, local, dist, comb_grou
                     "note": "device time of the in-place all-reduce on the team stream (events around the "
                             "combine), per shared step; host_ms is the callback's wall time"},
         "pir_scan_fold": fold, "pir_scan_answer": ans_roof,
+        "roofline_prf": prf_roofline(kprep["prep_offsets"], "k_prep_offsets of one client's preprocessing"),
         "check": {"ids_fetched": tot, "ids_answered": succ, "ranks_identical": None if same is None else bool(same)},
     }
     del sess, base, ctxs, pir
@@ -554,6 +568,21 @@ def dist_init():
     ndev = torch.cuda.device_count()   # counting devices does not initialise HIP
     # more ranks than GPUs (a rehearsal on one GPU): ranks share devices round-robin
     return dist, dist.get_rank(), ws, local % max(ndev, 1)
+
+
+def prf_roofline(entry, note):
+    """AES-PRF throughput of k_prep_offsets launches (timing entry: launches,
+    ms, PRFs evaluated) against the T-table lookup ceiling (PRF_PEAK_G)."""
+    n, ms, prfs = entry
+    if not n or not ms or not prfs:
+        return None
+    g = prfs / (ms / 1e3) / 1e9
+    return {"bound": "lds", "kernel": "prep_offsets", "achieved": round(g, 2), "peak": round(PRF_PEAK_G, 2),
+            "unit": "G PRF/s", "frac": round(g / PRF_PEAK_G, 4), "launches": n, "avg_ms": round(ms / n, 5),
+            "prfs_per_launch": prfs / n, "lookups_per_prf": AES_LOOKUPS_PER_PRF,
+            "note": f"{note}: AES-128 blocks per second against the conflict-free ds_read_b32 lookup rate "
+                    f"(~75 TB/s = 18.75 T lookups/s) / {AES_LOOKUPS_PER_PRF} lookups per PRF (pm_aes.h); the "
+                    "~2 VALU per lookup put the vector-issue ceiling at the same ~150-160 G PRF/s"}
 
 
 def rccl_group(dist, local, out):
@@ -748,7 +777,7 @@ def main():
     # the same kernels with ONE lock-step group alone on the GPU (no other
     # group's kernels beside them), and one client's maintenance alone: the
     # isolated per-launch times beside the contended ones above
-    isolated = None
+    isolated = one_prf = None
     if args.mode == "batched" and not args.no_kernel_timing:
         gsz = max(1, S // max(1, args.groups))
         grp = sess[:gsz]
@@ -777,6 +806,7 @@ def main():
             n, ms, _ = one.ctx.timing_get(k)
             if n:
                 isolated["kernel_avg_us"][f"{k}_one_client"] = round(ms / n * 1e3, 3)
+        one_prf = one.ctx.timing_get("prep_offsets")
     # recall@10 of every timed answer against exact kNN (ComputeRecall, build_graph.go:821-863)
     from pacmann_amd.report import compute_recall
     tq = qsess[:, args.warmup:args.warmup + args.steps].reshape(-1, DIM)
@@ -845,9 +875,18 @@ def main():
         H0 = c0["PrimaryHintNum"] + c0["SetSize"] * c0["MaxQueryPerChunk"]
         npv = stats["PartitionNum"] * -(-(k * H0) // 5120)
         attach_traffic(fold, SYMBOLS["prep_fold"], 8 * -(-npv // 8) * -(-(E // 4) // 2) * 2 * 1024)
-        fold["note"] = ("fold bytes (hint x chunk entry reads, SURVEY.md §8d) exceed HBM peak because the "
-                        "kernel serves them from LDS; 'compulsory' is the DB read once plus the parity writes "
-                        "of the clients folded in one launch")
+        # the fold is LDS-bound, not HBM-bound: its fold bytes (one entry read per
+        # (hint, chunk) pair) are ds_read_b128 reads of the staged
+        # chunks; HBM carries the staging (PMC traffic) and the parity writes
+        fold["bound"], fold["peak"] = "lds", LDS_B128_PEAK_GBS
+        fold["frac"] = round(fold["achieved"] / LDS_B128_PEAK_GBS, 4)
+        fold["hbm"] = {"traffic_vs_compulsory": round(fold["traffic"] / comp, 3) if fold.get("traffic") else None}
+        fold["note"] = ("bound lds: fold bytes (hint x chunk entry reads, SURVEY.md §8d) served from LDS by "
+                        "ds_read_b128 against the ~150 TB/s aggregate (MI355X_MICROARCH.md §LDS); 'compulsory' is "
+                        "the HBM side: the DB read once plus the parity writes of the clients folded in one launch")
+    prf = prf_roofline(ktime["prep_offsets"], "k_prep_offsets of the timed region's maintenance launches")
+    if prf and isolated and one_prf:
+        prf["isolated_one_client"] = prf_roofline(one_prf, "one client alone")
     note = None
     if dom == "step":
         note = ("k_step runs hint match, resolution and answer of a batch-PIR step in one launch; "
@@ -880,6 +919,7 @@ def main():
                    "parallelism": f"replicas{ws}"},
         "roofline": main_roof,
         "roofline_prep": fold,
+        "roofline_prf": prf,
         "single_session": single,
         "recall_at_10": round(float(recall), 4),
         "recall_queries": int(tq.shape[0]),

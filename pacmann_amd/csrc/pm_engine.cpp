@@ -558,7 +558,10 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
   CHK(g->hist.reserve(off_hist * 4));
   CHK(g->fqn.reserve(g->P * 4));
   CHK(g->arena.reserve(std::max<uint64_t>(8, off_ar * 8)));
-  CHK(g->tab.reserve(off_tab * 2));
+  // the chunk-major PRF table only where the fold reads it (every other reader uses tabT):
+  // SIFT1M's rotated fold and the BIGANN wide fold do not, saving H*SS*2 B per partition
+  const bool need_tab = pmk::fold_needs_tab(g->minCS, g->maxCS, (uint32_t)g->E, off_img != 0);
+  if (need_tab) CHK(g->tab.reserve(off_tab * 2));
   CHK(g->tabT.reserve(off_tabT * 2));
   CHK(g->cur.reserve(std::max<uint64_t>(2, off_cur * 2)));
   CHK(g->done.reserve(4 * (3 + 16 * 4096)));
@@ -588,7 +591,7 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
     d.fqn = g->fqn.as<uint32_t>() + i;
     d.arena = g->arena.as<uint64_t>() + (uintptr_t)d.arena;
     d.tabT = g->tabT.as<uint16_t>() + (uintptr_t)d.tabT;
-    d.tab = g->tab.as<uint16_t>() + (uintptr_t)d.tab;
+    d.tab = need_tab ? g->tab.as<uint16_t>() + (uintptr_t)d.tab : nullptr;
     d.cur = g->cur.as<uint16_t>() + (uintptr_t)d.cur;
     d.img = off_img ? g->img->as<uint64_t>() + (uintptr_t)d.img : nullptr;
   }

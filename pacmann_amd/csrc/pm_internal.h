@@ -85,7 +85,8 @@ struct PmPart {
   PM_G uint32_t* hist;    // [SS]  QueryHistogram
   PM_G uint32_t* fqn;     // [1]   FinishedQueryNum
   PM_G uint64_t* arena;   // [MaxQ*E] localCache rows (pir.go:120), slot = FinishedQueryNum at answer time
-  // PRF table: tab[c*H + t] = PRF(tag t, chunk c) & (CS-1) for every tag t in
+  // PRF table (only where the fold reads it, pmk::fold_needs_tab; else null):
+  // tab[c*H + t] = PRF(tag t, chunk c) & (CS-1) for every tag t in
   // [0, H) and chunk c in [0, SS) (kSkip at a backup tag's own chunk).  Every
   // tag a hint can carry is a hint index (primary tags start at h, a refresh
   // hands over backup tag PH+g*Qpc+j), so this table, built once per
@@ -229,6 +230,9 @@ void prep_repl(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxRep
 // The bank-rotated fold's DB image (CS 512, even E, E >= 4): whether it applies,
 // its size per partition (words) and the build of one partition's image.
 bool fold_image_ok(uint32_t minCS, uint32_t maxCS, uint32_t E);
+// whether the fold of these shapes reads the chunk-major PRF table PmPart::tab
+// (otherwise it is not allocated: every other reader uses tabT)
+bool fold_needs_tab(uint32_t minCS, uint32_t maxCS, uint32_t E, bool have_img);
 uint64_t fold_image_words(uint32_t SS, uint32_t E);
 void fold_image(hipStream_t st, uint64_t* img, const uint64_t* part_rows, uint64_t N, uint32_t SS, uint32_t E);
 // Timing events carried by a launch's own dispatch packet (null: untimed)

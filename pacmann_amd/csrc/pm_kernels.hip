@@ -74,7 +74,7 @@ __global__ void __launch_bounds__(kOffsBlock) k_prep_offsets(const PmPart* __res
     for (uint32_t c = c0; c < c1; ++c) {
       uint16_t v = (uint16_t)(prf_lo16_split(A, P.rk, r1u[tl][c - c0], r1v, c) & mask);
       v = (c == own) ? kSkip : v;
-      o[(uint64_t)c * H + h] = v;   // chunk-major: refreshed tags' re-evaluation, fold
+      if (o) o[(uint64_t)c * H + h] = v;   // chunk-major (only the folds that stage it read it)
       tile[c - c0] = v;
       if (h < P.PH) P.cur[(uint64_t)c * P.PH + h] = v;   // hint search (tags start at h)
     }
@@ -98,16 +98,16 @@ __global__ void __launch_bounds__(kBlock) k_prep_fold(const PmPart* __restrict__
   }
   const uint32_t h = (uint32_t)(e / NSEG), seg = (uint32_t)(e % NSEG);
   if (h >= H) return;
-  const uint16_t* o = P.tab + h;
   const uint64_t* base = db + (P.row0 * E) + (uint64_t)seg * W;
   const uint32_t CS = P.CS, SS = P.SS;
   const uint64_t N = P.N;
   uint64_t a0 = 0, a1 = 0;
   uint32_t c = 0;
-  for (; c + 4 <= SS; c += 4) {
+  for (; c + 4 <= SS; c += 4) {   // chunks c .. c+3 of hint h: 8 B of its tag-major tile (tabT)
+    const uint64_t t4 = *reinterpret_cast<const uint64_t*>(P.tabT + tabT_index(H, h, c));
     uint16_t v[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = o[(uint64_t)(c + u) * H];
+    for (int u = 0; u < 4; ++u) v[u] = (uint16_t)(t4 >> (16 * u));
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const uint64_t r = (uint64_t)(c + u) * CS + v[u];
@@ -124,7 +124,7 @@ __global__ void __launch_bounds__(kBlock) k_prep_fold(const PmPart* __restrict__
     }
   }
   for (; c < SS; ++c) {
-    uint16_t v = o[(uint64_t)c * H];
+    uint16_t v = P.tabT[tabT_index(H, h, c)];
     const uint64_t r = (uint64_t)c * CS + v;
     if (v != kSkip && r < N) {
       const uint64_t* p = base + r * E;
@@ -936,6 +936,20 @@ void prep_offsets(hipStream_t st, const PmPart* d, int np, uint32_t maxH, uint32
 bool fold_image_ok(uint32_t minCS, uint32_t maxCS, uint32_t E) {
   static const bool rot = [] { const char* e = getenv("PM_FOLD_ROT"); return !e || e[0] != '0'; }();
   return rot && minCS == kRotCS && maxCS == kRotCS && E % 2 == 0 && E >= 4;
+}
+bool fold_needs_tab(uint32_t minCS, uint32_t maxCS, uint32_t E, bool have_img) {
+  // the folds that stage a chunk-major PRF table row through LDS (k_prep_fold_pipe
+  // / _blk); the rotated fold and the unblocked gather read the tag-major one
+  if ((E & ~3u) == 0) return false;
+  if (have_img && fold_image_ok(minCS, maxCS, E)) return false;
+  const bool pipe = minCS == maxCS && (maxCS == 512 || maxCS == 1024 || maxCS == 2048) && E % 2 == 0;
+  if (pipe) return true;
+  auto fits = [&](uint32_t sw) {   // prep_fold's choice of the double-buffered fold
+    return 2ull * (maxCS + 1) * sw * 8 <= 150u * 1024 && (uint64_t)maxCS * (sw / 2) <= (uint64_t)kFoldMaxItems * kFoldThreads;
+  };
+  uint32_t sw = 8;
+  while (sw > 2 && !fits(sw)) sw /= 2;
+  return fits(sw) && E % 2 == 0;
 }
 uint64_t fold_image_words(uint32_t SS, uint32_t E) { return (uint64_t)(E / 4) * (SS / 4) * (kRotBufBytes / 8); }
 void fold_image(hipStream_t st, uint64_t* img, const uint64_t* rows, uint64_t N, uint32_t SS, uint32_t E) {

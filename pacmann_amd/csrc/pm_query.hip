@@ -286,7 +286,7 @@ __device__ __forceinline__ void match_role(const PmStep& S, uint32_t s, uint32_t
       const uint32_t cht = (uint32_t)(st.idx >> P.log2CS);
       const uint32_t pred = (live && sing < P.Qpc && chunk < P.SS) ? P.PH + chunk * P.Qpc + sing : kNone;
       uint32_t v = kSkip;
-      if (lane < pn && lane > k && validt && cht < P.SS && pred != kNone) v = P.tab[(uint64_t)cht * P.H + pred];
+      if (lane < pn && lane > k && validt && cht < P.SS && pred != kNone) v = P.tabT[tabT_index(P.H, pred, cht)];
       if (GRAN) {
         if (lane < pn) put_g(S.specg + (uint64_t)s * kSpecSubs + lane, v, S.token);
         sing_rec = sing;
@@ -417,7 +417,7 @@ __device__ __forceinline__ void match_part_predict(const PmStep& S, const PmPart
     const uint32_t cht = (uint32_t)(st.idx >> lg);
     const uint32_t pred = (live && sing < P.Qpc && chunk < P.SS) ? P.PH + chunk * P.Qpc + sing : kNone;
     uint32_t v = kSkip;
-    if (lane < pn && lane > k && validt && cht < P.SS && pred != kNone) v = P.tab[(uint64_t)cht * P.H + pred];
+    if (lane < pn && lane > k && validt && cht < P.SS && pred != kNone) v = P.tabT[tabT_index(P.H, pred, cht)];
     const uint64_t s = pb0 + k;
     if (lane < pn) S.spec[s * kSpecSubs + lane] = v;
     if (lane == 0) { S.meta[2 * s] = h0k; S.meta[2 * s + 1] = sing; }
@@ -879,7 +879,7 @@ __device__ __forceinline__ void resolve_role(const PmStep& S, uint32_t p, Resolv
         const uint32_t sk = __shfl(ing, kk), ck = __shfl(ch, kk), cj = __shfl(ch, j);
         const bool rk = __shfl(real ? 1u : 0u, kk) != 0, rj = __shfl(real ? 1u : 0u, j) != 0;
         if (e < n * n && kk < j && rk && rj && ck < P.SS && cj < P.SS && sk < P.Qpc)
-          spec_v[kk * kSpecSubs + j] = P.tab[(uint64_t)cj * H + P.PH + ck * P.Qpc + sk];
+          spec_v[kk * kSpecSubs + j] = P.tabT[tabT_index(H, P.PH + ck * P.Qpc + sk, cj)];
       }
     }
   }
@@ -1003,7 +1003,7 @@ __device__ __forceinline__ void resolve_role(const PmStep& S, uint32_t p, Resolv
           uint32_t cand = kNone;
           if (k < nmod) {
             const uint32_t o = mt == mpt ? (uint32_t)spec_v[ms * kSpecSubs + j]
-                                         : (uint32_t)P.tab[(uint64_t)chunk * H + mt];
+                                         : (uint32_t)P.tabT[tabT_index(H, mt, chunk)];
             if (o == off && (mp == kDefaultProgramPoint || (mp >> lg) != chunk)) cand = mh;
           }
           uint32_t bm = kNone, bk = 0;
@@ -1131,7 +1131,7 @@ __device__ __forceinline__ void resolve_role(const PmStep& S, uint32_t p, Resolv
             // the speculative value holds when sub ks received its predicted tag
             const uint32_t o = (spec && s_sing[ks] < P.Qpc && tg == P.PH + s_chunk[ks] * P.Qpc + s_sing[ks])
                                    ? (uint32_t)spec_v[ks * kSpecSubs + j]
-                                   : (uint32_t)P.tab[(uint64_t)chunk * H + tg];
+                                   : (uint32_t)P.tabT[tabT_index(H, tg, chunk)];
             if (o == off && (pp == kDefaultProgramPoint || (pp >> lg) != chunk)) cand = m_h[k];
           }
           const uint32_t mn = wave_min(cand);
@@ -1299,7 +1299,7 @@ __global__ void __launch_bounds__(NT) k_match_resolve_s(PmStep S) {
       const uint32_t sk = __shfl(ing, kk), ck = __shfl(ch, kk), cj = __shfl(ch, j);
       const bool rk = __shfl(real ? 1u : 0u, kk) != 0, rj = __shfl(real ? 1u : 0u, j) != 0;
       if (e < n * n && kk < j && rk && rj && ck < P.SS && cj < P.SS && sk < P.Qpc)
-        L.spec_v[kk * kSpecSubs + j] = P.tab[(uint64_t)cj * P.H + P.PH + ck * P.Qpc + sk];
+        L.spec_v[kk * kSpecSubs + j] = P.tabT[tabT_index(P.H, P.PH + ck * P.Qpc + sk, cj)];
     }
     if (k < n) {
       L.s_kind[k] = sub.kind; L.s_idx[k] = sub.idx; L.s_chunk[k] = ch; L.s_st[k] = kNone;
