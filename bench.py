@@ -934,7 +934,7 @@ def main():
         # result rows the host read at token time vs those whose bytes did not yet
         # match their header hash then; results are taken only after the step's
         # completion event (system-scope release), where a mismatch is an error
-        # (DESIGN.md §5, result publication)
+        # (DESIGN.md §5.2, result publication)
         "rows_check": {"seen": int(htime["host_rows_seen"][0]), "torn_at_token": int(htime["host_rows_torn"][0]),
                        "completion_waits": int(htime["host_wait_done"][0]),
                        "completion_wait_ms": round(htime["host_wait_done"][1], 3),

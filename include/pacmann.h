@@ -98,7 +98,7 @@ typedef struct {
 } pm_pir_config;
 
 /* NewPianoPIR(DBSize, DBEntryByteNum, rawDB, FailureProbLog2) (pir.go:479-514).
- * seed drives the key / replacement / dummy streams (DESIGN.md §3.2) that the
+ * seed drives the key / replacement / dummy streams (DESIGN.md §3) that the
  * reference draws from time-seeded math/rand (pir.go:132,208,305,366). */
 int    pm_pir_create(pm_ctx* ctx, uint64_t DBSize, uint64_t DBEntryByteNum, const uint64_t* rawDB,
                      uint64_t FailureProbLog2, uint64_t seed, pm_pir** out);

@@ -170,7 +170,7 @@ struct pm_ctx {
   // and fail the step, 2 = count it and wait for the row to match (PM_ROWS_CHECK)
   int rows_check = 2;
   std::vector<uint64_t> hash_mult;   // row_hash_mult(w) for every word a row can have
-  // Step completion (DESIGN.md §5, result publication): an event recorded
+  // Step completion (DESIGN.md §5.2, result publication): an event recorded
   // after the step's last kernel, with a system-scope release, so that once
   // hipEventQuery reports it, every result byte the step wrote into pinned
   // memory is visible to the host (HIP event semantics; the header tokens

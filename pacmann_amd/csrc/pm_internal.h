@@ -24,7 +24,7 @@ constexpr uint64_t kDefaultValue = 0xdeadbeefULL;        // batch-pir.go:15
 constexpr uint16_t kSkip = 0xffffu;                      // prep offset sentinel: backup hint's own chunk
 constexpr int kBlock = 256;
 
-// Randomness streams (DESIGN.md §3.2); identical spec to oracle/pm_oracle.cpp.
+// Randomness streams (DESIGN.md §3); identical spec to oracle/pm_oracle.cpp.
 enum : uint64_t { DOM_KEY = 1, DOM_REPL = 2, DOM_DUMMY = 3, DOM_SYNTH_DB = 9, DOM_SYNTH_VEC = 10, DOM_SYNTH_NB = 11 };
 __host__ __device__ inline uint64_t sm64(uint64_t x) {
   uint64_t z = x + 0x9e3779b97f4a7c15ULL;

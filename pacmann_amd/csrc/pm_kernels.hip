@@ -1,5 +1,5 @@
 // pm_kernels.hip — gfx950 kernels of the PianoPIR XOR fold / answer path and
-// the graphann distance path.  See DESIGN.md §4 for the roofline of each.
+// the graphann distance path.  See DESIGN.md §5 for the roofline of each.
 #include "pm_aes.h"
 #include "pm_internal.h"
 

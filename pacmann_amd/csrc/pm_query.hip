@@ -1487,7 +1487,7 @@ __device__ __forceinline__ uint64_t row_csum(const PmStep& S, const RB& row, boo
 // PmOutHdr).  (4: row stores acknowledged before a workgroup barrier and the
 // header, as in round 1 — rows still arrive after the token, measured.)  Two
 // in-kernel ordered forms, both measured with 0 torn rows in 49M but 2.8x /
-// 4.4x the kernel time, are kept as build options (DESIGN.md §5):
+// 4.4x the kernel time, are kept as build options (DESIGN.md §5.2):
 //   1: lane 0 stores the other header fields, then a SYSTEM-scope release
 //      (buffer_wbl2 sc0 sc1: the XCD L2's dirty lines, every wave's included,
 //      are written back) and an explicit s_waitcnt vmcnt(0) — inline asm, so
