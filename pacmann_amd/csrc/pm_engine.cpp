@@ -182,14 +182,23 @@ struct pm_ctx {
   // is the highest one known complete.  A later record of the event covers
   // the earlier steps of the stream.
   // PM_PUBLISH_WAIT=0: the token + row-hash acceptance alone (diagnostics).
+  // Each step's completion has an event of its own in a ring (step seq uses
+  // done_ring[seq % kDoneRing]): a waiter for step seq queries that step's
+  // event, not the newest one, so it never waits for steps recorded after its
+  // own (a slot re-recorded 64 steps later still completes after it: one stream).
   bool publish_wait = true;
-  hipEvent_t done_ev = nullptr;
+  static constexpr uint32_t kDoneRing = 64;
+  hipEvent_t done_ev = nullptr;   // done_ring[0] (creation check)
+  hipEvent_t done_ring[kDoneRing] = {};
   std::atomic<uint64_t> done_rec{0}, done_seen{0};
-  std::mutex done_mu;
+  std::mutex done_mu, rec_mu;
   uint64_t record_done(hipStream_t st) {
     if (!publish_wait) return 0;
-    (void)hipEventRecord(done_ev, st);
-    return done_rec.fetch_add(1) + 1;
+    std::lock_guard<std::mutex> lk(rec_mu);
+    const uint64_t seq = done_rec.load(std::memory_order_relaxed) + 1;
+    (void)hipEventRecord(done_ring[seq % kDoneRing], st);
+    done_rec.store(seq, std::memory_order_release);
+    return seq;
   }
   std::string last_kernel;
   // host-side wall-clock accumulators ("host_*" names in pm_timing_get)
@@ -231,7 +240,7 @@ struct pm_ctx {
   ~pm_ctx() {
     for (auto& t : launches) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
     for (auto e : pool) (void)hipEventDestroy(e);
-    if (done_ev) (void)hipEventDestroy(done_ev);
+    for (auto e : done_ring) if (e) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -265,10 +274,13 @@ extern "C" int pm_ctx_create(int device, pm_ctx** out) {
   c->hash_mult.resize(pmk::step_max_e());
   for (size_t w = 0; w < c->hash_mult.size(); ++w) c->hash_mult[w] = row_hash_mult(w);
   if (const char* pw = getenv("PM_PUBLISH_WAIT")) c->publish_wait = pw[0] != '0';
-  if (c->publish_wait &&
-      hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming | hipEventReleaseToSystem) != hipSuccess) {
-    delete c;
-    return fail(PM_EHIP, "hipEventCreateWithFlags(step completion) failed");
+  if (c->publish_wait) {
+    for (auto& e : c->done_ring)
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventReleaseToSystem) != hipSuccess) {
+        delete c;
+        return fail(PM_EHIP, "hipEventCreateWithFlags(step completion) failed");
+      }
+    c->done_ev = c->done_ring[0];
   }
   const char* ng = getenv("PM_NO_GUESS");
   c->no_guess = ng && ng[0] == '1';
@@ -701,7 +713,7 @@ static inline double ms_since(Clock::time_point t) {
 // landed: stores from the GPU to fine-grained host memory reach the host in no
 // guaranteed order.  The results are therefore taken only after the step's
 // completion event (recorded after its last kernel with a system-scope
-// release, pm_ctx::done_ev) is seen complete: from then on every byte the
+// release, pm_ctx::done_ring) is seen complete: from then on every byte the
 // step wrote is visible (HIP event semantics).  Rows are then checked against
 // their header hash (PmOutHdr::csum) as an assertion: a mismatch is an error,
 // never retried.  `torn` counts rows whose bytes did not yet match at token
@@ -710,7 +722,7 @@ static inline double ms_since(Clock::time_point t) {
 // token and a matching hash, re-read until they match (rows_check 2).
 // Debug runs (PM_DEBUG_SYNC), and a step not published within 5 s (a fault, or
 // a bug), fall back to the stream synchronisation, which reports errors.
-// sc: the context whose stream ran the step (its done_ev); c: the one whose
+// sc: the context whose stream ran the step (its done_ring); c: the one whose
 // counters are charged (a session of a shared step, or sc itself).
 static int wait_done(pm_ctx* sc, uint64_t seq) {
   if (sc->done_seen.load(std::memory_order_acquire) >= seq) return 0;
@@ -720,10 +732,11 @@ static int wait_done(pm_ctx* sc, uint64_t seq) {
     if (sc->done_mu.try_lock()) {   // one waiter asks the runtime; the others read done_seen
       std::lock_guard<std::mutex> lk(sc->done_mu, std::adopt_lock);
       if (sc->done_seen.load(std::memory_order_acquire) >= seq) return 0;
-      // every step counted so far was recorded before this query
-      const uint64_t rec = sc->done_rec.load(std::memory_order_acquire);
+      const uint64_t rec = seq;   // this step's own event (done_ring)
+      if (sc->done_rec.load(std::memory_order_acquire) < seq)
+        return fail(PM_EHIP, "step completion: waited for a step that was not recorded");
       for (uint64_t k = 0;; ++k) {
-        const hipError_t e = hipEventQuery(sc->done_ev);
+        const hipError_t e = hipEventQuery(sc->done_ring[seq % pm_ctx::kDoneRing]);
         if (e == hipSuccess) break;
         if (e != hipErrorNotReady) return fail(PM_EHIP, std::string("step completion: ") + hipGetErrorString(e));
         if ((k & 0xfff) == 0xfff && ms_since(t0) > 5000.0) {
@@ -734,7 +747,6 @@ static int wait_done(pm_ctx* sc, uint64_t seq) {
       }
       uint64_t prev = sc->done_seen.load(std::memory_order_relaxed);
       while (prev < rec && !sc->done_seen.compare_exchange_weak(prev, rec, std::memory_order_release)) {}
-      if (rec < seq) return fail(PM_EHIP, "step completion: waited for a step that was not recorded");
       return 0;
     }
     if ((spin & 0xffff) == 0xffff && ms_since(t0) > 10000.0) return fail(PM_EHIP, "step completion wait timed out");

@@ -159,3 +159,29 @@ def test_synthetic_graph_model_peers(ctx, oracle):
         total += Q
         assert sess[i].counts()[0] == ost[0], i   # ids fetched: same rounds
     assert same >= 0.75 * total, (same, total)
+
+
+def test_sharded_loop_odd_entry_layout(ctx, oracle):
+    """The records at an entry layout whose neighbour list starts mid-word
+    (d = 99, m = 31: 4*d = 396 B, so the list begins 4 B into word 49, and
+    E = 65 words with xorSlices' len & ~3 rule zeroing word 64 of every
+    answer, as the reference does): the sharded loop over one shard holding
+    every partition, two teams, equals unsharded oracle runs answer for answer
+    with equal counters."""
+    import pacmann_amd as pm
+    from pacmann_amd.synth import random_graph
+    n, dim, m = 30_000, 99, 31
+    rng = np.random.default_rng(41)
+    v = rng.random((n, dim), dtype=np.float32)
+    g = random_graph(n, m, seed=42)
+    base = pm.PIRGraphInfo.Shard(v, g, 0, 1, pir_seed=SEEDS[0][0], search_seed=SEEDS[0][1], ctx=ctx)
+    base.Preprocess()
+    sess = [base] + [base.Session(p, s_) for p, s_ in SEEDS[1:]]
+    for x in sess[1:]:
+        x.Preprocess()
+    qs = rng.random((S, Q, dim), dtype=np.float32)
+    ans, _, _, _ = pm.search_loop_sharded(sess, qs, K, 20, 3, NG, 4)
+    for i, (oa, ost) in enumerate(_oracle_runs(oracle, v, g, qs)):
+        assert np.array_equal(ans[i], oa), i
+        ps = sess[i].PIR.stats()
+        assert [*sess[i].counts(), ps["FinishedBatchNum"], ps["QueriesMadeInPartition"], ps["PrepCount"]] == ost, i
