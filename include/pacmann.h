@@ -189,6 +189,11 @@ int  pm_batchpir_stats_get(pm_batchpir* h, pm_batchpir_stats* s);
 typedef struct pm_batchpir_group pm_batchpir_group;
 int  pm_batchpir_group_create(pm_batchpir** clients, uint32_t S, pm_batchpir_group** out);
 int  pm_batchpir_group_query(pm_batchpir_group* g, const uint64_t* ids, uint64_t n, uint64_t* out, uint8_t* ok);
+/* SimpleBatchPianoPIR.Preprocessing (batch-pir.go:119-155) of every client of
+ * the group as ONE launch set on clients[0]'s stream: each partition's clients
+ * are folded side by side over the shared DB (the batched serving loop's
+ * maintenance).  Every client's state equals its own pm_batchpir_preprocessing. */
+int  pm_batchpir_group_preprocessing(pm_batchpir_group* g);
 void pm_batchpir_group_destroy(pm_batchpir_group* g);
 int  pm_batchpir_subconfig(pm_batchpir* h, uint64_t partition, pm_pir_config* cfg);
 

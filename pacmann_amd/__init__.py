@@ -115,6 +115,7 @@ SIGNATURES = {
                                           i64p, C.POINTER(dbl), C.POINTER(dbl), C.POINTER(dbl)]),
     "pm_batchpir_group_create": (C.c_int, [C.POINTER(vp), C.c_uint32, C.POINTER(vp)]),
     "pm_batchpir_group_query": (C.c_int, [vp, u64p, u64, u64p, C.POINTER(C.c_uint8)]),
+    "pm_batchpir_group_preprocessing": (C.c_int, [vp]),
     "pm_batchpir_group_destroy": (None, [vp]),
     "pm_search_loop_batched": (C.c_int, [C.POINTER(vp), C.c_uint32, f32p, u64, C.c_int, C.c_int, C.c_int, C.c_uint32,
                                          C.c_uint32, i64p, C.POINTER(dbl), C.POINTER(dbl), C.POINTER(dbl)]),
@@ -535,6 +536,10 @@ class BatchPIRGroup:
         if getattr(self, "h", None):
             lib().pm_batchpir_group_destroy(self.h)
         self.h = None
+
+    def Preprocessing(self):
+        """Every client's SimpleBatchPianoPIR.Preprocessing as one launch set."""
+        _check(lib().pm_batchpir_group_preprocessing(self.h))
 
     def QueryWithMask(self, ids):
         """ids [S, n] -> (entries [S, n, DBEntrySize] uint64, ok [S, n] bool)."""

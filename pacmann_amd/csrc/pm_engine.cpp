@@ -2495,7 +2495,7 @@ static int group_start_dist(StepGroup& G, pm_graph** gs) {
 // with need[s], as ONE launch set over all their partitions on the team's
 // stream (the clients share the server DB and parameters).  Each client's
 // maintenance time is the set's wall time.
-static int group_prep(StepGroup& G, pm_graph** gs, const std::vector<char>& need, std::vector<double>& mt) {
+static int group_prep(StepGroup& G, const std::vector<char>& need, std::vector<double>* mt) {
   std::vector<uint32_t> who;
   for (uint32_t s = 0; s < G.S; ++s)
     if (need[s]) who.push_back(s);
@@ -2504,27 +2504,27 @@ static int group_prep(StepGroup& G, pm_graph** gs, const std::vector<char>& need
   std::vector<PmPart> hp;
   std::vector<uint64_t> todo;
   for (uint32_t s : who) {
-    Engine* e = &gs[s]->pir->e;
+    Engine* e = G.es[s];
     e->FBN = 0; e->QMIP = 0;
     CHK(engine_prep_host(e, 0, e->P, todo));
   }
   // partition-major: the clients' folds of one partition run side by side and
   // share its DB rows through the caches instead of re-reading them per client
   for (uint32_t p : G.lp)
-    for (uint32_t s : who) hp.push_back(gs[s]->pir->e.parts[p].d);
-  const Engine* e0 = &gs[who[0]]->pir->e;
+    for (uint32_t s : who) hp.push_back(G.es[s]->parts[p].d);
+  const Engine* e0 = G.es[who[0]];
   bool skip = false;
-  for (uint32_t s : who) skip |= gs[s]->pir->e.skipPrep != e0->skipPrep;
+  for (uint32_t s : who) skip |= G.es[s]->skipPrep != e0->skipPrep;
   if (skip) return fail(PM_EINVAL, "batched sessions mix Preprocessing and DummyPreprocessing");
   CHK(G.prep_parts.reserve(hp.size() * sizeof(PmPart)));
   HIPCHK(hipMemcpyAsync(G.prep_parts.p, hp.data(), hp.size() * sizeof(PmPart), hipMemcpyHostToDevice, G.c->stream));
   CHK(engine_prep_launch(G.c, e0, G.prep_parts.as<PmPart>(), (int)hp.size(), hp.data(), (uint32_t)who.size()));
   const double t = std::chrono::duration<double>(Clock::now() - t0).count();
   for (uint32_t s : who) {
-    Engine* e = &gs[s]->pir->e;
+    Engine* e = G.es[s];
     e->prepCount++;
     record_stats(e, t);
-    mt[s] += t;
+    if (mt) (*mt)[s] += t;
   }
   return 0;
 }
@@ -2850,7 +2850,7 @@ static int run_batched_team(pm_graph** gs, uint32_t S, const float* queries, uin
       bar.wait();
       if (w == 0) {   // the triggered clients' preprocessings as one launch set
         if (!err.load()) {
-          const int rc = group_prep(G, gs, need_prep, mt);
+          const int rc = group_prep(G, need_prep, &mt);
           if (rc) set_err(rc, 0);
         }
         stop.store(err.load() != 0);
@@ -2901,6 +2901,12 @@ extern "C" int pm_batchpir_group_create(pm_batchpir** clients, uint32_t S, pm_ba
   return 0;
 }
 extern "C" void pm_batchpir_group_destroy(pm_batchpir_group* h) { delete h; }
+extern "C" int pm_batchpir_group_preprocessing(pm_batchpir_group* h) {
+  if (!h) return fail(PM_EINVAL, "NULL argument");
+  // SimpleBatchPianoPIR.Preprocessing (batch-pir.go:119-155) of every client,
+  // as ONE launch set: each partition's K clients fold side by side
+  return group_prep(h->G, std::vector<char>(h->G.S, 1), nullptr);
+}
 extern "C" int pm_batchpir_group_query(pm_batchpir_group* h, const uint64_t* ids, uint64_t n, uint64_t* out,
                                        uint8_t* ok) {
   if (!h || (!ids && n) || (!out && n)) return fail(PM_EINVAL, "NULL argument");

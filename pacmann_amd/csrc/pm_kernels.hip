@@ -417,6 +417,15 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_pipe(const PmPart* _
 #define PM_ROT_LW 2   // column slices of one (partition, group) pair dealt to an XCD back to back
                       // (64-client fold: 1 -> 31.5-31.7 ms, 2 -> 28.0-28.1, 4 -> 31.4-40.3, 5 -> 27.4-45.5)
 #endif
+#ifndef PM_ROT_ORDER
+#define PM_ROT_ORDER 1   // 1: XCD tiles of GB pairs x SB slices (below); 0: round 2's order (PM_ROT_LW)
+#endif
+#ifndef PM_ROT_GB
+#define PM_ROT_GB 8
+#endif
+#ifndef PM_ROT_SB
+#define PM_ROT_SB 4
+#endif
 #ifndef PM_ROT_PF
 #define PM_ROT_PF 0   // L2 prefetch of the image block two buffers ahead (measured no gain once the
                       // staging overlaps the fold: 24.2-25.4 vs 24.8-25.0 ms per 64-client launch)
@@ -455,8 +464,23 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_rot(const PmPart* __
   // client instead (no mixing).
   constexpr uint32_t LW = PM_ROT_LW, HB = kFoldThreads * kRotHPL;
   const uint32_t xcd = blockIdx.x % 8, kq = blockIdx.x / 8;
+#if PM_ROT_ORDER == 1
+  // Tiles of GB consecutive (partition, group) pairs x SB consecutive slices,
+  // one tile per XCD at a time (GB * SB = its 32 CUs): a group's tabT rows are
+  // read by SB workgroups and a slice's image blocks by GB workgroups out of
+  // the XCD's L2.  The eight XCDs take eight consecutive pair blocks of the
+  // SAME slice block, so the partition's image slices are shared through the
+  // Infinity Cache; then the next slice block of the same pairs (their tabT
+  // again, from the Infinity Cache).
+  constexpr uint32_t GB = PM_ROT_GB, SB = PM_ROT_SB;
+  const uint32_t nsb = (nsl + SB - 1) / SB, lt = kq / (GB * SB), wt = kq % (GB * SB);
+  const uint32_t pgv = ((lt / nsb) * 8 + xcd) * GB + wt % GB;
+  const uint32_t slice = (lt % nsb) * SB + wt / GB;
+  (void)M; (void)LW;
+#else
   const uint32_t loc = (kq / LW) % M, slice = (kq / (LW * M)) * LW + kq % LW;
   const uint32_t pgv = xcd * M + loc;
+#endif
   if (pgv >= npv || slice >= nsl) return;   // block-uniform
   const uint32_t part = pgv / nvg, vg = pgv % nvg;
   const PmPart& P = parts[part * K];   // H, SS and the fold image are the same for every client
@@ -999,8 +1023,10 @@ void prep_fold(hipStream_t st, const PmPart* d, int np, uint32_t maxH, const uin
       const uint32_t ngc = minH >= HB ? 0u : (uint32_t)cdiv(maxH, HB);
       const uint32_t nvg = ngc ? K * ngc : (uint32_t)cdiv((uint64_t)K * maxH, HB), npv = (np / K) * nvg;
       const uint32_t M = cdiv(npv, 8);
-      hipLaunchKernelGGL(k_prep_fold_rot<512>, dim3(8 * M * cdiv(nsl, PM_ROT_LW) * PM_ROT_LW), dim3(kFoldThreads), 0, st, d, E,
-                         nvg, nsl, npv, M, K, ngc);
+      const uint32_t grid = PM_ROT_ORDER == 1
+                                ? 8 * cdiv(cdiv(npv, PM_ROT_GB), 8) * cdiv(nsl, PM_ROT_SB) * PM_ROT_GB * PM_ROT_SB
+                                : 8 * M * cdiv(nsl, PM_ROT_LW) * PM_ROT_LW;
+      hipLaunchKernelGGL(k_prep_fold_rot<512>, dim3(grid), dim3(kFoldThreads), 0, st, d, E, nvg, nsl, npv, M, K, ngc);
       return;
     }
     const uint32_t nb = maxCS == 512 ? PM_FOLD_NB512 : 3;   // LDS buffers: <= 150 KB

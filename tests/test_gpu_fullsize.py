@@ -327,3 +327,37 @@ def test_search_msmarco_bench_group_shape(ctx, oracle):
     n_ans, _, by = kt["answer"]
     assert n_ans == 47 * 20 and kt["match_resolve"][0] == n_ans
     assert kt["prep_fold"][0] == 1
+
+
+# ---------------------------------------------------------------------------
+# configs[1]: the serving loop's maintenance fold of 64 clients in one launch
+# ---------------------------------------------------------------------------
+def test_group_preprocessing_sift1m_64_clients(ctx):
+    """pm_batchpir_group_preprocessing at the bench's group shape: 64 SIFT1M
+    clients (1e6 x 640 B, CS 512 / SS 124) folded in ONE k_prep_fold_rot launch
+    (virtual hint groups mixing clients) give, for every client and sampled
+    partitions, exactly the state of that client's own Preprocessing (the
+    single-client fold, oracle-checked in test_gpu_parity), through two
+    epochs."""
+    import pacmann_amd as pm
+    N, E, B, K = 1_000_000, 80, 32, 64
+    db = rand_db(N, E, seed=64)
+    server = pm.SimpleBatchPianoPIR(N, E * 8, B, db, 8, seed=SEED, ctx=ctx)
+    server.Preprocessing()
+    cg, ci = pm.Context(0), pm.Context(0)
+    seeds = [1000 + i for i in range(K)]
+    grouped = [server.Client(sd, cg) for sd in seeds]
+    alone = [server.Client(sd, ci) for sd in seeds]
+    for c in grouped + alone:
+        c.Preprocessing()   # epoch 0, one client at a time
+    grp = pm.BatchPIRGroup(grouped)
+    ctx.timing_reset()
+    for epoch in (1, 2):
+        grp.Preprocessing()
+        for c in alone:
+            c.Preprocessing()
+        for i in range(K):
+            for p in ((0, 15) if i % 8 else (0, 5, 10, 15)):
+                diff = state_diff(grouped[i].export_state(p), alone[i].export_state(p))
+                assert not diff, (epoch, i, p, diff)
+        assert grouped[0].stats()["PrepCount"] == alone[0].stats()["PrepCount"] == epoch + 1
