@@ -2408,7 +2408,34 @@ static int group_step(StepGroup& G, const std::vector<char>& in) {
     S.qset = G.qset.as<uint16_t>();
   }
   if (pmk::step_match_resolve_ok(S, lds)) {   // one launch: match + resolve per partition
+    if (pmk::step_match_resolve_small(G.ph8, G.maxPH, max_per_part)) S.np_live = 0;   // resolvers do not count in
+#ifdef PM_MR_STAMPS
+    static const char* mr_file = getenv("PM_MR_STAMPS");   // append {np} + np x 8 stamps per step
+    static std::atomic<int> mr_steps{0};   // the first 40 steps of the run
+    const bool mr_this = mr_file && mr_steps.fetch_add(1) < 40;
+    if (mr_this) {
+      CHK(G.stamps.reserve((uint64_t)np * 8 * 8));
+      HIPCHK(hipMemsetAsync(G.stamps.p, 0, (uint64_t)np * 8 * 8, st));
+      S.stamps = G.stamps.as<uint64_t>();
+    }
+#endif
     c->timed_ext("match_resolve", (double)nreal * G.maxPH, [&](pmk::PmEvents ev) { pmk::step_match_resolve(st, S, G.ph8, G.maxPH, max_per_part, ev); }, 2);
+#ifdef PM_MR_STAMPS
+    if (mr_this) {
+      HIPCHK(hipStreamSynchronize(st));
+      std::vector<uint64_t> t((uint64_t)np * 8);
+      HIPCHK(hipMemcpy(t.data(), G.stamps.p, t.size() * 8, hipMemcpyDeviceToHost));
+      static std::mutex mu;
+      std::lock_guard<std::mutex> lk(mu);
+      if (FILE* f = fopen(mr_file, "ab")) {
+        const uint64_t h = np;
+        fwrite(&h, 8, 1, f);
+        fwrite(t.data(), 8, t.size(), f);
+        fclose(f);
+      }
+      S.stamps = nullptr;
+    }
+#endif
   } else {
     c->timed_ext("hint_match", (double)nreal * G.maxPH, [&](pmk::PmEvents ev) { pmk::step_match(st, S, G.maxPH, ev); }, 2);
     c->timed_ext("resolve", 0, [&](pmk::PmEvents ev) { pmk::step_resolve(st, S, lds, ev); }, 2);

@@ -242,6 +242,7 @@ uint32_t step_match_blocks(uint32_t maxPH);   // k_match workgroups per sub-quer
 void step_resolve(hipStream_t st, const PmStep& S, bool lds, PmEvents ev = {});
 // k_match_part + k_resolve fused (batched serving; descriptor already in device memory)
 bool step_match_resolve_ok(const PmStep& S, bool lds);
+bool step_match_resolve_small(bool ph8, uint32_t maxPH, uint32_t max_sub_per_part);
 // ph8: every partition's PH is a multiple of 8
 void step_match_resolve(hipStream_t st, const PmStep& S, bool ph8, uint32_t maxPH, uint32_t max_sub_per_part,
                         PmEvents ev = {});

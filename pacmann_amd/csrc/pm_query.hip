@@ -116,6 +116,21 @@ constexpr uint32_t kNone = 0xffffffffu;
 #endif
 
 
+// PM_MR_STAMPS diagnostic builds: k_match_resolve_s records s_memrealtime at
+// its phase boundaries (thread 0), stamps[blockIdx * 8 + i]: 0 start,
+// 1 partition record loaded, 2 match issued + ballots done (wave 0),
+// 3 every wave's match in LDS, 4 candidates' tags / program points loaded,
+// 5 chain done and flushed, 6 expansion guesses loaded, 7 query sets issued.
+#ifdef PM_MR_STAMPS
+#define MRST(i)                                                                                  \
+  do {                                                                                           \
+    if (threadIdx.x == 0 && S.stamps)                                                            \
+      S.stamps[(uint64_t)blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime();               \
+  } while (0)
+#else
+#define MRST(i) do {} while (0)
+#endif
+
 // ---------------------------------------------------------------------------
 // LDS staging limits of the fast resolve path (SIFT1M / MS-MARCO shapes);
 // larger configurations take the global-memory path of the same kernel.
@@ -642,6 +657,9 @@ struct ResolveLds {
 // from borrowing, so the value is np_live << 32 | 2^31 exactly after the last
 // add of the step, in any order of the adds.  That add's workgroup decodes
 // the chain list (done[2] entries from done[3]) and re-arms the counters.
+// (k_match_resolve_s steps set np_live 0: their resolvers all finish before
+// the answer kernel starts, so only chains are counted, the value returns to
+// 2^31 after the last involved arrival, and no resolver waits for an atomic.)
 constexpr uint64_t kChainBias = 1ull << 31;
 __device__ __forceinline__ uint64_t chain_add(const PmStep& S, uint64_t d) {
   const uint64_t prev = __hip_atomic_fetch_add(reinterpret_cast<PM_G uint64_t*>(S.done), d, __ATOMIC_RELAXED,
@@ -1064,7 +1082,17 @@ __device__ __forceinline__ void resolve_role(const PmStep& S, uint32_t p, Resolv
       if (k < nchain) S.done[3 + pos + k] = cl;
     }
     if (k == 0) *P.fqn = fqn;
-    resolver_count(S, L, nchain, cadd);
+    if constexpr (MODE == 3) {
+      // k_match_resolve_s (S.np_live == 0): the answer kernel starts after every
+      // resolver is done, so resolvers do not count in; a partition with refresh
+      // chains subtracts its involved answer workgroups (no returned value, no
+      // wait), and the counter is back at its bias after their arrivals
+      if (k == 0 && cadd)
+        __hip_atomic_fetch_add(reinterpret_cast<PM_G uint64_t*>(S.done), (uint64_t)0 - cadd, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      resolver_count(S, L, nchain, cadd);
+    }
     STAMP(40);
     return;
   }
@@ -1261,16 +1289,38 @@ __global__ void __launch_bounds__(kResolveBlockG) k_match_resolve(PmStep S) {
 // wave reads the requests, QueryHistogram and FinishedQueryNum and makes the
 // predictions of resolve_role's staged prologue (in-chunk index, re-evaluation
 // values) meanwhile.  Results are identical to k_match_resolve's.
+// Measured alone at the bench's 64-session groups (k_match_resolve_s<2,256>):
+// 19.1-19.3 us with the defaults; 19.7 with all 6 sub-queries' search rows in
+// one round trip (PM_MR_G 0: 8 per round trip for NU <= 2, 6 for NU 4, 82
+// VGPRs and SGPR spills), with or without the candidates' tags loaded by the
+// matching wave (PM_MR_TAGPF 1) instead of by wave 0 after the barrier.
+#ifndef PM_MR_TAGPF
+#define PM_MR_TAGPF 0
+#endif
+#ifndef PM_MR_G
+#define PM_MR_G 8       // search rows of 8 / NU sub-queries per round trip (0: see above)
+#endif
 template <int NU, int NT>
 __global__ void __launch_bounds__(NT) k_match_resolve_s(PmStep S) {
-  constexpr int NW = NT / 64, G = 8 / NU;
+  // G sub-queries' search rows in flight together (the usual 6 per partition:
+  // one round trip); 2 * G * NU <= 64 candidates per wave, one per lane
+  constexpr int NW = NT / 64, G = PM_MR_G ? PM_MR_G / NU : NU <= 2 ? 8 : NU == 4 ? 6 : 8 / NU;
+  static_assert(2 * G * NU <= 64, "one lane per candidate");
   __shared__ ResolveLds<3> L;
-  __shared__ uint32_t s_m[kSpecSubs][NU][NW][2];   // each (sub-query, row block, wave): first two matches
+  // each (sub-query, row block, wave): first two matches, their tags and program points
+  __shared__ uint32_t s_m[kSpecSubs][NU][NW][2], s_mt[kSpecSubs][NU][NW][PM_MR_TAGPF ? 2 : 1],
+      s_mp[kSpecSubs][NU][NW][PM_MR_TAGPF ? 2 : 1];
   const uint32_t p = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  MRST(0);
+  // the partition record is loaded with the descriptor range (its field in the
+  // exit test keeps the load ahead of the branch: one round trip, not two)
   const uint32_t b0 = S.sb[p], n = S.sb[p + 1] - b0;   // device descriptor (never in the arguments here)
-  if (n == 0) return;
   const PmPart P = S.parts[p];
+  if (n == 0 || P.CS == 0) return;
   const uint32_t lg = P.log2CS, mask = P.CS - 1;
+#ifdef PM_MR_STAMPS
+  if (tid == 0 && S.stamps) { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); MRST(1); }
+#endif
   if (wave == NW - 1) {
     // requests, counters and predictions (resolve_role's staged prologue, from global memory)
     const uint32_t k = lane;
@@ -1316,6 +1366,7 @@ __global__ void __launch_bounds__(NT) k_match_resolve_s(PmStep S) {
   if (lane < n) mine = step_sub(S, b0 + lane);
   // the match: sub-queries j0 .. j0 + G - 1 at a time
   for (uint32_t j0 = 0; j0 < n; j0 += G) {
+    uint32_t cand = kNone;   // lane q: candidate i = q % 2 of (g, u) = (q / (2 NU), (q / 2) % NU)
     uint32_t off[G];
     uint4 v[G][NU];
 #pragma unroll
@@ -1362,11 +1413,23 @@ __global__ void __launch_bounds__(NT) k_match_resolve_s(PmStep S) {
             }
           }
         }
-        if (lane == 0) { s_m[j0 + g][u][wave][0] = a0; s_m[j0 + g][u][wave][1] = a1; }
+        if (lane == 2 * (g * NU + u)) cand = a0;
+        if (lane == 2 * (g * NU + u) + 1) cand = a1;
       }
     }
+    // the candidates' tags and program points, one lane each, all in flight
+    // together (the resolver's chain and the set expansion read them from LDS)
+    uint32_t ct = 0, cp = 0;
+    if (PM_MR_TAGPF && cand != kNone) { ct = P.tag[cand]; cp = P.pp[cand]; }
+    const uint32_t qg = lane / (2 * NU), qu = (lane / 2) % NU, qi = lane % 2;
+    if (lane < 2 * G * NU && j0 + qg < n) {
+      s_m[j0 + qg][qu][wave][qi] = cand;
+      if (PM_MR_TAGPF) { s_mt[j0 + qg][qu][wave][qi % 2] = ct; s_mp[j0 + qg][qu][wave][qi % 2] = cp; }
+    }
   }
+  MRST(2);
   __syncthreads();
+  MRST(3);
   if (wave == 0 && lane < n) {
     // each sub-query's first two matches in hint order, with their tag and program point
     const uint32_t j = lane;
@@ -1377,15 +1440,19 @@ __global__ void __launch_bounds__(NT) k_match_resolve_s(PmStep S) {
           for (int i = 0; i < 2; ++i) {
             const uint32_t h = s_m[j][u][w][i];
             if (h == kNone || c2 != kNone) continue;
-            if (c1 == kNone) c1 = h; else c2 = h;
+            const uint32_t ti = PM_MR_TAGPF ? i : 0;
+            if (c1 == kNone) { c1 = h; t1 = s_mt[j][u][w][ti]; p1 = s_mp[j][u][w][ti]; }
+            else { c2 = h; t2 = s_mt[j][u][w][ti]; p2 = s_mp[j][u][w][ti]; }
           }
-      if (c1 != kNone) { t1 = P.tag[c1]; p1 = P.pp[c1]; }
-      if (c2 != kNone) { t2 = P.tag[c2]; p2 = P.pp[c2]; }
+      if (!PM_MR_TAGPF && c1 != kNone) { t1 = P.tag[c1]; p1 = P.pp[c1]; }
+      if (!PM_MR_TAGPF && c2 != kNone) { t2 = P.tag[c2]; p2 = P.pp[c2]; }
     }
     L.s_c1[j] = c1; L.s_c2[j] = c2; L.s_t1[j] = t1; L.s_p1[j] = p1; L.s_t2[j] = t2; L.s_p2[j] = p2;
   }
   __syncthreads();
+  MRST(4);
   resolve_role<3, NT, false>(S, p, L);
+  MRST(5);
   // The query set of every successful sub-query (pir.go:424-444: the hit
   // hint's offsets, its program point, the chunk's replacement), expanded
   // here so that k_answer_s reads it with its resolution record in one round
@@ -1410,7 +1477,7 @@ __global__ void __launch_bounds__(NT) k_match_resolve_s(PmStep S) {
     }
   }
   __syncthreads();
-  if (L.fin && threadIdx.x == 0) chain_rearm(S);
+  MRST(6);
   if (S.qset) {
     for (uint32_t x = x0; x < n * nt8; x += NT) {
       const uint32_t j = x / nt8, t = x % nt8;
@@ -1432,6 +1499,7 @@ __global__ void __launch_bounds__(NT) k_match_resolve_s(PmStep S) {
       *reinterpret_cast<PM_G uint4*>(S.qset + (uint64_t)(b0 + j) * S.qw + c0) = make_uint4(w[0], w[1], w[2], w[3]);
     }
   }
+  MRST(7);
 }
 
 // L2Dist of the first `dim` floats of an LDS row against q (device), one
@@ -2111,11 +2179,15 @@ bool step_match_resolve_ok(const PmStep& S, bool lds) {
   return mode && !lds && !S.args_valid && S.subs == S.subs_h && S.sb == S.sb_h && S.np >= 128 &&
          S.nsub >= 4 * S.np && S.words <= 256;
 }
+// k_match_resolve_s serves the step (its resolvers do not count in: PmStep::np_live = 0)
+bool step_match_resolve_small(bool ph8, uint32_t maxPH, uint32_t max_sub_per_part) {
+  static const int mode = [] { const char* e = getenv("PM_MATCH_RESOLVE"); return e ? atoi(e) : 1; }();
+  return mode == 1 && max_sub_per_part <= kSpecSubs && ph8 && maxPH <= 16u * kResolveBlockG;
+}
 void step_match_resolve(hipStream_t st, const PmStep& S, bool ph8, uint32_t maxPH, uint32_t max_sub_per_part,
                         PmEvents ev) {
   // the one-round-trip form where its shapes hold (PM_MATCH_RESOLVE=2: always the general one)
-  static const int mode = [] { const char* e = getenv("PM_MATCH_RESOLVE"); return e ? atoi(e) : 1; }();
-  const bool small = mode == 1 && max_sub_per_part <= kSpecSubs && ph8;
+  const bool small = step_match_resolve_small(ph8, maxPH, max_sub_per_part);
   // workgroup size (PM_MR_NT): 256 leaves the GPU's wave slots to the other
   // groups' kernels while wave 0 runs the chain
   static const int nt = [] { const char* e = getenv("PM_MR_NT"); return e ? atoi(e) : 256; }();

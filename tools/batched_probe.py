@@ -46,7 +46,7 @@ for S in a.sessions:
     if a.timing:
         c = sess[0].ctx
         out["kernels_us"] = {k: round(c.timing_get(k)[1] / max(c.timing_get(k)[0], 1) * 1e3, 2)
-                             for k in ("hint_match", "resolve", "gather", "answer", "prep_fold")}
+                             for k in ("hint_match", "resolve", "match_resolve", "gather", "answer", "prep_offsets", "prep_fold")}
         for hname in ("host_step_launch", "host_step_wait", "host_step_post", "host_batch_query", "host_knn_update",
                       "host_gvi_parse", "host_knn_init"):
             n, ms, _ = c.timing_get(hname)
