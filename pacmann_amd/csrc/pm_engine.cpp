@@ -753,6 +753,25 @@ static int wait_done(pm_ctx* sc, uint64_t seq) {
   }
 }
 
+// Non-blocking form of wait_done: *ready once step `seq` of sc's stream has
+// completed (its done_ring event), or at once where steps are not ordered by
+// their completion event (PM_PUBLISH_WAIT=0: the results' tokens decide).
+static int poll_done(pm_ctx* sc, uint64_t seq, bool* ready) {
+  *ready = !(sc->publish_wait && sc->done_ev && seq) || sc->done_seen.load(std::memory_order_acquire) >= seq;
+  if (*ready || !sc->done_mu.try_lock()) return 0;
+  std::lock_guard<std::mutex> lk(sc->done_mu, std::adopt_lock);
+  if (sc->done_seen.load(std::memory_order_acquire) >= seq) { *ready = true; return 0; }
+  if (sc->done_rec.load(std::memory_order_acquire) < seq)
+    return fail(PM_EHIP, "step completion: polled a step that was not recorded");
+  const hipError_t e = hipEventQuery(sc->done_ring[seq % pm_ctx::kDoneRing]);
+  if (e == hipErrorNotReady) return 0;
+  if (e != hipSuccess) return fail(PM_EHIP, std::string("step completion: ") + hipGetErrorString(e));
+  uint64_t prev = sc->done_seen.load(std::memory_order_relaxed);
+  while (prev < seq && !sc->done_seen.compare_exchange_weak(prev, seq, std::memory_order_release)) {}
+  *ready = true;
+  return 0;
+}
+
 static int wait_step(pm_ctx* c, const PmOutHdr* hdr, uint32_t nsub, uint32_t token, const char* rows,
                      size_t row_bytes, size_t pf_off, size_t pf_len, uint64_t seq, pm_ctx* sc = nullptr) {
   if (!sc) sc = c;
@@ -770,6 +789,13 @@ static int wait_step(pm_ctx* c, const PmOutHdr* hdr, uint32_t nsub, uint32_t tok
   } else {
     const volatile uint32_t* tok = &hdr[0].token;
     const size_t stride = sizeof(PmOutHdr) / sizeof(uint32_t);
+    // the headers and checked row words are GPU-written pinned memory (cache
+    // misses): all their lines requested at once, not one miss after another
+    for (uint32_t s = 0; s < nsub; ++s) {
+      __builtin_prefetch(&hdr[s]);
+      if (c->rows_check)
+        for (size_t w = w0; w < w1; w += 8) __builtin_prefetch(rows + s * row_bytes + w * 8);
+    }
     auto t0 = Clock::now();
     uint32_t s = 0;
     bool first_look = true;   // the first read of sub-query s's row after its token appeared
@@ -2763,12 +2789,10 @@ static int group_shard_init(StepGroup& G, pm_graph** gs, uint32_t S, int paralle
   return 0;
 }
 
-// One lock-step team: sessions gs[0..S) share one step stream (gs[0]'s) and T
-// worker threads; maintenance seconds into mt[0..S).  Runs on the calling thread.
-static int run_batched_team(pm_graph** gs, uint32_t S, const float* queries, uint64_t q, int k, int step,
-                            int parallel, uint32_t T, int64_t* answers, double* mt_out, ShardComb* comb = nullptr,
-                            uint32_t team = 0) {
-  StepGroup G;
+// A lock-step team's device setup over sessions gs[0..S) (gs[0]'s stream):
+// start ids, query slots (each session's query pointer points into G.qbuf
+// until team_release), the clients' parts.
+static int team_init(StepGroup& G, pm_graph** gs, uint32_t S) {
   G.dim = (uint32_t)gs[0]->dim;
   G.rows_partial = true;   // GetVertexInfo reads the neighbour lists only
   for (uint32_t i = 0; i < S; ++i) G.es.push_back(&gs[i]->pir->e);
@@ -2786,15 +2810,27 @@ static int run_batched_team(pm_graph** gs, uint32_t S, const float* queries, uin
     for (uint32_t i = 0; i < S; ++i) ids.insert(ids.end(), gs[i]->start.begin(), gs[i]->start.end());
     if (!ids.empty()) HIPCHK(hipMemcpy(G.start_ids.p, ids.data(), ids.size() * 4, hipMemcpyHostToDevice));
   }
-  struct Unshare {   // the sessions' query pointers point into G.qbuf until the team ends
-    pm_graph** gs; uint32_t S;
-    ~Unshare() { for (uint32_t i = 0; i < S; ++i) gs[i]->q_shared = nullptr; }
-  } unshare{gs, S};
   for (uint32_t i = 0; i < S; ++i) {
     gs[i]->q_shared = G.qbuf.as<float>() + (uint64_t)i * G.dim;
     G.qv.push_back(gs[i]->qdev());
   }
-  CHK(group_init(G, gs[0]->ctx));
+  return group_init(G, gs[0]->ctx);
+}
+static void team_release(pm_graph** gs, uint32_t S) {
+  for (uint32_t i = 0; i < S; ++i) gs[i]->q_shared = nullptr;
+}
+
+// One lock-step team: sessions gs[0..S) share one step stream (gs[0]'s) and T
+// worker threads; maintenance seconds into mt[0..S).  Runs on the calling thread.
+static int run_batched_team(pm_graph** gs, uint32_t S, const float* queries, uint64_t q, int k, int step,
+                            int parallel, uint32_t T, int64_t* answers, double* mt_out, ShardComb* comb = nullptr,
+                            uint32_t team = 0) {
+  StepGroup G;
+  struct Unshare {   // the sessions' query pointers point into G.qbuf until the team ends
+    pm_graph** gs; uint32_t S;
+    ~Unshare() { team_release(gs, S); }
+  } unshare{gs, S};
+  CHK(team_init(G, gs, S));
   if (comb) CHK(group_shard_init(G, gs, S, parallel, comb, team));
   T = std::max(1u, std::min(T, S));
   std::vector<char> fast(S, 0), need_prep(S, 0);
@@ -2960,6 +2996,232 @@ extern "C" int pm_batchpir_group_query(pm_batchpir_group* h, const uint64_t* ids
   return 0;
 }
 
+// pm_search_loop_batched with the host work pooled (the default; PM_BATCH_POOL=0:
+// one worker subset per team, run_batched_team).  The NG lock-step teams keep
+// their shared steps (one stream each, the same launches), but every worker
+// serves every team: when a team's step has completed, all workers take its
+// sessions' host work (results, GetVertexInfo's post-processing, the search
+// update, the next round's ids and bucketing), one session at a time off an
+// atomic counter, and the worker that finishes the team's last session
+// launches its next step -- or, at the end of a query, runs its maintenance
+// and the next query's start (search.go:130-146).  A team's host phase then
+// takes about 1/T of its sessions' host time instead of NG/T, so the GPU is not
+// left waiting while a fixed subset of workers works through one team, and
+// teams that fall behind get more of the workers.  Every session performs the
+// same operations in the same order as in run_batched_team.
+// PM_TEAM_TRACE=<file> (diagnostics): the pooled loop's host spans, one CSV row
+// each: team, kind (0 session task, 1 step launch, 2 maintenance, 3 query
+// start, 4 step in flight until seen complete), worker, start and end in us.
+struct TeamTrace {
+  struct Rec { double t0, t1; uint32_t team, kind, worker; };
+  const char* file = getenv("PM_TEAM_TRACE");
+  Clock::time_point base = Clock::now();
+  std::mutex mu;
+  std::vector<Rec> recs;
+  double now() const { return std::chrono::duration<double, std::micro>(Clock::now() - base).count(); }
+  void add(double t0, uint32_t team, uint32_t kind, uint32_t worker) {
+    if (!file) return;
+    const double t1 = now();
+    std::lock_guard<std::mutex> lk(mu);
+    recs.push_back({t0, t1, team, kind, worker});
+  }
+  ~TeamTrace() {
+    if (!file || recs.empty()) return;
+    if (FILE* f = fopen(file, "w")) {
+      fprintf(f, "team,kind,worker,t0_us,t1_us\n");
+      for (auto& r : recs) fprintf(f, "%u,%u,%u,%.2f,%.2f\n", r.team, r.kind, r.worker, r.t0, r.t1);
+      fclose(f);
+    }
+  }
+};
+enum : int { kTeamStart, kTeamOpen, kTeamBusy, kTeamFlight, kTeamDone };
+constexpr uint32_t kNoSession = ~0u;
+struct PoolTeam {
+  StepGroup G;
+  pm_graph** gs = nullptr;
+  uint32_t S = 0, s0 = 0;
+  std::vector<char> fast, need_prep;
+  std::vector<double> mt;
+  uint64_t qi = 0;                 // the team's current query
+  int st = 0;                      // its current round
+  bool begin = false;              // the open phase: a query's start (true) or a round's results
+  std::atomic<int> state{kTeamStart};
+  std::unique_ptr<std::atomic<uint32_t>[]> lane;   // per worker w: sessions w, w + T, ... taken so far
+  std::atomic<uint32_t> ndone{0};
+  Clock::time_point launched;
+  double launched_us = 0;
+  uint32_t id = 0;
+};
+static int run_batched_pool(pm_graph** gs, uint32_t S, const float* queries, uint64_t q, int k, int step, int parallel,
+                            uint32_t NG, uint32_t T, int64_t* answers, double* mt_out) {
+  std::vector<std::unique_ptr<PoolTeam>> teams;
+  struct Release {
+    std::vector<std::unique_ptr<PoolTeam>>& t;
+    ~Release() { for (auto& x : t) team_release(x->gs, x->S); }
+  } release{teams};
+  for (uint32_t g = 0; g < NG; ++g) {
+    const uint32_t s0 = (uint32_t)((uint64_t)S * g / NG), s1 = (uint32_t)((uint64_t)S * (g + 1) / NG);
+    teams.emplace_back(new PoolTeam());
+    PoolTeam& t = *teams.back();
+    t.gs = gs + s0; t.S = s1 - s0; t.s0 = s0; t.id = g;
+    t.fast.assign(t.S, 0); t.need_prep.assign(t.S, 0); t.mt.assign(t.S, 0.0);
+    t.lane.reset(new std::atomic<uint32_t>[T]);
+    for (uint32_t w = 0; w < T; ++w) t.lane[w].store(0);
+    CHK(team_init(t.G, t.gs, t.S));
+  }
+  const uint32_t dim = (uint32_t)gs[0]->dim;
+  TeamTrace tr;
+  std::atomic<int> err{0};
+  std::atomic<uint32_t> finished{0};
+  std::string err_msg;
+  std::mutex err_mu;
+  auto set_err = [&](int rc, uint32_t s) {
+    std::lock_guard<std::mutex> lk(err_mu);
+    int z = 0;
+    if (rc && err.compare_exchange_strong(z, rc)) err_msg = "session " + std::to_string(s) + ": " + pm_last_error();
+  };
+  // the team's phase opens: its sessions' tasks become available
+  auto open = [&](PoolTeam& t, bool begin) {
+    t.begin = begin;
+    t.ndone.store(0, std::memory_order_relaxed);
+    for (uint32_t w = 0; w < T; ++w) t.lane[w].store(0, std::memory_order_release);
+    t.state.store(kTeamOpen, std::memory_order_release);
+  };
+  // a session of the open phase: worker w's own lane first (sessions i = w mod
+  // T: the same worker, hence core, serves a session every round and finds its
+  // search state and prefetched rows in cache), then the other lanes' leftovers
+  auto claim = [&](PoolTeam& t, uint32_t w) -> uint32_t {
+    for (uint32_t j = 0; j < T; ++j) {
+      const uint32_t l = (w + j) % T;
+      if (l >= t.S) continue;
+      if (t.lane[l].load(std::memory_order_relaxed) * T + l >= t.S) continue;
+      const uint32_t i = t.lane[l].fetch_add(1, std::memory_order_acq_rel) * T + l;
+      if (i < t.S) return i;
+    }
+    return kNoSession;
+  };
+  // SearchKNN begin for every session of the team: queries and start-set
+  // distances in one upload, one k_l2_rows launch and one download
+  auto start_query = [&](PoolTeam& t) -> int {
+    const double t0 = tr.now();
+    float* qst = t.G.qstage.as<float>();
+    for (uint32_t i = 0; i < t.S; ++i) {
+      pm_graph* g = t.gs[i];
+      knn_reset(g);
+      g->t_init = Clock::now();
+      memcpy(qst + (uint64_t)i * dim, queries + ((uint64_t)(t.s0 + i) * q + t.qi) * dim, (size_t)dim * 4);
+    }
+    CHK(group_start_dist(t.G, t.gs));
+    tr.add(t0, t.id, 3, 0);
+    open(t, true);
+    return 0;
+  };
+  // one session's share of the open phase (run_batched_team's per-session work)
+  auto task = [&](PoolTeam& t, uint32_t i, int64_t* stp) -> int {
+    pm_graph* g = t.gs[i];
+    if (t.begin) {
+      knn_begin_finish(g, parallel, 0, t.G.qstage.as<float>() + (uint64_t)t.S * dim + (uint64_t)i * t.G.ns);
+    } else {
+      if (t.fast[i]) CHK(group_collect(t.G, i));   // complete: only the tokens and host mirrors
+      CHK(gvi_post(g, true, t.fast[i]));
+      knn_update(g, t.st);
+      if (t.st + 1 == step) {   // top k, maintenance trigger (private-search.go:226-232)
+        knn_end(g, k, answers + ((uint64_t)(t.s0 + i) * q + t.qi) * k, stp);
+        Engine* e = &g->pir->e;
+        t.need_prep[i] = e->FBN + (uint64_t)step * (uint64_t)parallel + 10 >= e->Support;
+        return 0;
+      }
+    }
+    knn_batch(g, parallel, 0);   // the next round's ids -> sub-queries
+    bool f = false;
+    CHK(gvi_pre(g, true, &f));
+    t.fast[i] = f;
+    return 0;
+  };
+  // the worker that completed the phase's last session moves the team on
+  auto advance = [&](PoolTeam& t) -> int {
+    if (t.begin || t.st + 1 < step) {   // a round's ids are bucketed: its shared step
+      t.st = t.begin ? 0 : t.st + 1;
+      const double t0 = tr.now();
+      CHK(group_step(t.G, t.fast));
+      tr.add(t0, t.id, 1, 0);
+      t.launched = Clock::now();
+      t.launched_us = tr.now();
+      t.state.store(kTeamFlight, std::memory_order_release);
+      return 0;
+    }
+    const double t0 = tr.now();
+    CHK(group_prep(t.G, t.need_prep, &t.mt));   // the triggered clients' preprocessings as one launch set
+    tr.add(t0, t.id, 2, 0);
+    if (++t.qi == q) {
+      t.state.store(kTeamDone, std::memory_order_release);
+      finished.fetch_add(1);
+      return 0;
+    }
+    return start_query(t);
+  };
+  std::vector<int64_t> steps_buf((size_t)T * std::max(k, 1));
+  const int dev = gs[0]->ctx->device;
+  auto worker = [&](uint32_t w) {
+    if (hipSetDevice(dev) != hipSuccess) { set_err(PM_EHIP, 0); return; }
+    int64_t* stp = &steps_buf[(size_t)w * std::max(k, 1)];
+    uint32_t idle = 0;
+    while (!err.load(std::memory_order_relaxed) && finished.load(std::memory_order_acquire) < NG) {
+      bool did = false;
+      for (uint32_t j = 0; j < NG && !did; ++j) {
+        PoolTeam& t = *teams[(w + j) % NG];
+        int cur = t.state.load(std::memory_order_acquire);
+        if (cur == kTeamOpen) {
+          const uint32_t i = claim(t, w);
+          if (i == kNoSession) continue;
+          did = true;
+          const double t0 = tr.now();
+          int rc = task(t, i, stp);
+          tr.add(t0, t.id, 0, w);
+          if (rc) set_err(rc, t.s0 + i);
+          if (t.ndone.fetch_add(1, std::memory_order_acq_rel) + 1 == t.S && !err.load()) {
+            t.state.store(kTeamBusy, std::memory_order_relaxed);
+            rc = advance(t);
+            if (rc) set_err(rc, t.s0);
+          }
+        } else if (cur == kTeamStart || cur == kTeamFlight) {
+          bool ready = cur == kTeamStart;
+          if (!ready) {
+            const int rc = poll_done(t.G.c, t.G.seq, &ready);
+            if (rc) { set_err(rc, t.s0); break; }
+            if (!ready && std::chrono::duration<double>(Clock::now() - t.launched).count() > 10.0) {
+              set_err(fail(PM_EHIP, "shared step not complete after 10 s"), t.s0);
+              break;
+            }
+          }
+          if (ready && t.state.compare_exchange_strong(cur, kTeamBusy, std::memory_order_acq_rel)) {
+            did = true;
+            if (cur == kTeamFlight) tr.add(t.launched_us, t.id, 4, w);
+            const int rc = cur == kTeamStart ? start_query(t) : (open(t, false), 0);
+            if (rc) set_err(rc, t.s0);
+          }
+        }
+      }
+      if (did) {
+        idle = 0;
+      } else if (++idle > 32) {   // nothing to do: give the core to the workers that have work
+        std::this_thread::yield();
+      } else {
+        __builtin_ia32_pause();   // spin politely (an SMT sibling may be a working worker)
+      }
+    }
+  };
+  std::vector<std::thread> th;
+  for (uint32_t w = 1; w < T; ++w) th.emplace_back(worker, w);
+  worker(0);
+  for (auto& t : th) t.join();
+  for (auto& t : teams) HIPCHK(hipStreamSynchronize(t->G.c->stream));
+  if (err.load()) return fail(err.load(), err_msg);
+  for (auto& t : teams)
+    for (uint32_t s = 0; s < t->S; ++s) mt_out[t->s0 + s] = t->mt[s];
+  return 0;
+}
+
 extern "C" int pm_search_loop_batched(pm_graph** gs, uint32_t S, const float* queries, uint64_t q, int k, int step,
                                       int parallel, uint32_t ngroups, uint32_t nthreads, int64_t* answers,
                                       double* wall_s, double* online_s, double* maint_s) {
@@ -2985,6 +3247,17 @@ extern "C" int pm_search_loop_batched(pm_graph** gs, uint32_t S, const float* qu
   std::vector<std::thread> teams;
   const float* qbase = queries;
   auto t0 = Clock::now();
+  static const int pool = [] { const char* e = getenv("PM_BATCH_POOL"); return e ? atoi(e) : 1; }();
+  if (pool && NG > 1) {   // the pooled workers (run_batched_pool); one team: the workers serve it alone anyway
+    CHK(run_batched_pool(gs, S, queries, q, k, step, parallel, NG, TT, answers, mt.data()));
+    const double wall = std::chrono::duration<double>(Clock::now() - t0).count();
+    if (wall_s) *wall_s = wall;
+    for (uint32_t s = 0; s < S; ++s) {
+      if (online_s) online_s[s] = wall - mt[s];
+      if (maint_s) maint_s[s] = mt[s];
+    }
+    return 0;
+  }
   for (uint32_t g = 0; g < NG; ++g) {
     const uint32_t s0 = (uint32_t)((uint64_t)S * g / NG), s1 = (uint32_t)((uint64_t)S * (g + 1) / NG);
     const uint32_t Tg = std::max(1u, std::min(s1 - s0, (uint32_t)((uint64_t)TT * (g + 1) / NG - (uint64_t)TT * g / NG)));

@@ -434,7 +434,7 @@ def test_search_sessions_concurrent(ctx, oracle):
         assert sess[i].PIR.stats()["PrepCount"] == o.pir().stats()["PrepCount"] > 1, i
 
 
-@pytest.mark.parametrize("ngroups,nthreads", [(1, 0), (1, 2), (2, 3)])
+@pytest.mark.parametrize("ngroups,nthreads", [(1, 0), (1, 2), (2, 3), (3, 4), (5, 2)])
 def test_search_sessions_batched(ctx, oracle, ngroups, nthreads):
     """pm_search_loop_batched: five sessions in lock-step, every round of all
     of them one shared step over 5 x 16 partitions; each session's answers,
