@@ -3090,8 +3090,9 @@ static int run_batched_pool(pm_graph** gs, uint32_t S, const float* queries, uin
   // a session of the open phase: worker w's own lane first (sessions i = w mod
   // T: the same worker, hence core, serves a session every round and finds its
   // search state and prefetched rows in cache), then the other lanes' leftovers
+  static const int steal = [] { const char* e = getenv("PM_POOL_STEAL"); return e ? atoi(e) : 1; }();
   auto claim = [&](PoolTeam& t, uint32_t w) -> uint32_t {
-    for (uint32_t j = 0; j < T; ++j) {
+    for (uint32_t j = 0; j < (steal ? T : 1u); ++j) {
       const uint32_t l = (w + j) % T;
       if (l >= t.S) continue;
       if (t.lane[l].load(std::memory_order_relaxed) * T + l >= t.S) continue;
