@@ -487,10 +487,16 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_rot(const PmPart* __
   // SAME slice block, so the partition's image slices are shared through the
   // Infinity Cache; then the next slice block of the same pairs (their tabT
   // again, from the Infinity Cache).
+  // Tile T = (its index on the XCD) * 8 + XCD; a last group of fewer than 8
+  // pair blocks is dealt over the XCDs the same way (small launches, e.g. one
+  // client's 48 pairs, keep every XCD busy).
   constexpr uint32_t GB = PM_ROT_GB, SB = PM_ROT_SB;
-  const uint32_t nsb = (nsl + SB - 1) / SB, lt = kq / (GB * SB), wt = kq % (GB * SB);
-  const uint32_t pgv = ((lt / nsb) * 8 + xcd) * GB + wt % GB;
-  const uint32_t slice = (lt % nsb) * SB + wt / GB;
+  const uint32_t nsb = (nsl + SB - 1) / SB, ngb = (npv + GB - 1) / GB;
+  const uint32_t T = (kq / (GB * SB)) * 8 + xcd, wt = kq % (GB * SB);
+  if (T >= ngb * nsb) return;   // block-uniform
+  const uint32_t gsup = T / (8 * nsb), m = min(8u, ngb - gsup * 8), r = T - gsup * 8 * nsb;
+  const uint32_t pgv = (gsup * 8 + r % m) * GB + wt % GB;
+  const uint32_t slice = (r / m) * SB + wt / GB;
   (void)M; (void)LW;
 #else
   const uint32_t loc = (kq / LW) % M, slice = (kq / (LW * M)) * LW + kq % LW;
@@ -1038,7 +1044,7 @@ void prep_fold(hipStream_t st, const PmPart* d, int np, uint32_t maxH, const uin
       const uint32_t nvg = ngc ? K * ngc : (uint32_t)cdiv((uint64_t)K * maxH, HB), npv = (np / K) * nvg;
       const uint32_t M = cdiv(npv, 8);
       const uint32_t grid = PM_ROT_ORDER == 1
-                                ? 8 * cdiv(cdiv(npv, PM_ROT_GB), 8) * cdiv(nsl, PM_ROT_SB) * PM_ROT_GB * PM_ROT_SB
+                                ? 8 * cdiv((uint64_t)cdiv(npv, PM_ROT_GB) * cdiv(nsl, PM_ROT_SB), 8) * PM_ROT_GB * PM_ROT_SB
                                 : 8 * M * cdiv(nsl, PM_ROT_LW) * PM_ROT_LW;
       hipLaunchKernelGGL(k_prep_fold_rot<512>, dim3(grid), dim3(kFoldThreads), 0, st, d, E, nvg, nsl, npv, M, K, ngc);
       return;
