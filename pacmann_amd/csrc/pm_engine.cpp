@@ -2544,42 +2544,50 @@ static int group_start_dist(StepGroup& G, pm_graph** gs) {
   return 0;
 }
 
-// SimpleBatchPianoPIR.Preprocessing (batch-pir.go:119-155) of every client
-// with need[s], as ONE launch set over all their partitions on the team's
-// stream (the clients share the server DB and parameters).  Each client's
-// maintenance time is the set's wall time.
-static int group_prep(StepGroup& G, const std::vector<char>& need, std::vector<double>* mt) {
-  std::vector<uint32_t> who;
-  for (uint32_t s = 0; s < G.S; ++s)
-    if (need[s]) who.push_back(s);
+// SimpleBatchPianoPIR.Preprocessing (batch-pir.go:119-155) of the clients
+// `who` (batch PIR engines of one server: same DB and parameters, partitions
+// lp), as ONE launch set over all their partitions on c's stream, with its
+// parts staged in pbuf.  Each client's maintenance time is the set's wall time
+// (added to *mt[i] when given).
+static int prep_clients(pm_ctx* c, DevBuf& pbuf, const std::vector<uint32_t>& lp, const std::vector<Engine*>& who,
+                        const std::vector<double*>* mt) {
   if (who.empty()) return 0;
   auto t0 = Clock::now();
   std::vector<PmPart> hp;
   std::vector<uint64_t> todo;
-  for (uint32_t s : who) {
-    Engine* e = G.es[s];
+  for (Engine* e : who) {
     e->FBN = 0; e->QMIP = 0;
     CHK(engine_prep_host(e, 0, e->P, todo));
   }
   // partition-major: the clients' folds of one partition run side by side and
   // share its DB rows through the caches instead of re-reading them per client
-  for (uint32_t p : G.lp)
-    for (uint32_t s : who) hp.push_back(G.es[s]->parts[p].d);
-  const Engine* e0 = G.es[who[0]];
+  for (uint32_t p : lp)
+    for (Engine* e : who) hp.push_back(e->parts[p].d);
+  const Engine* e0 = who[0];
   bool skip = false;
-  for (uint32_t s : who) skip |= G.es[s]->skipPrep != e0->skipPrep;
+  for (Engine* e : who) skip |= e->skipPrep != e0->skipPrep;
   if (skip) return fail(PM_EINVAL, "batched sessions mix Preprocessing and DummyPreprocessing");
-  CHK(G.prep_parts.reserve(hp.size() * sizeof(PmPart)));
-  HIPCHK(hipMemcpyAsync(G.prep_parts.p, hp.data(), hp.size() * sizeof(PmPart), hipMemcpyHostToDevice, G.c->stream));
-  CHK(engine_prep_launch(G.c, e0, G.prep_parts.as<PmPart>(), (int)hp.size(), hp.data(), (uint32_t)who.size()));
+  CHK(pbuf.reserve(hp.size() * sizeof(PmPart)));
+  HIPCHK(hipMemcpyAsync(pbuf.p, hp.data(), hp.size() * sizeof(PmPart), hipMemcpyHostToDevice, c->stream));
+  CHK(engine_prep_launch(c, e0, pbuf.as<PmPart>(), (int)hp.size(), hp.data(), (uint32_t)who.size()));
   const double t = std::chrono::duration<double>(Clock::now() - t0).count();
-  for (uint32_t s : who) {
-    Engine* e = G.es[s];
-    e->prepCount++;
-    record_stats(e, t);
-    if (mt) (*mt)[s] += t;
+  for (size_t i = 0; i < who.size(); ++i) {
+    who[i]->prepCount++;
+    record_stats(who[i], t);
+    if (mt) *(*mt)[i] += t;
   }
   return 0;
+}
+// The clients of team G with need[s], as one launch set on the team's stream.
+static int group_prep(StepGroup& G, const std::vector<char>& need, std::vector<double>* mt) {
+  std::vector<Engine*> who;
+  std::vector<double*> mts;
+  for (uint32_t s = 0; s < G.S; ++s)
+    if (need[s]) {
+      who.push_back(G.es[s]);
+      if (mt) mts.push_back(&(*mt)[s]);
+    }
+  return prep_clients(G.c, G.prep_parts, G.lp, who, mt ? &mts : nullptr);
 }
 
 // ---- sharded private search (pm_search_loop_sharded) --------------------
@@ -3034,7 +3042,7 @@ struct TeamTrace {
     }
   }
 };
-enum : int { kTeamStart, kTeamOpen, kTeamBusy, kTeamFlight, kTeamDone };
+enum : int { kTeamStart, kTeamOpen, kTeamBusy, kTeamFlight, kTeamPrep, kTeamDone };
 constexpr uint32_t kNoSession = ~0u;
 struct PoolTeam {
   StepGroup G;
@@ -3048,13 +3056,23 @@ struct PoolTeam {
   std::atomic<int> state{kTeamStart};
   std::unique_ptr<std::atomic<uint32_t>[]> lane;   // per worker w: sessions w, w + T, ... taken so far
   std::atomic<uint32_t> ndone{0};
-  Clock::time_point launched;
+  Clock::time_point launched, prep_since;
   double launched_us = 0;
   uint32_t id = 0;
 };
 static int run_batched_pool(pm_graph** gs, uint32_t S, const float* queries, uint64_t q, int k, int step, int parallel,
                             uint32_t NG, uint32_t T, int64_t* answers, double* mt_out) {
   std::vector<std::unique_ptr<PoolTeam>> teams;
+  DevBuf prep_buf;   // the merged maintenance's parts
+  std::mutex prep_mu;
+  // Maintenance (the end-of-query re-preprocessing, private-search.go:226-232)
+  // of the teams that reach it together runs as ONE launch set: a team whose
+  // clients need it waits (kTeamPrep) until every running team waits too, or
+  // PM_PREP_WAIT_MS after the first one arrived.  The maintenance kernels fill
+  // the GPU, so teams' maintenances run one after another either way; merged,
+  // the teams also resume together, instead of finishing the timed work one
+  // after another with the GPU partly idle.  PM_PREP_WAIT_MS=0: each team alone.
+  static const double prep_wait = [] { const char* e = getenv("PM_PREP_WAIT_MS"); return e ? atof(e) : 20.0; }();
   struct Release {
     std::vector<std::unique_ptr<PoolTeam>>& t;
     ~Release() { for (auto& x : t) team_release(x->gs, x->S); }
@@ -3152,6 +3170,13 @@ static int run_batched_pool(pm_graph** gs, uint32_t S, const float* queries, uin
       return 0;
     }
     const double t0 = tr.now();
+    bool any = false;
+    for (char c : t.need_prep) any |= c != 0;
+    if (any && prep_wait > 0) {   // with the other teams' (above)
+      t.prep_since = Clock::now();
+      t.state.store(kTeamPrep, std::memory_order_release);
+      return 0;
+    }
     CHK(group_prep(t.G, t.need_prep, &t.mt));   // the triggered clients' preprocessings as one launch set
     tr.add(t0, t.id, 2, 0);
     if (++t.qi == q) {
@@ -3184,6 +3209,42 @@ static int run_batched_pool(pm_graph** gs, uint32_t S, const float* queries, uin
             t.state.store(kTeamBusy, std::memory_order_relaxed);
             rc = advance(t);
             if (rc) set_err(rc, t.s0);
+          }
+        } else if (cur == kTeamPrep) {
+          if (!prep_mu.try_lock()) continue;   // one worker runs the merged maintenance
+          std::lock_guard<std::mutex> lk(prep_mu, std::adopt_lock);
+          const auto now = Clock::now();
+          bool all = true;
+          auto first = now;
+          for (auto& u : teams) {
+            const int us = u->state.load(std::memory_order_acquire);
+            if (us == kTeamPrep) first = std::min(first, u->prep_since);
+            else if (us != kTeamDone) all = false;
+          }
+          if (!all && std::chrono::duration<double, std::milli>(now - first).count() < prep_wait) continue;
+          std::vector<PoolTeam*> ts;
+          for (auto& u : teams) {
+            int e = kTeamPrep;
+            if (u->state.compare_exchange_strong(e, kTeamBusy, std::memory_order_acq_rel)) ts.push_back(u.get());
+          }
+          if (ts.empty()) continue;
+          did = true;
+          const double t0 = tr.now();
+          std::vector<Engine*> who;
+          std::vector<double*> mts;
+          for (PoolTeam* u : ts)
+            for (uint32_t s = 0; s < u->S; ++s)
+              if (u->need_prep[s]) { who.push_back(u->G.es[s]); mts.push_back(&u->mt[s]); }
+          const int rc = prep_clients(ts[0]->G.c, prep_buf, ts[0]->G.lp, who, &mts);
+          if (rc) { set_err(rc, ts[0]->s0); break; }
+          for (PoolTeam* u : ts) {
+            tr.add(t0, u->id, 2, w);
+            if (++u->qi == q) {
+              u->state.store(kTeamDone, std::memory_order_release);
+              finished.fetch_add(1);
+            } else {
+              u->state.store(kTeamStart, std::memory_order_release);   // a worker starts its next query
+            }
           }
         } else if (cur == kTeamStart || cur == kTeamFlight) {
           bool ready = cur == kTeamStart;
