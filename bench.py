@@ -870,11 +870,13 @@ def main():
         fold["clients_per_launch"] = k
         fold["compulsory"] = {"bytes": comp, "achieved": round(ach_c, 1), "frac": round(ach_c / HBM_PEAK_GBS, 4)}
         # PMC bytes of launches of this shape (k_prep_fold_rot<512>: the k clients' hints of a
-        # partition in virtual groups of 5,120, (partition, group) pairs spread over 8 XCDs, 20
-        # column slices in groups of 2 (PM_ROT_LW), 1,024 threads per workgroup; pm_kernels.hip prep_fold)
+        # partition in virtual groups of 5,120; XCD tiles of 4 (partition, group) pairs x 8 of the
+        # 20 column slices, dealt to the 8 XCDs in turn; 1,024 threads per workgroup;
+        # pm_kernels.hip prep_fold)
         H0 = c0["PrimaryHintNum"] + c0["SetSize"] * c0["MaxQueryPerChunk"]
         npv = stats["PartitionNum"] * -(-(k * H0) // 5120)
-        attach_traffic(fold, SYMBOLS["prep_fold"], 8 * -(-npv // 8) * -(-(E // 4) // 2) * 2 * 1024)
+        tiles = -(-npv // 4) * -(-(E // 4) // 8)
+        attach_traffic(fold, SYMBOLS["prep_fold"], 8 * -(-tiles // 8) * 32 * 1024)
         # the fold is LDS-bound, not HBM-bound: its fold bytes (one entry read per
         # (hint, chunk) pair) are ds_read_b128 reads of the staged
         # chunks; HBM carries the staging (PMC traffic) and the parity writes
