@@ -2024,9 +2024,17 @@ __global__ void __launch_bounds__(NT, PM_ANSWER_WGS) k_answer_s(PmStep S) {
 // entry.  k_answer folds the nsplit partials, so a sub-query's 0.5-2.4 MB of
 // rows are read by nsplit CUs instead of one.
 constexpr int kGatherBlock = 256;
+constexpr uint32_t kGatherMaxRange = 4096;   // chunks per workgroup (SetSize / nsplit; BIGANN-1B: 3,816 at nsplit 1)
+#ifndef PM_GATHER_KG
+#define PM_GATHER_KG 8
+#endif
+#ifndef PM_GATHER_WAVES
+#define PM_GATHER_WAVES 8   // min waves per SIMD: <= 64 VGPRs, eight 256-thread workgroups per CU
+#endif
 template <int W>
-__global__ void __launch_bounds__(kGatherBlock) k_gather(PmStep S) {
+__global__ void __launch_bounds__(kGatherBlock, PM_GATHER_WAVES) k_gather(PmStep S) {
   __shared__ uint64_t red[kGatherBlock * 2];
+  __shared__ uint32_t rows_l[kGatherMaxRange];   // the range's partition rows (set expansion), ~0u: none
   const uint32_t j = blockIdx.x, s = blockIdx.y, tid = threadIdx.x;
   const PmRes r = S.res[s];
   const uint32_t mode = answer_mode(r);
@@ -2038,41 +2046,48 @@ __global__ void __launch_bounds__(kGatherBlock) k_gather(PmStep S) {
   const bool real = mode != A_DUMMY;
   const uint32_t pchunk = real && r.pp != kDefaultProgramPoint ? (r.pp >> lg) : kNone;
   const uint32_t rchunk = real ? r.chunk : kNone;
-  const uint32_t rep = real ? (P.ridx[r.chunk * P.Qpc + r.ing] & mask) : 0;
+  // the range's set first, every offset load in flight together, into LDS
+  // (expanded inside the row batches, each batch waited for its offsets and then
+  // for its rows: two round trips per batch)
+  const uint32_t rep = real && rchunk - c0 < c1 - c0 ? (P.ridx[r.chunk * P.Qpc + r.ing] & mask) : 0;
+  for (uint32_t i = c0 + tid; i < c1; i += kGatherBlock) {
+    uint32_t o;
+    if (real) {
+      o = P.tabT[tabT_index(P.H, r.tag, i)];
+      if (i == pchunk) o = r.pp & mask;
+      if (i == rchunk) o = rep;
+    } else {
+      o = (uint32_t)(hash4(P.seed, DOM_DUMMY, P.idx, sub.idx, i) & mask);
+    }
+    const uint64_t row = (uint64_t)i * P.CS + o;
+    rows_l[i - c0] = row < P.N ? (uint32_t)row : ~0u;
+  }
+  __syncthreads();
 
   const PM_G uint64_t* base = S.db + P.row0 * E;
   PM_G uint64_t* out = S.part_x + ((uint64_t)s * S.nsplit + j) * EX;
   typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+  const uint32_t nr = c1 - c0;
   for (uint32_t seg0 = 0; seg0 < NSEG; seg0 += kGatherBlock) {
     const uint32_t nseg = min(NSEG - seg0, (uint32_t)kGatherBlock);
     const uint32_t nsl = kGatherBlock / nseg;
     const uint32_t sl = tid / nseg, seg = seg0 + tid % nseg;
     uint64_t a0 = 0, a1 = 0;
     if (sl < nsl) {
-      constexpr int kG = 16;   // every row load of a batch in flight together
-      for (uint32_t i0 = c0 + sl; i0 < c1; i0 += kG * nsl) {
-        uint64_t rr[kG];
+      constexpr int kG = PM_GATHER_KG;   // every row load of a batch in flight together
+      for (uint32_t i0 = sl; i0 < nr; i0 += kG * nsl) {
+        uint32_t rr[kG];
 #pragma unroll
-        for (int u = 0; u < kG; ++u) {
-          const uint32_t i = i0 + u * nsl;
-          uint32_t o = 0;
-          if (i < c1) {
-            if (real) {
-              o = P.tabT[tabT_index(P.H, r.tag, i)];
-              if (i == pchunk) o = r.pp & mask;
-              if (i == rchunk) o = rep;
-            } else {
-              o = (uint32_t)(hash4(P.seed, DOM_DUMMY, P.idx, sub.idx, i) & mask);
-            }
-          }
-          rr[u] = i < c1 ? (uint64_t)i * P.CS + o : P.N;
-        }
+        for (int u = 0; u < kG; ++u) rr[u] = rows_l[min(i0 + u * nsl, nr - 1)];
+#pragma unroll
+        for (int u = 0; u < kG; ++u)
+          if (i0 + u * nsl >= nr) rr[u] = ~0u;
         u64x2 x[kG];
 #pragma unroll
         for (int u = 0; u < kG; ++u) {
           x[u] = u64x2{0, 0};
-          if (rr[u] < P.N) {
-            const PM_G uint64_t* q = base + rr[u] * E + (uint64_t)seg * W;
+          if (rr[u] != ~0u) {
+            const PM_G uint64_t* q = base + (uint64_t)rr[u] * E + (uint64_t)seg * W;
             if (W == 2) x[u] = *reinterpret_cast<const PM_G u64x2*>(q);
             else x[u].x = *q;
           }
@@ -2250,7 +2265,8 @@ uint32_t step_gather_split(uint32_t maxSS, uint32_t nsub) {
   if (maxSS < 256 || nsub == 0) return 1;
   // >= 48 rows per workgroup, about 2,048 workgroups in all, at most 64 per sub-query
   uint32_t n = std::min(cdiv(maxSS, 48), cdiv(2048, nsub));
-  return std::max(1u, std::min(n, 64u));
+  n = std::max(1u, std::min(n, 64u));
+  return n > 1 ? std::max(n, cdiv(maxSS, kGatherMaxRange)) : 1u;   // a range's set fits k_gather's LDS
 }
 void step_gather(hipStream_t st, const PmStep& S, PmEvents ev) {
   const dim3 grid(S.nsplit, S.nsub);
