@@ -237,7 +237,8 @@ uint64_t fold_image_words(uint32_t SS, uint32_t E);
 void fold_image(hipStream_t st, uint64_t* img, const uint64_t* part_rows, uint64_t N, uint32_t SS, uint32_t E);
 // Timing events carried by a launch's own dispatch packet (null: untimed)
 struct PmEvents { hipEvent_t a = nullptr, b = nullptr; };
-void step_match(hipStream_t st, const PmStep& S, uint32_t maxPH, PmEvents ev = {});
+// ph8: every partition's PH is a multiple of 8 (k_match_part8)
+void step_match(hipStream_t st, const PmStep& S, bool ph8, uint32_t maxPH, PmEvents ev = {});
 uint32_t step_match_blocks(uint32_t maxPH);   // k_match workgroups per sub-query
 void step_resolve(hipStream_t st, const PmStep& S, bool lds, PmEvents ev = {});
 // k_match_part + k_resolve fused (batched serving; descriptor already in device memory)

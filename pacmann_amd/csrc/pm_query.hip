@@ -550,6 +550,106 @@ __global__ void __launch_bounds__(kBlock, PM_MATCHPART_WAVES) k_match_part(PmSte
   match_part_block<HPT, NT, G>(S, P, pb0, pn, blk, tid, s_cand);
 }
 
+// k_match_part for steps whose partitions all have PH % 8 == 0 (16-B aligned
+// search rows): one WAVE per (partition, kMatchHints block).  Lane l holds
+// hints 8l.. and 512 + 8l.. of its block (two 16-B loads per sub-query, G
+// sub-queries in flight), so the block's match bits are 128 contiguous bytes
+// (lane l writes bytes l and 64 + l) and its first two matches come from two
+// ballots of the lanes' 8-bit masks: no LDS, no barrier, NW blocks per
+// workgroup.  Same bits, records and predictions as k_match_part.
+#ifndef PM_MATCHPART8_NW
+#define PM_MATCHPART8_NW 4
+#endif
+__device__ __forceinline__ uint32_t match8(uint4 v, uint32_t off) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t m = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    m |= (((w[i] & 0xffffu) == off) ? 1u : 0u) << (2 * i) | (((w[i] >> 16) == off) ? 1u : 0u) << (2 * i + 1);
+  return m;
+}
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) k_match_part8(PmStep S) {
+  constexpr int G = PM_MATCHPART_G;
+  constexpr uint32_t kHalf = kMatchHints / 2;   // 512: the second load's hints
+  static_assert(kMatchHints == 1024, "one wave x 16 hints per lane");
+  const uint32_t p = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t pb0 = desc_sb(S, p), pn = desc_sb(S, p + 1) - pb0;
+  if (!S.args_valid && blockIdx.x == 0 && S.subs != S.subs_h) {   // stage the descriptor for the later kernels
+    for (uint32_t i = tid; i < pn; i += 64 * NW) S.subs[pb0 + i] = S.subs_h[pb0 + i];
+    if (p == 0)
+      for (uint32_t i = tid; i <= S.np; i += 64 * NW) S.sb[i] = S.sb_h[i];
+  }
+  if (pn == 0) return;
+  const PmPart P = S.parts[p];
+  const uint32_t nb = (P.PH + kMatchHints - 1) / kMatchHints, nwg = (nb + NW - 1) / NW;
+  if (blockIdx.x >= nwg) return;
+  match_part_predict(S, P, pb0, pn, blockIdx.x + nwg * wave, nwg * NW);
+  const uint32_t blk = blockIdx.x * NW + wave;
+  if (blk >= nb) return;   // whole wave; nothing below synchronises
+  const uint32_t base = blk * kMatchHints, mask = P.CS - 1, lg = P.log2CS;
+  const uint32_t hA = base + 8 * lane, hB = hA + kHalf;   // first hint of each load
+  for (uint32_t j0 = 0; j0 < pn; j0 += G) {
+    uint32_t kind[G], off[G];
+    uint4 rv[G][2];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      PmSub sub{0, SUB_NONE, 0};
+      if (j0 + g < pn) sub = desc_sub(S, pb0 + j0 + g);
+      kind[g] = __builtin_amdgcn_readfirstlane(sub.kind);
+      const uint64_t idx = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(sub.idx >> 32)) << 32) |
+                           __builtin_amdgcn_readfirstlane((uint32_t)sub.idx);
+      const bool lv = kind[g] == SUB_REAL && idx < P.N;
+      off[g] = (uint32_t)(idx & mask);
+      const PM_G uint4* crow = reinterpret_cast<const PM_G uint4*>(P.cur + (uint64_t)(uint32_t)(idx >> lg) * P.PH);
+      // unconditional 16-B loads (a dead lane reads the partition's first
+      // vector), then kSkip x 8 by value: a select of the loaded VALUE keeps
+      // them global_load_dwordx4
+      const bool okA = lv && hA < P.PH, okB = lv && hB < P.PH;
+      const uint4 a = okA ? crow[hA >> 3] : *reinterpret_cast<const PM_G uint4*>(P.cur);
+      const uint4 b = okB ? crow[hB >> 3] : *reinterpret_cast<const PM_G uint4*>(P.cur);
+      rv[g][0] = okA ? a : make_uint4(~0u, ~0u, ~0u, ~0u);
+      rv[g][1] = okB ? b : make_uint4(~0u, ~0u, ~0u, ~0u);
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (j0 + g >= pn || kind[g] != SUB_REAL) continue;   // wave-uniform
+      const uint64_t s = pb0 + j0 + g;
+      const uint32_t mA = match8(rv[g][0], off[g]), mB = match8(rv[g][1], off[g]);
+      PM_G uint8_t* bb = reinterpret_cast<PM_G uint8_t*>(S.bits + s * S.words);
+      // every byte of a 64-hint word that starts below PH (zero past PH)
+      if ((hA & ~63u) < P.PH) bb[hA >> 3] = (uint8_t)mA;
+      if ((hB & ~63u) < P.PH) bb[hB >> 3] = (uint8_t)mB;
+      uint32_t h0 = kNone, h1 = kNone;   // the block's first two matches, wave-uniform
+      auto scan = [&](uint32_t mu, uint32_t hbase) {   // lanes in hint order
+        uint64_t bal = __ballot(mu != 0);
+        while (bal && h1 == kNone) {
+          const uint32_t fl = (uint32_t)__builtin_ctzll(bal);
+          uint32_t mm = __builtin_amdgcn_readlane(mu, fl);
+          const uint32_t hb = hbase + 8 * fl;
+          while (mm && h1 == kNone) {
+            const uint32_t hh = hb + (uint32_t)__builtin_ctz(mm);
+            mm &= mm - 1;
+            if (h0 == kNone) h0 = hh;
+            else h1 = hh;
+          }
+          bal &= bal - 1;
+        }
+      };
+      scan(mA, base);
+      if (h1 == kNone) scan(mB, base + kHalf);
+      uint32_t t0 = 0, p0 = 0, t1 = 0, p1 = 0;
+      if (h0 != kNone) { t0 = P.tag[h0]; p0 = P.pp[h0]; }
+      if (h1 != kNone) { t1 = P.tag[h1]; p1 = P.pp[h1]; }
+      if (lane < 6) {
+        const uint32_t v = lane == 0 ? h0 : lane == 1 ? t0 : lane == 2 ? p0 : lane == 3 ? h1 : lane == 4 ? t1 : p1;
+        S.cand[(s * S.cblk + blk) * 6 + lane] = v;
+      }
+    }
+  }
+}
+
 // First set bit at position >= start in a sub-query's match bitmask (one wave).
 __device__ __forceinline__ uint32_t find_next(const uint64_t* __restrict__ bw, uint32_t nw, uint32_t start) {
   const uint32_t lane = threadIdx.x & 63;
@@ -2176,12 +2276,17 @@ uint32_t step_match_blocks(uint32_t maxPH) { return cdiv(maxPH, kMatchHints); }
     if ((ev).a) hipExtLaunchKernelGGL(kern, grid, blk, 0, st, (ev).a, (ev).b, 0, __VA_ARGS__); \
     else hipLaunchKernelGGL(kern, grid, blk, 0, st, __VA_ARGS__);                             \
   } while (0)
-void step_match(hipStream_t st, const PmStep& S, uint32_t maxPH, PmEvents ev) {
+void step_match(hipStream_t st, const PmStep& S, bool ph8, uint32_t maxPH, PmEvents ev) {
   // many partitions with several sub-queries each (batched serving): one
   // workgroup per (partition, hint block); otherwise one per (sub-query, block)
   static const int mode = [] { const char* e = getenv("PM_MATCH_PART"); return e ? atoi(e) : -1; }();
   const bool part = mode == 1 || (mode == -1 && S.np >= 128 && S.nsub >= 4 * S.np);
-  if (part)
+  // PM_MATCH_PART8=0: the LDS-merged form for every PH
+  static const int v8 = [] { const char* e = getenv("PM_MATCH_PART8"); return e ? atoi(e) : 1; }();
+  if (part && ph8 && v8)
+    PM_LAUNCH(ev, k_match_part8<PM_MATCHPART8_NW>, dim3(cdiv(step_match_blocks(maxPH), PM_MATCHPART8_NW), S.np),
+              dim3(64 * PM_MATCHPART8_NW), st, S);
+  else if (part)
     PM_LAUNCH(ev, k_match_part<kMatchHints / kBlock>, dim3(step_match_blocks(maxPH), S.np), dim3(kBlock), st, S);
   else
     PM_LAUNCH(ev, k_match, dim3(step_match_blocks(maxPH), S.nsub), dim3(kBlock), st, S);
