@@ -1082,7 +1082,7 @@ static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
 #endif
     return 0;
   }
-  c->timed_ext("hint_match", (double)nreal * g->maxPH, [&](pmk::PmEvents ev) { pmk::step_match(st, S, g->ph8, g->maxPH, ev); }, 2);
+  c->timed_ext("hint_match", (double)nreal * g->maxPH, [&](pmk::PmEvents ev) { pmk::step_match(st, S, g->ph8, g->maxPH, max_per_part, ev); }, 2);
   const bool lds = pmk::step_resolve_lds_ok(g->maxPH, max_per_part);
   c->timed_ext("resolve", 0, [&](pmk::PmEvents ev) { pmk::step_resolve(st, S, lds, ev); }, 2);
   if (c->debug_sync) {   // validate every resolution record before k_answer consumes it
@@ -2484,7 +2484,7 @@ static int group_step(StepGroup& G, const std::vector<char>& in) {
     }
 #endif
   } else {
-    c->timed_ext("hint_match", (double)nreal * G.maxPH, [&](pmk::PmEvents ev) { pmk::step_match(st, S, G.ph8, G.maxPH, ev); }, 2);
+    c->timed_ext("hint_match", (double)nreal * G.maxPH, [&](pmk::PmEvents ev) { pmk::step_match(st, S, G.ph8, G.maxPH, max_per_part, ev); }, 2);
     c->timed_ext("resolve", 0, [&](pmk::PmEvents ev) { pmk::step_resolve(st, S, lds, ev); }, 2);
   }
   if (S.nsplit > 1) {

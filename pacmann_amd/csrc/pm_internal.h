@@ -238,7 +238,8 @@ void fold_image(hipStream_t st, uint64_t* img, const uint64_t* part_rows, uint64
 // Timing events carried by a launch's own dispatch packet (null: untimed)
 struct PmEvents { hipEvent_t a = nullptr, b = nullptr; };
 // ph8: every partition's PH is a multiple of 8 (k_match_part8)
-void step_match(hipStream_t st, const PmStep& S, bool ph8, uint32_t maxPH, PmEvents ev = {});
+void step_match(hipStream_t st, const PmStep& S, bool ph8, uint32_t maxPH, uint32_t max_sub_per_part,
+                PmEvents ev = {});
 uint32_t step_match_blocks(uint32_t maxPH);   // k_match workgroups per sub-query
 void step_resolve(hipStream_t st, const PmStep& S, bool lds, PmEvents ev = {});
 // k_match_part + k_resolve fused (batched serving; descriptor already in device memory)

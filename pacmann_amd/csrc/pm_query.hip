@@ -239,10 +239,10 @@ constexpr uint32_t kMatchHints = 1024;   // hints per match workgroup (any block
 // lane t returns sub-query pb0 + t in `st` and whether it is valid in `validt`.
 __device__ __forceinline__ uint32_t predict_ing(const PmStep& S, const PmPart& P, uint32_t pb0, uint32_t pn,
                                                 uint32_t k, uint32_t chunk, uint32_t h0k, PmSub& st,
-                                                bool& validt) {
+                                                bool& validt, const PmSub* ls = nullptr) {
   const uint32_t lane = threadIdx.x & 63;
   st = PmSub{0, SUB_NONE, ~0ull};
-  if (lane < pn) st = desc_sub(S, pb0 + lane);
+  if (lane < pn) st = ls ? ls[lane] : desc_sub(S, pb0 + lane);
   validt = lane < pn && st.kind == SUB_REAL && st.idx < P.N;
   const uint32_t cht = (uint32_t)(st.idx >> P.log2CS);
   bool first = validt;
@@ -416,11 +416,11 @@ __global__ void __launch_bounds__(kBlock) k_match(PmStep S) {
 // partition (one wave each): the chunk's QueryHistogram, the predicted
 // in-chunk index and the PRF values the refreshed hints would need.
 __device__ __forceinline__ void match_part_predict(const PmStep& S, const PmPart& P, uint32_t pb0, uint32_t pn,
-                                                   uint32_t k0, uint32_t kstep) {
+                                                   uint32_t k0, uint32_t kstep, const PmSub* ls = nullptr) {
   if (pn > kSpecSubs) return;
   const uint32_t lane = threadIdx.x & 63, lg = P.log2CS;
   for (uint32_t k = k0; k < pn; k += kstep) {
-    PmSub sub = desc_sub(S, pb0 + k);
+    PmSub sub = ls ? ls[k] : desc_sub(S, pb0 + k);
     sub.kind = __builtin_amdgcn_readfirstlane(sub.kind);
     if (sub.kind != SUB_REAL) continue;
     const bool live = sub.idx < P.N;
@@ -428,7 +428,7 @@ __device__ __forceinline__ void match_part_predict(const PmStep& S, const PmPart
     const uint32_t h0k = live ? P.hist[chunk] : 0;
     PmSub st;
     bool validt;
-    const uint32_t sing = predict_ing(S, P, pb0, pn, k, chunk, h0k, st, validt);
+    const uint32_t sing = predict_ing(S, P, pb0, pn, k, chunk, h0k, st, validt, ls);
     const uint32_t cht = (uint32_t)(st.idx >> lg);
     const uint32_t pred = (live && sing < P.Qpc && chunk < P.SS) ? P.PH + chunk * P.Qpc + sing : kNone;
     uint32_t v = kSkip;
@@ -560,6 +560,13 @@ __global__ void __launch_bounds__(kBlock, PM_MATCHPART_WAVES) k_match_part(PmSte
 #ifndef PM_MATCHPART8_NW
 #define PM_MATCHPART8_NW 4
 #endif
+#ifndef PM_MATCHPART8_G
+#define PM_MATCHPART8_G 4   // sub-queries' search rows in flight together (BIGANN-100M: 4 35-38 us, 6 38-40 us)
+#endif
+#ifndef PM_MATCHPART8_WAVES
+#define PM_MATCHPART8_WAVES 1   // min waves per SIMD (launch bounds)
+#endif
+constexpr uint32_t kPart8Subs = 256;   // a partition's descriptors held in LDS (more: read in place)
 __device__ __forceinline__ uint32_t match8(uint4 v, uint32_t off) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
   uint32_t m = 0;
@@ -569,15 +576,25 @@ __device__ __forceinline__ uint32_t match8(uint4 v, uint32_t off) {
   return m;
 }
 template <int NW>
-__global__ void __launch_bounds__(64 * NW) k_match_part8(PmStep S) {
-  constexpr int G = PM_MATCHPART_G;
+__global__ void __launch_bounds__(64 * NW, PM_MATCHPART8_WAVES) k_match_part8(PmStep S) {
+  constexpr int G = PM_MATCHPART8_G;
   constexpr uint32_t kHalf = kMatchHints / 2;   // 512: the second load's hints
   static_assert(kMatchHints == 1024, "one wave x 16 hints per lane");
   const uint32_t p = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint32_t pb0 = desc_sb(S, p), pn = desc_sb(S, p + 1) - pb0;
+  // the partition's descriptors, read once per workgroup into LDS (the host
+  // copy is read over PCIe: one request per wave and descriptor took the
+  // kernel from ~25 to ~45 us at BIGANN-100M's 2,240 workgroups)
+  // (launched only when every partition has <= kPart8Subs sub-queries)
+  __shared__ uint32_t s_sb[2];
+  __shared__ PmSub s_sub[kPart8Subs];
+  if (tid < 2) s_sb[tid] = desc_sb(S, p + tid);
+  __syncthreads();
+  const uint32_t pb0 = s_sb[0], pn = min(s_sb[1] - pb0, kPart8Subs);
+  for (uint32_t i = tid; i < pn; i += 64 * NW) s_sub[i] = desc_sub(S, pb0 + i);
+  __syncthreads();
   if (!S.args_valid && blockIdx.x == 0 && S.subs != S.subs_h) {   // stage the descriptor for the later kernels
-    for (uint32_t i = tid; i < pn; i += 64 * NW) S.subs[pb0 + i] = S.subs_h[pb0 + i];
+    for (uint32_t i = tid; i < pn; i += 64 * NW) S.subs[pb0 + i] = s_sub[i];
     if (p == 0)
       for (uint32_t i = tid; i <= S.np; i += 64 * NW) S.sb[i] = S.sb_h[i];
   }
@@ -585,7 +602,7 @@ __global__ void __launch_bounds__(64 * NW) k_match_part8(PmStep S) {
   const PmPart P = S.parts[p];
   const uint32_t nb = (P.PH + kMatchHints - 1) / kMatchHints, nwg = (nb + NW - 1) / NW;
   if (blockIdx.x >= nwg) return;
-  match_part_predict(S, P, pb0, pn, blockIdx.x + nwg * wave, nwg * NW);
+  match_part_predict(S, P, pb0, pn, blockIdx.x + nwg * wave, nwg * NW, s_sub);
   const uint32_t blk = blockIdx.x * NW + wave;
   if (blk >= nb) return;   // whole wave; nothing below synchronises
   const uint32_t base = blk * kMatchHints, mask = P.CS - 1, lg = P.log2CS;
@@ -596,7 +613,7 @@ __global__ void __launch_bounds__(64 * NW) k_match_part8(PmStep S) {
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       PmSub sub{0, SUB_NONE, 0};
-      if (j0 + g < pn) sub = desc_sub(S, pb0 + j0 + g);
+      if (j0 + g < pn) sub = s_sub[j0 + g];
       kind[g] = __builtin_amdgcn_readfirstlane(sub.kind);
       const uint64_t idx = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(sub.idx >> 32)) << 32) |
                            __builtin_amdgcn_readfirstlane((uint32_t)sub.idx);
@@ -2276,14 +2293,14 @@ uint32_t step_match_blocks(uint32_t maxPH) { return cdiv(maxPH, kMatchHints); }
     if ((ev).a) hipExtLaunchKernelGGL(kern, grid, blk, 0, st, (ev).a, (ev).b, 0, __VA_ARGS__); \
     else hipLaunchKernelGGL(kern, grid, blk, 0, st, __VA_ARGS__);                             \
   } while (0)
-void step_match(hipStream_t st, const PmStep& S, bool ph8, uint32_t maxPH, PmEvents ev) {
+void step_match(hipStream_t st, const PmStep& S, bool ph8, uint32_t maxPH, uint32_t max_sub_per_part, PmEvents ev) {
   // many partitions with several sub-queries each (batched serving): one
   // workgroup per (partition, hint block); otherwise one per (sub-query, block)
   static const int mode = [] { const char* e = getenv("PM_MATCH_PART"); return e ? atoi(e) : -1; }();
   const bool part = mode == 1 || (mode == -1 && S.np >= 128 && S.nsub >= 4 * S.np);
   // PM_MATCH_PART8=0: the LDS-merged form for every PH
   static const int v8 = [] { const char* e = getenv("PM_MATCH_PART8"); return e ? atoi(e) : 1; }();
-  if (part && ph8 && v8)
+  if (part && ph8 && v8 && max_sub_per_part <= kPart8Subs)
     PM_LAUNCH(ev, k_match_part8<PM_MATCHPART8_NW>, dim3(cdiv(step_match_blocks(maxPH), PM_MATCHPART8_NW), S.np),
               dim3(64 * PM_MATCHPART8_NW), st, S);
   else if (part)
