@@ -400,7 +400,7 @@ def bigann_search(key, name, n_entries, layout, rank, ws, local, dist, comb_grou
     nq = BIG_SEARCH_WARMUP + BIG_SEARCH_Q
     qs = np.random.default_rng(63).random((S, nq, BIG_DIM), dtype=np.float32)   # genRandomMatrix queries
     comb = RecordCombiner(group=comb_group, device=local) if combine else None
-    groups = min(BIG_GROUPS, S)
+    groups = min(args.big_groups or BIG_GROUPS, S)
     pm.search_loop_sharded(sess, qs[:, :BIG_SEARCH_WARMUP], K_TOP, STEP, PARALLEL, groups, args.threads,
                            combiner=comb, model_peers=modelled)
     for c in ctxs:
@@ -710,6 +710,7 @@ def main():
     ap.add_argument("--no-bigann", action="store_true", help="skip the BIGANN-100M / 1B batch-PIR blocks")
     ap.add_argument("--no-config0", action="store_true", help="skip the InnerProduct scan block")
     ap.add_argument("--big-sessions", type=int, default=0, help="cap on the BIGANN blocks' sessions per GPU")
+    ap.add_argument("--big-groups", type=int, default=0, help="lock-step teams of the BIGANN blocks (0: BIG_GROUPS)")
     ap.add_argument("--combine", choices=["rccl", "gloo"], default="rccl",
                     help="collective of the sharded BIGANN rounds (gloo: host tensors, e.g. ranks sharing one GPU)")
     ap.add_argument("--no-kernel-timing", action="store_true",

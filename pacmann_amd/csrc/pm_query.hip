@@ -2300,7 +2300,10 @@ void step_match(hipStream_t st, const PmStep& S, bool ph8, uint32_t maxPH, uint3
   const bool part = mode == 1 || (mode == -1 && S.np >= 128 && S.nsub >= 4 * S.np);
   // PM_MATCH_PART8=0: the LDS-merged form for every PH
   static const int v8 = [] { const char* e = getenv("PM_MATCH_PART8"); return e ? atoi(e) : 1; }();
-  if (part && ph8 && v8 && max_sub_per_part <= kPart8Subs)
+  // k_match_part8 from 64 partitions with 2+ sub-queries each (BIGANN teams of
+  // 4-6 sessions: k_match's workgroup per (sub-query, block) took 85 us there)
+  const bool part8 = ph8 && v8 && max_sub_per_part <= kPart8Subs && (part || (mode == -1 && S.np >= 64 && S.nsub >= 2 * S.np));
+  if (part8)
     PM_LAUNCH(ev, k_match_part8<PM_MATCHPART8_NW>, dim3(cdiv(step_match_blocks(maxPH), PM_MATCHPART8_NW), S.np),
               dim3(64 * PM_MATCHPART8_NW), st, S);
   else if (part)
