@@ -426,7 +426,8 @@ def bigann_search(key, name, n_entries, layout, rank, ws, local, dist, comb_grou
     kt = {k: tsum(k) for k in ("hint_match", "resolve", "match_resolve", "gather", "answer", "pack_records",
                                 "synth_records", "combine", "prep_offsets", "prep_fold", "prep_repl", "l2_rows")}
     ht = {k: tsum(k) for k in ("host_combine", "host_combine_turn", "host_step_wait", "host_batch_query",
-                                "host_gvi_parse")}
+                                "host_gvi_parse", "host_step_launch", "host_step_post", "host_knn_update",
+                                "host_knn_batch", "host_knn_init")}
     rounds = BIG_SEARCH_Q * STEP * groups   # shared steps in the timed region (every team)
     same = None if modelled else 1   # modelled layouts: each rank serves another shard (its own failures)
     if dist and not modelled:   # every rank holds the same answers (the combined records drive identical searches)
@@ -498,6 +499,7 @@ def bigann_search(key, name, n_entries, layout, rank, ws, local, dist, comb_grou
                     "turn_wait_ms_per_round": round(ht["host_combine_turn"][1] / max(1, ht["host_combine_turn"][0]), 5),
                     "note": "device time of the in-place all-reduce on the team stream (events around the "
                             "combine), per shared step; host_ms is the callback's wall time"},
+        "host_ms_per_round": {k[5:]: round(v[1] / (BIG_SEARCH_Q * STEP), 4) for k, v in ht.items() if v[1]},
         "pir_scan_fold": fold, "pir_scan_answer": ans_roof,
         "roofline_prf": prf_roofline(kprep["prep_offsets"], "k_prep_offsets of one client's preprocessing"),
         "check": {"ids_fetched": tot, "ids_answered": succ, "ranks_identical": None if same is None else bool(same)},
