@@ -61,7 +61,9 @@ int         pm_ctx_mem_info(pm_ctx* ctx, uint64_t* free_bytes, uint64_t* total_b
  * times the kernels of every online step ("step", "hint_match", "resolve",
  * "gather", "answer") with events carried in their own dispatch packets
  * (hipExtLaunchKernelGGL); steps are not synchronised for it (the events are
- * read by pm_timing_get).  Host wall-clock
+ * read by pm_timing_get).  Level 3 is level 2 with the kernels of a lock-step
+ * team's shared steps timed on every 7th step of its stream only (the serving
+ * bench: a sample, at a fraction of the events' cost).  Host wall-clock
  * accumulators are always on: "host_step_launch", "host_step_wait",
  * "host_step_post", "host_batch_query", "host_gvi_parse", "host_search_knn",
  * "host_knn_init", "host_knn_batch", "host_knn_update", "host_knn_final". */

@@ -157,7 +157,11 @@ struct TimedLaunch { std::string name; hipEvent_t a, b; double bytes; };
 struct pm_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  int timing = 0;   // 0 off, 1 preprocessing / leaf kernels, 2 also the per-step kernels
+  int timing = 0;   // 0 off, 1 preprocessing / leaf kernels, 2 also the per-step kernels,
+                    // 3 as 2 with the shared steps' kernels timed on every kSampleSteps-th step
+  // timing 3: whether the current shared step's kernels carry events (group_step)
+  bool sample_now = true;
+  uint64_t sample_ctr = 0;
   bool no_fuse = false;      // PM_NO_FUSE=1: the three step kernels even when k_step fits
   bool no_split = false;     // PM_NO_SPLIT=1: k_answer gathers wide sets itself (no k_gather)
   bool no_guess = false;
@@ -232,7 +236,7 @@ struct pm_ctx {
   template <class F> void timed_ext(const char* name, double bytes, F&& f, int level) {
     last_kernel = name;
     if (debug_sync) { timed(name, bytes, [&] { f(pmk::PmEvents{}); }, level); return; }
-    if (timing < level) { f(pmk::PmEvents{}); return; }
+    if (timing < level || (timing == 3 && level == 2 && !sample_now)) { f(pmk::PmEvents{}); return; }
     TimedLaunch t{name, ev(), ev(), bytes};
     f(pmk::PmEvents{t.a, t.b});
     launches.push_back(t);
@@ -2269,6 +2273,23 @@ struct StepGroup {
   uint64_t seq = 0;   // the last shared step's completion sequence number (pm_ctx::record_done)
   std::vector<PmSub> subs;
   std::vector<uint32_t> sb, base;
+  uint32_t nsub = 0;           // the last shared step's sub-queries
+  // Descriptor staging (pooled serving, group_stage_session): each session's
+  // task writes its next sub-queries into its own slot of stage_h (stride
+  // PmSubs each), so the launching worker only compacts the slots instead of
+  // reading every session's sub-queries out of other cores' caches.
+  struct alignas(64) SessStage {
+    uint64_t step = ~0ull;   // the shared step (G.nstep) the slot was written for
+    uint32_t n = 0, nreal = 0, maxpp = 0, live = 0;
+    double bytes = 0;
+    bool ok = false;
+    std::vector<uint32_t> pc;   // [Pl] sub-queries per partition
+  };
+  bool stage_on = false;
+  uint32_t stride = 0;
+  uint64_t nstep = 0;
+  HostBuf stage_h;
+  std::vector<SessStage> stg;
   std::vector<uint64_t> gen;   // each session's Engine::prep_gen at the last upload of its parts
   std::vector<Engine*> es;     // the clients (batch PIR engines) sharing the steps
   std::vector<const float*> qv;   // each client's search query on the device (null: no distances)
@@ -2343,38 +2364,117 @@ static int group_init(StepGroup& G, pm_ctx* c) {
   return group_upload_parts(G);
 }
 
+// Session s's sub-queries for the next shared step into its stage slot (the
+// session's own task, after gvi_pre: the data is in this core's cache).  A
+// session with more than `stride` sub-queries leaves its slot invalid and the
+// step is built the general way (group_step raises the stride).
+static void group_stage_session(StepGroup& G, uint32_t s) {
+  StepGroup::SessStage& ss = G.stg[s];
+  ss.ok = false;
+  if (!G.stage_on || !G.stride) return;
+  const Engine* e = G.es[s];
+  PmSub* dst = G.stage_h.as<PmSub>() + (uint64_t)s * G.stride;
+  uint32_t n = 0, nreal = 0, maxpp = 0, live = 0;
+  double bytes = 0;
+  ss.pc.resize(G.Pl);
+  for (uint32_t li = 0; li < G.Pl; ++li) {
+    const uint32_t p = G.lp[li], a = e->sb[p], b = e->sb[p + 1];
+    if (n + (b - a) > G.stride) { ss.n = n + (b - a); return; }
+    const double ab = answer_bytes(e->parts[p].d, G.E);
+    for (uint32_t j = a; j < b; ++j) {
+      PmSub x = e->subs[j];
+      x.part = s * G.Pl + li;
+      dst[n++] = x;
+      if (x.kind == SUB_REAL || x.kind == SUB_DUMMY) bytes += ab;
+      nreal += x.kind == SUB_REAL;
+    }
+    ss.pc[li] = b - a;
+    maxpp = std::max(maxpp, b - a);
+    live += b > a;
+  }
+  ss.n = n; ss.nreal = nreal; ss.maxpp = maxpp; ss.live = live; ss.bytes = bytes;
+  ss.step = G.nstep;
+  ss.ok = true;
+}
+
 // One shared step over the clients whose sub-queries are ready (in[s]).
 static int group_step(StepGroup& G, const std::vector<char>& in) {
   pm_ctx* c = G.c;
   hipStream_t st = c->stream;
+  // timing 3: events on every kSampleSteps-th shared step of this stream (7: coprime
+  // with the 20 rounds of a search, so every round position is sampled); the
+  // events' dispatch-packet and completion handling cost ~5 % of the serving
+  // rate when every launch carries them
+  constexpr uint64_t kSampleSteps = 7;
+  c->sample_now = c->sample_ctr++ % kSampleSteps == 0;
   bool stale = false;   // a client re-preprocessed since its parts were copied
   for (uint32_t s = 0; s < G.S; ++s) stale |= G.es[s]->prep_gen != G.gen[s];
   if (stale) CHK(group_upload_parts(G));
-  G.subs.clear();
   G.sb.assign(1, 0);
   G.base.assign(G.S, 0);
-  uint32_t max_per_part = 0, np_live = 0;
+  uint32_t max_per_part = 0, np_live = 0, nreal = 0, nsub = 0;
   double ans_bytes = 0;
-  for (uint32_t s = 0; s < G.S; ++s) {
-    Engine* e = G.es[s];
-    G.base[s] = (uint32_t)G.subs.size();
-    for (uint32_t li = 0; li < G.Pl; ++li) {
-      const uint32_t p = G.lp[li];
-      if (in[s]) {
-        for (uint32_t j = e->sb[p]; j < e->sb[p + 1]; ++j) {
-          PmSub x = e->subs[j];
-          x.part = s * G.Pl + li;
-          G.subs.push_back(x);
-          if (x.kind == SUB_REAL || x.kind == SUB_DUMMY) ans_bytes += answer_bytes(e->parts[p].d, G.E);
-        }
-        const uint32_t n = e->sb[p + 1] - e->sb[p];
-        max_per_part = std::max(max_per_part, n);
-        np_live += n > 0;
-      }
-      G.sb.push_back((uint32_t)G.subs.size());
-    }
+  const uint32_t np = G.S * G.Pl;
+  // the sessions' staged slots (group_stage_session), if every one is current
+  bool staged = G.stage_on && G.stride > 0 && G.stg.size() == G.S;
+  uint32_t need = 0;   // the largest session's sub-queries (the next stride)
+  for (uint32_t s = 0; staged && s < G.S; ++s) {
+    const StepGroup::SessStage& ss = G.stg[s];
+    if (!in[s]) continue;
+    need = std::max(need, ss.n);
+    if (!ss.ok || ss.step != G.nstep) staged = false;
+    nsub += ss.n;
   }
-  const uint32_t nsub = (uint32_t)G.subs.size(), np = G.S * G.Pl;
+  if (staged && nsub <= kArgSubs && np <= kArgParts) staged = false;   // kernel-argument descriptors: the general way
+  G.nstep++;
+  PmSub* const stage = G.stage_h.as<PmSub>();
+  if (staged) {   // compact the slots in place; the partition offsets follow the subs
+    uint32_t off = 0;
+    for (uint32_t s = 0; s < G.S; ++s) {
+      const StepGroup::SessStage& ss = G.stg[s];
+      G.base[s] = off;
+      const uint32_t n = in[s] ? ss.n : 0;
+      if (n && off != s * G.stride) memmove(stage + off, stage + (uint64_t)s * G.stride, (size_t)n * sizeof(PmSub));
+      for (uint32_t li = 0; li < G.Pl; ++li) G.sb.push_back(G.sb.back() + (in[s] ? ss.pc[li] : 0));
+      if (in[s]) {
+        max_per_part = std::max(max_per_part, ss.maxpp);
+        np_live += ss.live;
+        ans_bytes += ss.bytes;
+        nreal += ss.nreal;
+      }
+      off += n;
+    }
+  } else {
+    G.subs.clear();
+    for (uint32_t s = 0; s < G.S; ++s) {
+      Engine* e = G.es[s];
+      G.base[s] = (uint32_t)G.subs.size();
+      for (uint32_t li = 0; li < G.Pl; ++li) {
+        const uint32_t p = G.lp[li];
+        if (in[s]) {
+          for (uint32_t j = e->sb[p]; j < e->sb[p + 1]; ++j) {
+            PmSub x = e->subs[j];
+            x.part = s * G.Pl + li;
+            G.subs.push_back(x);
+            if (x.kind == SUB_REAL || x.kind == SUB_DUMMY) ans_bytes += answer_bytes(e->parts[p].d, G.E);
+            nreal += x.kind == SUB_REAL;
+          }
+          const uint32_t n = e->sb[p + 1] - e->sb[p];
+          max_per_part = std::max(max_per_part, n);
+          np_live += n > 0;
+        }
+        G.sb.push_back((uint32_t)G.subs.size());
+      }
+      need = std::max(need, in[s] ? (uint32_t)G.subs.size() - G.base[s] : 0u);
+    }
+    nsub = (uint32_t)G.subs.size();
+  }
+  G.nsub = nsub;
+  if (G.stage_on && need > G.stride) {   // slots for the next step's staging (the tasks write them after this step)
+    G.stride = (need + 7) & ~7u;
+    CHK(G.stage_h.reserve((size_t)G.S * G.stride * sizeof(PmSub) + (size_t)(np + 1) * 4));
+    if (G.stg.size() != G.S) G.stg.resize(G.S);
+  }
   if (nsub == 0) return 0;
   const uint32_t words = (G.maxPH + 63) / 64, cblk = pmk::step_match_blocks(G.maxPH);
   CHK(G.subs_d.reserve(nsub * sizeof(PmSub)));
@@ -2386,11 +2486,17 @@ static int group_step(StepGroup& G, const std::vector<char>& in) {
   CHK(G.res_d.reserve(nsub * sizeof(PmRes)));
   CHK(G.ans.reserve((uint64_t)nsub * G.E * 8));
   const size_t dsub = nsub * sizeof(PmSub);
-  CHK(G.desc_h.reserve(dsub + (np + 1) * 4));
   if (!G.comb) CHK(G.out_h.reserve(nsub * sizeof(PmOutHdr) + (size_t)nsub * G.E * 8));
-  char* dh = G.desc_h.as<char>();
-  memcpy(dh, G.subs.data(), dsub);
-  memcpy(dh + dsub, G.sb.data(), (np + 1) * 4);
+  char* dh;
+  if (staged) {   // the compacted slots are the descriptor; the offsets right after them
+    dh = G.stage_h.as<char>();
+    memcpy(dh + dsub, G.sb.data(), (np + 1) * 4);
+  } else {
+    CHK(G.desc_h.reserve(dsub + (np + 1) * 4));
+    dh = G.desc_h.as<char>();
+    memcpy(dh, G.subs.data(), dsub);
+    memcpy(dh + dsub, G.sb.data(), (np + 1) * 4);
+  }
   PmStep S{};
   S.parts = G.parts_d.as<PmPart>();
   S.subs_h = (const PmSub*)dh;
@@ -2431,7 +2537,7 @@ static int group_step(StepGroup& G, const std::vector<char>& in) {
   S.words = words; S.E = G.E; S.dim = G.dim; S.nsub = nsub; S.np = np;
   S.np_live = np_live;
   S.args_valid = (nsub <= kArgSubs && np <= kArgParts) ? 1u : 0u;
-  if (S.args_valid) {
+  if (S.args_valid) {   // (never the staged form)
     memcpy(S.subs_a, G.subs.data(), dsub);
     memcpy(S.sb_a, G.sb.data(), (np + 1) * 4);
   }
@@ -2445,8 +2551,6 @@ static int group_step(StepGroup& G, const std::vector<char>& in) {
     S.rows_partial = G.rows_partial && !c->verify_rows && !c->debug_cache ? 1u : 0u;
   }
   auto t0 = Clock::now();
-  uint32_t nreal = 0;
-  for (auto& x : G.subs) nreal += x.kind == SUB_REAL;
   const bool lds = pmk::step_resolve_lds_ok(G.maxPH, max_per_part);
   S.nsplit = c->no_split ? 1 : pmk::step_gather_split(G.maxSS, nsub);
   if (pmk::step_qset_ok(S, lds, G.ph8, G.maxPH, max_per_part, G.maxSS)) {
@@ -2532,7 +2636,7 @@ static int group_collect(StepGroup& G, uint32_t s) {
   Engine* e = G.es[s];
   const uint32_t n = (uint32_t)e->subs.size();
   PmOutHdr* hdr = G.out_h.as<PmOutHdr>();
-  uint64_t* rows = (uint64_t*)(G.out_h.as<char>() + G.subs.size() * sizeof(PmOutHdr));
+  uint64_t* rows = (uint64_t*)(G.out_h.as<char>() + (size_t)G.nsub * sizeof(PmOutHdr));
   auto t_wait = Clock::now();
   CHK(wait_step(e->ctx, hdr + G.base[s], n, G.token, (const char*)(rows + (uint64_t)G.base[s] * G.E),
                 (size_t)G.E * 8, (size_t)G.pf_w0 * 8, (size_t)(G.pf_w1 - G.pf_w0) * 8, G.seq, G.c));
@@ -2687,7 +2791,7 @@ static int gvi_pre_sharded(pm_graph* g, StepGroup& G, uint32_t s, bool* fast) {
 static int group_exchange(StepGroup& G, const std::vector<char>& in) {
   pm_ctx* c = G.c;
   hipStream_t st = c->stream;
-  const uint32_t nrec = G.S * G.npos, nsub = (uint32_t)G.subs.size();
+  const uint32_t nrec = G.S * G.npos, nsub = G.nsub;
   const uint64_t nw = (uint64_t)nrec * G.W;
   int32_t* map = G.map_h.as<int32_t>();
   for (uint32_t s = 0; s < G.S; ++s)   // client-local sub-query indices -> the shared step's
@@ -3107,6 +3211,9 @@ static int run_batched_pool(pm_graph** gs, uint32_t S, const float* queries, uin
     t.lane.reset(new std::atomic<uint32_t>[T]);
     for (uint32_t w = 0; w < T; ++w) t.lane[w].store(0);
     CHK(team_init(t.G, t.gs, t.S));
+    static const int stage = [] { const char* e = getenv("PM_DESC_STAGE"); return e ? atoi(e) : 1; }();
+    t.G.stage_on = stage != 0;
+    t.G.stg.resize(t.S);
   }
   const uint32_t dim = (uint32_t)gs[0]->dim;
   TeamTrace tr;
@@ -3176,6 +3283,7 @@ static int run_batched_pool(pm_graph** gs, uint32_t S, const float* queries, uin
     bool f = false;
     CHK(gvi_pre(g, true, &f));
     t.fast[i] = f;
+    if (f) group_stage_session(t.G, i);
     return 0;
   };
   // the worker that completed the phase's last session moves the team on
