@@ -2388,8 +2388,12 @@ void step_answer(hipStream_t st, const PmStep& S, uint32_t maxSS, PmEvents ev) {
 }
 uint32_t step_gather_split(uint32_t maxSS, uint32_t nsub) {
   if (maxSS < 256 || nsub == 0) return 1;
-  // >= 48 rows per workgroup, about 2,048 workgroups in all, at most 64 per sub-query
-  uint32_t n = std::min(cdiv(maxSS, 48), cdiv(2048, nsub));
+  static const int forced = [] { const char* e = getenv("PM_GATHER_SPLIT"); return e ? atoi(e) : 0; }();
+  // >= 48 rows per workgroup, about 4,096 workgroups in all (two rounds of the
+  // GPU's 2,048 resident 256-thread workgroups; BIGANN-100M's 960 sub-queries:
+  // 5 ranges, 96-104 us, vs 3 ranges at ~2,048 workgroups, 124-143 us), at most
+  // 64 per sub-query; PM_GATHER_SPLIT=n forces n
+  uint32_t n = forced > 0 ? (uint32_t)forced : std::min(cdiv(maxSS, 48), cdiv(4096, nsub));
   n = std::max(1u, std::min(n, 64u));
   return n > 1 ? std::max(n, cdiv(maxSS, kGatherMaxRange)) : 1u;   // a range's set fits k_gather's LDS
 }
