@@ -68,6 +68,14 @@ int         pm_ctx_mem_info(pm_ctx* ctx, uint64_t* free_bytes, uint64_t* total_b
  * "host_step_post", "host_batch_query", "host_gvi_parse", "host_search_knn",
  * "host_knn_init", "host_knn_batch", "host_knn_update", "host_knn_final". */
 int pm_timing_enable(pm_ctx* ctx, int level);
+/* Process-wide choice among equivalent kernel paths (no reference counterpart:
+ * the same results by every path; tests drive each one).  "match_part": the
+ * hint search per (partition, block) instead of per (sub-query, block), -1
+ * automatic / 0 / 1; "match_part8": its one-wave-per-block form where PH % 8 ==
+ * 0, 0 / 1; "match_resolve": k_match_resolve* for search-sized steps, 0 / 1 /
+ * 2 (the general form).  -2 restores the environment's choice (PM_MATCH_PART,
+ * PM_MATCH_PART8, PM_MATCH_RESOLVE).  PM_EINVAL for an unknown name. */
+int pm_set_option(const char* name, int value);
 int pm_timing_reset(pm_ctx* ctx);
 int pm_timing_get(pm_ctx* ctx, const char* kernel, uint64_t* launches, double* total_ms,
                   double* alg_bytes);

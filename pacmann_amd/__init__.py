@@ -70,6 +70,7 @@ SIGNATURES = {
     "pm_ctx_sync": (C.c_int, [vp]),
     "pm_ctx_mem_info": (C.c_int, [vp, u64p, u64p]),
     "pm_timing_enable": (C.c_int, [vp, C.c_int]),
+    "pm_set_option": (C.c_int, [C.c_char_p, C.c_int]),
     "pm_timing_reset": (C.c_int, [vp]),
     "pm_timing_get": (C.c_int, [vp, C.c_char_p, u64p, C.POINTER(dbl), C.POINTER(dbl)]),
     "pm_expand_key": (C.c_int, [u8p, u32p]),
@@ -256,6 +257,12 @@ def prf_batch(rk: np.ndarray, tags, xs, ctx: Context | None = None) -> np.ndarra
     out = np.zeros(len(t), dtype=np.uint64)
     _check(lib().pm_prf_batch(ctx.h, _p(rk, u32p), _p(t, u64p), _p(x, u64p), len(t), _p(out, u64p)))
     return out
+
+
+def set_option(name: str, value: int) -> None:
+    """pm_set_option: choose among equivalent kernel paths process-wide
+    ("match_part", "match_part8", "match_resolve"); -2 restores the default."""
+    _check(lib().pm_set_option(name.encode(), int(value)))
 
 
 def l2_batch(query, rows, ctx: Context | None = None) -> np.ndarray:

@@ -305,6 +305,11 @@ extern "C" int pm_ctx_mem_info(pm_ctx* c, uint64_t* free_b, uint64_t* total_b) {
   return 0;
 }
 extern "C" int pm_timing_enable(pm_ctx* c, int on) { c->timing = on; return 0; }
+extern "C" int pm_set_option(const char* name, int value) {
+  if (!name) return fail(PM_EINVAL, "NULL argument");
+  if (pmk::set_option(name, value)) return fail(PM_EINVAL, std::string("unknown option ") + name);
+  return 0;
+}
 extern "C" int pm_timing_reset(pm_ctx* c) {
   HIPCHK(hipStreamSynchronize(c->stream));
   for (auto& t : c->launches) { c->pool.push_back(t.a); c->pool.push_back(t.b); }

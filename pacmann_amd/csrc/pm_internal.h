@@ -237,6 +237,11 @@ uint64_t fold_image_words(uint32_t SS, uint32_t E);
 void fold_image(hipStream_t st, uint64_t* img, const uint64_t* part_rows, uint64_t N, uint32_t SS, uint32_t E);
 // Timing events carried by a launch's own dispatch packet (null: untimed)
 struct PmEvents { hipEvent_t a = nullptr, b = nullptr; };
+// pm_set_option: the hint-search path selectors ("match_part" -1 auto / 0 / 1,
+// "match_part8" 0 / 1, "match_resolve" 0 / 1 / 2); -2 restores the environment's
+// choice (PM_MATCH_PART, PM_MATCH_PART8, PM_MATCH_RESOLVE).  Returns -1 for an
+// unknown name.
+int set_option(const char* name, int value);
 // ph8: every partition's PH is a multiple of 8 (k_match_part8)
 void step_match(hipStream_t st, const PmStep& S, bool ph8, uint32_t maxPH, uint32_t max_sub_per_part,
                 PmEvents ev = {});

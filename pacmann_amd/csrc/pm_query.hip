@@ -30,7 +30,10 @@
 
 #include "pm_aes.h"
 #include "pm_internal.h"
+#include <atomic>
+#include <climits>
 #include <cstdlib>
+#include <cstring>
 
 namespace pm {
 
@@ -2285,6 +2288,26 @@ __global__ void __launch_bounds__(kStepBlock) k_step(PmStep S) {
 
 namespace pmk {
 static inline unsigned cdiv(uint64_t a, uint64_t b) { return (unsigned)((a + b - 1) / b); }
+// Path selectors: the environment's choice (read once), unless pm_set_option
+// overrides it (the tests drive every hint-search form through the same steps).
+// value -2 (kOptUnset here) restores the environment's choice.
+constexpr int kOptUnset = INT32_MIN;
+static int env_int(const char* name, int def) { const char* e = getenv(name); return e ? atoi(e) : def; }
+static const int env_match_part = env_int("PM_MATCH_PART", -1), env_match_part8 = env_int("PM_MATCH_PART8", 1),
+                 env_match_resolve = env_int("PM_MATCH_RESOLVE", 1);
+static std::atomic<int> ov_match_part{kOptUnset}, ov_match_part8{kOptUnset}, ov_match_resolve{kOptUnset};
+static int opt(const std::atomic<int>& ov, int env) {
+  const int v = ov.load(std::memory_order_relaxed);
+  return v != kOptUnset ? v : env;
+}
+int set_option(const char* name, int value) {
+  std::atomic<int>* o = !strcmp(name, "match_part") ? &ov_match_part
+                      : !strcmp(name, "match_part8") ? &ov_match_part8
+                      : !strcmp(name, "match_resolve") ? &ov_match_resolve : nullptr;
+  if (!o) return -1;
+  o->store(value <= -2 ? kOptUnset : value, std::memory_order_relaxed);
+  return 0;
+}
 uint32_t step_match_blocks(uint32_t maxPH) { return cdiv(maxPH, kMatchHints); }
 // With events, the launch carries them in its own dispatch packet
 // (hipExtLaunchKernelGGL): the kernel's execution time as the profiler sees it.
@@ -2296,10 +2319,10 @@ uint32_t step_match_blocks(uint32_t maxPH) { return cdiv(maxPH, kMatchHints); }
 void step_match(hipStream_t st, const PmStep& S, bool ph8, uint32_t maxPH, uint32_t max_sub_per_part, PmEvents ev) {
   // many partitions with several sub-queries each (batched serving): one
   // workgroup per (partition, hint block); otherwise one per (sub-query, block)
-  static const int mode = [] { const char* e = getenv("PM_MATCH_PART"); return e ? atoi(e) : -1; }();
+  const int mode = opt(ov_match_part, env_match_part);
   const bool part = mode == 1 || (mode == -1 && S.np >= 128 && S.nsub >= 4 * S.np);
   // PM_MATCH_PART8=0: the LDS-merged form for every PH
-  static const int v8 = [] { const char* e = getenv("PM_MATCH_PART8"); return e ? atoi(e) : 1; }();
+  const int v8 = opt(ov_match_part8, env_match_part8);
   // k_match_part8 from 64 partitions with 2+ sub-queries each (BIGANN teams of
   // 4-6 sessions: k_match's workgroup per (sub-query, block) took 85 us there)
   const bool part8 = ph8 && v8 && max_sub_per_part <= kPart8Subs && (part || (mode == -1 && S.np >= 64 && S.nsub >= 2 * S.np));
@@ -2312,7 +2335,7 @@ void step_match(hipStream_t st, const PmStep& S, bool ph8, uint32_t maxPH, uint3
     PM_LAUNCH(ev, k_match, dim3(step_match_blocks(maxPH), S.nsub), dim3(kBlock), st, S);
 }
 bool step_match_resolve_ok(const PmStep& S, bool lds) {
-  static const int mode = [] { const char* e = getenv("PM_MATCH_RESOLVE"); return e ? atoi(e) : 1; }();
+  const int mode = opt(ov_match_resolve, env_match_resolve);
   // one workgroup per partition matches every hint of it: search-sized hint
   // counts only (PH <= 16,384; BIGANN's 57,344 / 114,688 hints per partition
   // go to k_match_part's workgroup per (partition, hint block) instead)
@@ -2321,7 +2344,7 @@ bool step_match_resolve_ok(const PmStep& S, bool lds) {
 }
 // k_match_resolve_s serves the step (its resolvers do not count in: PmStep::np_live = 0)
 bool step_match_resolve_small(bool ph8, uint32_t maxPH, uint32_t max_sub_per_part) {
-  static const int mode = [] { const char* e = getenv("PM_MATCH_RESOLVE"); return e ? atoi(e) : 1; }();
+  const int mode = opt(ov_match_resolve, env_match_resolve);
   return mode == 1 && max_sub_per_part <= kSpecSubs && ph8 && maxPH <= 16u * kResolveBlockG;
 }
 void step_match_resolve(hipStream_t st, const PmStep& S, bool ph8, uint32_t maxPH, uint32_t max_sub_per_part,
@@ -2348,7 +2371,7 @@ void step_match_resolve(hipStream_t st, const PmStep& S, bool ph8, uint32_t maxP
 }
 bool step_qset_ok(const PmStep& S, bool lds, bool ph8, uint32_t maxPH, uint32_t max_sub_per_part,
                   uint32_t maxSS) {
-  static const int mode = [] { const char* e = getenv("PM_MATCH_RESOLVE"); return e ? atoi(e) : 1; }();
+  const int mode = opt(ov_match_resolve, env_match_resolve);
   static const int qs = [] { const char* e = getenv("PM_QSET"); return e ? atoi(e) : 1; }();
   return qs && mode == 1 && step_match_resolve_ok(S, lds) && max_sub_per_part <= kSpecSubs && ph8 &&
          maxPH <= 16u * kResolveBlockG && maxSS <= kSmallSS && S.nsplit <= 1;

@@ -497,6 +497,63 @@ def test_batch_pir_group(ctx, oracle):
         assert c.stats()["PrepCount"] > 1
 
 
+@pytest.mark.parametrize("opts", [
+    {"match_resolve": 0, "match_part": 1, "match_part8": 1},   # k_match_part8 -> k_resolve
+    {"match_resolve": 0, "match_part": 1, "match_part8": 0},   # k_match_part (LDS-merged) -> k_resolve
+    {"match_resolve": 0, "match_part": 0},                      # k_match per (sub-query, block) -> k_resolve
+], ids=["part8", "part", "per_subquery"])
+def test_batch_pir_group_hint_search_paths(ctx, oracle, opts):
+    """Every hint-search form (pm_set_option) answers a group's batches exactly
+    as the oracle: five clients, PH 1,792 (one full and one partial 1,024-hint
+    block; PH % 8 == 0 so k_match_part8 applies), repeated ids, through the
+    batch layer's re-preprocessing; entries, flags and counters compared."""
+    import pacmann_amd as pm
+    N, E, B = 30_000, 8, 8
+    db = rand_db(N, E, 93)
+    try:
+        for k, v in opts.items():
+            pm.set_option(k, v)
+        server = pm.SimpleBatchPianoPIR(N, E * 8, B, db, 8, seed=SEED, ctx=ctx)
+        server.Preprocessing()
+        assert server.SubConfig(0)["PrimaryHintNum"] == 1792
+        seeds = [SEED, 21, 22, 23, 24]
+        clients = [server] + [server.Client(sd, pm.Context(0)) for sd in seeds[1:]]
+        for c in clients[1:]:
+            c.Preprocessing()
+        grp = pm.BatchPIRGroup(clients)
+        ors = [oracle.SimpleBatchPianoPIR(N, E * 8, B, db, 8, seed=sd) for sd in seeds]
+        for o in ors:
+            o.Preprocessing()
+        rng = np.random.default_rng(23)
+        maxq = server.SubConfig(0)["MaxQueryNum"]
+        ctx.timing_reset()
+        ctx.timing(2)   # the shared steps run on the first client's context: which kernels ran
+        for b in range(int(maxq // 3) + 3):
+            q = rng.integers(0, N, size=(len(clients), 3 * B), dtype=np.uint64)
+            q[:, 5] = q[:, 2]
+            out, ok = grp.QueryWithMask(q)
+            for i, o in enumerate(ors):
+                want, _ = o.Query(q[i])
+                assert np.array_equal(out[i], want), (b, i)
+        ctx.sync()
+        ctx.timing(False)
+        assert ctx.timing_get("hint_match")[0] > 0 and ctx.timing_get("resolve")[0] > 0
+        for c, o in zip(clients, ors):
+            for k in ("FinishedBatchNum", "QueriesMadeInPartition", "PrepCount"):
+                assert c.stats()[k] == o.stats()[k], k
+            assert c.stats()["PrepCount"] > 1
+    finally:
+        ctx.timing(False)
+        for k in ("match_part", "match_part8", "match_resolve"):
+            pm.set_option(k, -2)
+
+
+def test_set_option_rejects_unknown():
+    import pacmann_amd as pm
+    with pytest.raises(RuntimeError, match="unknown option"):
+        pm.set_option("no_such_path", 1)
+
+
 def test_batch_pir_group_rejects(ctx):
     """pm_batchpir_group_create refuses clients of different servers and a
     client listed twice; the ids must hold one row per client."""
