@@ -644,6 +644,9 @@ static int upload_parts(Engine* g) {
 // 21 ms for 256 SIFT1M clients).  The stage is rewritten only by this
 // client's next preprocessing, after that synchronisation.
 static int upload_parts_async(Engine* g, hipStream_t st) {
+  // the parts are read by kernels on the client's own stream too: anything still
+  // queued there finishes first (idle in batched serving: no wait)
+  if (g->ctx->stream != st && hipStreamQuery(g->ctx->stream) != hipSuccess) HIPCHK(hipStreamSynchronize(g->ctx->stream));
   const size_t no = g->owned_list.size();
   CHK(g->parts_stage.reserve((g->P + no) * sizeof(PmPart)));
   PmPart* h = g->parts_stage.as<PmPart>();
