@@ -585,10 +585,9 @@ __global__ void __launch_bounds__(64 * NW, PM_MATCHPART8_WAVES) k_match_part8(Pm
   static_assert(kMatchHints == 1024, "one wave x 16 hints per lane");
   const uint32_t p = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // the partition's descriptors, read once per workgroup into LDS (the host
-  // copy is read over PCIe: one request per wave and descriptor took the
-  // kernel from ~25 to ~45 us at BIGANN-100M's 2,240 workgroups)
-  // (launched only when every partition has <= kPart8Subs sub-queries)
+  // the partition's descriptors, read once per workgroup into LDS instead of
+  // once per wave and sub-query (BIGANN-100M: 35-38 vs 40-42 us per team
+  // step); launched only when every partition has <= kPart8Subs sub-queries
   __shared__ uint32_t s_sb[2];
   __shared__ PmSub s_sub[kPart8Subs];
   if (tid < 2) s_sb[tid] = desc_sb(S, p + tid);
