@@ -153,6 +153,54 @@ def test_batch_pir_msmarco_full_vs_oracle(ctx, oracle):
         assert not diff, (p, diff)
 
 
+def test_batch_pir_group_msmarco_bench_shape(ctx, oracle):
+    """The bench's config2 `clients_grouped` shape: 32 clients of the one
+    3,201,821 x 896 B server, every round ONE shared step over their 512
+    partitions (2 sub-queries each: the grouped hint search k_match_part8,
+    k_resolve, k_answer); 40 rounds of 32 uniform ids per client; clients 0,
+    9, 20 and 31 compared response for response with independent oracle
+    clients of the same seeds, then their counters."""
+    import pacmann_amd as pm
+    from concurrent.futures import ThreadPoolExecutor
+    N, E, B, K = 3_201_821, 112, 32, 32
+    db = rand_db(N, E, seed=79)
+    g = pm.SimpleBatchPianoPIR(N, E * 8, B, db, 8, seed=SEED, ctx=ctx)
+    g.Preprocessing()
+    seeds = [SEED] + [2000 + i for i in range(1, K)]
+    clients = [g] + [g.Client(sd, pm.Context(0)) for sd in seeds[1:]]
+    for c in clients[1:]:
+        c.Preprocessing()
+    grp = pm.BatchPIRGroup(clients)
+    check = [0, 9, 20, 31]
+
+    def make(i):
+        o = oracle.SimpleBatchPianoPIR(N, E * 8, B, db, 8, seed=seeds[i])
+        o.Preprocessing()
+        return i, o
+    with ThreadPoolExecutor(max_workers=len(check)) as ex:
+        ors = dict(ex.map(make, check))
+    rng = np.random.default_rng(80)
+    ctx.timing_reset()
+    ctx.timing(2)   # the shared steps run on the first client's context
+    try:
+        for b in range(40):
+            q = rng.integers(0, N, size=(K, B), dtype=np.uint64)
+            if b % 4 == 0:
+                q[:, 7] = q[:, 3]
+            out, ok = grp.QueryWithMask(q)
+            for i in check:
+                want, _ = ors[i].Query(q[i])
+                assert np.array_equal(out[i], want), (b, i)
+        ctx.sync()
+    finally:
+        ctx.timing(False)
+    assert ctx.timing_get("hint_match")[0] > 0 and ctx.timing_get("answer")[0] > 0
+    for i in check:
+        sc, so = clients[i].stats(), ors[i].stats()
+        for k in ("FinishedBatchNum", "QueriesMadeInPartition", "PrepCount"):
+            assert sc[k] == so[k], (i, k)
+
+
 # ---------------------------------------------------------------------------
 # private search at full size: SIFT1M (configs[1]) and MS-MARCO d=192
 # ---------------------------------------------------------------------------
