@@ -36,12 +36,32 @@ def needs_build() -> bool:
     return any(p.stat().st_mtime > t for p in SOURCES + HEADERS)
 
 
-def build(force: bool = False, verbose: bool = True) -> Path:
-    if force or needs_build():
-        cmd = [HIPCC, *FLAGS, "-o", str(LIB), *map(str, SOURCES)]
+def _compile_link(out: Path, defines: list[str], verbose: bool) -> None:
+    """Each translation unit compiled on its own core (pm_query.hip dominates),
+    then one link; the objects go to build/obj_<name>/."""
+    from concurrent.futures import ThreadPoolExecutor
+    objdir = ROOT / "build" / f"obj_{out.stem}"
+    objdir.mkdir(parents=True, exist_ok=True)
+    cflags = [f for f in FLAGS if f != "-shared"]
+
+    def cc(src: Path) -> Path:
+        obj = objdir / (src.name + ".o")
+        cmd = [HIPCC, *cflags, *defines, "-c", "-o", str(obj), str(src)]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True, cwd=CSRC)
+        return obj
+    with ThreadPoolExecutor(max_workers=min(len(SOURCES), os.cpu_count() or 1)) as ex:
+        objs = list(ex.map(cc, SOURCES))
+    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", str(out), *map(str, objs), "-ldl"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True, cwd=CSRC)
+
+
+def build(force: bool = False, verbose: bool = True) -> Path:
+    if force or needs_build():
+        _compile_link(LIB, [], verbose)
     return LIB
 
 
@@ -50,9 +70,7 @@ def build_variant(name: str, defines: list[str]) -> Path:
     loaded instead of the default with PM_LIB=<path>."""
     out = ROOT / "build" / f"libpacmann_{name}.so"
     out.parent.mkdir(exist_ok=True)
-    cmd = [HIPCC, *FLAGS, *defines, "-o", str(out), *map(str, SOURCES)]
-    print(" ".join(cmd), flush=True)
-    subprocess.run(cmd, check=True, cwd=CSRC)
+    _compile_link(out, defines, True)
     return out
 
 

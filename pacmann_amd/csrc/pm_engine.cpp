@@ -149,8 +149,12 @@ struct HostBuf {
 };
 
 // Host wall-clock accumulators, read back as "host_*" through pm_timing_get.
-enum HostTimer : int { HT_STEP_LAUNCH, HT_STEP_WAIT, HT_STEP_POST, HT_BATCH_QUERY, HT_GVI_PARSE, HT_SEARCH_KNN, HT_KNN_INIT, HT_KNN_BATCH, HT_KNN_UPDATE, HT_KNN_FINAL, HT_WAIT_FIRST, HT_WAIT_ALL, HT_ROWS_SEEN, HT_ROWS_TORN, HT_WAIT_DONE, HT_COMBINE, HT_COMBINE_TURN, HT_COUNT };
-static const char* const kHostTimerName[HT_COUNT] = {"host_step_launch", "host_step_wait", "host_step_post", "host_batch_query", "host_gvi_parse", "host_search_knn", "host_knn_init", "host_knn_batch", "host_knn_update", "host_knn_final", "host_wait_first_token", "host_wait_all_tokens", "host_rows_seen", "host_rows_torn", "host_wait_done", "host_combine", "host_combine_turn"};
+// The "host_path_*" entries count the hint-search kernel each step launched
+// (k_match / k_match_part / k_match_part8; total_ms 0), "host_prep_sets" the
+// re-preprocessing launch sets of the serving loops, with total_ms = the number
+// of clients they folded (a count, not a time).
+enum HostTimer : int { HT_STEP_LAUNCH, HT_STEP_WAIT, HT_STEP_POST, HT_BATCH_QUERY, HT_GVI_PARSE, HT_SEARCH_KNN, HT_KNN_INIT, HT_KNN_BATCH, HT_KNN_UPDATE, HT_KNN_FINAL, HT_WAIT_FIRST, HT_WAIT_ALL, HT_ROWS_SEEN, HT_ROWS_TORN, HT_WAIT_DONE, HT_COMBINE, HT_COMBINE_TURN, HT_PATH_MATCH, HT_PATH_MATCH_PART, HT_PATH_MATCH_PART8, HT_PREP_SETS, HT_COUNT };
+static const char* const kHostTimerName[HT_COUNT] = {"host_step_launch", "host_step_wait", "host_step_post", "host_batch_query", "host_gvi_parse", "host_search_knn", "host_knn_init", "host_knn_batch", "host_knn_update", "host_knn_final", "host_wait_first_token", "host_wait_all_tokens", "host_rows_seen", "host_rows_torn", "host_wait_done", "host_combine", "host_combine_turn", "host_path_match", "host_path_match_part", "host_path_match_part8", "host_prep_sets"};
 
 struct TimedLaunch { std::string name; hipEvent_t a, b; double bytes; };
 
@@ -209,6 +213,9 @@ struct pm_ctx {
   uint64_t host_n[HT_COUNT] = {};
   double host_ms[HT_COUNT] = {};
   void host_add(HostTimer t, double ms) { host_n[t]++; host_ms[t] += ms; }
+  void count_match_path(int path) {
+    host_add(path == pmk::MATCH_PART8 ? HT_PATH_MATCH_PART8 : path == pmk::MATCH_PART ? HT_PATH_MATCH_PART : HT_PATH_MATCH, 0.0);
+  }
   std::vector<TimedLaunch> launches;
   std::vector<hipEvent_t> pool;
   hipEvent_t ev() {
@@ -1094,7 +1101,10 @@ static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
 #endif
     return 0;
   }
-  c->timed_ext("hint_match", (double)nreal * g->maxPH, [&](pmk::PmEvents ev) { pmk::step_match(st, S, g->ph8, g->maxPH, max_per_part, ev); }, 2);
+  const pmk::StepOpts opts = pmk::step_opts();
+  int path = 0;
+  c->timed_ext("hint_match", (double)nreal * g->maxPH, [&](pmk::PmEvents ev) { path = pmk::step_match(st, S, opts, g->ph8, g->maxPH, max_per_part, ev); }, 2);
+  c->count_match_path(path);
   const bool lds = pmk::step_resolve_lds_ok(g->maxPH, max_per_part);
   c->timed_ext("resolve", 0, [&](pmk::PmEvents ev) { pmk::step_resolve(st, S, lds, ev); }, 2);
   if (c->debug_sync) {   // validate every resolution record before k_answer consumes it
@@ -2561,13 +2571,14 @@ static int group_step(StepGroup& G, const std::vector<char>& in) {
   auto t0 = Clock::now();
   const bool lds = pmk::step_resolve_lds_ok(G.maxPH, max_per_part);
   S.nsplit = c->no_split ? 1 : pmk::step_gather_split(G.maxSS, nsub);
-  if (pmk::step_qset_ok(S, lds, G.ph8, G.maxPH, max_per_part, G.maxSS)) {
+  const pmk::StepOpts opts = pmk::step_opts();   // one snapshot: np_live, the qset and the kernels agree
+  if (pmk::step_qset_ok(S, opts, lds, G.ph8, G.maxPH, max_per_part, G.maxSS)) {
     S.qw = (G.maxSS + 7) & ~7u;
     CHK(G.qset.reserve((uint64_t)nsub * S.qw * 2));
     S.qset = G.qset.as<uint16_t>();
   }
-  if (pmk::step_match_resolve_ok(S, lds)) {   // one launch: match + resolve per partition
-    if (pmk::step_match_resolve_small(G.ph8, G.maxPH, max_per_part)) S.np_live = 0;   // resolvers do not count in
+  if (pmk::step_match_resolve_ok(S, opts, lds)) {   // one launch: match + resolve per partition
+    if (pmk::step_match_resolve_small(opts, G.ph8, G.maxPH, max_per_part)) S.np_live = 0;   // resolvers do not count in
 #ifdef PM_MR_STAMPS
     static const char* mr_file = getenv("PM_MR_STAMPS");   // append {np} + np x 8 stamps per step
     static std::atomic<int> mr_steps{0};   // the first 40 steps of the run
@@ -2578,7 +2589,7 @@ static int group_step(StepGroup& G, const std::vector<char>& in) {
       S.stamps = G.stamps.as<uint64_t>();
     }
 #endif
-    c->timed_ext("match_resolve", (double)nreal * G.maxPH, [&](pmk::PmEvents ev) { pmk::step_match_resolve(st, S, G.ph8, G.maxPH, max_per_part, ev); }, 2);
+    c->timed_ext("match_resolve", (double)nreal * G.maxPH, [&](pmk::PmEvents ev) { pmk::step_match_resolve(st, S, opts, G.ph8, G.maxPH, max_per_part, ev); }, 2);
 #ifdef PM_MR_STAMPS
     if (mr_this) {
       HIPCHK(hipStreamSynchronize(st));
@@ -2596,7 +2607,9 @@ static int group_step(StepGroup& G, const std::vector<char>& in) {
     }
 #endif
   } else {
-    c->timed_ext("hint_match", (double)nreal * G.maxPH, [&](pmk::PmEvents ev) { pmk::step_match(st, S, G.ph8, G.maxPH, max_per_part, ev); }, 2);
+    int path = 0;
+    c->timed_ext("hint_match", (double)nreal * G.maxPH, [&](pmk::PmEvents ev) { path = pmk::step_match(st, S, opts, G.ph8, G.maxPH, max_per_part, ev); }, 2);
+    c->count_match_path(path);
     c->timed_ext("resolve", 0, [&](pmk::PmEvents ev) { pmk::step_resolve(st, S, lds, ev); }, 2);
   }
   if (S.nsplit > 1) {
@@ -2703,6 +2716,7 @@ static int prep_clients(pm_ctx* c, DevBuf& pbuf, const std::vector<uint32_t>& lp
   CHK(pbuf.reserve(hp.size() * sizeof(PmPart)));
   HIPCHK(hipMemcpyAsync(pbuf.p, hp.data(), hp.size() * sizeof(PmPart), hipMemcpyHostToDevice, c->stream));
   CHK(engine_prep_launch(c, e0, pbuf.as<PmPart>(), (int)hp.size(), hp.data(), (uint32_t)who.size()));
+  c->host_add(HT_PREP_SETS, (double)who.size());
   const double t = std::chrono::duration<double>(Clock::now() - t0).count();
   for (size_t i = 0; i < who.size(); ++i) {
     who[i]->prepCount++;
@@ -3183,7 +3197,7 @@ struct PoolTeam {
   uint32_t S = 0, s0 = 0;
   std::vector<char> fast, need_prep;
   std::vector<double> mt;
-  uint64_t qi = 0;                 // the team's current query
+  std::atomic<uint64_t> qi{0};     // the team's current query (read by the merged maintenance's worker)
   int st = 0;                      // its current round
   bool begin = false;              // the open phase: a query's start (true) or a round's results
   std::atomic<int> state{kTeamStart};
@@ -3199,13 +3213,18 @@ static int run_batched_pool(pm_graph** gs, uint32_t S, const float* queries, uin
   DevBuf prep_buf;   // the merged maintenance's parts
   std::mutex prep_mu;
   // Maintenance (the end-of-query re-preprocessing, private-search.go:226-232)
-  // of the teams that reach it together runs as ONE launch set: a team whose
-  // clients need it waits (kTeamPrep) until every running team waits too, or
-  // PM_PREP_WAIT_MS after the first one arrived.  The maintenance kernels fill
-  // the GPU, so teams' maintenances run one after another either way; merged,
-  // the teams also resume together, instead of finishing the timed work one
-  // after another with the GPU partly idle.  PM_PREP_WAIT_MS=0: each team alone.
-  static const double prep_wait = [] { const char* e = getenv("PM_PREP_WAIT_MS"); return e ? atof(e) : 20.0; }();
+  // of the teams that need it at the same query runs as ONE launch set: a team
+  // whose clients need it after query Q waits (kTeamPrep) until every other
+  // team has finished query Q (it waits at Q too, has moved past Q, or is
+  // done); the teams waiting at Q are then re-preprocessed together.  The set
+  // is a function of the sessions' triggers alone (no timeout: the bench's
+  // 256 sessions always fold in one launch, which the headline parity test
+  // asserts), and no wait is unbounded: every other team is running its query
+  // Q.  The maintenance kernels fill the GPU, so teams' maintenances run one
+  // after another either way; merged, the teams also resume together instead
+  // of finishing the timed work one after another with the GPU partly idle.
+  // PM_PREP_WAIT_MS=0: each team alone.
+  static const double prep_wait = [] { const char* e = getenv("PM_PREP_WAIT_MS"); return e ? atof(e) : 1.0; }();
   struct Release {
     std::vector<std::unique_ptr<PoolTeam>>& t;
     ~Release() { for (auto& x : t) team_release(x->gs, x->S); }
@@ -3350,19 +3369,24 @@ static int run_batched_pool(pm_graph** gs, uint32_t S, const float* queries, uin
         } else if (cur == kTeamPrep) {
           if (!prep_mu.try_lock()) continue;   // one worker runs the merged maintenance
           std::lock_guard<std::mutex> lk(prep_mu, std::adopt_lock);
-          const auto now = Clock::now();
+          // Q: the earliest query a team waits at; the set: the teams waiting at Q,
+          // once every team still running has finished query Q
+          uint64_t Q = ~0ull;
+          for (auto& u : teams)
+            if (u->state.load(std::memory_order_acquire) == kTeamPrep) Q = std::min(Q, u->qi.load(std::memory_order_acquire));
+          if (Q == ~0ull) continue;
           bool all = true;
-          auto first = now;
           for (auto& u : teams) {
             const int us = u->state.load(std::memory_order_acquire);
-            if (us == kTeamPrep) first = std::min(first, u->prep_since);
-            else if (us != kTeamDone) all = false;
+            if (us != kTeamPrep && us != kTeamDone && u->qi.load(std::memory_order_acquire) <= Q) all = false;
           }
-          if (!all && std::chrono::duration<double, std::milli>(now - first).count() < prep_wait) continue;
+          if (!all) continue;
           std::vector<PoolTeam*> ts;
           for (auto& u : teams) {
             int e = kTeamPrep;
-            if (u->state.compare_exchange_strong(e, kTeamBusy, std::memory_order_acq_rel)) ts.push_back(u.get());
+            if (u->qi.load(std::memory_order_acquire) == Q &&
+                u->state.compare_exchange_strong(e, kTeamBusy, std::memory_order_acq_rel))
+              ts.push_back(u.get());
           }
           if (ts.empty()) continue;
           did = true;

@@ -242,25 +242,31 @@ struct PmEvents { hipEvent_t a = nullptr, b = nullptr; };
 // choice (PM_MATCH_PART, PM_MATCH_PART8, PM_MATCH_RESOLVE).  Returns -1 for an
 // unknown name.
 int set_option(const char* name, int value);
-// ph8: every partition's PH is a multiple of 8 (k_match_part8)
-void step_match(hipStream_t st, const PmStep& S, bool ph8, uint32_t maxPH, uint32_t max_sub_per_part,
-                PmEvents ev = {});
+// The selectors' values for one step (read once per step and passed to every
+// selector below, so one step never mixes two settings).
+struct StepOpts { int match_part, match_part8, match_resolve; };
+StepOpts step_opts();
+// ph8: every partition's PH is a multiple of 8 (k_match_part8).  Returns the
+// hint-search kernel launched.
+enum : int { MATCH_SUB = 0, MATCH_PART = 1, MATCH_PART8 = 2 };
+int step_match(hipStream_t st, const PmStep& S, const StepOpts& O, bool ph8, uint32_t maxPH,
+               uint32_t max_sub_per_part, PmEvents ev = {});
 uint32_t step_match_blocks(uint32_t maxPH);   // k_match workgroups per sub-query
 void step_resolve(hipStream_t st, const PmStep& S, bool lds, PmEvents ev = {});
 // k_match_part + k_resolve fused (batched serving; descriptor already in device memory)
-bool step_match_resolve_ok(const PmStep& S, bool lds);
-bool step_match_resolve_small(bool ph8, uint32_t maxPH, uint32_t max_sub_per_part);
+bool step_match_resolve_ok(const PmStep& S, const StepOpts& O, bool lds);
+bool step_match_resolve_small(const StepOpts& O, bool ph8, uint32_t maxPH, uint32_t max_sub_per_part);
 // ph8: every partition's PH is a multiple of 8
-void step_match_resolve(hipStream_t st, const PmStep& S, bool ph8, uint32_t maxPH, uint32_t max_sub_per_part,
-                        PmEvents ev = {});
+void step_match_resolve(hipStream_t st, const PmStep& S, const StepOpts& O, bool ph8, uint32_t maxPH,
+                        uint32_t max_sub_per_part, PmEvents ev = {});
 // k_step: match, resolve and answer in one launch (descriptor in the kernel
 // arguments, <= 64 sub-queries and <= 8192 hints per partition, <= 256 workgroups)
 bool step_fused_ok(const PmStep& S, uint32_t maxPH, uint32_t max_sub_per_part);
 void step_fused(hipStream_t st, const PmStep& S, PmEvents ev = {});
 bool step_resolve_lds_ok(uint32_t maxPH, uint32_t max_sub_per_part);
 // k_match_resolve_s writes the query sets for the answer (PmStep::qset); S.nsplit set
-bool step_qset_ok(const PmStep& S, bool lds, bool ph8, uint32_t maxPH, uint32_t max_sub_per_part,
-                  uint32_t maxSS);
+bool step_qset_ok(const PmStep& S, const StepOpts& O, bool lds, bool ph8, uint32_t maxPH,
+                  uint32_t max_sub_per_part, uint32_t maxSS);
 void step_answer(hipStream_t st, const PmStep& S, uint32_t maxSS, PmEvents ev = {});
 // Split gather ahead of k_answer for wide query sets (SetSize >= 256, BIGANN
 // scale): how many workgroups per sub-query (1: no split), and the launch.

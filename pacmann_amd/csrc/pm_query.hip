@@ -2299,6 +2299,13 @@ static int opt(const std::atomic<int>& ov, int env) {
   const int v = ov.load(std::memory_order_relaxed);
   return v != kOptUnset ? v : env;
 }
+// One snapshot per step: every selector of the step reads the same values, so
+// a pm_set_option on another thread cannot split a step between two paths
+// (e.g. np_live = 0 with the general k_match_resolve).
+StepOpts step_opts() {
+  return StepOpts{opt(ov_match_part, env_match_part), opt(ov_match_part8, env_match_part8),
+                  opt(ov_match_resolve, env_match_resolve)};
+}
 int set_option(const char* name, int value) {
   std::atomic<int>* o = !strcmp(name, "match_part") ? &ov_match_part
                       : !strcmp(name, "match_part8") ? &ov_match_part8
@@ -2315,26 +2322,31 @@ uint32_t step_match_blocks(uint32_t maxPH) { return cdiv(maxPH, kMatchHints); }
     if ((ev).a) hipExtLaunchKernelGGL(kern, grid, blk, 0, st, (ev).a, (ev).b, 0, __VA_ARGS__); \
     else hipLaunchKernelGGL(kern, grid, blk, 0, st, __VA_ARGS__);                             \
   } while (0)
-void step_match(hipStream_t st, const PmStep& S, bool ph8, uint32_t maxPH, uint32_t max_sub_per_part, PmEvents ev) {
+int step_match(hipStream_t st, const PmStep& S, const StepOpts& O, bool ph8, uint32_t maxPH,
+               uint32_t max_sub_per_part, PmEvents ev) {
   // many partitions with several sub-queries each (batched serving): one
   // workgroup per (partition, hint block); otherwise one per (sub-query, block)
-  const int mode = opt(ov_match_part, env_match_part);
+  const int mode = O.match_part;
   const bool part = mode == 1 || (mode == -1 && S.np >= 128 && S.nsub >= 4 * S.np);
   // PM_MATCH_PART8=0: the LDS-merged form for every PH
-  const int v8 = opt(ov_match_part8, env_match_part8);
+  const int v8 = O.match_part8;
   // k_match_part8 from 64 partitions with 2+ sub-queries each (BIGANN teams of
   // 4-6 sessions: k_match's workgroup per (sub-query, block) took 85 us there)
   const bool part8 = ph8 && v8 && max_sub_per_part <= kPart8Subs && (part || (mode == -1 && S.np >= 64 && S.nsub >= 2 * S.np));
-  if (part8)
+  if (part8) {
     PM_LAUNCH(ev, k_match_part8<PM_MATCHPART8_NW>, dim3(cdiv(step_match_blocks(maxPH), PM_MATCHPART8_NW), S.np),
               dim3(64 * PM_MATCHPART8_NW), st, S);
-  else if (part)
+    return MATCH_PART8;
+  }
+  if (part) {
     PM_LAUNCH(ev, k_match_part<kMatchHints / kBlock>, dim3(step_match_blocks(maxPH), S.np), dim3(kBlock), st, S);
-  else
-    PM_LAUNCH(ev, k_match, dim3(step_match_blocks(maxPH), S.nsub), dim3(kBlock), st, S);
+    return MATCH_PART;
+  }
+  PM_LAUNCH(ev, k_match, dim3(step_match_blocks(maxPH), S.nsub), dim3(kBlock), st, S);
+  return MATCH_SUB;
 }
-bool step_match_resolve_ok(const PmStep& S, bool lds) {
-  const int mode = opt(ov_match_resolve, env_match_resolve);
+bool step_match_resolve_ok(const PmStep& S, const StepOpts& O, bool lds) {
+  const int mode = O.match_resolve;
   // one workgroup per partition matches every hint of it: search-sized hint
   // counts only (PH <= 16,384; BIGANN's 57,344 / 114,688 hints per partition
   // go to k_match_part's workgroup per (partition, hint block) instead)
@@ -2342,14 +2354,14 @@ bool step_match_resolve_ok(const PmStep& S, bool lds) {
          S.nsub >= 4 * S.np && S.words <= 256;
 }
 // k_match_resolve_s serves the step (its resolvers do not count in: PmStep::np_live = 0)
-bool step_match_resolve_small(bool ph8, uint32_t maxPH, uint32_t max_sub_per_part) {
-  const int mode = opt(ov_match_resolve, env_match_resolve);
+bool step_match_resolve_small(const StepOpts& O, bool ph8, uint32_t maxPH, uint32_t max_sub_per_part) {
+  const int mode = O.match_resolve;
   return mode == 1 && max_sub_per_part <= kSpecSubs && ph8 && maxPH <= 16u * kResolveBlockG;
 }
-void step_match_resolve(hipStream_t st, const PmStep& S, bool ph8, uint32_t maxPH, uint32_t max_sub_per_part,
-                        PmEvents ev) {
+void step_match_resolve(hipStream_t st, const PmStep& S, const StepOpts& O, bool ph8, uint32_t maxPH,
+                        uint32_t max_sub_per_part, PmEvents ev) {
   // the one-round-trip form where its shapes hold (PM_MATCH_RESOLVE=2: always the general one)
-  const bool small = step_match_resolve_small(ph8, maxPH, max_sub_per_part);
+  const bool small = step_match_resolve_small(O, ph8, maxPH, max_sub_per_part);
   // workgroup size (PM_MR_NT): 256 leaves the GPU's wave slots to the other
   // groups' kernels while wave 0 runs the chain
   static const int nt = [] { const char* e = getenv("PM_MR_NT"); return e ? atoi(e) : 256; }();
@@ -2368,11 +2380,11 @@ void step_match_resolve(hipStream_t st, const PmStep& S, bool ph8, uint32_t maxP
   else
     PM_LAUNCH(ev, k_match_resolve<kMatchHints / kBlock>, dim3(S.np), dim3(kResolveBlockG), st, S);
 }
-bool step_qset_ok(const PmStep& S, bool lds, bool ph8, uint32_t maxPH, uint32_t max_sub_per_part,
-                  uint32_t maxSS) {
-  const int mode = opt(ov_match_resolve, env_match_resolve);
+bool step_qset_ok(const PmStep& S, const StepOpts& O, bool lds, bool ph8, uint32_t maxPH,
+                  uint32_t max_sub_per_part, uint32_t maxSS) {
+  const int mode = O.match_resolve;
   static const int qs = [] { const char* e = getenv("PM_QSET"); return e ? atoi(e) : 1; }();
-  return qs && mode == 1 && step_match_resolve_ok(S, lds) && max_sub_per_part <= kSpecSubs && ph8 &&
+  return qs && mode == 1 && step_match_resolve_ok(S, O, lds) && max_sub_per_part <= kSpecSubs && ph8 &&
          maxPH <= 16u * kResolveBlockG && maxSS <= kSmallSS && S.nsplit <= 1;
 }
 void step_resolve(hipStream_t st, const PmStep& S, bool lds, PmEvents ev) {

@@ -497,16 +497,18 @@ def test_batch_pir_group(ctx, oracle):
         assert c.stats()["PrepCount"] > 1
 
 
-@pytest.mark.parametrize("opts", [
-    {"match_resolve": 0, "match_part": 1, "match_part8": 1},   # k_match_part8 -> k_resolve
-    {"match_resolve": 0, "match_part": 1, "match_part8": 0},   # k_match_part (LDS-merged) -> k_resolve
-    {"match_resolve": 0, "match_part": 0},                      # k_match per (sub-query, block) -> k_resolve
+@pytest.mark.parametrize("opts,path", [
+    ({"match_resolve": 0, "match_part": 1, "match_part8": 1}, "part8"),   # k_match_part8 -> k_resolve
+    ({"match_resolve": 0, "match_part": 1, "match_part8": 0}, "part"),    # k_match_part (LDS-merged) -> k_resolve
+    ({"match_resolve": 0, "match_part": 0}, ""),                           # k_match per (sub-query, block)
 ], ids=["part8", "part", "per_subquery"])
-def test_batch_pir_group_hint_search_paths(ctx, oracle, opts):
+def test_batch_pir_group_hint_search_paths(ctx, oracle, opts, path):
     """Every hint-search form (pm_set_option) answers a group's batches exactly
     as the oracle: five clients, PH 1,792 (one full and one partial 1,024-hint
     block; PH % 8 == 0 so k_match_part8 applies), repeated ids, through the
-    batch layer's re-preprocessing; entries, flags and counters compared."""
+    batch layer's re-preprocessing; entries, flags and counters compared.  The
+    engine's per-path launch counters (host_path_match*) prove that the forced
+    kernel, and only it, ran every step."""
     import pacmann_amd as pm
     N, E, B = 30_000, 8, 8
     db = rand_db(N, E, 93)
@@ -537,7 +539,10 @@ def test_batch_pir_group_hint_search_paths(ctx, oracle, opts):
                 assert np.array_equal(out[i], want), (b, i)
         ctx.sync()
         ctx.timing(False)
-        assert ctx.timing_get("hint_match")[0] > 0 and ctx.timing_get("resolve")[0] > 0
+        n_match = ctx.timing_get("hint_match")[0]
+        assert n_match > 0 and ctx.timing_get("resolve")[0] > 0
+        counts = {p: ctx.timing_get("host_path_match" + ("_" + p if p else ""))[0] for p in ("part8", "part", "")}
+        assert counts[path] == n_match and sum(counts.values()) == n_match, counts
         for c, o in zip(clients, ors):
             for k in ("FinishedBatchNum", "QueriesMadeInPartition", "PrepCount"):
                 assert c.stats()[k] == o.stats()[k], k
