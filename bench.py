@@ -403,10 +403,28 @@ def bigann_search(key, name, n_entries, layout, rank, ws, local, dist, comb_grou
     ctxs = [x.ctx for x in sess]
     nq = BIG_SEARCH_WARMUP + BIG_SEARCH_Q
     qs = np.random.default_rng(63).random((S, nq, BIG_DIM), dtype=np.float32)   # genRandomMatrix queries
-    comb = RecordCombiner(group=comb_group, device=local) if combine else None
+    if not combine:
+        comb = None
+    elif comb_group == "native":   # the library's own RCCL communicators (pm_rccl_combine)
+        from pacmann_amd.shard import RcclCombiner
+        comb = RcclCombiner(group=None, device=local)
+    else:
+        comb = RecordCombiner(group=comb_group, device=local)
     groups = min(args.big_groups or BIG_GROUPS, S)
-    pm.search_loop_sharded(sess, qs[:, :BIG_SEARCH_WARMUP], K_TOP, STEP, PARALLEL, groups, args.threads,
-                           combiner=comb, model_peers=modelled)
+    # the warm-up queries with every record checked on the host (pm_set_option
+    # "verify_records": answered records against the graph's spec and the
+    # reference-order L2, unanswered ids against their explanation); off in the
+    # timed region
+    for c in ctxs:
+        c.timing_reset()
+    pm.set_option("verify_records", 1)
+    try:
+        pm.search_loop_sharded(sess, qs[:, :BIG_SEARCH_WARMUP], K_TOP, STEP, PARALLEL, groups, args.threads,
+                               combiner=comb, model_peers=modelled)
+    finally:
+        pm.set_option("verify_records", 0)
+    recs = {k: sum(c.timing_get("host_records_" + k)[0] for c in ctxs)
+            for k in ("verified", "bad", "dropped", "failed", "peer", "unexplained")}
     for c in ctxs:
         c.sync()
         c.timing_reset()
@@ -432,6 +450,9 @@ def bigann_search(key, name, n_entries, layout, rank, ws, local, dist, comb_grou
     ht = {k: tsum(k) for k in ("host_combine", "host_combine_turn", "host_step_wait", "host_batch_query",
                                 "host_gvi_parse", "host_step_launch", "host_step_post", "host_knn_update",
                                 "host_knn_batch", "host_knn_init")}
+    combine_paths = None
+    if key == "config3_bigann_100m" and ws == 1 and not args.no_combine_probe:
+        combine_paths = combine_probe(sess, qs, groups, args, local)
     rounds = BIG_SEARCH_Q * STEP * groups   # shared steps in the timed region (every team)
     same = None if modelled else 1   # modelled layouts: each rank serves another shard (its own failures)
     if dist and not modelled:   # every rank holds the same answers (the combined records drive identical searches)
@@ -481,7 +502,10 @@ def bigann_search(key, name, n_entries, layout, rank, ws, local, dist, comb_grou
         "n_ranks": ws, "layout_shards": layout, "shard": shard,
         "peers": ("modelled: the other shards' answers generated from the graph's spec on the device "
                   f"({layout} shards, {ws} GPU(s); their PIR work is not measured)" if modelled else
-                  "RCCL all-reduce of the team's records per shared step" if combine and comb_group is not None else
+                  "RCCL all-reduce of the team's records per shared step, inside libpacmann.so (pm_rccl_combine)"
+                  if combine and comb_group == "native" else
+                  "RCCL all-reduce of the team's records per shared step (torch.distributed callback)"
+                  if combine and comb_group is not None else
                   "gloo all-reduce of the team's records per shared step" if combine else
                   "none (one rank holds every partition)"),
         "sessions": S, "lockstep_groups": groups, "queries_per_session": BIG_SEARCH_Q,
@@ -504,9 +528,14 @@ def bigann_search(key, name, n_entries, layout, rank, ws, local, dist, comb_grou
                     "note": "device time of the in-place all-reduce on the team stream (events around the "
                             "combine), per shared step; host_ms is the callback's wall time"},
         "host_ms_per_round": {k[5:]: round(v[1] / (BIG_SEARCH_Q * STEP), 4) for k, v in ht.items() if v[1]},
+        "combine_paths_world1": combine_paths,
         "pir_scan_fold": fold, "pir_scan_answer": ans_roof,
         "roofline_prf": prf_roofline(kprep["prep_offsets"], "k_prep_offsets of one client's preprocessing"),
-        "check": {"ids_fetched": tot, "ids_answered": succ, "ranks_identical": None if same is None else bool(same)},
+        "check": {"ids_fetched": tot, "ids_answered": succ, "ranks_identical": None if same is None else bool(same),
+                  "records_checked_in_warmup": recs,
+                  "note": "warm-up rounds: every answered record equal to the graph's row (synthetic spec) and the "
+                          "reference-order L2 (verified) or not (bad); unanswered ids explained by the overflow "
+                          "drop (batch-pir.go:195-200), a failed sub-query of this rank, or another rank's"},
     }
     del sess, base, ctxs, pir
     gc.collect()
@@ -556,6 +585,64 @@ def inner_product_scan(ctx, with_cpu: bool):
         out["cpu_baseline"] = {"value": round(cpu[1], 2), "unit": "GB/s", "cores": 1, "kind": "port",
                                "all_cores": {"value": round(cpu[ncores], 2), "cores": ncores},
                                "sample": f"{C0_CPU_ROWS:,} materialised rows (4.3 GB) of the same fill"}
+    return out
+
+
+def combine_probe(sess, qs, groups, args, local):
+    """World 1: the sharded loop's two combine paths over a one-rank job, a
+    few queries each on the block's sessions (results not in the block's
+    numbers): the torch.distributed callback over an RCCL group
+    (RecordCombiner) and the library-native RCCL communicators
+    (pm_rccl_combine).  Per shared step: the device time of the all-reduce on
+    the team stream and the host wall time of the combine call."""
+    import datetime
+    import socket
+
+    import torch
+    import torch.distributed as dist
+
+    import pacmann_amd as pm
+    from pacmann_amd.shard import RcclCombiner, RecordCombiner
+    out = {}
+    try:
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                timeout=datetime.timedelta(seconds=120))
+        torch.cuda.set_device(local)
+        ng = dist.new_group(backend="nccl")
+        ctxs = [x.ctx for x in sess]
+        nq = 2
+        for name, comb in (("torch_callback", RecordCombiner(group=ng, device=local)),
+                           ("native", RcclCombiner(group=None, device=local))):
+            pm.search_loop_sharded(sess, qs[:, :1], K_TOP, STEP, PARALLEL, groups, args.threads, combiner=comb)
+            for c in ctxs:
+                c.sync()
+                c.timing_reset()
+                c.timing(1)
+            t0 = time.perf_counter()
+            pm.search_loop_sharded(sess, qs[:, 1:1 + nq], K_TOP, STEP, PARALLEL, groups, args.threads, combiner=comb)
+            for c in ctxs:
+                c.sync()
+            wall = time.perf_counter() - t0
+            for c in ctxs:
+                c.timing(False)
+            n, ms, _ = (sum(x) for x in zip(*[c.timing_get("combine") for c in ctxs]))
+            hn, hms, _ = (sum(x) for x in zip(*[c.timing_get("host_combine") for c in ctxs]))
+            out[name] = {"rounds": int(hn), "device_ms_per_round": round(ms / n, 5) if n else None,
+                         "host_ms_per_round": round(hms / hn, 5) if hn else None,
+                         "private_queries_per_s": round(len(sess) * nq / wall, 2)}
+            if name == "native":
+                comb.close()
+        out["note"] = ("one-rank job: the all-reduce moves nothing between GPUs; the host time is the per-step "
+                       "cost of issuing it (torch callback: ctypes -> GIL -> ProcessGroupNCCL; native: one "
+                       "ncclAllReduce call inside libpacmann.so)")
+    except Exception as e:   # recorded, never fatal
+        out["error"] = f"{type(e).__name__}: {e}"
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
     return out
 
 
@@ -717,8 +804,12 @@ def main():
     ap.add_argument("--no-config0", action="store_true", help="skip the InnerProduct scan block")
     ap.add_argument("--big-sessions", type=int, default=0, help="cap on the BIGANN blocks' sessions per GPU")
     ap.add_argument("--big-groups", type=int, default=0, help="lock-step teams of the BIGANN blocks (0: BIG_GROUPS)")
-    ap.add_argument("--combine", choices=["rccl", "gloo"], default="rccl",
-                    help="collective of the sharded BIGANN rounds (gloo: host tensors, e.g. ranks sharing one GPU)")
+    ap.add_argument("--combine", choices=["rccl", "torch-rccl", "gloo"], default="rccl",
+                    help="collective of the sharded BIGANN rounds: rccl = the library's own RCCL communicators "
+                         "(pm_rccl_combine), torch-rccl = torch.distributed's nccl group through a callback, "
+                         "gloo = host tensors (e.g. ranks sharing one GPU)")
+    ap.add_argument("--no-combine-probe", action="store_true",
+                    help="skip the world-1 comparison of the two RCCL combine paths (BIGANN-100M block)")
     ap.add_argument("--kernel-timing-sample", action="store_true",
                     help="kernel-timing pass: events on every 7th shared step of each team only")
     ap.add_argument("--no-kernel-timing", action="store_true",
@@ -733,6 +824,10 @@ def main():
     S = max(1, args.sessions)
 
     dist, rank, ws, local = dist_init()
+    # torch before libpacmann.so: both then share torch's HIP runtime (the same
+    # SONAME; loaded the other way round, torch sees no GPU), which the
+    # BIGANN blocks' RCCL combine probe needs
+    import torch  # noqa: F401
     import pacmann_amd as pm
 
     ctx0 = pm.Context(local)
@@ -1051,8 +1146,10 @@ def main():
     # configs[4] (BIGANN-1B in 8 shards): every rank takes part
     if not args.no_bigann:
         nccl_group = None
-        if dist and args.combine == "rccl":
+        if dist and args.combine == "torch-rccl":
             nccl_group = rccl_group(dist, local, out)
+        elif dist and args.combine == "rccl":
+            nccl_group = "native"
         for key, nm, n_entries, layout in (("config3_bigann_100m", "BIGANN-100M-shaped (configs[3])",
                                             100_000_000, ws),
                                            ("config4_bigann_1b", "BIGANN-1B-shaped (configs[4]), 8-way layout",

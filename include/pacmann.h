@@ -267,6 +267,30 @@ int  pm_search_loop_batched(pm_graph** sessions, uint32_t S, const float* querie
                             double* online_s, double* maintenance_s);
 pm_batchpir* pm_graph_pir(pm_graph* g);
 
+/* ---- the GetGraphInfo plugin surface (graphann/search.go:20-25) ---------
+ * PIRGraphInfo's methods as batch calls, for a caller that keeps its own beam
+ * search (graphann.SearchKNN) and plugs the GPU in behind GetGraphInfo:
+ *   pm_graph_preprocess       Preprocess()       private-search.go:355-412
+ *   pm_graph_get_metadata     GetMetadata()      private-search.go (n, dim, m)
+ *   pm_graph_get_vertex_info  GetVertexInfo(ids) private-search.go:441-506
+ *   pm_graph_get_start_vertex GetStartVertex()   private-search.go:508-531
+ * pm_graph_get_vertex_info fetches every id through the batch PIR
+ * (SimpleBatchPianoPIR.Query, one call per batch) and decodes the entries
+ * (Entry2VectorAndNeighbors, :418-439) into vecs (n x dim f32) and nbrs
+ * (n x m u32); a failed or dropped id decodes as zeros (ok[i] = 0), as in the
+ * reference.  With a query (dim f32), dist[i] = L2Dist(vector i, query)
+ * (build_graph.go:119-127, l2_distance_amd64.s order, 0 for a failed id) is
+ * computed on the GPU next to the decode.  Any output may be NULL (dist needs
+ * query).  Counts totalQueryNum / succQueryNum as the reference does
+ * (pm_graph_counts).  pm_graph_get_start_vertex: the ⌊√n⌋ start vertices
+ * chosen by pm_graph_preprocess (non-private), *count = their number, the
+ * first min(cap, count) written. */
+int pm_graph_get_metadata(pm_graph* g, uint64_t* n, uint64_t* dim, uint64_t* m);
+int pm_graph_get_vertex_info(pm_graph* g, const uint64_t* ids, uint64_t n, float* vecs, uint32_t* nbrs, uint8_t* ok,
+                             const float* query, float* dist);
+int pm_graph_get_start_vertex(pm_graph* g, uint64_t cap, uint64_t* ids, float* vecs, uint32_t* nbrs,
+                              uint64_t* count);
+
 /* ---- private search over a SHARDED graph DB (multi-GPU) --
  * The reference's PIRGraphInfo (private-search.go:336-531) fetches every
  * vertex record through SimpleBatchPianoPIR.Query (batch-pir.go:170-248),
@@ -299,8 +323,30 @@ int pm_graph_synth_rows(uint64_t n, uint64_t dim, uint64_t m, uint64_t data_seed
  * same (round, team) sequence.  0 = success. */
 typedef int (*pm_combine_fn)(void* user, uint32_t team, uint64_t* dev_words, uint64_t nwords, void* stream);
 /* Words of one team's records: sessions x parallel x m x W (W = the entry
- * words holding the neighbour list, + 1 for {dist, ok}). */
+ * words holding the neighbour list, + 1 for {dist, ok}), + 1 error word.  The
+ * error word is 0 from a healthy rank and 1 from a rank whose team failed: such
+ * a rank still takes the team's next combine turn (zero records, error word 1),
+ * and every rank stops the team at that turn with PM_EHIP, so no rank is left
+ * waiting inside a collective. */
 uint64_t pm_sharded_record_words(pm_graph* g, uint32_t sessions, int parallel);
+
+/* The library-native combine (replaces the per-step hop into the caller's
+ * runtime, e.g. torch.distributed): RCCL communicators over xGMI, one per
+ * lock-step team, created inside libpacmann.so from `nteams` ncclUniqueIds
+ * that rank 0 makes (pm_rccl_unique_id) and the caller broadcasts over any
+ * channel; pm_rccl_combine is a pm_combine_fn (user = the pm_rccl handle):
+ * ncclAllReduce(ncclUint64, ncclSum) in place on the team's stream.  RCCL is
+ * loaded on first use (dlopen of librccl.so.1, the copy already mapped into
+ * the process if any).  The batch-pir.go:62-85 partitions are the shards; the
+ * all-reduce is the north_star's final XOR-reduce (one rank answers each id,
+ * so the integer sum is the XOR). */
+#define PM_RCCL_ID_BYTES 128
+typedef struct pm_rccl pm_rccl;
+int  pm_rccl_unique_id(uint8_t id[PM_RCCL_ID_BYTES]);
+int  pm_rccl_create(int device, int nranks, int rank, const uint8_t* ids /* nteams x PM_RCCL_ID_BYTES */,
+                    uint32_t nteams, pm_rccl** out);
+void pm_rccl_destroy(pm_rccl* r);
+int  pm_rccl_combine(void* user, uint32_t team, uint64_t* dev_words, uint64_t nwords, void* stream);
 /* pm_search_loop_batched over a sharded graph DB: S sessions (clients of one
  * shard's server DB) in ngroups lock-step teams; every round of a team is one
  * shared step over this shard's partitions followed by ONE combine of the

@@ -84,6 +84,8 @@ SIG = {
     "or_build_graph": (C.c_int, [f32p, u64, u64, u64, C.c_float, u64, u32p]),
     "or_search_loop": (None, [vp, f32p, u64, C.c_int, C.c_int, C.c_int, C.c_int, i64p,
                               C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    "or_graph_get_vertex_info": (None, [vp, i64p, u64, f32p, u32p]),
+    "or_graph_get_start_vertex": (u64, [vp, u64, i64p, f32p, u32p]),
 }
 
 
@@ -324,6 +326,26 @@ class Graph:
         t, s = C.c_uint64(), C.c_uint64()
         lib().or_graph_counts(self.h, C.byref(t), C.byref(s))
         return t.value, s.value
+
+    def GetMetadata(self):
+        return self.N, self.Dim, self.M
+
+    def GetVertexInfo(self, ids):
+        """PIRGraphInfo.GetVertexInfo (private-search.go:441-506): (vectors [n, dim], neighbours [n, m])."""
+        i = np.ascontiguousarray(ids, np.int64).ravel()
+        vec = np.zeros((len(i), self.Dim), np.float32)
+        nb = np.zeros((len(i), self.M), np.uint32)
+        lib().or_graph_get_vertex_info(self.h, _p(i, i64p), len(i), _p(vec, f32p), _p(nb, u32p))
+        return vec, nb
+
+    def GetStartVertex(self):
+        """PIRGraphInfo.GetStartVertex (private-search.go:508-531): (ids, vectors, neighbours)."""
+        n = int(lib().or_graph_get_start_vertex(self.h, 0, None, None, None))
+        ids = np.zeros(n, np.int64)
+        vec = np.zeros((n, self.Dim), np.float32)
+        nb = np.zeros((n, self.M), np.uint32)
+        lib().or_graph_get_start_vertex(self.h, n, _p(ids, i64p), _p(vec, f32p), _p(nb, u32p))
+        return ids, vec, nb
 
     def pir(self) -> SimpleBatchPianoPIR:
         return SimpleBatchPianoPIR(0, 0, 0, None, 0, _handle=lib().or_graph_pir(self.h), _keep=self._v)

@@ -624,6 +624,27 @@ static std::vector<Vtx> get_vertex_info(or_graph* g, const std::vector<int64_t>&
   return out;
 }
 
+// The GetGraphInfo surface (graphann/search.go:20-25) of PIRGraphInfo, flat:
+// GetVertexInfo of n ids (vecs n x dim, nbrs n x m as uint32; either NULL)
+// and GetStartVertex (up to cap entries; returns the start set's size).
+extern "C" void or_graph_get_vertex_info(or_graph* g, const int64_t* ids, uint64_t n, float* vecs, uint32_t* nbrs) {
+  const std::vector<Vtx> out = get_vertex_info(g, std::vector<int64_t>(ids, ids + n));
+  for (uint64_t i = 0; i < n; ++i) {
+    if (vecs) memcpy(vecs + i * g->dim, out[i].vec.data(), g->dim * 4);
+    if (nbrs) for (uint64_t j = 0; j < g->m; ++j) nbrs[i * g->m + j] = (uint32_t)out[i].nb[j];
+  }
+}
+extern "C" uint64_t or_graph_get_start_vertex(const or_graph* g, uint64_t cap, int64_t* ids, float* vecs,
+                                              uint32_t* nbrs) {
+  for (uint64_t i = 0; i < g->start.size() && i < cap; ++i) {
+    const Vtx& v = g->start[i];
+    if (ids) ids[i] = v.id;
+    if (vecs) memcpy(vecs + i * g->dim, v.vec.data(), g->dim * 4);
+    if (nbrs) for (uint64_t j = 0; j < g->m; ++j) nbrs[i * g->m + j] = (uint32_t)v.nb[j];
+  }
+  return g->start.size();
+}
+
 // container/heap (Go stdlib) on a min-heap of VD keyed by dist.
 static void heap_up(std::vector<VD>& h, int64_t j) {
   for (;;) { int64_t i = (j - 1) / 2; if (i == j || !(h[j].dist < h[i].dist)) break; std::swap(h[i], h[j]); j = i; }

@@ -128,7 +128,15 @@ SIGNATURES = {
     "pm_search_loop_sharded": (C.c_int, [C.POINTER(vp), C.c_uint32, f32p, u64, C.c_int, C.c_int, C.c_int, C.c_uint32,
                                          C.c_uint32, COMBINE_FN, vp, C.POINTER(vp), C.c_int, i64p, C.POINTER(dbl),
                                          C.POINTER(dbl), C.POINTER(dbl)]),
+    "pm_graph_get_metadata": (C.c_int, [vp, u64p, u64p, u64p]),
+    "pm_graph_get_vertex_info": (C.c_int, [vp, u64p, u64, f32p, u32p, u8p, f32p, f32p]),
+    "pm_graph_get_start_vertex": (C.c_int, [vp, u64, u64p, f32p, u32p, u64p]),
+    "pm_rccl_unique_id": (C.c_int, [u8p]),
+    "pm_rccl_create": (C.c_int, [C.c_int, C.c_int, C.c_int, u8p, C.c_uint32, C.POINTER(vp)]),
+    "pm_rccl_destroy": (None, [vp]),
+    "pm_rccl_combine": (C.c_int, [vp, C.c_uint32, vp, u64, vp]),
 }
+RCCL_ID_BYTES = 128   # PM_RCCL_ID_BYTES
 
 Q_OK, Q_EBUDGET, Q_ECHUNK, Q_ENOHIT, Q_ERANGE = range(5)
 _QERR = {
@@ -585,7 +593,37 @@ class PIRGraphInfo:
             self.h = None
 
     def GetMetadata(self):
-        return self.N, self.Dim, self.M
+        n, d, m = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        _check(lib().pm_graph_get_metadata(self.h, C.byref(n), C.byref(d), C.byref(m)))
+        return n.value, d.value, m.value
+
+    def GetVertexInfo(self, ids, query=None):
+        """PIRGraphInfo.GetVertexInfo (private-search.go:441-506) of a batch of
+        vertex ids (pm_graph_get_vertex_info): (vectors [n, dim] f32,
+        neighbours [n, m] u32, ok [n] bool), plus, given a query, the L2
+        distances [n] computed on the GPU beside the decode."""
+        i = _u64(ids).ravel()
+        n = len(i)
+        vec = np.zeros((n, self.Dim), dtype=np.float32)
+        nb = np.zeros((n, self.M), dtype=np.uint32)
+        ok = np.zeros(n, dtype=np.uint8)
+        q = None if query is None else np.ascontiguousarray(query, dtype=np.float32).ravel()
+        d = np.zeros(n, dtype=np.float32) if q is not None else None
+        _check(lib().pm_graph_get_vertex_info(self.h, _p(i, u64p), n, _p(vec, f32p), _p(nb, u32p), _p(ok, u8p),
+                                              None if q is None else _p(q, f32p), None if d is None else _p(d, f32p)))
+        return (vec, nb, ok.astype(bool)) if d is None else (vec, nb, ok.astype(bool), d)
+
+    def GetStartVertex(self):
+        """PIRGraphInfo.GetStartVertex (private-search.go:508-531): the start
+        set chosen by Preprocess, (ids [k] int64, vectors [k, dim], neighbours [k, m])."""
+        cnt = C.c_uint64()
+        _check(lib().pm_graph_get_start_vertex(self.h, 0, None, None, None, C.byref(cnt)))
+        k = cnt.value
+        ids = np.zeros(k, dtype=np.uint64)
+        vec = np.zeros((k, self.Dim), dtype=np.float32)
+        nb = np.zeros((k, self.M), dtype=np.uint32)
+        _check(lib().pm_graph_get_start_vertex(self.h, k, _p(ids, u64p), _p(vec, f32p), _p(nb, u32p), C.byref(cnt)))
+        return ids.astype(np.int64), vec, nb
 
     def Preprocess(self):
         _check(lib().pm_graph_preprocess(self.h))
@@ -737,13 +775,17 @@ def search_loop_sharded(sessions, queries, k: int, step: int, parallel: int, ngr
     wall = C.c_double()
     on = np.zeros(S, dtype=np.float64)
     mt = np.zeros(S, dtype=np.float64)
-    fn, bufs = COMBINE_FN(), None
+    fn, bufs, user = COMBINE_FN(), None, None
     if combiner is not None:
         words = [int(lib().pm_sharded_record_words(sessions[0].h, n, parallel)) for n in team_sizes(S, ngroups)]
-        ptrs = combiner.prepare(words)
-        bufs = (vp * len(ptrs))(*ptrs)
-        fn = COMBINE_FN(combiner.callback)
-    rc = lib().pm_search_loop_sharded(hs, S, _p(qs, f32p), q, k, step, parallel, ngroups, nthreads, fn, None, bufs,
+        if getattr(combiner, "native", False):   # pm_rccl_combine: the C entry point itself, no Python per step
+            user = combiner.prepare(words)
+            fn = COMBINE_FN(C.cast(lib().pm_rccl_combine, vp).value)
+        else:
+            ptrs = combiner.prepare(words)
+            bufs = (vp * len(ptrs))(*ptrs)
+            fn = COMBINE_FN(combiner.callback)
+    rc = lib().pm_search_loop_sharded(hs, S, _p(qs, f32p), q, k, step, parallel, ngroups, nthreads, fn, user, bufs,
                                       int(model_peers), _p(ans, i64p), C.byref(wall),
                                       on.ctypes.data_as(C.POINTER(dbl)), mt.ctypes.data_as(C.POINTER(dbl)))
     if combiner is not None:

@@ -2,7 +2,9 @@
 // engine (device-resident DB, hints and client state; batched steps), the
 // graphann beam search over PIRGraphInfo, and the extern "C" boundary of
 // include/pacmann.h.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>   // types only: the functions are resolved at run time (rccl_api)
 
 #include <algorithm>
 #include <atomic>
@@ -153,8 +155,13 @@ struct HostBuf {
 // (k_match / k_match_part / k_match_part8; total_ms 0), "host_prep_sets" the
 // re-preprocessing launch sets of the serving loops, with total_ms = the number
 // of clients they folded (a count, not a time).
-enum HostTimer : int { HT_STEP_LAUNCH, HT_STEP_WAIT, HT_STEP_POST, HT_BATCH_QUERY, HT_GVI_PARSE, HT_SEARCH_KNN, HT_KNN_INIT, HT_KNN_BATCH, HT_KNN_UPDATE, HT_KNN_FINAL, HT_WAIT_FIRST, HT_WAIT_ALL, HT_ROWS_SEEN, HT_ROWS_TORN, HT_WAIT_DONE, HT_COMBINE, HT_COMBINE_TURN, HT_PATH_MATCH, HT_PATH_MATCH_PART, HT_PATH_MATCH_PART8, HT_PREP_SETS, HT_COUNT };
-static const char* const kHostTimerName[HT_COUNT] = {"host_step_launch", "host_step_wait", "host_step_post", "host_batch_query", "host_gvi_parse", "host_search_knn", "host_knn_init", "host_knn_batch", "host_knn_update", "host_knn_final", "host_wait_first_token", "host_wait_all_tokens", "host_rows_seen", "host_rows_torn", "host_wait_done", "host_combine", "host_combine_turn", "host_path_match", "host_path_match_part", "host_path_match_part8", "host_prep_sets"};
+// The "host_records_*" entries count the sharded loop's record checks
+// (pm_set_option "verify_records"): answered records equal to the graph's row
+// and the reference-order L2 (verified) or not (bad); unanswered ids explained
+// by the batch layer's overflow drop (dropped), by a failed sub-query of this
+// rank (failed), by another rank's sub-query (peer), or not at all (unexplained).
+enum HostTimer : int { HT_STEP_LAUNCH, HT_STEP_WAIT, HT_STEP_POST, HT_BATCH_QUERY, HT_GVI_PARSE, HT_SEARCH_KNN, HT_KNN_INIT, HT_KNN_BATCH, HT_KNN_UPDATE, HT_KNN_FINAL, HT_WAIT_FIRST, HT_WAIT_ALL, HT_ROWS_SEEN, HT_ROWS_TORN, HT_WAIT_DONE, HT_COMBINE, HT_COMBINE_TURN, HT_PATH_MATCH, HT_PATH_MATCH_PART, HT_PATH_MATCH_PART8, HT_PREP_SETS, HT_REC_VERIFIED, HT_REC_BAD, HT_REC_DROPPED, HT_REC_FAILED, HT_REC_PEER, HT_REC_UNEXPLAINED, HT_COUNT };
+static const char* const kHostTimerName[HT_COUNT] = {"host_step_launch", "host_step_wait", "host_step_post", "host_batch_query", "host_gvi_parse", "host_search_knn", "host_knn_init", "host_knn_batch", "host_knn_update", "host_knn_final", "host_wait_first_token", "host_wait_all_tokens", "host_rows_seen", "host_rows_torn", "host_wait_done", "host_combine", "host_combine_turn", "host_path_match", "host_path_match_part", "host_path_match_part8", "host_prep_sets", "host_records_verified", "host_records_bad", "host_records_dropped", "host_records_failed", "host_records_peer", "host_records_unexplained"};
 
 struct TimedLaunch { std::string name; hipEvent_t a, b; double bytes; };
 
@@ -312,8 +319,12 @@ extern "C" int pm_ctx_mem_info(pm_ctx* c, uint64_t* free_b, uint64_t* total_b) {
   return 0;
 }
 extern "C" int pm_timing_enable(pm_ctx* c, int on) { c->timing = on; return 0; }
+// "verify_records" (sharded loop): check the records of every value-th shared
+// step of each team on the host (0: off); read when a loop starts
+static std::atomic<int> g_verify_records{0};
 extern "C" int pm_set_option(const char* name, int value) {
   if (!name) return fail(PM_EINVAL, "NULL argument");
+  if (!strcmp(name, "verify_records")) { g_verify_records.store(value < 0 ? 0 : value); return 0; }
   if (pmk::set_option(name, value)) return fail(PM_EINVAL, std::string("unknown option ") + name);
   return 0;
 }
@@ -2042,6 +2053,88 @@ static int get_vertex_info(pm_graph* g, bool with_q) {
   return gvi_post(g, with_q, fast);
 }
 
+// ---- the GetGraphInfo plugin surface (graphann/search.go:20-25) ----------
+// PIRGraphInfo's methods (private-search.go:441-531) as batch calls, so a
+// caller that keeps its own beam search (graphann.SearchKNN in Go) still gets
+// the private fetch, the decode and the L2 on the GPU.
+extern "C" int pm_graph_get_metadata(pm_graph* g, uint64_t* n, uint64_t* dim, uint64_t* m) {
+  if (!g) return fail(PM_EINVAL, "NULL argument");
+  if (n) *n = g->n;
+  if (dim) *dim = g->dim;
+  if (m) *m = g->m;
+  return 0;
+}
+
+extern "C" int pm_graph_get_vertex_info(pm_graph* g, const uint64_t* ids, uint64_t n, float* vecs, uint32_t* nbrs,
+                                        uint8_t* ok, const float* query, float* dist) {
+  if (!g || (n && !ids)) return fail(PM_EINVAL, "NULL argument");
+  if (dist && !query) return fail(PM_EINVAL, "dist needs a query");
+  if (g->nshards > 1) return fail(PM_EINVAL, "a sharded graph searches through pm_search_loop_sharded (the shards' combine)");
+  if (!g->nonprivate && !g->pir) return fail(PM_EINVAL, "graph not preprocessed");
+  for (uint64_t i = 0; i < n; ++i)
+    if (ids[i] >= g->n) return fail(PM_EINVAL, "vertex id " + std::to_string(ids[i]) + " out of range");
+  if (n == 0) return 0;
+  HIPCHK(hipSetDevice(g->ctx->device));
+  if (query) HIPCHK(hipMemcpy(g->dq.p, query, g->dim * 4, hipMemcpyHostToDevice));
+  const uint64_t dim = g->dim, m = g->m;
+  uint32_t tmp[64];
+  g->total += n;   // totalQueryNum (:443)
+  if (g->nonprivate) {   // :445-455, BasicGraphInfo-style direct access
+    for (uint64_t i = 0; i < n; ++i) {
+      if (vecs) {
+        if (g->synth) for (uint64_t j = 0; j < dim; ++j) vecs[i * dim + j] = graph_synth_vec(sm64(g->data_seed + DOM_SYNTH_VEC), ids[i], (uint32_t)dim, (uint32_t)j);
+        else memcpy(vecs + i * dim, g->vectors + ids[i] * dim, dim * 4);
+      }
+      if (nbrs) memcpy(nbrs + i * m, g->true_nb(ids[i], tmp), m * 4);
+      if (ok) ok[i] = 1;
+    }
+    if (dist) {
+      g->batch.assign(ids, ids + n);
+      g->nb.resize(n * m);
+      g->dist.assign(n, 0.0f);
+      CHK(gvi_nonprivate(g, true));
+      memcpy(dist, g->dist.data(), n * 4);
+    }
+    return 0;
+  }
+  Engine* e = &g->pir->e;
+  g->rowp.resize(n);
+  std::vector<uint8_t> okv(n);
+  std::vector<float> dv(n);
+  e->rows_partial = false;   // whole rows: the caller reads the vectors too
+  CHK(batch_query(e, ids, n, nullptr, query ? g->qdev() : nullptr, (uint32_t)dim, query ? dv.data() : nullptr,
+                  g->rowp.data(), okv.data()));
+  for (uint64_t i = 0; i < n; ++i) {   // Entry2VectorAndNeighbors (:418-439) + the success count (:483-497)
+    const char* r = (const char*)g->rowp[i];
+    if (vecs) memcpy(vecs + i * dim, r, dim * 4);
+    if (nbrs) memcpy(nbrs + i * m, r + dim * 4, m * 4);
+    if (memcmp(r + dim * 4, g->true_nb(ids[i], tmp), m * 4) == 0) g->succ++;
+    if (ok) ok[i] = okv[i];
+    if (dist) dist[i] = dv[i];
+  }
+  return 0;
+}
+
+extern "C" int pm_graph_get_start_vertex(pm_graph* g, uint64_t cap, uint64_t* ids, float* vecs, uint32_t* nbrs,
+                                         uint64_t* count) {
+  if (!g) return fail(PM_EINVAL, "NULL argument");
+  if (!g->nonprivate && !g->pir) return fail(PM_EINVAL, "graph not preprocessed");
+  const uint64_t ns = g->start.size(), dim = g->dim, m = g->m;
+  if (count) *count = ns;
+  uint32_t tmp[64];
+  const uint64_t kv = sm64(g->data_seed + DOM_SYNTH_VEC);
+  for (uint64_t i = 0; i < ns && i < cap; ++i) {   // non-private (:508-531)
+    const uint64_t x = g->start[i];
+    if (ids) ids[i] = x;
+    if (vecs) {
+      if (g->synth) for (uint64_t j = 0; j < dim; ++j) vecs[i * dim + j] = graph_synth_vec(kv, x, (uint32_t)dim, (uint32_t)j);
+      else memcpy(vecs + i * dim, g->vectors + x * dim, dim * 4);
+    }
+    if (nbrs) memcpy(nbrs + i * m, g->true_nb(x, tmp), m * 4);
+  }
+  return 0;
+}
+
 // SearchKNN (graphann/search.go:114-234).  Same tie rules as oracle/pm_oracle.cpp.
 static int search_knn_impl(pm_graph* g, const float* query, int k, int max_step, int parallel,
                            int benchmarking, int64_t* ids_out, int64_t* steps_out);
@@ -2325,7 +2418,10 @@ struct StepGroup {
   std::vector<pm_graph*> gs;
   uint32_t npos = 0, W = 0, w0 = 0, nb_off = 0;   // ids per session per round, record words, first row word
   DevBuf out_d, map_d, ids_d, rec_own;            // step outputs (device), map, ids; the records if not the caller's
-  uint64_t* rec_d = nullptr;                      // [S*npos*W] records (all-reduced) then [nsub] {status, ref}
+  uint64_t* rec_d = nullptr;                      // [S*npos*W] records + 1 error word (all-reduced)
+  std::atomic<bool> peer_failed{false};           // a combine's error word was nonzero: no further turns
+  uint32_t verify_every = 0;                      // pm_set_option("verify_records") at the loop's start
+  bool combine_dead = false;                      // the collective itself failed / timed out: no further turns
   DevBuf st_d;                                    // ... the status words when the records are the caller's buffer
   HostBuf map_h, ids_h, slow_h, rec_h;
   std::vector<char> slow;                         // sessions served by the multi-step path this round
@@ -2810,28 +2906,38 @@ static int gvi_pre_sharded(pm_graph* g, StepGroup& G, uint32_t s, bool* fast) {
 // After the shared step (group_step): the records of this rank's answers, the
 // multi-step sessions' host-packed records, the modelled peers' records, the
 // combine, and one copy of all records (and the step's statuses) to the host.
-static int group_exchange(StepGroup& G, const std::vector<char>& in) {
+//
+// Failure protocol (every rank must issue the same collectives): the team's
+// records end in ONE error word, 0 from a healthy rank.  A rank whose team (or
+// another team of the same rank: ShardComb::abort) failed still takes the
+// team's next combine turn, with zero records and the error word 1 (poison);
+// every rank then reads a nonzero sum in that turn's records and stops the
+// team there (group_collect_sharded).  So all ranks issue each team's
+// collectives up to the same turn and none is left waiting in a collective.
+static int group_exchange(StepGroup& G, const std::vector<char>& in, bool poison) {
   pm_ctx* c = G.c;
   hipStream_t st = c->stream;
-  const uint32_t nrec = G.S * G.npos, nsub = G.nsub;
+  const uint32_t nrec = G.S * G.npos, nsub = poison ? 0u : G.nsub;
   const uint64_t nw = (uint64_t)nrec * G.W;
   int32_t* map = G.map_h.as<int32_t>();
   for (uint32_t s = 0; s < G.S; ++s)   // client-local sub-query indices -> the shared step's
     for (uint32_t i = 0; i < G.npos; ++i) {
       int32_t& v = map[(uint64_t)s * G.npos + i];
-      if (v >= 0) v = in[s] ? v + (int32_t)G.base[s] : -1;
+      if (poison) v = -1;
+      else if (v >= 0) v = in[s] ? v + (int32_t)G.base[s] : -1;
     }
   HIPCHK(hipMemcpyAsync(G.map_d.p, map, (uint64_t)nrec * 4, hipMemcpyHostToDevice, st));
   uint32_t* st2 = G.st_d.as<uint32_t>();
   const PmOutHdr* hdr = G.out_d.as<PmOutHdr>();
-  const uint64_t* rows = (const uint64_t*)(G.out_d.as<char>() + nsub * sizeof(PmOutHdr));
+  const uint64_t* rows = (const uint64_t*)(G.out_d.as<char>() + (uint64_t)G.nsub * sizeof(PmOutHdr));
   c->timed("pack_records", (double)nw * 8, [&] {
-    pmk::pack_records(st, G.map_d.as<int32_t>(), nrec, hdr, rows, G.E, G.w0, G.W, G.rec_d, nsub, st2); });
-  for (uint32_t s = 0; s < G.S; ++s)
+    pmk::pack_records(st, G.map_d.as<int32_t>(), nrec, hdr, rows, G.E, G.w0, G.W, G.rec_d, nsub, st2,
+                      poison ? 1u : 0u); });
+  for (uint32_t s = 0; s < G.S && !poison; ++s)
     if (G.slow[s])
       HIPCHK(hipMemcpyAsync(G.rec_d + (uint64_t)s * G.npos * G.W, G.slow_h.as<uint64_t>() + (uint64_t)s * G.npos * G.W,
                             (uint64_t)G.npos * G.W * 8, hipMemcpyHostToDevice, st));
-  if (G.comb->model_peers) {
+  if (G.comb->model_peers && !poison) {
     HIPCHK(hipMemcpyAsync(G.ids_d.p, G.ids_h.p, (uint64_t)nrec * 8, hipMemcpyHostToDevice, st));
     const pm_graph* g0 = G.gs[0];
     c->timed("synth_records", 0, [&] {
@@ -2843,23 +2949,105 @@ static int group_exchange(StepGroup& G, const std::vector<char>& in) {
     ShardComb* cb = G.comb;
     const uint64_t turn = G.round * cb->NG + G.team;
     auto tw = Clock::now();
+    // no early exit on cb->abort: a failed team still takes its turn (poisoned);
+    // bounded so a rank whose peer died ends instead of spinning forever
+    static const double limit_s = [] { const char* e = getenv("PM_COMBINE_TIMEOUT_S"); return e ? atof(e) : 600.0; }();
+    uint32_t spins = 0;
     while (cb->ticket.load(std::memory_order_acquire) != turn) {
-      if (cb->abort.load()) return fail(PM_EHIP, "sharded search: another team failed");
+      if (++spins % 1024 == 0 && ms_since(tw) > limit_s * 1e3) {
+        G.combine_dead = true;
+        return fail(PM_EHIP, "sharded search: combine turn " + std::to_string(turn) + " not reached in " +
+                                 std::to_string(limit_s) + " s");
+      }
       std::this_thread::yield();
     }
     c->host_add(HT_COMBINE_TURN, ms_since(tw));
     auto t0 = Clock::now();
     int rc = 0;
-    c->timed("combine", (double)nw * 8, [&] { rc = cb->fn(cb->user, G.team, G.rec_d, nw, (void*)st); });
+    c->timed("combine", (double)nw * 8, [&] { rc = cb->fn(cb->user, G.team, G.rec_d, nw + 1, (void*)st); });
     c->host_add(HT_COMBINE, ms_since(t0));
     cb->ticket.fetch_add(1, std::memory_order_acq_rel);
-    if (rc) return fail(PM_EHIP, "sharded search: the combine callback failed (" + std::to_string(rc) + ")");
+    G.round++;
+    if (rc) {   // the collective itself failed: no further turn of this team can match the peers'
+      G.combine_dead = true;
+      return fail(PM_EHIP, "sharded search: the combine callback failed (" + std::to_string(rc) + ")");
+    }
+  } else {
+    G.round++;
   }
-  HIPCHK(hipMemcpyAsync(G.rec_h.p, G.rec_d, nw * 8, hipMemcpyDeviceToHost, st));
-  if (nsub) HIPCHK(hipMemcpyAsync(G.rec_h.as<uint64_t>() + nw, st2, (uint64_t)nsub * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(G.rec_h.p, G.rec_d, (nw + 1) * 8, hipMemcpyDeviceToHost, st));
+  if (nsub) HIPCHK(hipMemcpyAsync(G.rec_h.as<uint64_t>() + nw + 1, st2, (uint64_t)nsub * 8, hipMemcpyDeviceToHost, st));
   G.seq = c->record_done(st);
-  G.round++;
   return 0;
+}
+
+// L2Dist in the reference's order (l2_distance_amd64.s:4-36 via
+// build_graph.go:119-127): eight lane sums of separately rounded sub / mul /
+// add, ((l0+l1)+(l2+l3))+((l4+l5)+(l6+l7)), then the scalar tail.  Host-side
+// check of the GPU's records only (the translation unit is built without FMA
+// contraction).
+static float l2_reference_order(const float* a, const float* b, uint64_t dim) {
+  const uint64_t dimS = dim & ~7ull;
+  float l[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (uint64_t t = 0; t < dimS; t += 8)
+    for (int k = 0; k < 8; ++k) {
+      const float d = a[t + k] - b[t + k];
+      const float sq = d * d;
+      l[k] = l[k] + sq;
+    }
+  float d = dimS ? ((l[0] + l[1]) + (l[2] + l[3])) + ((l[4] + l[5]) + (l[6] + l[7])) : 0.0f;
+  for (uint64_t i = dimS; i < dim; ++i) {
+    const float x = a[i] - b[i];
+    const float sq = x * x;
+    d = d + sq;
+  }
+  return d;
+}
+
+// The record check (pm_set_option "verify_records"): every answered record of
+// session s's batch against the graph itself (the synthetic spec or the host
+// arrays) — neighbour words bit for bit, and the distance bits against
+// l2_reference_order of the vertex's vector and the session's query — and
+// every unanswered id against its explanation (private-search.go:441-506 over
+// batch-pir.go:170-248).  Counts go to the session's host counters.
+static void verify_records(StepGroup& G, uint32_t s, bool fast, const uint64_t* rec, const uint32_t* st2) {
+  pm_graph* g = G.gs[s];
+  Engine* e = G.es[s];
+  const uint64_t dim = g->dim, m = g->m;
+  const float* q = G.qstage.as<float>() + (uint64_t)s * dim;
+  const uint64_t kv = sm64(g->data_seed + DOM_SYNTH_VEC);
+  std::vector<float> vec(dim);
+  uint32_t tmp[64];
+  for (uint64_t i = 0; i < G.npos; ++i) {
+    const uint64_t* r = rec + ((uint64_t)s * G.npos + i) * G.W;
+    const uint64_t id = (uint64_t)g->batch[i], p = id / e->PS;
+    const bool ok = (r[G.W - 1] >> 32) & 1;
+    if (ok) {
+      const uint32_t* nb = g->true_nb(id, tmp);
+      if (g->synth) for (uint64_t j = 0; j < dim; ++j) vec[j] = graph_synth_vec(kv, id, (uint32_t)dim, (uint32_t)j);
+      else memcpy(vec.data(), g->vectors + id * dim, dim * 4);
+      const float d = l2_reference_order(vec.data(), q, dim);
+      uint32_t dbits;
+      memcpy(&dbits, &d, 4);
+      const bool good = memcmp((const char*)r + G.nb_off, nb, m * 4) == 0 && (uint32_t)r[G.W - 1] == dbits;
+      g->ctx->host_add(good ? HT_REC_VERIFIED : HT_REC_BAD, 0.0);
+      continue;
+    }
+    bool made = false;   // was a sub-query made for it (among the first qn of its partition, batch-pir.go:195-200)?
+    for (uint64_t j = 0; j < e->qn && j < e->pq[p].size(); ++j) made |= e->pq[p][j] == id;
+    HostTimer why = HT_REC_UNEXPLAINED;
+    if (!made) {
+      why = HT_REC_DROPPED;
+    } else if (!e->parts[p].owned) {
+      why = G.comb->model_peers ? HT_REC_UNEXPLAINED : HT_REC_PEER;   // a modelled peer always answers
+    } else if (!fast) {
+      why = HT_REC_FAILED;   // the multi-step path: its sub-queries' statuses stay on the host path
+    } else if (const uint32_t* j = e->resp_map.find(id)) {
+      const uint32_t st = st2[2 * ((uint64_t)G.base[s] + *j)];
+      if (st == ST_ENOHIT || st == ST_ECHUNK || st == ST_EBUDGET) why = HT_REC_FAILED;
+    }
+    g->ctx->host_add(why, 0.0);
+  }
 }
 
 // Session s's share of the exchanged records: host mirrors of its sub-queries
@@ -2875,7 +3063,12 @@ static int group_collect_sharded(StepGroup& G, uint32_t s, bool fast) {
   e->ctx->host_add(HT_STEP_WAIT, ms_since(t_wait));
   const uint64_t nw = (uint64_t)G.S * G.npos * G.W, m = g->m;
   const uint64_t* rec = G.rec_h.as<uint64_t>();
-  const uint32_t* st2 = (const uint32_t*)(rec + nw);
+  if (rec[nw]) {   // the error word: rec[nw] ranks poisoned this turn (group_exchange)
+    G.peer_failed.store(true);
+    return fail(PM_EHIP, "sharded search: " + std::to_string(rec[nw]) + " rank(s) failed; this team stops at the "
+                         "same combine turn on every rank");
+  }
+  const uint32_t* st2 = (const uint32_t*)(rec + nw + 1);
   if (fast) {
     auto tp = Clock::now();
     for (size_t j = 0; j < e->subs.size(); ++j) {
@@ -2899,6 +3092,7 @@ static int group_collect_sharded(StepGroup& G, uint32_t s, bool fast) {
     memcpy(&g->dist[i], &db, 4);
     if (memcmp(nbi, g->true_nb((uint64_t)g->batch[i], tmp), m * 4) == 0) g->succ++;
   }
+  if (G.verify_every && (G.round - 1) % G.verify_every == 0) verify_records(G, s, fast, rec, st2);
   e->rows_partial = false;
   g->ctx->host_add(HT_GVI_PARSE, ms_since(t_parse));
   return 0;
@@ -2909,6 +3103,7 @@ static int group_shard_init(StepGroup& G, pm_graph** gs, uint32_t S, int paralle
   G.comb = comb;
   G.team = team;
   G.round = 0;
+  G.verify_every = (uint32_t)g_verify_records.load();
   G.gs.assign(gs, gs + S);
   const Engine& e = gs[0]->pir->e;
   G.npos = (uint32_t)(parallel * gs[0]->m);
@@ -2922,7 +3117,7 @@ static int group_shard_init(StepGroup& G, pm_graph** gs, uint32_t S, int paralle
     G.rec_d = comb->bufs[team];
     if (!G.rec_d) return fail(PM_EINVAL, "sharded search: NULL team buffer");
   } else {
-    CHK(G.rec_own.reserve(nw * 8));
+    CHK(G.rec_own.reserve((nw + 1) * 8));
     G.rec_d = G.rec_own.as<uint64_t>();
   }
   CHK(G.st_d.reserve(std::max<uint64_t>(8, nrec * 8)));   // at most one sub-query per position
@@ -2931,7 +3126,7 @@ static int group_shard_init(StepGroup& G, pm_graph** gs, uint32_t S, int paralle
   CHK(G.map_h.reserve(nrec * 4));
   CHK(G.ids_h.reserve(nrec * 8));
   CHK(G.slow_h.reserve(nw * 8));
-  CHK(G.rec_h.reserve(nw * 8 + nrec * 8));
+  CHK(G.rec_h.reserve((nw + 1) * 8 + nrec * 8));
   G.slow.assign(S, 0);
   if (!gs[0]->dvec->p) {   // the sessions' start vectors side by side for the team's one k_l2_rows launch
     const uint64_t per = (uint64_t)G.ns * G.dim;
@@ -3034,12 +3229,34 @@ static int run_batched_team(pm_graph** gs, uint32_t S, const float* queries, uin
         }
         bar.wait();
         if (w == 0) {
-          if (!err.load()) {
-            int rc = group_step(G, fast);
-            if (!rc && comb) rc = group_exchange(G, fast);   // records, combine, read-back
-            if (rc) set_err(rc, 0);
+          if (comb && comb->fn) {   // sharded: this round's combine is taken on every rank (see group_exchange)
+            if (G.peer_failed.load() || G.combine_dead) {
+              stop.store(true);
+            } else {
+              bool poison = err.load() != 0 || comb->abort.load();
+              // fault seam (tests/test_shard_search_gpu.py): team 0 fails at shared step PM_FAULT_ROUND
+              static const long fault_round = [] { const char* e = getenv("PM_FAULT_ROUND"); return e ? atol(e) : -1L; }();
+              if (!poison && team == 0 && fault_round >= 0 && G.round == (uint64_t)fault_round) {
+                set_err(fail(PM_EHIP, "injected fault (PM_FAULT_ROUND)"), 0);
+                poison = true;
+              }
+              if (!poison) {
+                const int rc = group_step(G, fast);
+                if (rc) set_err(rc, 0);
+                poison = rc != 0;
+              }
+              const int rx = group_exchange(G, fast, poison);   // records, combine, read-back
+              if (rx) set_err(rx, 0);
+              stop.store(poison || rx != 0);
+            }
+          } else {
+            if (!err.load()) {
+              int rc = group_step(G, fast);
+              if (!rc && comb) rc = group_exchange(G, fast, false);   // records, read-back (no collective)
+              if (rc) set_err(rc, 0);
+            }
+            stop.store(err.load() != 0);
           }
-          stop.store(err.load() != 0);
         }
         bar.wait();
         if (stop.load()) return;
@@ -3072,6 +3289,9 @@ static int run_batched_team(pm_graph** gs, uint32_t S, const float* queries, uin
           if (rc) set_err(rc, 0);
         }
         stop.store(err.load() != 0);
+        // a sharded team that failed here still owes its peers its next combine turn, poisoned
+        if (stop.load() && comb && comb->fn && !G.peer_failed.load() && !G.combine_dead && qi + 1 < q)
+          (void)group_exchange(G, fast, true);
       }
       bar.wait();
       if (stop.load()) return;
@@ -3503,12 +3723,101 @@ extern "C" int pm_search_loop_batched(pm_graph** gs, uint32_t S, const float* qu
   return 0;
 }
 
+// ---- the library-native combine: RCCL over xGMI (no Python on the step path) ----
+// RCCL is resolved with dlopen on first use, not linked: the library loads on
+// CPU-only machines, and a process that already mapped RCCL (torch's ROCm
+// wheel ships librccl.so.1 too) shares that one copy (RTLD_NOLOAD by SONAME).
+struct RcclApi {
+  void* h = nullptr;
+  std::string err;
+  decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+  decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+  decltype(&ncclAllReduce) all_reduce = nullptr;
+  decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  decltype(&ncclGetErrorString) error_string = nullptr;
+};
+static const RcclApi& rccl_api() {
+  static const RcclApi api = [] {
+    RcclApi a;
+    a.h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+    if (!a.h) a.h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!a.h) a.h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!a.h) { const char* e = dlerror(); a.err = e ? e : "dlopen(librccl.so.1) failed"; return a; }
+    a.get_unique_id = (decltype(a.get_unique_id))dlsym(a.h, "ncclGetUniqueId");
+    a.comm_init_rank = (decltype(a.comm_init_rank))dlsym(a.h, "ncclCommInitRank");
+    a.all_reduce = (decltype(a.all_reduce))dlsym(a.h, "ncclAllReduce");
+    a.comm_destroy = (decltype(a.comm_destroy))dlsym(a.h, "ncclCommDestroy");
+    a.error_string = (decltype(a.error_string))dlsym(a.h, "ncclGetErrorString");
+    if (!a.get_unique_id || !a.comm_init_rank || !a.all_reduce || !a.comm_destroy || !a.error_string)
+      a.err = "librccl.so.1 lacks an NCCL entry point";
+    return a;
+  }();
+  return api;
+}
+#define RCCLCHK(call)                                                                              \
+  do {                                                                                             \
+    const ncclResult_t r_ = (call);                                                                \
+    if (r_ != ncclSuccess) return fail(PM_EHIP, std::string(#call ": ") + rccl_api().error_string(r_)); \
+  } while (0)
+
+struct pm_rccl {
+  int device = 0, nranks = 1, rank = 0;
+  std::vector<ncclComm_t> comms;   // one per lock-step team: a team's collectives never wait for another's
+  ~pm_rccl() {
+    for (ncclComm_t c : comms)
+      if (c) (void)rccl_api().comm_destroy(c);
+  }
+};
+
+extern "C" int pm_rccl_unique_id(uint8_t id[PM_RCCL_ID_BYTES]) {
+  if (!id) return fail(PM_EINVAL, "NULL argument");
+  const RcclApi& a = rccl_api();
+  if (!a.err.empty()) return fail(PM_EHIP, "RCCL unavailable: " + a.err);
+  static_assert(sizeof(ncclUniqueId) == PM_RCCL_ID_BYTES, "ncclUniqueId size");
+  ncclUniqueId u;
+  RCCLCHK(a.get_unique_id(&u));
+  memcpy(id, &u, sizeof u);
+  return 0;
+}
+
+extern "C" int pm_rccl_create(int device, int nranks, int rank, const uint8_t* ids, uint32_t nteams, pm_rccl** out) {
+  if (!ids || !out || nteams == 0 || nranks < 1 || rank < 0 || rank >= nranks) return fail(PM_EINVAL, "bad argument");
+  const RcclApi& a = rccl_api();
+  if (!a.err.empty()) return fail(PM_EHIP, "RCCL unavailable: " + a.err);
+  HIPCHK(hipSetDevice(device));
+  std::unique_ptr<pm_rccl> r(new pm_rccl());
+  r->device = device; r->nranks = nranks; r->rank = rank;
+  r->comms.assign(nteams, nullptr);
+  for (uint32_t t = 0; t < nteams; ++t) {   // every rank creates the teams' communicators in the same order
+    ncclUniqueId u;
+    memcpy(&u, ids + (size_t)t * PM_RCCL_ID_BYTES, sizeof u);
+    RCCLCHK(a.comm_init_rank(&r->comms[t], nranks, u, rank));
+  }
+  *out = r.release();
+  return 0;
+}
+
+extern "C" void pm_rccl_destroy(pm_rccl* r) {
+  if (!r) return;
+  (void)hipSetDevice(r->device);
+  delete r;
+}
+
+extern "C" int pm_rccl_combine(void* user, uint32_t team, uint64_t* dev_words, uint64_t nwords, void* stream) {
+  pm_rccl* r = (pm_rccl*)user;
+  if (!r || r->comms.empty() || !dev_words) return fail(PM_EINVAL, "bad argument");
+  // in place, on the team's stream: ordered after the records' pack and before their read-back
+  RCCLCHK(rccl_api().all_reduce(dev_words, dev_words, nwords, ncclUint64, ncclSum, r->comms[team % r->comms.size()],
+                                (hipStream_t)stream));
+  return 0;
+}
+
 // Words of one team's records in pm_search_loop_sharded: sessions x (parallel
 // x m) ids x W, W = the row words holding the neighbour list + 1.
 extern "C" uint64_t pm_sharded_record_words(pm_graph* g, uint32_t sessions, int parallel) {
   if (!g || parallel <= 0) return 0;
   const uint64_t w0 = g->dim * 4 / 8, w1 = (g->dim * 4 + g->m * 4 + 7) / 8;
-  return (uint64_t)sessions * (uint64_t)parallel * g->m * (w1 - w0 + 1);
+  return (uint64_t)sessions * (uint64_t)parallel * g->m * (w1 - w0 + 1) + 1;   // + the error word
 }
 
 // The batched serving loop over a sharded graph DB (every rank calls it with

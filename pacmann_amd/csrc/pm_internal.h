@@ -48,14 +48,17 @@ __host__ __device__ inline uint64_t hash4(uint64_t seed, uint64_t dom, uint64_t 
 // own rows and anyone can recompute any row.  u32 element e of vertex v's
 // PIRGraphInfo entry (private-search.go:363-397: f32[dim] || u32[m]):
 //   e <  dim: float((sm64(kv ^ (v*dim + e)) >> 40) * 2^-24)        (24 random bits, rand.Float32)
-//   e >= dim: x = sm64(kg ^ (v*m + e - dim)) % n, x + 1 (mod n) if x == v
+//   e >= dim: x = sm64(kg ^ (v*m + k) ^ (a << 56)) % n for a = 0, 1, ... until
+//             x != v (k = e - dim; genRandomGraph redraws a self loop, so the
+//             neighbours are uniform over the other n - 1 vertices)
 // with kv = sm64(seed + DOM_SYNTH_VEC), kg = sm64(seed + DOM_SYNTH_NB).
 __host__ __device__ inline float graph_synth_vec(uint64_t kv, uint64_t v, uint32_t dim, uint32_t j) {
   return (float)(sm64(kv ^ (v * dim + j)) >> 40) * 0x1.0p-24f;
 }
 __host__ __device__ inline uint32_t graph_synth_nb(uint64_t kg, uint64_t n, uint64_t v, uint32_t m, uint32_t k) {
-  uint64_t x = sm64(kg ^ (v * m + k)) % n;
-  if (x == v) x = (x + 1) % n;
+  const uint64_t c = v * m + k;
+  uint64_t x = sm64(kg ^ c) % n;
+  for (uint64_t a = 1; x == v; ++a) x = sm64(kg ^ c ^ (a << 56)) % n;   // n > 1 (pm_graph_create_synth)
   return (uint32_t)x;
 }
 __host__ __device__ inline uint32_t graph_synth_elem(uint64_t kv, uint64_t kg, uint64_t n, uint32_t dim, uint32_t m,
@@ -299,9 +302,10 @@ void graph_synth_vecs(hipStream_t st, const uint64_t* ids, uint64_t nids, uint32
 // words [w0, w0 + W - 1) of its answer (the neighbour list) and one word
 // {dist f32 bits | ok << 32}; map[r] = the answering sub-query of the step
 // (a DUP followed to its source) or < 0 (no local answer: zeros).  Also
-// st2[j] = {status, ref} of every sub-query j < nsub (the host's mirrors).
+// st2[j] = {status, ref} of every sub-query j < nsub (the host's mirrors), and
+// the error word rec[nrec * W] = errw (0, or 1 from a failed rank: group_exchange).
 void pack_records(hipStream_t st, const int32_t* map, uint32_t nrec, const PmOutHdr* hdr, const uint64_t* rows,
-                  uint32_t E, uint32_t w0, uint32_t W, uint64_t* rec, uint32_t nsub, uint32_t* st2);
+                  uint32_t E, uint32_t w0, uint32_t W, uint64_t* rec, uint32_t nsub, uint32_t* st2, uint64_t errw);
 // Modelled peers (a shard layout wider than the job): records with map[r] ==
 // -2 are those another shard of the layout answers; they are filled from the
 // synthetic graph's spec, the distance to session r / npos's query (qbuf) in

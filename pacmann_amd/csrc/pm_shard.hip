@@ -47,8 +47,9 @@ __global__ void __launch_bounds__(kBlock) k_pack_records(const int32_t* __restri
                                                          const PmOutHdr* __restrict__ hdr,
                                                          const uint64_t* __restrict__ rows, uint32_t E, uint32_t w0,
                                                          uint32_t W, uint64_t* __restrict__ rec, uint32_t nsub,
-                                                         uint32_t* __restrict__ st2) {
+                                                         uint32_t* __restrict__ st2, uint64_t errw) {
   const uint64_t f = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (f == 0) rec[(uint64_t)nrec * W] = errw;   // the records' error word (pm_engine.cpp group_exchange)
   if (f < (uint64_t)nrec * W) {
     const uint32_t r = (uint32_t)(f / W), w = (uint32_t)(f % W);
     int32_t s = map[r];
@@ -135,11 +136,10 @@ void graph_synth_vecs(hipStream_t st, const uint64_t* ids, uint64_t nids, uint32
                      out);
 }
 void pack_records(hipStream_t st, const int32_t* map, uint32_t nrec, const PmOutHdr* hdr, const uint64_t* rows,
-                  uint32_t E, uint32_t w0, uint32_t W, uint64_t* rec, uint32_t nsub, uint32_t* st2) {
-  const uint64_t nthr = std::max<uint64_t>((uint64_t)nrec * W, nsub);
-  if (!nthr) return;
+                  uint32_t E, uint32_t w0, uint32_t W, uint64_t* rec, uint32_t nsub, uint32_t* st2, uint64_t errw) {
+  const uint64_t nthr = std::max<uint64_t>({(uint64_t)nrec * W, (uint64_t)nsub, 1});
   hipLaunchKernelGGL(k_pack_records, dim3(cdiv_(nthr, kBlock)), dim3(kBlock), 0, st, map, nrec, hdr, rows, E, w0, W,
-                     rec, nsub, st2);
+                     rec, nsub, st2, errw);
 }
 void synth_records(hipStream_t st, const int32_t* map, const uint64_t* ids, uint32_t nrec, uint32_t npos,
                    const float* qbuf, uint32_t dim, uint32_t m, uint64_t n, uint64_t seed, uint32_t w0, uint32_t W,

@@ -191,3 +191,70 @@ class RecordCombiner:
         self._torch.cuda.synchronize(self.device)
         if self.error is not None:
             raise self.error
+
+
+class RcclCombiner:
+    """The library-native combine of pm_search_loop_sharded: RCCL
+    communicators over xGMI inside libpacmann.so (pm_rccl_create), one per
+    lock-step team, and the C entry point pm_rccl_combine as the loop's
+    pm_combine_fn, so no Python and no GIL sit on the per-step path (the
+    RecordCombiner's callback is the alternative through torch.distributed).
+
+    `group`: any torch.distributed group of the ranks (gloo is enough): it only
+    carries rank 0's ncclUniqueIds to the others, once per team count.  The
+    records live in the library's own device buffers."""
+
+    native = True
+
+    def __init__(self, group=None, device: int | None = None):
+        import torch.distributed as dist
+        self._dist = dist
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        if device is None:
+            device = int(os.environ.get("LOCAL_RANK", "0"))
+        self.device = device
+        self.h = None
+        self.nteams = 0
+
+    def prepare(self, words_per_team):
+        """Communicators for len(words_per_team) teams (created collectively on
+        first use or when the team count changes); returns the pm_rccl handle."""
+        import ctypes as C
+
+        import torch
+
+        from . import RCCL_ID_BYTES, _check, lib
+        n = len(words_per_team)
+        if self.h is not None and self.nteams == n:
+            return self.h
+        self.close()
+        ids = np.zeros(n * RCCL_ID_BYTES, dtype=np.uint8)
+        if self.rank == 0:
+            for t in range(n):
+                _check(lib().pm_rccl_unique_id(ids[t * RCCL_ID_BYTES:].ctypes.data_as(C.POINTER(C.c_uint8))))
+        t_ids = torch.from_numpy(ids.view(np.int64).copy())
+        self._dist.broadcast(t_ids, src=self._dist.get_global_rank(self.group, 0) if self.group else 0,
+                             group=self.group)
+        ids = t_ids.numpy().view(np.uint8).copy()
+        h = C.c_void_p()
+        _check(lib().pm_rccl_create(self.device, self.world, self.rank, ids.ctypes.data_as(C.POINTER(C.c_uint8)), n,
+                                    C.byref(h)))
+        self.h, self.nteams = h, n
+        return h
+
+    def finish(self):
+        pass
+
+    def close(self):
+        if self.h is not None:
+            from . import lib
+            lib().pm_rccl_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -409,3 +409,58 @@ def test_group_preprocessing_sift1m_64_clients(ctx):
                 diff = state_diff(grouped[i].export_state(p), alone[i].export_state(p))
                 assert not diff, (epoch, i, p, diff)
         assert grouped[0].stats()["PrepCount"] == alone[0].stats()["PrepCount"] == epoch + 1
+
+
+# ---------------------------------------------------------------------------
+# configs[3] / configs[4]: the sharded private graph search at full size, every
+# record checked (pm_set_option "verify_records": the loop checks each
+# answered record against the graph's spec and the reference-order L2 on the
+# host, and explains each unanswered id)
+# ---------------------------------------------------------------------------
+def _bigann_search_checked(ctx, n, shard, nshards, model_peers, S=4, Q=12):
+    import pacmann_amd as pm
+    base = pm.PIRGraphInfo.Synthetic(n, 128, 32, data_seed=51, shard=shard, nshards=nshards, pir_seed=61,
+                                     search_seed=62, ctx=ctx)
+    base.Preprocess()
+    sess = [base] + [base.Session(61 + i, 62 + i, pm.Context(0)) for i in range(1, S)]
+    for x in sess[1:]:
+        x.Preprocess()
+    qs = np.random.default_rng(63).random((S, Q, 128), dtype=np.float32)   # genRandomMatrix queries
+    for x in sess:
+        x.ctx.timing_reset()
+    pm.set_option("verify_records", 1)
+    try:
+        ans, _, _, _ = pm.search_loop_sharded(sess, qs, 10, 20, 3, 2, 8, model_peers=model_peers)
+    finally:
+        pm.set_option("verify_records", 0)
+
+    def cnt(name):
+        return sum(x.ctx.timing_get("host_records_" + name)[0] for x in sess)
+    c = {k: cnt(k) for k in ("verified", "bad", "dropped", "failed", "peer", "unexplained")}
+    fetched = sum(x.counts()[0] for x in sess)
+    assert fetched == S * Q * 20 * 96
+    assert sum(c.values()) == fetched, c               # every record of every round was checked
+    assert c["bad"] == 0 and c["unexplained"] == 0 and c["peer"] == 0, c
+    assert c["verified"] > 0.6 * fetched, c            # most ids are answered (the rest: overflow, 2^-8 no-hits)
+    assert c["failed"] <= 0.02 * fetched, c
+    assert sum(x.counts()[1] for x in sess) == c["verified"]   # the reference's success count agrees
+    assert (ans >= 0).all()
+    return c
+
+
+def test_sharded_search_bigann_100m_full_size_records(ctx):
+    """configs[3] as the bench serves it on one GPU: the 100M-vertex synthetic
+    graph DB (64 GB generated on the device, CS 8,192 / SS 764 partitions),
+    one rank holding all partitions, 4 sessions in 2 lock-step teams, 12
+    queries each (k 10, step 20, parallel 3): all 92,160 records checked."""
+    _bigann_search_checked(ctx, 100_000_000, 0, 1, False)
+
+
+def test_sharded_search_bigann_1b_shard0_full_size_records(ctx):
+    """configs[4]: shard 0 of the 1B-vertex graph's 8-way layout (partitions 0
+    and 8, 80 GB generated on the device, CS 16,384 / SS 3,816) with the other
+    shards' records generated from the spec (modelled peers): every record the
+    loop consumed — this shard's PIR answers and the modelled ones — equals
+    the graph's row and the reference-order L2, and every unanswered id is an
+    overflow drop or a failed sub-query of this shard."""
+    _bigann_search_checked(ctx, 1_000_000_000, 0, 8, True)

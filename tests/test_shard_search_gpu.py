@@ -44,16 +44,20 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _rank(rank, world, port, out_dir, backend):
+def _rank(rank, world, port, out_dir, backend, fault=None):
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if fault and rank == fault[0]:   # this rank's team 0 fails at shared step fault[1] (pm_engine.cpp fault seam)
+        os.environ["PM_FAULT_ROUND"] = str(fault[1])
     if backend == "nccl":
         torch.cuda.set_device(0)
-    dist.init_process_group(backend, rank=rank, world_size=world)
+    # "native": gloo carries the ncclUniqueIds, the records go through the
+    # library's own RCCL communicators (pm_rccl_combine)
+    dist.init_process_group("gloo" if backend == "native" else backend, rank=rank, world_size=world)
     try:
         import pacmann_amd as pm
-        from pacmann_amd.shard import RecordCombiner
+        from pacmann_amd.shard import RcclCombiner, RecordCombiner
         v, g, qs = _data()
         base = pm.PIRGraphInfo.Shard(v, g, rank, world, pir_seed=SEEDS[0][0], search_seed=SEEDS[0][1],
                                      ctx=pm.Context(0))
@@ -61,14 +65,26 @@ def _rank(rank, world, port, out_dir, backend):
         sess = [base] + [base.Session(p, s_, pm.Context(0)) for p, s_ in SEEDS[1:]]
         for x in sess[1:]:
             x.Preprocess()
-        comb = RecordCombiner(device=0)
-        ans, wall, on, mt = pm.search_loop_sharded(sess, qs, K, 20, 3, NG, 4, combiner=comb)
-        assert comb.calls == Q * 20 * NG, comb.calls   # one combine per shared step of each team
+        comb = RcclCombiner(device=0) if backend == "native" else RecordCombiner(device=0)
+        for x in sess:
+            x.ctx.timing_reset()
+        try:
+            ans, wall, on, mt = pm.search_loop_sharded(sess, qs, K, 20, 3, NG, 4, combiner=comb)
+        except RuntimeError as e:
+            with open(os.path.join(out_dir, f"err{rank}.txt"), "w") as fh:
+                fh.write(str(e))
+            return
+        ncomb = sum(x.ctx.timing_get("host_combine")[0] for x in sess)
+        assert ncomb == Q * 20 * NG, ncomb   # one combine per shared step of each team
+        if backend != "native":
+            assert comb.calls == ncomb, comb.calls
         st = np.array([[*x.counts(), *(x.PIR.stats()[k] for k in ("FinishedBatchNum", "QueriesMadeInPartition",
                                                                   "PrepCount"))] for x in sess])
         np.save(os.path.join(out_dir, f"ans{rank}.npy"), ans)
         np.save(os.path.join(out_dir, f"st{rank}.npy"), st)
     finally:
+        if backend == "native" and "comb" in locals():
+            comb.close()
         dist.destroy_process_group()
 
 
@@ -106,6 +122,31 @@ def test_sharded_search_gloo_world2(oracle):
 
 def test_sharded_search_rccl_world1(oracle):
     _run(1, "nccl", oracle)
+
+
+def test_sharded_search_native_rccl_world1(oracle):
+    """The library-native combine (pm_rccl_combine on communicators created
+    inside libpacmann.so, no Python on the step path) equals the oracle."""
+    _run(1, "native", oracle)
+
+
+def test_sharded_search_rank_failure_gloo_world2():
+    """A failure on one rank mid-search (team 0 of rank 1 at its 7th shared
+    step, through the PM_FAULT_ROUND seam) ends the loop on BOTH ranks with an
+    error instead of leaving rank 0 inside a collective: the failed rank takes
+    its team's next combine turn with the error word set, every rank reads the
+    nonzero sum and stops that team, and the other team stops at its next
+    turn (pm_engine.cpp group_exchange)."""
+    import torch.multiprocessing as mp
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_rank, args=(2, _free_port(), d, "gloo", (1, 7)), nprocs=2, join=True)
+        errs = {}
+        for r in range(2):
+            f = os.path.join(d, f"err{r}.txt")
+            assert os.path.exists(f), f"rank {r} finished without an error"
+            errs[r] = open(f).read()
+    assert "injected" in errs[1], errs
+    assert "rank(s) failed" in errs[0], errs
 
 
 def _synth_materialised(n, dim, m, seed):

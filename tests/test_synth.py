@@ -39,3 +39,25 @@ def test_synthetic_graph_rows():
     assert np.array_equal(v2, v[[999, 3]]) and np.array_equal(nb2, nb[[999, 3]])
     v3, _ = pm.graph_synth_rows(1000, 16, 8, 6, [3])
     assert not np.array_equal(v3, v[[3]])
+
+
+def test_synthetic_graph_neighbour_spec_redraws_self_loops():
+    """The neighbour rule exactly (pm_internal.h graph_synth_nb): draw
+    sm64(kg ^ (v*m + k) ^ (a << 56)) % n for a = 0, 1, ... until it is not v —
+    the redraw of genRandomGraph (private-search.go:54-69), uniform over the
+    other n - 1 vertices.  n = 3 forces many redraws."""
+    import pacmann_amd as pm
+    n, dim, m, seed = 3, 4, 8, 9
+    _, nb = pm.graph_synth_rows(n, dim, m, seed, np.arange(n))
+    kg = sm64(seed + 11)
+    redraws = 0
+    for v in range(n):
+        for k in range(m):
+            c, a = v * m + k, 0
+            x = sm64(kg ^ c) % n
+            while x == v:
+                a += 1
+                redraws += 1
+                x = sm64(kg ^ c ^ (a << 56)) % n
+            assert nb[v, k] == x, (v, k)
+    assert redraws > 0
