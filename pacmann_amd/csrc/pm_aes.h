@@ -175,4 +175,33 @@ __device__ __forceinline__ uint32_t prf_lo16_split(const AesLane& A, const uint3
   const uint32_t t1 = aes_x3(aes_x3(A.Tk<0>(s1), A.T2k<2>(s3), rk[37]), rotl32(A.Tk<1>(s2) ^ A.T2k<3>(s0), 8), 0u);
   return ((A.Sk<0>(t0) | (A.Sk<1>(t1) << 8)) ^ rk[40] ^ x) & 0xffffu;
 }
+// Chunks x < 256 (SetSize <= 256: SIFT1M's 124, MS-MARCO's 196): after the
+// whitening only byte 0 of s0 depends on x, so of round 1's output only column
+// 0 does (u0; u1..u3 see bytes 3, 2, 1 of s0).  Then every column of round 2
+// takes exactly one byte of that column and three bytes fixed by the hint:
+//   t0 = Te0[s0.b0]        ^ k0    t1 = rotl8(Te2[s0.b3]) ^ k1
+//   t2 = Te2[s0.b2]        ^ k2    t3 = rotl8(Te0[s0.b1]) ^ k3
+// (rotl8 is linear over XOR).  R2Hint holds k0..k3, 12 lookups once per hint;
+// a PRF then costs 4 round-2 lookups instead of 16: 112 per PRF instead of
+// 122.5, bit for bit the same function.
+struct R2Hint { uint32_t k0, k1, k2, k3; };
+__device__ __forceinline__ R2Hint r2_hint(const AesLane& A, const uint32_t* __restrict__ rk, const R1Uniform& u,
+                                          const R1Lane& v) {
+  const uint32_t s1 = u.u1 ^ v.v1, s2 = u.u2 ^ v.v2, s3 = u.u3 ^ v.v3;   // the same for every x < 256
+  return R2Hint{A.T2k<2>(s2) ^ rk[8] ^ rotl32(A.Tk<1>(s1) ^ A.T2k<3>(s3), 8),
+                A.Tk<0>(s1) ^ A.T2k<2>(s3) ^ rk[9] ^ rotl32(A.Tk<1>(s2), 8),
+                A.Tk<0>(s2) ^ rk[10] ^ rotl32(A.Tk<1>(s3) ^ A.T2k<3>(s1), 8),
+                A.Tk<0>(s3) ^ A.T2k<2>(s1) ^ rk[11] ^ rotl32(A.T2k<3>(s2), 8)};
+}
+// = prf_lo16_split(A, rk, u, v, x) for x < 256, given u0 = r1_uniform(x).u0 and r2_hint.
+__device__ __forceinline__ uint32_t prf_lo16_r2(const AesLane& A, const uint32_t* __restrict__ rk, uint32_t u0,
+                                                const R1Lane& v, const R2Hint& k, uint32_t x) {
+  const uint32_t s = u0 ^ v.v0;
+  uint32_t s0 = A.Tk<0>(s) ^ k.k0, s1 = rotl32(A.T2k<3>(s), 8) ^ k.k1;
+  uint32_t s2 = A.T2k<2>(s) ^ k.k2, s3 = rotl32(A.Tk<1>(s), 8) ^ k.k3;
+  aes_rounds<3, 9>(A, rk, s0, s1, s2, s3);
+  const uint32_t t0 = aes_x3(aes_x3(A.Tk<0>(s0), A.T2k<2>(s2), rk[36]), rotl32(A.Tk<1>(s1) ^ A.T2k<3>(s3), 8), 0u);
+  const uint32_t t1 = aes_x3(aes_x3(A.Tk<0>(s1), A.T2k<2>(s3), rk[37]), rotl32(A.Tk<1>(s2) ^ A.T2k<3>(s0), 8), 0u);
+  return ((A.Sk<0>(t0) | (A.Sk<1>(t1) << 8)) ^ rk[40] ^ x) & 0xffffu;
+}
 }  // namespace pm

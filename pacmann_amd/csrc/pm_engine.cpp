@@ -30,34 +30,39 @@ using namespace pm;
 // Open-addressing uint64 -> uint32 map with O(1) clear (generation stamps).
 // Replaces node-allocating std::unordered_map on the per-round host path
 // (knownVertices, the batch response map, the per-partition localCache index).
+// One 16-B slot {key, value, generation} per entry: a probe touches one cache
+// line (the serving loop's session state is cold when its task runs, so the
+// probes are cache misses; prefetch() issues a key's line ahead of a batch).
 struct FlatMap {
-  std::vector<uint64_t> key;
-  std::vector<uint32_t> val, gen;
+  struct Slot { uint64_t key; uint32_t val, gen; };
+  std::vector<Slot> slot;
   uint32_t cur = 1, count = 0, mask = 0;
   explicit FlatMap(uint32_t cap_pow2 = 256) { rehash(cap_pow2); }
   static uint64_t mix(uint64_t x) { x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; return x; }
   void rehash(uint32_t cap) {
-    std::vector<uint64_t> k0; std::vector<uint32_t> v0, g0;
-    k0.swap(key); v0.swap(val); g0.swap(gen);
-    key.assign(cap, 0); val.assign(cap, 0); gen.assign(cap, 0);
+    std::vector<Slot> s0;
+    s0.swap(slot);
+    slot.assign(cap, Slot{0, 0, 0});
     mask = cap - 1; count = 0;
     const uint32_t old = cur; cur = 1;
-    for (size_t i = 0; i < k0.size(); ++i) if (g0[i] == old) put(k0[i], v0[i]);
+    for (const Slot& x : s0) if (x.gen == old) put(x.key, x.val);
   }
-  void clear() { if (++cur == 0) { std::fill(gen.begin(), gen.end(), 0); cur = 1; } count = 0; }
-  void reserve(uint32_t n) { uint32_t c = (uint32_t)key.size(); while (c < 2 * n) c *= 2; if (c != key.size()) rehash(c); }
-  // returns pointer to the value (inserting `v` if absent) and whether it was inserted
+  void clear() { if (++cur == 0) { for (Slot& x : slot) x.gen = 0; cur = 1; } count = 0; }
+  void reserve(uint32_t n) { uint32_t c = (uint32_t)slot.size(); while (c < 2 * n) c *= 2; if (c != slot.size()) rehash(c); }
+  void prefetch(uint64_t k) const { __builtin_prefetch(&slot[(uint32_t)mix(k) & mask]); }
   uint32_t* find(uint64_t k) {
     for (uint32_t i = (uint32_t)mix(k) & mask;; i = (i + 1) & mask) {
-      if (gen[i] != cur) return nullptr;
-      if (key[i] == k) return &val[i];
+      Slot& x = slot[i];
+      if (x.gen != cur) return nullptr;
+      if (x.key == k) return &x.val;
     }
   }
   void put(uint64_t k, uint32_t v) {   // insert or overwrite
-    if (2 * (count + 1) > key.size()) rehash((uint32_t)key.size() * 2);
+    if (2 * (count + 1) > slot.size()) rehash((uint32_t)slot.size() * 2);
     for (uint32_t i = (uint32_t)mix(k) & mask;; i = (i + 1) & mask) {
-      if (gen[i] != cur) { gen[i] = cur; key[i] = k; val[i] = v; ++count; return; }
-      if (key[i] == k) { val[i] = v; return; }
+      Slot& x = slot[i];
+      if (x.gen != cur) { x.gen = cur; x.key = k; x.val = v; ++count; return; }
+      if (x.key == k) { x.val = v; return; }
     }
   }
   bool emplace(uint64_t k, uint32_t v) {   // insert if absent; true if inserted
@@ -837,6 +842,18 @@ static int wait_step(pm_ctx* c, const PmOutHdr* hdr, uint32_t nsub, uint32_t tok
   };
   if (c->debug_sync) {
     HIPCHK(hipStreamSynchronize(stream));
+  } else if (ordered && !c->timing) {
+    // the results are taken after the step's completion event anyway: wait for
+    // it first, then ONE pass over the tokens and row hashes below (the serving
+    // loop opens a team's phase only once the event has completed, so this is
+    // no wait at all there)
+    for (uint32_t s = 0; s < nsub; ++s) {
+      __builtin_prefetch(&hdr[s]);
+      if (c->rows_check)
+        for (size_t w = w0; w < w1; w += 8) __builtin_prefetch(rows + s * row_bytes + w * 8);
+    }
+    CHK(wait_done(sc, seq));
+    std::atomic_thread_fence(std::memory_order_acquire);
   } else {
     const volatile uint32_t* tok = &hdr[0].token;
     const size_t stride = sizeof(PmOutHdr) / sizeof(uint32_t);
@@ -1410,6 +1427,12 @@ static int bq_prepare(Engine* g, const uint64_t* idx, uint64_t n, bool* fast) {
   }
   *fast = !any_slow && qn <= pmk::step_max_sub_per_part() && qn > 0;
   if (*fast) {
+    // the localCache slots every real sub-query looks up (add_sub), requested
+    // together: the session's state is cold when the serving loop reaches it
+    for (uint64_t p = 0; p < P; ++p)
+      if (g->parts[p].owned)
+        for (uint64_t j = 0; j < qn; ++j)
+          if (g->pq[p][j] != kDefaultValue) g->parts[p].cache.prefetch(g->pq[p][j] - p * g->PS);
     begin_step(g);
     for (uint64_t p = 0; p < P; ++p) {
       for (uint64_t j = 0; j < qn; ++j) {
@@ -2233,6 +2256,11 @@ static void knn_batch(pm_graph* g, int parallel, int benchmarking) {
 static void knn_update(pm_graph* g, int step) {
   auto t_round = Clock::now();
   const uint64_t m = g->m;
+  for (size_t i = 0; i < g->batch.size(); ++i) g->known.prefetch((uint64_t)g->batch[i]);
+  if (g->known_id.capacity() < 4096) {   // a search keeps ~2,000 known vertices (20 steps x 96 ids)
+    g->known_id.reserve(4096); g->known_dist.reserve(4096); g->known_reach.reserve(4096);
+    g->known_nb.reserve(4096 * m);
+  }
   for (size_t i = 0; i < g->batch.size(); ++i) {
     const int64_t id = g->batch[i];
     if (g->known.find((uint64_t)id)) continue;
@@ -2752,6 +2780,8 @@ static int group_step(StepGroup& G, const std::vector<char>& in) {
 static int group_collect(StepGroup& G, uint32_t s) {
   Engine* e = G.es[s];
   const uint32_t n = (uint32_t)e->subs.size();
+  for (uint32_t j = 0; j < n; ++j)   // the localCache slots post_results fills, requested ahead
+    if (e->subs[j].kind == SUB_REAL) e->parts[e->subs[j].part].cache.prefetch(e->subs[j].idx);
   PmOutHdr* hdr = G.out_h.as<PmOutHdr>();
   uint64_t* rows = (uint64_t*)(G.out_h.as<char>() + (size_t)G.nsub * sizeof(PmOutHdr));
   auto t_wait = Clock::now();
@@ -3516,6 +3546,14 @@ static int run_batched_pool(pm_graph** gs, uint32_t S, const float* queries, uin
     if (t.begin) {
       knn_begin_finish(g, parallel, 0, t.G.qstage.as<float>() + (uint64_t)t.S * dim + (uint64_t)i * t.G.ns);
     } else {
+      if (g->graph) {   // the ground-truth rows of the success check (gvi_post), requested before the results' reads
+        const uint64_t m = g->m;
+        for (size_t b = 0; b < g->batch.size(); ++b) {
+          const char* gr = (const char*)&g->graph[(uint64_t)g->batch[b] * m];
+          __builtin_prefetch(gr);
+          __builtin_prefetch(gr + m * 4 - 1);
+        }
+      }
       if (t.fast[i]) CHK(group_collect(t.G, i));   // complete: only the tokens and host mirrors
       CHK(gvi_post(g, true, t.fast[i]));
       knn_update(g, t.st);

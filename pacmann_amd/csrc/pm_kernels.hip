@@ -63,6 +63,9 @@ __global__ void __launch_bounds__(kOffsBlock) k_prep_offsets(const PmPart* __res
   const uint32_t own = h >= P.PH ? (h - P.PH) / P.Qpc : 0xffffffffu;
   uint16_t* o = P.tab;
   const R1Lane r1v = r1_lane(A, P.rk, h);   // initial tag of hint h is h
+  // SetSize <= 256: round 2's hint-only part once per hint (pm_aes.h r2_hint)
+  const bool r2 = SS <= 256;
+  const R2Hint r2k = r2 ? r2_hint(A, P.rk, r1u[0][0], r1v) : R2Hint{0, 0, 0, 0};
   static_assert(kOffsChunksPerBlock == 8, "one 16-B tabT tile of 8 chunks per thread");
   for (int tl = 0; tl < kOffsTiles; ++tl) {
     const uint32_t c0 = cb + tl * kOffsChunksPerBlock;
@@ -72,7 +75,8 @@ __global__ void __launch_bounds__(kOffsBlock) k_prep_offsets(const PmPart* __res
 #pragma unroll
     for (int j = 0; j < 8; ++j) tile[j] = kSkip;   // chunks past SetSize: padding
     for (uint32_t c = c0; c < c1; ++c) {
-      uint16_t v = (uint16_t)(prf_lo16_split(A, P.rk, r1u[tl][c - c0], r1v, c) & mask);
+      uint16_t v = (uint16_t)((r2 ? prf_lo16_r2(A, P.rk, r1u[tl][c - c0].u0, r1v, r2k, c)
+                                  : prf_lo16_split(A, P.rk, r1u[tl][c - c0], r1v, c)) & mask);
       v = (c == own) ? kSkip : v;
       if (o) o[(uint64_t)c * H + h] = v;   // chunk-major (only the folds that stage it read it)
       tile[c - c0] = v;
