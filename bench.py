@@ -818,6 +818,8 @@ def main():
                     help="time every kernel with events inside the timed region itself (round-3 behaviour: "
                          "the events cost 5-7 %% of the rate) instead of in a separate pass")
     ap.add_argument("--no-msmarco-search", action="store_true", help="skip the MS-MARCO d=192 private-search block")
+    ap.add_argument("--stagger-teams", action="store_true",
+                    help="desynchronise the teams' maintenance windows (extra warm-up queries per team)")
     ap.add_argument("--graph", choices=["built", "random"], default="built",
                     help="GPU-built kNN+robustPrune graph (default) or the reference's synthetic random graph")
     args = ap.parse_args()
@@ -851,6 +853,26 @@ def main():
         return pm.search_loop_sessions(sess, qq, K_TOP, STEP, PARALLEL)
     if args.warmup:
         serve(qsess[:, :args.warmup])
+    stagger = None
+    if args.stagger_teams and args.mode == "batched" and args.groups > 1:
+        # Desynchronise the teams' maintenance windows (a server's clients do not
+        # all re-preprocess at the same query): team g serves g * step extra
+        # warm-up queries, so its trigger (private-search.go:226-232, every 23
+        # queries) falls `g * step` queries earlier inside the timed region, and
+        # the other teams keep querying while its maintenance runs.  Every
+        # session still re-preprocesses exactly once in the region (asserted in
+        # maintenance_in_region).
+        window = int(base.PIR.stats()["SupportBatchNum"] // (STEP * PARALLEL))
+        stride = max(1, min(args.steps, window) // args.groups)
+        stagger = {"teams": args.groups, "extra_warmup_queries_per_team": []}
+        G = args.groups
+        for g in range(1, G):
+            s0, s1 = S * g // G, S * (g + 1) // G
+            extra = g * stride
+            xq = make_queries(v, (s1 - s0) * extra, seed=7000 + g).reshape(s1 - s0, extra, -1)
+            pm.search_loop_batched(sess[s0:s1], xq, K_TOP, STEP, PARALLEL, 1, min(args.threads, s1 - s0))
+            stagger["extra_warmup_queries_per_team"].append(extra)
+        stagger["extra_warmup_queries_per_team"].insert(0, 0)
     progress(f"SIFT1M: {S} sessions ready, warm-up done; timed region")
 
     # `value` is measured with no per-launch events (timing level 0): the
@@ -906,6 +928,9 @@ def main():
         tk = time.perf_counter() - tk
         for c in ctxs:
             c.timing(False)
+        if os.environ.get("PM_TIMELINE"):   # diagnostics: the pass's GPU timeline (tools/timeline.py)
+            for c in ctxs:
+                c.timing_timeline(os.environ["PM_TIMELINE"])
         ktime = {k: tsum(k) for k in KERNELS}
         kt_pass = {"queries_per_session": KT_QUERIES, "wall_s": round(tk, 4),
                    "private_queries_per_s": round(S * KT_QUERIES / tk, 2),
@@ -1101,6 +1126,7 @@ def main():
                                           "steady state's (steps shorter than a window)"
                                           if prep_in_region < S else "at least one per session"},
         "kernel_timing_pass": kt_pass,
+        "maintenance_stagger": stagger,
         # result rows the host read at token time vs those whose bytes did not yet
         # match their header hash then; results are taken only after the step's
         # completion event (system-scope release), where a mismatch is an error

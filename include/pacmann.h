@@ -77,6 +77,10 @@ int pm_timing_enable(pm_ctx* ctx, int level);
  * PM_MATCH_PART8, PM_MATCH_RESOLVE).  PM_EINVAL for an unknown name. */
 int pm_set_option(const char* name, int value);
 int pm_timing_reset(pm_ctx* ctx);
+/* Diagnostics: append one line "kernel,start_us,end_us,ctx" per timed launch
+ * of ctx (level >= 2 timing) to the file at `path`, on one time axis for every
+ * context of the process (the GPU timeline of a serving run). */
+int pm_timing_timeline(pm_ctx* ctx, const char* path);
 int pm_timing_get(pm_ctx* ctx, const char* kernel, uint64_t* launches, double* total_ms,
                   double* alg_bytes);
 

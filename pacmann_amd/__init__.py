@@ -73,6 +73,7 @@ SIGNATURES = {
     "pm_set_option": (C.c_int, [C.c_char_p, C.c_int]),
     "pm_timing_reset": (C.c_int, [vp]),
     "pm_timing_get": (C.c_int, [vp, C.c_char_p, u64p, C.POINTER(dbl), C.POINTER(dbl)]),
+    "pm_timing_timeline": (C.c_int, [vp, C.c_char_p]),
     "pm_expand_key": (C.c_int, [u8p, u32p]),
     "pm_prf_batch": (C.c_int, [vp, u32p, u64p, u64p, u64, u64p]),
     "pm_l2_batch": (C.c_int, [vp, f32p, f32p, u64, u64, f32p]),
@@ -164,6 +165,8 @@ def lib() -> C.CDLL:
                                "(there is no CPU fallback)")
         L = C.CDLL(str(LIB_PATH))
         for name, (res, args) in SIGNATURES.items():
+            if _os.environ.get("PM_LIB") and not hasattr(L, name):
+                continue   # an older diagnostic build (A/B runs): its missing entry points stay unbound
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
@@ -229,6 +232,10 @@ class Context:
 
     def timing_reset(self):
         _check(lib().pm_timing_reset(self.h))
+
+    def timing_timeline(self, path: str):
+        """Append this context's timed launches (start/end on the process's time axis) to `path`."""
+        _check(lib().pm_timing_timeline(self.h, str(path).encode()))
 
     def timing_get(self, kernel: str):
         n = C.c_uint64()

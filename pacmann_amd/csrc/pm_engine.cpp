@@ -323,7 +323,40 @@ extern "C" int pm_ctx_mem_info(pm_ctx* c, uint64_t* free_b, uint64_t* total_b) {
   if (total_b) *total_b = t;
   return 0;
 }
-extern "C" int pm_timing_enable(pm_ctx* c, int on) { c->timing = on; return 0; }
+// Timeline base: one event recorded when kernel timing is first enabled in the
+// process; every timed launch's start / end can then be placed on one time axis
+// (hipEventElapsedTime between events of one device, any streams).
+static std::mutex g_tl_mu;
+static hipEvent_t g_tl_base = nullptr;
+extern "C" int pm_timing_enable(pm_ctx* c, int on) {
+  c->timing = on;
+  if (on >= 2) {
+    std::lock_guard<std::mutex> lk(g_tl_mu);
+    if (!g_tl_base) {
+      HIPCHK(hipEventCreate(&g_tl_base));
+      HIPCHK(hipEventRecord(g_tl_base, c->stream));
+    }
+  }
+  return 0;
+}
+// Diagnostics: append "name,start_us,end_us,ctx" for every timed launch of c
+// (relative to the process's timeline base) to `path`.
+extern "C" int pm_timing_timeline(pm_ctx* c, const char* path) {
+  if (!c || !path) return fail(PM_EINVAL, "NULL argument");
+  HIPCHK(hipStreamSynchronize(c->stream));
+  std::lock_guard<std::mutex> lk(g_tl_mu);
+  if (!g_tl_base) return fail(PM_EINVAL, "no timeline (kernel timing level 2 never enabled)");
+  FILE* f = fopen(path, "a");
+  if (!f) return fail(PM_EINVAL, std::string("cannot open ") + path);
+  for (auto& t : c->launches) {
+    float a = 0, b = 0;
+    if (hipEventElapsedTime(&a, g_tl_base, t.a) != hipSuccess || hipEventElapsedTime(&b, g_tl_base, t.b) != hipSuccess)
+      continue;
+    fprintf(f, "%s,%.3f,%.3f,%p\n", t.name.c_str(), a * 1e3, b * 1e3, (void*)c);
+  }
+  fclose(f);
+  return 0;
+}
 // "verify_records" (sharded loop): check the records of every value-th shared
 // step of each team on the host (0: off); read when a loop starts
 static std::atomic<int> g_verify_records{0};
@@ -2774,6 +2807,24 @@ static int group_step(StepGroup& G, const std::vector<char>& in) {
   return 0;
 }
 
+// The lines session s's collect will read (its result headers and the row
+// words the host reads, its localCache slots, its ids' ground-truth rows),
+// requested one task ahead by the worker that will most likely take it: the
+// misses then resolve while the worker serves the session before it.
+static void prefetch_session(StepGroup& G, uint32_t s, const pm_graph* g) {
+  const Engine* e = G.es[s];
+  const uint32_t n = (uint32_t)e->subs.size();
+  const PmOutHdr* hdr = G.out_h.as<PmOutHdr>() + G.base[s];
+  const char* rows = G.out_h.as<char>() + (size_t)G.nsub * sizeof(PmOutHdr) + (size_t)G.base[s] * G.E * 8;
+  for (uint32_t j = 0; j < n; j += 2) __builtin_prefetch(hdr + j);
+  for (uint32_t j = 0; j < n; ++j)
+    for (uint32_t w = G.pf_w0; w < G.pf_w1; w += 8) __builtin_prefetch(rows + ((size_t)j * G.E + w) * 8);
+  for (uint32_t j = 0; j < n; ++j)
+    if (e->subs[j].kind == SUB_REAL) e->parts[e->subs[j].part].cache.prefetch(e->subs[j].idx);
+  if (g->graph)
+    for (size_t b = 0; b < g->batch.size(); ++b) __builtin_prefetch(&g->graph[(uint64_t)g->batch[b] * g->m]);
+}
+
 // Session s's share of the last shared step: wait for its results (tokens and
 // row checksums, polled by the session's own worker, so a team checks its
 // sub-queries in parallel) and update its host mirrors.
@@ -3546,6 +3597,8 @@ static int run_batched_pool(pm_graph** gs, uint32_t S, const float* queries, uin
     if (t.begin) {
       knn_begin_finish(g, parallel, 0, t.G.qstage.as<float>() + (uint64_t)t.S * dim + (uint64_t)i * t.G.ns);
     } else {
+      // the next session of this worker's lane, one task ahead (prefetch_session)
+      if (i + T < t.S && t.fast[i + T] && !t.G.comb) prefetch_session(t.G, i + T, t.gs[i + T]);
       if (g->graph) {   // the ground-truth rows of the success check (gvi_post), requested before the results' reads
         const uint64_t m = g->m;
         for (size_t b = 0; b < g->batch.size(); ++b) {
