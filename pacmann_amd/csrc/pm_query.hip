@@ -2135,6 +2135,271 @@ __global__ void __launch_bounds__(NT, PM_ANSWER_WGS) k_answer_s(PmStep S) {
   answer_role<W, false, NT>(S, blockIdx.x, L);
 }
 
+// ---- k_answer_p: two sub-queries per workgroup, software-pipelined --------
+// k_answer_s at the batched serving shape (6,144 sub-queries over 4,096
+// resident slots) starts every resident workgroup in its latency phases at
+// once (record + query set, then decode and publication), so HBM idles at the
+// kernel's start, between the two rounds of workgroups and at its end: 75 us
+// alone for 332 MB, where the bare gather of 480 MB takes 66 us
+// (tools/gather_bench.hip, fresh rows every launch).  Here a workgroup owns
+// sub-queries A = blockIdx.x and B = blockIdx.x + gridDim.x (grid = nsub / 2:
+// every workgroup resident from the start), loads both records and query sets
+// in one round trip, gathers A, issues B's first row batch, and decodes and
+// publishes A while those rows are in flight: B's prologue hides behind A's
+// gather and A's epilogue behind B's first batch.  Same results as
+// answer_role (pre-expanded query sets, S.qset; no split gather).
+constexpr int kAnsPNT = 128;
+template <int NT>
+struct AnswerPLds {
+  __attribute__((aligned(16))) uint16_t qo[2][kSmallSS];
+  uint64_t red[NT * 2];
+  __attribute__((aligned(16))) RowBufT<kSmallE> row;
+  uint32_t s_last;
+};
+struct AnsQ {   // one sub-query's operands in k_answer_p
+  uint32_t s, part, mode;
+  PmRes r;
+  uint64_t idx;   // the sub-query's index (DUMMY: the dummy counter)
+  uint64_t e_rv, e_bp, e_pp;
+  uint32_t e_cur;
+  float q0, q1;
+};
+template <int W, int NT>
+__device__ __forceinline__ void ansp_decode_ops(const PmStep& S, AnsQ& a) {
+  const PmPart& P = S.parts[a.part];
+  const uint32_t tid = threadIdx.x, E = S.E;
+  a.e_rv = a.e_bp = a.e_pp = 0;
+  a.e_cur = kSkip;
+  if (a.mode != A_FINAL) return;
+  const PmRes& r = a.r;
+  const uint64_t dslot = (uint64_t)r.chunk * P.Qpc + r.ing;
+  if (!(r.flags & 2u) && tid < P.SS) a.e_cur = P.tabT[tabT_index(P.H, P.PH + r.chunk * P.Qpc + r.ing, tid)];
+  if (tid < E) {
+    a.e_rv = P.rval[dslot * E + tid];
+    a.e_bp = P.parity[((uint64_t)P.PH + dslot) * E + tid];
+    a.e_pp = P.parity[(uint64_t)r.hit * E + tid];
+  }
+}
+// the query set of a gathering sub-query into qo (pre-expanded, or the dummy's)
+__device__ __forceinline__ void ansp_set(const PmStep& S, const AnsQ& a, uint4 qpv, uint16_t* qo) {
+  const uint32_t tid = threadIdx.x;
+  if (a.mode == A_FINAL || a.mode == A_CHAINED) {
+    if (tid < S.qw / 8) *reinterpret_cast<uint4*>(qo + 8 * tid) = qpv;
+  } else if (a.mode == A_DUMMY) {
+    const PmPart& P = S.parts[a.part];
+    const uint32_t mask = P.CS - 1;
+    for (uint32_t i = tid; i < P.SS; i += blockDim.x) qo[i] = (uint16_t)(hash4(P.seed, DOM_DUMMY, P.idx, a.idx, i) & mask);
+  }
+}
+template <int W, int NT, int KG>
+struct AnsGather {   // one thread's share of a sub-query's XOR gather (HOT LOOP E)
+  typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+  uint32_t seg, sl, nsl;
+  uint64_t a0 = 0, a1 = 0;
+  u64x2 x[KG];
+  __device__ __forceinline__ void init(uint32_t E) {
+    const uint32_t NSEG = (E & ~3u) / W;   // <= NT at the shapes this kernel serves (E <= kSmallE, W 2)
+    nsl = NT / NSEG;
+    sl = threadIdx.x / NSEG;
+    seg = threadIdx.x % NSEG;
+  }
+  // batch b: rows i = sl + (b * KG + u) * nsl
+  __device__ __forceinline__ void load(const PmStep& S, const PmPart& P, const uint16_t* qo, uint32_t b) {
+    const uint32_t i0 = sl + b * KG * nsl;
+    uint32_t rr[KG];
+#pragma unroll
+    for (int u = 0; u < KG; ++u) rr[u] = qo[min(i0 + u * nsl, P.SS - 1)];
+#pragma unroll
+    for (int u = 0; u < KG; ++u) {
+      const uint32_t i = i0 + u * nsl;
+      rr[u] = (sl < nsl && i < P.SS) ? i * P.CS + rr[u] : ~0u;
+    }
+    const PM_G uint64_t* base = S.db + P.row0 * S.E;
+#pragma unroll
+    for (int u = 0; u < KG; ++u) {
+      x[u] = u64x2{0, 0};
+      if (rr[u] < P.N) {
+        const PM_G uint64_t* q = base + (uint64_t)rr[u] * S.E + (uint64_t)seg * W;
+        if (W == 2) x[u] = *reinterpret_cast<const PM_G u64x2*>(q);
+        else x[u].x = *q;
+      }
+    }
+  }
+  __device__ __forceinline__ void fold() {
+#pragma unroll
+    for (int u = 0; u < KG; ++u) { a0 ^= x[u].x; a1 ^= x[u].y; }
+  }
+  __device__ __forceinline__ uint32_t batches(const PmPart& P) const { return (P.SS + KG * nsl - 1) / (KG * nsl); }
+  // the slices' partial XORs -> row.w[0 .. E & ~3)
+  template <class LDS>
+  __device__ __forceinline__ void reduce(LDS& L, uint32_t E) {
+    const uint32_t tid = threadIdx.x, NSEG = (E & ~3u) / W;
+    L.red[tid * 2] = a0;
+    L.red[tid * 2 + 1] = a1;
+    __syncthreads();
+    if (tid < NSEG) {
+      uint64_t x0 = 0, x1 = 0;
+      for (uint32_t k = 0; k < nsl; ++k) {
+        x0 ^= L.red[(k * NSEG + tid) * 2];
+        x1 ^= L.red[(k * NSEG + tid) * 2 + 1];
+      }
+      L.row.w[tid * W] = x0;
+      if (W == 2) L.row.w[tid * W + 1] = x1;
+    }
+    __syncthreads();
+  }
+};
+// decode + refresh, publication and the refresh-chain arrival of sub-query a
+// whose gathered row is in L.row (answer_role's epilogue)
+template <int W, int NT, class LDS>
+__device__ __forceinline__ void ansp_epilogue(const PmStep& S, const AnsQ& a, LDS& L) {
+  const PmPart& P = S.parts[a.part];
+  const PmRes& r = a.r;
+  const uint32_t tid = threadIdx.x, E = S.E, EX = E & ~3u, s = a.s, mode = a.mode;
+  auto& row = L.row;
+  const uint64_t dslot = (uint64_t)r.chunk * P.Qpc + r.ing;
+  uint64_t* pp = P.parity + (uint64_t)r.hit * E;
+  if (mode == A_FINAL) {   // pir.go:450-468
+    if (!(r.flags & 2u)) {
+      if (tid < P.SS) P.cur[(uint64_t)tid * P.PH + r.hit] = (uint16_t)a.e_cur;
+      if (P.SS > NT) refresh_cur(P, r, tid + NT, NT);
+    }
+    const uint64_t* rv = P.rval + dslot * E;
+    const uint64_t* bp = P.parity + ((uint64_t)P.PH + dslot) * E;
+    for (uint32_t w = tid; w < E; w += NT) {
+      const uint64_t rvw = w < NT ? a.e_rv : rv[w], bpw = w < NT ? a.e_bp : bp[w], ppw = w < NT ? a.e_pp : pp[w];
+      uint64_t v = 0;
+      if (w < EX) {
+        v = row.w[w] ^ rvw ^ ppw;
+        pp[w] = bpw ^ v;
+      } else {
+        pp[w] = bpw;
+      }
+      row.w[w] = v;
+    }
+  } else if (mode == A_CHAINED) {
+    for (uint32_t w = tid; w < E; w += NT) S.ans[(uint64_t)s * E + w] = w < EX ? row.w[w] : 0;
+  } else if (mode == A_CACHED) {
+    const uint64_t* ar = P.arena + (uint64_t)r.slot * E;
+    for (uint32_t w = tid; w < E; w += NT) row.w[w] = ar[w];
+  }
+  const float* const qq = P.qv ? P.qv : S.q;
+  const bool q_lds = qq && S.dim <= 2 * NT;
+  float* const qf = reinterpret_cast<float*>(L.red);
+  if (q_lds) {
+    if (tid < S.dim) qf[tid] = a.q0;
+    if (tid + NT < S.dim) qf[tid + NT] = a.q1;
+  }
+  __syncthreads();
+  if (mode != A_CHAINED) {
+    const bool has_row = (mode == A_FINAL || mode == A_CACHED);
+    PM_G uint64_t* const orow = S.rows_h + (uint64_t)s * E;
+    for (uint32_t w = (S.rows_partial ? S.pf_w0 : 0) + tid; w < (S.rows_partial ? S.pf_w1 : E); w += NT)
+      row_store(orow + w, has_row ? row.w[w] : 0);
+    if (mode == A_FINAL) {
+      uint64_t* ar = P.arena + (uint64_t)r.slot * E;
+      for (uint32_t w = tid; w < E; w += NT) ar[w] = row.w[w];
+    }
+    float d = 0.0f;
+    if (has_row && qq && tid < 8) d = l2_lds(row.f, q_lds ? qf : qq, S.dim);
+    uint64_t cs = 0;
+    if (tid < 64) cs = row_csum(S, row, has_row);
+    publish_hdr(S, s, r.status, r.slot, d, cs);
+  }
+  // arrival of a refresh-chain member; the last one decodes the chained
+  // sub-queries in order (answer_role)
+  if (r.status == ST_OK && (r.flags & 3u)) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      L.s_last = (uint32_t)chain_add(S, 1);
+      if (L.s_last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    __syncthreads();
+    if (L.s_last) finish_step<false>(S, row);
+  }
+  __syncthreads();   // row and red are the next sub-query's
+}
+#ifndef PM_ANSWER_P_WAVES
+#define PM_ANSWER_P_WAVES 6   // min waves per SIMD: <= 80 VGPRs (B's row batch stays live through A's epilogue);
+                              // 12 two-wave workgroups per CU = the 3,072 of a 6,144-sub-query step, all resident
+#endif
+template <int W, int NT>
+__global__ void __launch_bounds__(NT, PM_ANSWER_P_WAVES) k_answer_p(PmStep S) {
+  __shared__ AnswerPLds<NT> L;
+  constexpr int KG = PM_ANSWER_KG;
+  const uint32_t tid = threadIdx.x;
+  AnsQ q[2];
+  uint4 qpv[2];
+  const uint32_t ns = S.nsub;
+  const bool hasB = blockIdx.x + gridDim.x < ns;
+  // ---- prologue: both records, both query sets and A's query vector, one round trip
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    q[k].s = blockIdx.x + k * gridDim.x;
+    const uint32_t sk = k == 0 || hasB ? q[k].s : q[0].s;
+    const PmSub sub = step_sub(S, sk);
+    q[k].part = sub.part;
+    q[k].idx = sub.idx;
+    q[k].r = S.res[sk];
+    qpv[k] = make_uint4(0, 0, 0, 0);
+    if (tid < S.qw / 8) qpv[k] = *reinterpret_cast<const PM_G uint4*>(S.qset + (uint64_t)sk * S.qw + 8 * tid);
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const PmPart& P = S.parts[q[k].part];
+    const float* const qq = P.qv ? P.qv : S.q;
+    q[k].q0 = q[k].q1 = 0.0f;
+    if (qq && S.dim <= 2 * NT) {
+      if (tid < S.dim) q[k].q0 = qq[tid];
+      if (tid + NT < S.dim) q[k].q1 = qq[tid + NT];
+    }
+  }
+  q[0].mode = answer_mode(q[0].r);
+  q[1].mode = answer_mode(q[1].r);
+  ansp_decode_ops<W, NT>(S, q[0]);
+  ansp_set(S, q[0], qpv[0], L.qo[0]);
+  if (hasB) ansp_set(S, q[1], qpv[1], L.qo[1]);
+  __syncthreads();
+  // ---- A's gather
+  AnsGather<W, NT, KG> gA;
+  gA.init(S.E);
+  const bool gathA = q[0].mode == A_FINAL || q[0].mode == A_CHAINED || q[0].mode == A_DUMMY;
+  const bool gathB = hasB && (q[1].mode == A_FINAL || q[1].mode == A_CHAINED || q[1].mode == A_DUMMY);
+  if (gathA) {
+    const PmPart& P = S.parts[q[0].part];
+    const uint32_t nb = gA.batches(P);
+    for (uint32_t b = 0; b < nb; ++b) {
+      gA.load(S, P, L.qo[0], b);
+      gA.fold();
+    }
+  }
+  // ---- B's first row batch in flight, then A's epilogue under it
+  AnsGather<W, NT, KG> gB;
+  gB.init(S.E);
+  if (gathB) gB.load(S, S.parts[q[1].part], L.qo[1], 0);
+  if (gathA) gA.reduce(L, S.E);
+  ansp_epilogue<W, NT>(S, q[0], L);
+  if (!hasB) return;
+  ansp_decode_ops<W, NT>(S, q[1]);
+  if (gathB) {
+    const PmPart& P = S.parts[q[1].part];
+    gB.fold();
+    const uint32_t nb = gB.batches(P);
+    for (uint32_t b = 1; b < nb; ++b) {
+      gB.load(S, P, L.qo[1], b);
+      gB.fold();
+    }
+    gB.reduce(L, S.E);
+  }
+  ansp_epilogue<W, NT>(S, q[1], L);
+}
+
 // ---- k_gather: the server's XOR gather of wide sets, split ----------------
 // (HOT LOOP D + E for SetSize >= 256: BIGANN's 764 / 3,816 chunks.)  One
 // workgroup per (sub-query s, chunk range j of nsplit); it expands its range
@@ -2403,6 +2668,14 @@ void step_answer(hipStream_t st, const PmStep& S, uint32_t maxSS, PmEvents ev) {
   // search-sized shapes: the small-LDS instance (PM_ANSWER_NT threads per
   // workgroup, 0 = the generic instance)
   static const int nt = [] { const char* e = getenv("PM_ANSWER_NT"); return e ? atoi(e) : 128; }();
+  // the pipelined pair form (k_answer_p) where its shapes hold: pre-expanded
+  // query sets, one gather segment per thread slice (E & ~3 <= 2 * 128 words)
+  static const int pair = [] { const char* e = getenv("PM_ANSWER_PAIR"); return e ? atoi(e) : 1; }();
+  if (pair && S.qset && S.nsplit <= 1 && maxSS <= kSmallSS && S.E % 2 == 0 && (S.E & ~3u) <= 2u * kAnsPNT &&
+      S.nsub >= 2 * 256) {
+    PM_LAUNCH(ev, (k_answer_p<2, kAnsPNT>), dim3((S.nsub + 1) / 2), dim3(kAnsPNT), st, S);
+    return;
+  }
   if (nt && S.nsplit <= 1 && maxSS <= kSmallSS && S.E <= kSmallE) {
     const bool w2 = S.E % 2 == 0;
     if (nt == 128) {
