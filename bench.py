@@ -81,6 +81,16 @@ ANSWER_NT = int(os.environ.get("PM_ANSWER_NT", "128"))
 ANSWER_BLOCK = ANSWER_NT or 512
 SYMBOLS["answer"] = (f"void pm::k_answer_s<2, {ANSWER_NT}>(pm::PmStep)" if ANSWER_NT
                      else "void pm::k_answer<2>(pm::PmStep)")
+# the batched steps' answer (>= 512 sub-queries with pre-expanded query sets):
+# k_answer_p, two sub-queries per 128-thread workgroup (PM_ANSWER_PAIR=0: k_answer_s)
+ANSWER_PAIR = os.environ.get("PM_ANSWER_PAIR", "1") != "0"
+if ANSWER_PAIR:
+    SYMBOLS["answer"] = "void pm::k_answer_p<2, 128>(pm::PmStep)"
+
+
+def answer_grid(nsub: int) -> int:
+    """Work-items of the answer launch of a shared step of nsub sub-queries."""
+    return (nsub + 1) // 2 * 128 if ANSWER_PAIR and nsub >= 512 else nsub * ANSWER_BLOCK
 HOST = ["host_search_knn", "host_knn_init", "host_knn_final", "host_knn_batch", "host_knn_update",
         "host_gvi_parse", "host_batch_query", "host_step_launch", "host_step_wait", "host_step_post",
         "host_wait_first_token", "host_wait_all_tokens", "host_rows_seen", "host_rows_torn", "host_wait_done"]
@@ -231,7 +241,9 @@ def batch_pir_msmarco(ctx, with_cpu: bool):
             "alg_bytes_per_launch": by / n,
             "kernel_avg_us": {k: round(v[1] / v[0] * 1e3, 3) for k, v in
                               ((k, clients[0].ctx.timing_get(k)) for k in ("hint_match", "resolve", "match_resolve", "answer")) if v[0]}}
-        attach_traffic(out["clients_grouped"]["roofline"], SYMBOLS["answer"], C2_CLIENTS * C2_B * ANSWER_BLOCK)
+        # (the grouped batch PIR's steps take k_match_part8 -> k_resolve -> k_answer_s: no pre-expanded sets)
+        attach_traffic(out["clients_grouped"]["roofline"], f"void pm::k_answer_s<2, {ANSWER_NT}>(pm::PmStep)",
+                       C2_CLIENTS * C2_B * ANSWER_BLOCK)
     del grp, clients
     if with_cpu:
         from oracle import oracle as O
@@ -323,7 +335,7 @@ def private_search_msmarco(local, args, with_cpu: bool):
                            "launches": n, "alg_bytes_per_launch": by / n,
                            "aggregate": {"achieved": round(by / wall / 1e9, 1),
                                          "frac": round(by / wall / 1e9 / HBM_PEAK_GBS, 4)}}
-        attach_traffic(out["roofline"], SYMBOLS["answer"], (S2 // MS_GROUPS) * PARALLEL * M * ANSWER_BLOCK)
+        attach_traffic(out["roofline"], SYMBOLS["answer"], answer_grid((S2 // MS_GROUPS) * PARALLEL * M))
     if with_cpu:   # the oracle replaying session 0's workload, one core
         cb = cpu_baseline(v, g, qs[0], MS_WARMUP, ans[0], ctx, 601, 602, k=MS_K)
         out["cpu_baseline"] = cb
@@ -1017,7 +1029,7 @@ def main():
         ach = (by / n) / (ms / n / 1e3) / 1e9
         grid = None
         if name == "answer" and args.mode == "batched":   # the PMC summary by launch shape: one workgroup per sub-query
-            grid = (S // max(1, args.groups)) * PARALLEL * M * ANSWER_BLOCK
+            grid = answer_grid((S // max(1, args.groups)) * PARALLEL * M)
         r = {"bound": "hbm", "kernel": name, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
              "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
              "launches": n, "avg_ms": round(ms / n, 5), "alg_bytes_per_launch": by / n}

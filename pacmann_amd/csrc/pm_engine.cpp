@@ -3468,24 +3468,27 @@ extern "C" int pm_batchpir_group_query(pm_batchpir_group* h, const uint64_t* ids
 // PM_TEAM_TRACE=<file> (diagnostics): the pooled loop's host spans, one CSV row
 // each: team, kind (0 session task, 1 step launch, 2 maintenance, 3 query
 // start, 4 step in flight until seen complete), worker, start and end in us.
+// Host trace of the pooled loop (PM_TEAM_TRACE=<file>): one record per task,
+// launch, maintenance, query start and step flight, kept per worker (no lock
+// on the serving path) and written when the loop ends.
 struct TeamTrace {
   struct Rec { double t0, t1; uint32_t team, kind, worker; };
   const char* file = getenv("PM_TEAM_TRACE");
   Clock::time_point base = Clock::now();
-  std::mutex mu;
-  std::vector<Rec> recs;
+  std::vector<std::vector<Rec>> recs;   // [worker]
+  explicit TeamTrace(uint32_t workers) { if (file) { recs.resize(workers); for (auto& v : recs) v.reserve(1 << 16); } }
   double now() const { return std::chrono::duration<double, std::micro>(Clock::now() - base).count(); }
-  void add(double t0, uint32_t team, uint32_t kind, uint32_t worker) {
+  static inline thread_local uint32_t tl_worker = 0;   // the calling worker (set when it starts)
+  void add(double t0, uint32_t team, uint32_t kind, uint32_t /*worker*/) {
     if (!file) return;
-    const double t1 = now();
-    std::lock_guard<std::mutex> lk(mu);
-    recs.push_back({t0, t1, team, kind, worker});
+    recs[tl_worker].push_back({t0, now(), team, kind, tl_worker});
   }
   ~TeamTrace() {
-    if (!file || recs.empty()) return;
+    if (!file) return;
     if (FILE* f = fopen(file, "w")) {
       fprintf(f, "team,kind,worker,t0_us,t1_us\n");
-      for (auto& r : recs) fprintf(f, "%u,%u,%u,%.2f,%.2f\n", r.team, r.kind, r.worker, r.t0, r.t1);
+      for (auto& v : recs)
+        for (auto& r : v) fprintf(f, "%u,%u,%u,%.2f,%.2f\n", r.team, r.kind, r.worker, r.t0, r.t1);
       fclose(f);
     }
   }
@@ -3544,7 +3547,7 @@ static int run_batched_pool(pm_graph** gs, uint32_t S, const float* queries, uin
     t.G.stg.resize(t.S);
   }
   const uint32_t dim = (uint32_t)gs[0]->dim;
-  TeamTrace tr;
+  TeamTrace tr(T);
   std::atomic<int> err{0};
   std::atomic<uint32_t> finished{0};
   std::string err_msg;
@@ -3656,6 +3659,7 @@ static int run_batched_pool(pm_graph** gs, uint32_t S, const float* queries, uin
   std::vector<int64_t> steps_buf((size_t)T * std::max(k, 1));
   const int dev = gs[0]->ctx->device;
   auto worker = [&](uint32_t w) {
+    TeamTrace::tl_worker = w;
     if (hipSetDevice(dev) != hipSuccess) { set_err(PM_EHIP, 0); return; }
     int64_t* stp = &steps_buf[(size_t)w * std::max(k, 1)];
     uint32_t idle = 0;
