@@ -56,7 +56,17 @@ LDS_B128_PEAK_GBS, LDS_B32_PEAK_GBS = 150_000.0, 75_000.0
 # (the tables are 32x bank-replicated), and ~2 VALU per lookup (v_perm address,
 # v_bitop3 XORs, one rotation per column)
 AES_LOOKUPS_PER_PRF = 122.5
-PRF_PEAK_G = LDS_B32_PEAK_GBS * 1e9 / 4 / AES_LOOKUPS_PER_PRF / 1e9   # ~153 G PRF/s: the lookup ceiling
+# SetSize <= 256 (SIFT1M, MS-MARCO): round 2 hoisted per hint (pm_aes.h r2_hint):
+# round 2 takes 4 lookups per PRF + 12 per hint per 8 chunks = 112 per PRF
+AES_LOOKUPS_PER_PRF_R2 = 112.0
+
+
+def prf_peak_g(lookups: float) -> float:
+    """The T-table lookup ceiling in G PRF/s (conflict-free ds_read_b32)."""
+    return LDS_B32_PEAK_GBS * 1e9 / 4 / lookups / 1e9
+
+
+PRF_PEAK_G = prf_peak_g(AES_LOOKUPS_PER_PRF)   # ~153 G PRF/s
 METRIC = "private queries/sec + PIR-scan HBM GB/s, SIFT1M d=128 at 1/2/4/8 GPUs"
 PREP_KERNELS = ["prep_offsets", "prep_fold", "prep_repl", "l2_rows"]
 STEP_KERNELS = ["step", "hint_match", "resolve", "match_resolve", "gather", "answer"]   # timed in the measured region too
@@ -542,7 +552,8 @@ def bigann_search(key, name, n_entries, layout, rank, ws, local, dist, comb_grou
         "host_ms_per_round": {k[5:]: round(v[1] / (BIG_SEARCH_Q * STEP), 4) for k, v in ht.items() if v[1]},
         "combine_paths_world1": combine_paths,
         "pir_scan_fold": fold, "pir_scan_answer": ans_roof,
-        "roofline_prf": prf_roofline(kprep["prep_offsets"], "k_prep_offsets of one client's preprocessing"),
+        "roofline_prf": prf_roofline(kprep["prep_offsets"], "k_prep_offsets of one client's preprocessing",
+                                     subs[0]["SetSize"]),
         "check": {"ids_fetched": tot, "ids_answered": succ, "ranks_identical": None if same is None else bool(same),
                   "records_checked_in_warmup": recs,
                   "note": "warm-up rounds: every answered record equal to the graph's row (synthetic spec) and the "
@@ -675,19 +686,22 @@ def dist_init():
     return dist, dist.get_rank(), ws, local % max(ndev, 1)
 
 
-def prf_roofline(entry, note):
+def prf_roofline(entry, note, set_size=None):
     """AES-PRF throughput of k_prep_offsets launches (timing entry: launches,
-    ms, PRFs evaluated) against the T-table lookup ceiling (PRF_PEAK_G)."""
+    ms, PRFs evaluated) against the T-table lookup ceiling of the form that
+    ran (SetSize <= 256: round 2 hoisted, 112 lookups per PRF; else 122.5)."""
     n, ms, prfs = entry
     if not n or not ms or not prfs:
         return None
+    lk = AES_LOOKUPS_PER_PRF_R2 if set_size is not None and set_size <= 256 else AES_LOOKUPS_PER_PRF
+    peak = prf_peak_g(lk)
     g = prfs / (ms / 1e3) / 1e9
-    return {"bound": "lds", "kernel": "prep_offsets", "achieved": round(g, 2), "peak": round(PRF_PEAK_G, 2),
-            "unit": "G PRF/s", "frac": round(g / PRF_PEAK_G, 4), "launches": n, "avg_ms": round(ms / n, 5),
-            "prfs_per_launch": prfs / n, "lookups_per_prf": AES_LOOKUPS_PER_PRF,
+    return {"bound": "lds", "kernel": "prep_offsets", "achieved": round(g, 2), "peak": round(peak, 2),
+            "unit": "G PRF/s", "frac": round(g / peak, 4), "launches": n, "avg_ms": round(ms / n, 5),
+            "prfs_per_launch": prfs / n, "lookups_per_prf": lk,
             "note": f"{note}: AES-128 blocks per second against the conflict-free ds_read_b32 lookup rate "
-                    f"(~75 TB/s = 18.75 T lookups/s) / {AES_LOOKUPS_PER_PRF} lookups per PRF (pm_aes.h); the "
-                    "~2 VALU per lookup put the vector-issue ceiling at the same ~150-160 G PRF/s"}
+                    f"(~75 TB/s = 18.75 T lookups/s) / {lk} lookups per PRF (pm_aes.h); the "
+                    "~2 VALU per lookup put the vector-issue ceiling at about the same rate"}
 
 
 def rccl_group(dist, local, out):
@@ -1074,9 +1088,10 @@ def main():
         fold["note"] = ("bound lds: fold bytes (hint x chunk entry reads, SURVEY.md §8d) served from LDS by "
                         "ds_read_b128 against the ~150 TB/s aggregate (MI355X_MICROARCH.md §LDS); 'compulsory' is "
                         "the HBM side: the DB read once plus the parity writes of the clients folded in one launch")
-    prf = prf_roofline(ktime["prep_offsets"], "k_prep_offsets of the timed region's maintenance launches")
+    ss0 = base.PIR.SubConfig(0)["SetSize"]
+    prf = prf_roofline(ktime["prep_offsets"], "k_prep_offsets of the kernel-timing pass's maintenance launch", ss0)
     if prf and isolated and one_prf:
-        prf["isolated_one_client"] = prf_roofline(one_prf, "one client alone")
+        prf["isolated_one_client"] = prf_roofline(one_prf, "one client alone", ss0)
     note = None
     if dom == "step":
         note = ("k_step runs hint match, resolution and answer of a batch-PIR step in one launch; "
