@@ -293,7 +293,8 @@ def private_search_msmarco(local, args, with_cpu: bool):
     g, tm = pm.build_graph(v, M, 1.2, seed=502, ctx=ctx)
     build = {k: round(x, 4) for k, x in tm.items()}
     build["total_s"] = round(time.perf_counter() - t0, 4)
-    S2, nq = MS_SESSIONS, MS_WARMUP + MS_QUERIES
+    S2, nq = args.ms_sessions or MS_SESSIONS, MS_WARMUP + MS_QUERIES
+    ms_groups = args.ms_groups or MS_GROUPS
     rng = np.random.default_rng(503)
     qs = (v[rng.integers(0, MS_N, S2 * nq)] + rng.normal(0, 0.1, (S2 * nq, MS_DIM))).astype(np.float32)
     qs = qs.reshape(S2, nq, MS_DIM)
@@ -303,13 +304,13 @@ def private_search_msmarco(local, args, with_cpu: bool):
     for s_ in sess[1:]:
         s_.Preprocess()
     ctxs = [s_.ctx for s_ in sess]
-    pm.search_loop_batched(sess, qs[:, :MS_WARMUP], MS_K, STEP, PARALLEL, MS_GROUPS, args.threads)
+    pm.search_loop_batched(sess, qs[:, :MS_WARMUP], MS_K, STEP, PARALLEL, ms_groups, args.threads)
     for c in ctxs:
         c.sync()
         c.timing_reset()
         c.timing(2)
     t0 = time.perf_counter()
-    ans, _, online, maint = pm.search_loop_batched(sess, qs[:, MS_WARMUP:], MS_K, STEP, PARALLEL, MS_GROUPS,
+    ans, _, online, maint = pm.search_loop_batched(sess, qs[:, MS_WARMUP:], MS_K, STEP, PARALLEL, ms_groups,
                                                    args.threads)
     for c in ctxs:
         c.sync()
@@ -330,7 +331,7 @@ def private_search_msmarco(local, args, with_cpu: bool):
                        "vectors (16-d latent mixture, per-dimension sigma 0.82 -> 0.29 as the reference's PCA "
                        "fixture), degree-32 graph built on the GPU, 896-B PIR entries "
                        "(16 partitions, CS 1,024 / SS 196), k = 100, step 20, parallel 3",
-           "sessions": S2, "lockstep_groups": MS_GROUPS, "queries_per_session": MS_QUERIES,
+           "sessions": S2, "lockstep_groups": ms_groups, "queries_per_session": MS_QUERIES,
            "private_queries_per_s": round(S2 * MS_QUERIES / wall, 2), "wall_s": round(wall, 4),
            "online_s_per_query": round(float(np.mean(online)) / MS_QUERIES, 6),
            "maintenance_s_per_query": round(float(np.mean(maint)) / MS_QUERIES, 6),
@@ -345,7 +346,7 @@ def private_search_msmarco(local, args, with_cpu: bool):
                            "launches": n, "alg_bytes_per_launch": by / n,
                            "aggregate": {"achieved": round(by / wall / 1e9, 1),
                                          "frac": round(by / wall / 1e9 / HBM_PEAK_GBS, 4)}}
-        attach_traffic(out["roofline"], SYMBOLS["answer"], answer_grid((S2 // MS_GROUPS) * PARALLEL * M))
+        attach_traffic(out["roofline"], SYMBOLS["answer"], answer_grid((S2 // ms_groups) * PARALLEL * M))
     if with_cpu:   # the oracle replaying session 0's workload, one core
         cb = cpu_baseline(v, g, qs[0], MS_WARMUP, ans[0], ctx, 601, 602, k=MS_K)
         out["cpu_baseline"] = cb
@@ -844,6 +845,8 @@ def main():
                     help="time every kernel with events inside the timed region itself (round-3 behaviour: "
                          "the events cost 5-7 %% of the rate) instead of in a separate pass")
     ap.add_argument("--no-msmarco-search", action="store_true", help="skip the MS-MARCO d=192 private-search block")
+    ap.add_argument("--ms-sessions", type=int, default=0, help="MS-MARCO private-search sessions (0: MS_SESSIONS)")
+    ap.add_argument("--ms-groups", type=int, default=0, help="MS-MARCO private-search lock-step teams (0: MS_GROUPS)")
     ap.add_argument("--stagger-teams", action="store_true",
                     help="desynchronise the teams' maintenance windows (extra warm-up queries per team)")
     ap.add_argument("--graph", choices=["built", "random"], default="built",

@@ -3,6 +3,8 @@
 // graphann beam search over PIRGraphInfo, and the extern "C" boundary of
 // include/pacmann.h.
 #include <dlfcn.h>
+#include <pthread.h>
+#include <sched.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>   // types only: the functions are resolved at run time (rccl_api)
 
@@ -414,6 +416,12 @@ struct Engine {
   bool is_batch = false;
   uint64_t N = 0, E = 0, Ebytes = 0, F = 0, seed = 0;
   uint64_t B = 0, P = 1, PS = 0;
+  // id -> partition without a 64-bit division on the per-round path: for ids
+  // and PartitionSize below 2^32, floor(id * ceil(2^64 / PS) / 2^64) = id / PS
+  uint64_t ps_magic = 0;
+  uint64_t part_of(uint64_t id) const {
+    return ps_magic && id < (1ull << 32) ? (uint64_t)(((unsigned __int128)id * ps_magic) >> 64) : id / PS;
+  }
   uint32_t shard = 0, nshards = 1;   // partition p is owned when p % nshards == shard
   bool skipPrep = false;
   // SimpleBatchPianoPIR stats (batch-pir.go:46-52)
@@ -532,6 +540,7 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
     g->P = B / 2;   // BatchSize / RealQueryPerPartition (batch-pir.go:62)
     if (g->P == 0) return fail(PM_EINVAL, "BatchSize must be >= 2");
     g->PS = (N + g->P - 1) / g->P;
+    if (g->PS > 1 && g->PS < (1ull << 32)) g->ps_magic = ~0ull / g->PS + 1;
   } else {
     g->P = 1; g->PS = N;
   }
@@ -1443,7 +1452,7 @@ static int bq_prepare(Engine* g, const uint64_t* idx, uint64_t n, bool* fast) {
   g->qn = qn;
   g->pq.resize(P);
   for (auto& v : g->pq) v.clear();
-  for (uint64_t i = 0; i < n; ++i) g->pq[idx[i] / g->PS].push_back(idx[i]);
+  for (uint64_t i = 0; i < n; ++i) g->pq[g->part_of(idx[i])].push_back(idx[i]);
   for (auto& v : g->pq) while (v.size() < qn) v.push_back(kDefaultValue);
   g->resp_map.clear();
   g->resp_rows.resize(std::max<size_t>(g->resp_rows.size(), n * E));
@@ -3658,8 +3667,31 @@ static int run_batched_pool(pm_graph** gs, uint32_t S, const float* queries, uin
   };
   std::vector<int64_t> steps_buf((size_t)T * std::max(k, 1));
   const int dev = gs[0]->ctx->device;
+  // PM_PIN_WORKERS=1: worker w runs on the w-th CPU of the process's affinity
+  // mask, so the sessions of its lane keep their state in one core's caches
+  static const int pin = [] { const char* e = getenv("PM_PIN_WORKERS"); return e ? atoi(e) : 0; }();
+  std::vector<int> cpus;
+  if (pin) {
+    cpu_set_t cs;
+    if (sched_getaffinity(0, sizeof cs, &cs) == 0)
+      for (int c = 0; c < CPU_SETSIZE; ++c)
+        if (CPU_ISSET(c, &cs)) cpus.push_back(c);
+    if (cpus.size() < T) cpus.clear();
+  }
   auto worker = [&](uint32_t w) {
     TeamTrace::tl_worker = w;
+    cpu_set_t old_set;
+    const bool pinned = !cpus.empty() && pthread_getaffinity_np(pthread_self(), sizeof old_set, &old_set) == 0;
+    if (pinned) {
+      cpu_set_t one;
+      CPU_ZERO(&one);
+      CPU_SET(cpus[w], &one);
+      (void)pthread_setaffinity_np(pthread_self(), sizeof one, &one);
+    }
+    struct Unpin {   // worker 0 is the caller's thread: its affinity is restored
+      bool on; cpu_set_t set;
+      ~Unpin() { if (on) (void)pthread_setaffinity_np(pthread_self(), sizeof set, &set); }
+    } unpin{pinned, old_set};
     if (hipSetDevice(dev) != hipSuccess) { set_err(PM_EHIP, 0); return; }
     int64_t* stp = &steps_buf[(size_t)w * std::max(k, 1)];
     uint32_t idle = 0;
