@@ -347,6 +347,12 @@ def private_search_msmarco(local, args, with_cpu: bool):
                            "aggregate": {"achieved": round(by / wall / 1e9, 1),
                                          "frac": round(by / wall / 1e9 / HBM_PEAK_GBS, 4)}}
         attach_traffic(out["roofline"], SYMBOLS["answer"], answer_grid((S2 // ms_groups) * PARALLEL * M))
+    n, ms, by = kt["prep_fold"]
+    if n and by:   # the maintenance fold's entry reads against the LDS ds_read_b128 aggregate
+        ach = (by / n) / (ms / n / 1e3) / 1e9
+        out["roofline_prep"] = {"bound": "lds", "kernel": "prep_fold", "achieved": round(ach, 1),
+                                "peak": LDS_B128_PEAK_GBS, "unit": "GB/s", "frac": round(ach / LDS_B128_PEAK_GBS, 4),
+                                "avg_ms": round(ms / n, 3), "launches": n, "alg_bytes_per_launch": by / n}
     if with_cpu:   # the oracle replaying session 0's workload, one core
         cb = cpu_baseline(v, g, qs[0], MS_WARMUP, ans[0], ctx, 601, 602, k=MS_K)
         out["cpu_baseline"] = cb

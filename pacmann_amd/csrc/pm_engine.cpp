@@ -604,7 +604,7 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
     HIPCHK(hipStreamSynchronize(ctx->stream));
   }
   // the fold image: a second copy of the owned partitions' rows, laid out for
-  // k_prep_fold_rot (CS 512 shapes only; PM_FOLD_ROT=0 disables it).  It is
+  // k_prep_fold_rot (CS 512 and 1,024 shapes; PM_FOLD_ROT=0 disables it).  It is
   // skipped, and the fold reads the rows themselves (k_prep_fold_pipe), when
   // it would take more than a quarter of the device memory still free.
   uint64_t off_img = 0;
@@ -612,7 +612,7 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
     for (uint32_t i : g->owned_list) {
       PmPart& d = g->parts[i].d;
       d.img = (const uint64_t*)(uintptr_t)off_img;
-      off_img += pmk::fold_image_words(d.SS, (uint32_t)g->E);
+      off_img += pmk::fold_image_words(d.SS, (uint32_t)g->E, (uint32_t)g->maxCS);
     }
     size_t free_b = 0, total_b = 0;
     if (!server && hipMemGetInfo(&free_b, &total_b) == hipSuccess && off_img * 8 > free_b / 4) {
@@ -631,7 +631,7 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
       for (uint32_t i : g->owned_list) {
         const PmPart& d = g->parts[i].d;
         pmk::fold_image(ctx->stream, g->img->as<uint64_t>() + (uintptr_t)d.img, g->db->as<uint64_t>() + d.row0 * g->E,
-                        d.N, d.SS, (uint32_t)g->E);
+                        d.N, d.SS, (uint32_t)g->E, (uint32_t)g->maxCS);
       }
       HIPCHK(hipGetLastError());
       HIPCHK(hipStreamSynchronize(ctx->stream));

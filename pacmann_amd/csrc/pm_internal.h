@@ -109,8 +109,9 @@ struct PmPart {
   const PM_G float* qv;
   // The partition's fold image (server-side, built once with the DB; null
   // where k_prep_fold_rot does not apply): per 32-B column slice s and group
-  // of 4 chunks b, the 64 KB LDS image k_prep_fold_rot stages, line k =
-  // row k of chunks 4b..4b+3 (rows past N zero).  pmk::fold_image_words.
+  // of NCH chunks b (4 at CS 512, 2 at CS 1,024), the 64 KB LDS image
+  // k_prep_fold_rot stages, line k = row k of chunks NCH b .. (rows past N
+  // zero).  pmk::fold_image_words.
   const PM_G uint64_t* img;
 };
 
@@ -236,8 +237,9 @@ bool fold_image_ok(uint32_t minCS, uint32_t maxCS, uint32_t E);
 // whether the fold of these shapes reads the chunk-major PRF table PmPart::tab
 // (otherwise it is not allocated: every other reader uses tabT)
 bool fold_needs_tab(uint32_t minCS, uint32_t maxCS, uint32_t E, bool have_img);
-uint64_t fold_image_words(uint32_t SS, uint32_t E);
-void fold_image(hipStream_t st, uint64_t* img, const uint64_t* part_rows, uint64_t N, uint32_t SS, uint32_t E);
+uint64_t fold_image_words(uint32_t SS, uint32_t E, uint32_t CS);
+void fold_image(hipStream_t st, uint64_t* img, const uint64_t* part_rows, uint64_t N, uint32_t SS, uint32_t E,
+                uint32_t CS);
 // Timing events carried by a launch's own dispatch packet (null: untimed)
 struct PmEvents { hipEvent_t a = nullptr, b = nullptr; };
 // pm_set_option: the hint-search path selectors ("match_part" -1 auto / 0 / 1,

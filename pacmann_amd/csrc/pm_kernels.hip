@@ -419,6 +419,11 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_pipe(const PmPart* _
 // 32-B pieces at 640-B stride).  Hint offsets come from the tag-major table
 // (tabT: 8 chunks in 16 B per tag; hint h's initial tag is h).
 // Two buffers of (CS + 1) lines (line CS is zero: kSkip), 128.3 KB.
+// CS = 1,024 (MS-MARCO's 200K-row partitions): two chunks per block instead
+// of four (64-B lines, the same 64 KB per block, nbuf = SS / 2), so the double
+// buffer still fits (131.2 KB).  A 16-lane ds_read_b128 group then holds each
+// (slot, half) four times and its lanes collide when their rows agree mod 4
+// (about 2.6 instead of 2 LDS cycles per group for random rows).
 #ifndef PM_ROT_HPL
 #define PM_ROT_HPL 5
 #endif
@@ -454,23 +459,32 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_pipe(const PmPart* _
                        // wave (no bank conflicts), 4 = 2 and 3, 5 = no fold work at all (B128 form), 6 = 4 without
                        // the tabT loads in the loop
 #endif
+#ifndef PM_ROT_HPL2
+#define PM_ROT_HPL2 5   // hints per lane at CS 1,024 (2-B tiles: 2 VGPRs fewer per hint)
+#endif
 constexpr int kRotHPL = PM_ROT_HPL;   // hints per lane (SIFT1M's 12,512 hints: 3 groups of 4,171)
-constexpr uint32_t kRotCS = 512, kRotBufBytes = kRotCS * 128;   // one image block per (slice, 4 chunks)
+__host__ __device__ constexpr int rot_hpl(uint32_t cs) { return cs == 512 ? kRotHPL : PM_ROT_HPL2; }
+constexpr uint32_t kRotBufBytes = 512 * 128;   // one image block per (slice, 4 chunks of 512 / 2 of 1,024 rows)
+__host__ __device__ constexpr uint32_t rot_nch(uint32_t cs) { return cs == 512 ? 4 : 2; }   // chunks per block
 template <int CS>
 __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_rot(const PmPart* __restrict__ parts, uint32_t E,
                                                                 uint32_t nvg, uint32_t nsl, uint32_t npv,
                                                                 uint32_t M, uint32_t K, uint32_t ngc) {
-  constexpr uint32_t LINE = 32, BUFW = (CS + 1) * LINE;
+  constexpr uint32_t NCH = rot_nch(CS), LINE = NCH * 8, BUFW = (CS + 1) * LINE;
+  constexpr int HPL = rot_hpl(CS);
+  static_assert(CS == 512 || (CS == 1024 && PM_ROT_B128 && PM_ROT_PF == 0 && PM_ROT_ABL == 0),
+                "CS 1,024: the 16-B read form only");
+  static_assert(CS * LINE * 4 == kRotBufBytes, "64 KB blocks");
   // static (not extern) LDS: its address is a constant the reads fold into
   // their offsets
   __shared__ __attribute__((aligned(16))) uint32_t rot_lds[2 * BUFW];
   __shared__ uint32_t pf_lds[PM_ROT_PF ? kFoldThreads : 1];   // landing area of the L2 prefetch (never read)
-  constexpr uint32_t ITEMS = CS * 8;   // 16-B staging items per buffer (4 chunks x CS rows x 2)
+  constexpr uint32_t ITEMS = CS * NCH * 2;   // 16-B staging items per buffer (NCH chunks x CS rows x 2)
   static_assert(ITEMS % kFoldThreads == 0, "whole staging items per thread");
   constexpr uint32_t G = ITEMS / kFoldThreads;
   // Virtual hint groups: the K clients' hint lists of a partition, concatenated
   // (client c's hint h is virtual hint c * H + h), cut into groups of HB =
-  // 1,024 x kRotHPL lane slots.  A group spans at most two clients (HB <= H),
+  // 1,024 x HPL lane slots.  A group spans at most two clients (HB <= H),
   // and only the partition's last group has idle slots: 157 workgroups per
   // (partition, slice) for 64 SIFT1M clients instead of 3 per client (192),
   // each staging the slice's image once.  Order: XCD x takes the (partition,
@@ -481,7 +495,7 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_rot(const PmPart* __
   // 10-15 % faster than all clients of one slice back to back.)  ngc != 0:
   // partitions with fewer than HB hints (small configs) keep ngc groups per
   // client instead (no mixing).
-  constexpr uint32_t LW = PM_ROT_LW, HB = kFoldThreads * kRotHPL;
+  constexpr uint32_t LW = PM_ROT_LW, HB = kFoldThreads * HPL;
   const uint32_t xcd = blockIdx.x % 8, kq = blockIdx.x / 8;
 #if PM_ROT_ORDER == 1
   // Tiles of GB consecutive (partition, group) pairs x SB consecutive slices,
@@ -528,20 +542,20 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_rot(const PmPart* __
   const PM_G uint16_t* const tabA = PA.tabT;
   const PM_G uint16_t* const tabB = PB.tabT;
   const uint32_t hA = cA * H;
-  const uint32_t w = slice * 4, nbuf = SS / 4;   // SetSize is a multiple of 4 (pir.go:497)
+  const uint32_t w = slice * 4, nbuf = SS / NCH;   // SetSize is a multiple of 4 (pir.go:497)
   const PM_G char* img = (const PM_G char*)P.img + (uint64_t)slice * nbuf * kRotBufBytes;
 #if PM_ROT_B128
-  // 16-B reads: lane l reads chunk slot (s + phase) & 3, halves f then f ^ 1
-  // (s = l & 3, f = (l >> 2) & 1: every ds_read_b128 lane group of 16 holds
-  // each (slot, half) twice, MI355X_MICROARCH.md §LDS)
-  const uint32_t lane = tid & 63, j = (lane >> 2) & 1, ks = lane & 3;
+  // 16-B reads: lane l reads chunk slot (s + phase) % NCH, halves f then f ^ 1
+  // (s = l % NCH, f = (l / NCH) & 1: every ds_read_b128 lane group of 16 holds
+  // each (slot, half) 8 / NCH times, MI355X_MICROARCH.md §LDS)
+  const uint32_t lane = tid & 63, j = (lane / NCH) & 1, ks = lane & (NCH - 1);
 #else
   const uint32_t lane = tid & 63, j = lane & 7, ks = (lane >> 3) & 3;
 #endif
   const uint32_t vl = v0 + tid;   // virtual hint of lane slot k: vl + k * kFoldThreads
-  uint32_t acc[kRotHPL][8];
+  uint32_t acc[HPL][8];
 #pragma unroll
-  for (int k = 0; k < kRotHPL; ++k)
+  for (int k = 0; k < HPL; ++k)
 #pragma unroll
     for (int t = 0; t < 8; ++t) acc[k][t] = 0;
   const uint32_t wave_item0 = tid & ~63u;
@@ -553,27 +567,28 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_rot(const PmPart* __
       lds_dma16(src + (tid + i * kFoldThreads) * 16u, L + (i * kFoldThreads + wave_item0) * 4);
   };
   typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-  auto load_tab = [&](uint32_t b, u32x2* out) {   // chunks 4b .. 4b+3 of each hint: 8 B of its tabT tile
+  using Tile = std::conditional_t<NCH == 4, u32x2, uint32_t>;   // the NCH 2-B offsets of a hint's block
+  auto load_tab = [&](uint32_t b, Tile* out) {   // chunks NCH b .. of each hint: 2 NCH B of its tabT tile
 #pragma unroll
-    for (int k = 0; k < kRotHPL; ++k) {
+    for (int k = 0; k < HPL; ++k) {
       const uint32_t v = min(vl + k * kFoldThreads, vend - 1);
       const bool inB = v >= vb;
-      out[k] = *reinterpret_cast<const PM_G u32x2*>(
-          (const PM_G char*)(inB ? tabB : tabA) + (uint32_t)tabT_index(H, v - (inB ? vb : hA), 4 * b) * 2u);
+      const PM_G char* src = (const PM_G char*)(inB ? tabB : tabA) + (uint32_t)tabT_index(H, v - (inB ? vb : hA), NCH * b) * 2u;
+      out[k] = *reinterpret_cast<const PM_G Tile*>(src);
     }
   };
   for (uint32_t x = tid; x < 2 * LINE; x += kFoldThreads) rot_lds[(x / LINE) * BUFW + CS * LINE + x % LINE] = 0;
-  u32x2 tv[kRotHPL], tn[kRotHPL];
+  Tile tv[HPL], tn[HPL];
   stage(0, 0);
   // lane slots past the group read the zero line (kSkip).  Applied when a tile
   // is taken into use, not at its load: a select on the loaded value right
   // after the load made every iteration wait for its prefetched staging and
   // tabT loads before folding the current buffer (the double buffer's
   // overlap lost)
-  auto skip_idle = [&](u32x2* t) {
+  auto skip_idle = [&](Tile* t) {
 #pragma unroll
-    for (int k = 0; k < kRotHPL; ++k)
-      if (PM_ROT_B128 && vl + k * kFoldThreads >= v1) t[k] = u32x2{0xffffffffu, 0xffffffffu};
+    for (int k = 0; k < HPL; ++k)
+      if (PM_ROT_B128 && vl + k * kFoldThreads >= v1) t[k] = ~Tile{};
   };
   load_tab(0, tv);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -596,19 +611,22 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_rot(const PmPart* __
     const uint32_t lb = (b & 1) * BUFW * 4;   // byte offset of this buffer
 #if PM_ROT_B128
     {
-      uint32_t cso[4], psel[4];
+      uint32_t cso[NCH], psel[NCH];
 #pragma unroll
-      for (uint32_t ph = 0; ph < 4; ++ph) {
-        const uint32_t sl = (ks + ph) & 3;
+      for (uint32_t ph = 0; ph < NCH; ++ph) {
+        const uint32_t sl = (ks + ph) & (NCH - 1);
         cso[ph] = lb + sl * 32 + 16 * j;
         psel[ph] = 0x0c0c0000u | ((2 * sl + 1) << 8) | (2 * sl);   // v_perm: tile word sl, zero-extended
       }
 #pragma unroll
-      for (int k = 0; k < (PM_ROT_ABL == 5 ? 0 : kRotHPL); ++k) {
-        uint32_t v[4][8];
+      for (int k = 0; k < (PM_ROT_ABL == 5 ? 0 : HPL); ++k) {
+        uint32_t v[NCH][8];
 #pragma unroll
-        for (uint32_t ph = 0; ph < 4; ++ph) {
-          uint32_t o = min(__builtin_amdgcn_perm(tv[k].y, tv[k].x, psel[ph]), (uint32_t)CS);   // kSkip -> zero line
+        for (uint32_t ph = 0; ph < NCH; ++ph) {
+          uint32_t o;
+          if constexpr (NCH == 4) o = __builtin_amdgcn_perm(tv[k].y, tv[k].x, psel[ph]);
+          else o = __builtin_amdgcn_perm(0u, tv[k], psel[ph]);
+          o = min(o, (uint32_t)CS);   // kSkip -> zero line
           if (PM_ROT_ABL == 3 || PM_ROT_ABL == 4 || PM_ROT_ABL == 6) o = __builtin_amdgcn_readfirstlane(o);   // one row per wave: no conflicts
           const uint32_t a = o * (LINE * 4) + cso[ph];
           const uint4 x0 = *reinterpret_cast<const uint4*>(lds0 + a);
@@ -617,18 +635,21 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_rot(const PmPart* __
           v[ph][4] = x1.x; v[ph][5] = x1.y; v[ph][6] = x1.z; v[ph][7] = x1.w;
         }
 #pragma unroll
-        for (int t = 0; t < 8; ++t) acc[k][t] = xor3(xor3(acc[k][t], v[0][t], v[1][t]), v[2][t], v[3][t]);
+        for (int t = 0; t < 8; ++t) {
+          if constexpr (NCH == 4) acc[k][t] = xor3(xor3(acc[k][t], v[0][t], v[1][t]), v[2][t], v[3][t]);
+          else acc[k][t] = xor3(acc[k][t], v[0][t], v[1][t]);
+        }
       }
     }
     if (false)
 #endif
-    {
+    if constexpr (NCH == 4) {
     // per phase: this lane's chunk slot and its word base in the line
     uint32_t cso[4];
 #pragma unroll
     for (uint32_t ph = 0; ph < 4; ++ph) cso[ph] = lb + ((ks + ph) & 3) * 32 + (PM_ROT_B64 ? 8 * (j & 3) : 4 * j);
 #pragma unroll
-    for (int k = 0; k < (PM_ROT_ABL == 1 ? 0 : kRotHPL); ++k) {
+    for (int k = 0; k < (PM_ROT_ABL == 1 ? 0 : HPL); ++k) {
       const bool hv = vl + k * kFoldThreads < v1;   // lane slots past the group: zero line
       // the 4 offsets in phase order: rotate the 64-bit tile right by 16 ks
       const uint64_t t64 = ((uint64_t)tv[k].y << 32) | tv[k].x;
@@ -671,11 +692,14 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_rot(const PmPart* __
       __syncthreads();
     }
 #pragma unroll
-    for (int k = 0; k < kRotHPL; ++k) tv[k] = PM_ROT_ABL == 6 ? tv[k] + u32x2{1u, 3u} : tn[k];
+    for (int k = 0; k < HPL; ++k) {
+      if constexpr (NCH == 4) tv[k] = PM_ROT_ABL == 6 ? tv[k] + u32x2{1u, 3u} : tn[k];
+      else tv[k] = tn[k];
+    }
     skip_idle(tv);
   }
 #pragma unroll
-  for (int k = 0; k < kRotHPL; ++k) {
+  for (int k = 0; k < HPL; ++k) {
     const uint32_t v = vl + k * kFoldThreads;
     if (v >= v1) continue;
     const bool inB = v >= vb;
@@ -690,15 +714,18 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_rot(const PmPart* __
   }
 }
 
-// One partition's fold image: 16-B item it of block (slice s, chunks 4b..) =
-// line it / 8, chunk slot (it / 2) % 4, half it % 2 of row (4b + slot)*512 + line.
+// One partition's fold image: 16-B item it of block (slice s, chunks NCH b..)
+// = line it / (2 NCH), chunk slot (it / 2) % NCH, half it % 2 of row
+// (NCH b + slot) CS + line (NCH = rot_nch(CS); 4,096 items per block).
 __global__ void __launch_bounds__(kBlock) k_fold_image(uint4* __restrict__ img, const uint64_t* __restrict__ rows,
-                                                      uint64_t N, uint32_t nbuf, uint32_t E, uint64_t nitems) {
+                                                      uint64_t N, uint32_t nbuf, uint32_t E, uint64_t nitems,
+                                                      uint32_t CS) {
+  const uint32_t lg = CS == 512 ? 2 : 1;   // log2 NCH
   for (uint64_t x = (uint64_t)blockIdx.x * kBlock + threadIdx.x; x < nitems; x += (uint64_t)gridDim.x * kBlock) {
-    const uint32_t it = (uint32_t)(x % (kRotCS * 8));
-    const uint64_t blk = x / (kRotCS * 8);
+    const uint32_t it = (uint32_t)(x % (kRotBufBytes / 16));
+    const uint64_t blk = x / (kRotBufBytes / 16);
     const uint32_t b = (uint32_t)(blk % nbuf), s = (uint32_t)(blk / nbuf);
-    const uint64_t r = (uint64_t)(4 * b + ((it >> 1) & 3)) * kRotCS + (it >> 3);
+    const uint64_t r = (uint64_t)((b << lg) + ((it >> 1) & ((1u << lg) - 1))) * CS + (it >> (lg + 1));
     uint4 v = make_uint4(0, 0, 0, 0);
     if (r < N) v = *reinterpret_cast<const uint4*>(rows + r * E + 4 * s + (it & 1) * 2);
     img[x] = v;
@@ -983,7 +1010,7 @@ void prep_offsets(hipStream_t st, const PmPart* d, int np, uint32_t maxH, uint32
 }
 bool fold_image_ok(uint32_t minCS, uint32_t maxCS, uint32_t E) {
   static const bool rot = [] { const char* e = getenv("PM_FOLD_ROT"); return !e || e[0] != '0'; }();
-  return rot && minCS == kRotCS && maxCS == kRotCS && E % 2 == 0 && E >= 4;
+  return rot && minCS == maxCS && (maxCS == 512 || maxCS == 1024) && E % 2 == 0 && E >= 4;
 }
 bool fold_needs_tab(uint32_t minCS, uint32_t maxCS, uint32_t E, bool have_img) {
   // the folds that stage a chunk-major PRF table row through LDS (k_prep_fold_pipe
@@ -999,12 +1026,15 @@ bool fold_needs_tab(uint32_t minCS, uint32_t maxCS, uint32_t E, bool have_img) {
   while (sw > 2 && !fits(sw)) sw /= 2;
   return fits(sw) && E % 2 == 0;
 }
-uint64_t fold_image_words(uint32_t SS, uint32_t E) { return (uint64_t)(E / 4) * (SS / 4) * (kRotBufBytes / 8); }
-void fold_image(hipStream_t st, uint64_t* img, const uint64_t* rows, uint64_t N, uint32_t SS, uint32_t E) {
-  const uint64_t nitems = fold_image_words(SS, E) / 2;
+uint64_t fold_image_words(uint32_t SS, uint32_t E, uint32_t CS) {
+  return (uint64_t)(E / 4) * (SS / rot_nch(CS)) * (kRotBufBytes / 8);
+}
+void fold_image(hipStream_t st, uint64_t* img, const uint64_t* rows, uint64_t N, uint32_t SS, uint32_t E, uint32_t CS) {
+  const uint64_t nitems = fold_image_words(SS, E, CS) / 2;
   unsigned grid = cdiv(nitems, kBlock);
   if (grid > 256 * 32) grid = 256 * 32;
-  hipLaunchKernelGGL(k_fold_image, dim3(grid), dim3(kBlock), 0, st, (uint4*)img, rows, N, SS / 4, E, nitems);
+  hipLaunchKernelGGL(k_fold_image, dim3(grid), dim3(kBlock), 0, st, (uint4*)img, rows, N, SS / rot_nch(CS), E, nitems,
+                     CS);
 }
 void prep_fold(hipStream_t st, const PmPart* d, int np, uint32_t maxH, const uint64_t* db, uint32_t E,
                uint32_t minCS, uint32_t maxCS, const uint64_t* zero16, uint32_t clients, bool have_img,
@@ -1043,14 +1073,17 @@ void prep_fold(hipStream_t st, const PmPart* d, int np, uint32_t maxH, const uin
 #endif
     if (have_img && fold_image_ok(minCS, maxCS, E)) {   // the bank-rotated fold (same slices and block order)
       // virtual hint groups over the K clients of each partition (see the kernel)
-      const uint64_t HB = (uint64_t)kFoldThreads * kRotHPL;
+      const uint64_t HB = (uint64_t)kFoldThreads * rot_hpl(maxCS);
       const uint32_t ngc = minH >= HB ? 0u : (uint32_t)cdiv(maxH, HB);
       const uint32_t nvg = ngc ? K * ngc : (uint32_t)cdiv((uint64_t)K * maxH, HB), npv = (np / K) * nvg;
       const uint32_t M = cdiv(npv, 8);
       const uint32_t grid = PM_ROT_ORDER == 1
                                 ? 8 * cdiv((uint64_t)cdiv(npv, PM_ROT_GB) * cdiv(nsl, PM_ROT_SB), 8) * PM_ROT_GB * PM_ROT_SB
                                 : 8 * M * cdiv(nsl, PM_ROT_LW) * PM_ROT_LW;
-      hipLaunchKernelGGL(k_prep_fold_rot<512>, dim3(grid), dim3(kFoldThreads), 0, st, d, E, nvg, nsl, npv, M, K, ngc);
+      if (maxCS == 512)
+        hipLaunchKernelGGL(k_prep_fold_rot<512>, dim3(grid), dim3(kFoldThreads), 0, st, d, E, nvg, nsl, npv, M, K, ngc);
+      else
+        hipLaunchKernelGGL(k_prep_fold_rot<1024>, dim3(grid), dim3(kFoldThreads), 0, st, d, E, nvg, nsl, npv, M, K, ngc);
       return;
     }
     const uint32_t nb = maxCS == 512 ? PM_FOLD_NB512 : 3;   // LDS buffers: <= 150 KB
