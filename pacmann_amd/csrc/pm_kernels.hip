@@ -460,7 +460,7 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_pipe(const PmPart* _
                        // the tabT loads in the loop
 #endif
 #ifndef PM_ROT_HPL2
-#define PM_ROT_HPL2 5   // hints per lane at CS 1,024 (2-B tiles: 2 VGPRs fewer per hint)
+#define PM_ROT_HPL2 7   // hints per lane at CS 1,024 (2-B tiles; 128 VGPRs, no spills): 140 / 126 / 118 ms at 5 / 6 / 7
 #endif
 constexpr int kRotHPL = PM_ROT_HPL;   // hints per lane (SIFT1M's 12,512 hints: 3 groups of 4,171)
 __host__ __device__ constexpr int rot_hpl(uint32_t cs) { return cs == 512 ? kRotHPL : PM_ROT_HPL2; }
