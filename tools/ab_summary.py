@@ -13,7 +13,8 @@ for f in sys.argv[3:]:
         k, iso = d["kernel_avg_us"], (d.get("isolated") or {}).get("kernel_avg_us", {})
         print(label, d["value"], d["ms_per_step"],
               *(f"{n} {k.get(n)}" for n in ("answer", "match_resolve", "prep_fold", "prep_offsets")),
-              *(f"iso_{n} {iso.get(n)}" for n in ("answer", "match_resolve")))
+              *(f"iso_{n} {iso.get(n)}" for n in ("answer", "match_resolve")),
+              "single_ms", (d.get("single_session") or {}).get("ms_per_query"))
     else:
         for c in ("config3_bigann_100m", "config4_bigann_1b"):
             if c in d:
