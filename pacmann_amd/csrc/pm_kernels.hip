@@ -459,6 +459,9 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_pipe(const PmPart* _
                        // wave (no bank conflicts), 4 = 2 and 3, 5 = no fold work at all (B128 form), 6 = 4 without
                        // the tabT loads in the loop
 #endif
+#ifndef PM_ROT_PAIRS
+#define PM_ROT_PAIRS 0   // the B128 fold XORs two phases' rows at a time (16 VGPRs of rows in flight, not 32)
+#endif
 #ifndef PM_ROT_HPL2
 #define PM_ROT_HPL2 7   // hints per lane at CS 1,024 (2-B tiles; 128 VGPRs, no spills): 140 / 126 / 118 ms at 5 / 6 / 7
 #endif
@@ -620,6 +623,28 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_rot(const PmPart* __
       }
 #pragma unroll
       for (int k = 0; k < (PM_ROT_ABL == 5 ? 0 : HPL); ++k) {
+#if PM_ROT_PAIRS
+#pragma unroll
+       for (uint32_t p0 = 0; p0 < NCH; p0 += 2) {   // two phases' rows in flight, then their XOR
+        uint32_t v[2][8];
+#pragma unroll
+        for (uint32_t pp = 0; pp < 2; ++pp) {
+          const uint32_t ph = p0 + pp;
+          uint32_t o;
+          if constexpr (NCH == 4) o = __builtin_amdgcn_perm(tv[k].y, tv[k].x, psel[ph]);
+          else o = __builtin_amdgcn_perm(0u, tv[k], psel[ph]);
+          o = min(o, (uint32_t)CS);
+          const uint32_t a = o * (LINE * 4) + cso[ph];
+          const uint4 x0 = *reinterpret_cast<const uint4*>(lds0 + a);
+          const uint4 x1 = *reinterpret_cast<const uint4*>(lds0 + (a ^ 16u));
+          v[pp][0] = x0.x; v[pp][1] = x0.y; v[pp][2] = x0.z; v[pp][3] = x0.w;
+          v[pp][4] = x1.x; v[pp][5] = x1.y; v[pp][6] = x1.z; v[pp][7] = x1.w;
+        }
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc[k][t] = xor3(acc[k][t], v[0][t], v[1][t]);
+       }
+       continue;
+#endif
         uint32_t v[NCH][8];
 #pragma unroll
         for (uint32_t ph = 0; ph < NCH; ++ph) {
