@@ -460,7 +460,7 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_pipe(const PmPart* _
                        // the tabT loads in the loop
 #endif
 #ifndef PM_ROT_PAIRS
-#define PM_ROT_PAIRS 0   // the B128 fold XORs two phases' rows at a time (16 VGPRs of rows in flight, not 32)
+#define PM_ROT_PAIRS 1   // the B128 fold XORs two phases' rows at a time (16 VGPRs of rows in flight, not 32)
 #endif
 #ifndef PM_ROT_HPL2
 #define PM_ROT_HPL2 7   // hints per lane at CS 1,024 (2-B tiles; 128 VGPRs, no spills): 140 / 126 / 118 ms at 5 / 6 / 7
