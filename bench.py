@@ -10,7 +10,7 @@ private-search.go harness (run-private-search.sh flags).  Data are synthetic
 [0,255] and a degree-32 graph built on the GPU (exact kNN + robustPrune; --graph
 random: the reference's genRandomGraph, private-search.go:54-69).
 
-Serving: one GPU serves S client sessions at once (--sessions, default 256).
+Serving: one GPU serves S client sessions at once (--sessions, default 288).
 Every session is a full PianoPIR client (own keys, hint state, cache,
 maintenance) over the one server DB on the device.  Default (--mode batched,
 pm_search_loop_batched): the sessions run in G lock-step groups (--groups,
@@ -76,7 +76,7 @@ PROFILE_QUERIES = 8
 # launch shapes; events on every launch): 24 queries, so it holds one
 # maintenance of every session (window 23 queries, private-search.go:226-232)
 KT_QUERIES = 24
-SESSIONS = 256  # client sessions per GPU (128: 9.9K q/s, 256: 11.0K, 384: 11.5K, 512: 11.3K)
+SESSIONS = 288  # client sessions per GPU, 4 teams of 72 (round 4 ABBA, one box: 256: 16.8K q/s, 288: 17.3K, 320: 17.3K)
 GROUPS = 4      # lock-step groups (GPU_MAX_HW_QUEUES = 4 hardware queues per process)
 THREADS = 16    # host worker threads of the batched loop (the box gives a GPU 16 host cores)
 SYMBOLS = {"prep_fold": "void pm::k_prep_fold_rot<512>(pm::PmPart const*, unsigned int, unsigned int, unsigned int, "

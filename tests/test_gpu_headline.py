@@ -3,13 +3,13 @@
 
   * the bench's data: `sift_like_vectors(1e6, 128, seed=100)` and the graph
     `pm.build_graph(v, 32, 1.2, seed=7)` built on the GPU (kNN + robustPrune);
-  * the bench's serving shape: 256 sessions in 4 lock-step teams of 64 with 16
+  * the bench's serving shape: 288 sessions in 4 lock-step teams of 72 with 16
     pooled host workers (pm_search_loop_batched -> run_batched_pool), every
-    round of a team ONE shared step over 64 x 16 partitions;
-  * the merged maintenance: the 256 sessions reach their re-preprocessing at
+    round of a team ONE shared step over 72 x 16 partitions;
+  * the merged maintenance: the 288 sessions reach their re-preprocessing at
     the same query (window 23, private-search.go:226-232), and the waiting
     teams' clients are re-preprocessed as ONE launch set (one k_prep_fold_rot
-    launch for all 256 clients);
+    launch for all 288 clients);
   * 24 queries per session (past the trigger), k 10, step 20, parallel 3.
 
 Sixteen sessions spread over all four teams are replayed by independent
@@ -22,11 +22,11 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 N, DIM, M, K, STEP, PAR = 1_000_000, 128, 32, 10, 20, 3
-S, TEAMS, THREADS, QUERIES = 256, 4, 16, 24
-CHECK = [0, 1, 37, 63, 64, 65, 100, 127, 128, 150, 190, 191, 192, 200, 254, 255]
+S, TEAMS, THREADS, QUERIES = 288, 4, 16, 24   # bench.py SESSIONS, lockstep teams, threads
+CHECK = [0, 1, 37, 71, 72, 73, 100, 143, 144, 150, 200, 215, 216, 250, 286, 287]
 
 
-def test_headline_256_sessions_4_teams_vs_oracle(oracle):
+def test_headline_bench_sessions_4_teams_vs_oracle(oracle):
     import pacmann_amd as pm
     from pacmann_amd.synth import sift_like_vectors
     ctx0 = pm.Context(0)
@@ -54,12 +54,12 @@ def test_headline_256_sessions_4_teams_vs_oracle(oracle):
         r = [c.timing_get(name) for c in ctxs]
         return tuple(sum(x[i] for x in r) for i in range(3))
     # the launch shapes of the bench line: every shared step of every team is one
-    # k_match_resolve_s + one k_answer_s over 64 sessions' partitions ...
+    # k_match_resolve_s + one k_answer_p over 72 sessions' partitions ...
     n_ans, _, by = tsum("answer")
     assert n_ans == TEAMS * QUERIES * STEP, n_ans
     assert tsum("match_resolve")[0] == n_ans
-    assert by / n_ans > 300e6   # ~6,144 sub-queries x ~80.5 KB per step (minus cache hits)
-    # ... and the maintenance ran ONCE, merged: one launch set of all 256
+    assert by / n_ans > 330e6   # ~6,912 sub-queries x ~80.5 KB per step (minus cache hits)
+    # ... and the maintenance ran ONCE, merged: one launch set of all 288
     # clients, one fold launch over all their hints
     sets, clients, _ = tsum("host_prep_sets")
     assert (sets, clients) == (1, S), (sets, clients)
@@ -71,7 +71,7 @@ def test_headline_256_sessions_4_teams_vs_oracle(oracle):
     assert n_fold == 1 and abs(fby / one - S) < 0.5, (n_fold, fby / one)
     assert (mt > 0).all() and wall > 0
     got = {i: (sess[i].counts(), sess[i].PIR.stats()) for i in CHECK}
-    del sess, base, ctxs   # free the 256 clients' device state before the oracle runs
+    del sess, base, ctxs   # free the 288 clients' device state before the oracle runs
 
     def run_oracle(i):
         p, s_ = seeds[i]
