@@ -324,8 +324,10 @@ def test_search_msmarco_full_shared_step(ctx, oracle):
 
 
 # ---------------------------------------------------------------------------
-# the bench's exact serving shapes (bench.py: SIFT1M 256 sessions in 4
-# lock-step groups of 64; MS-MARCO 64 sessions in 2 groups of 32)
+# the bench's serving shapes one group at a time (bench.py: SIFT1M 288
+# sessions in 4 lock-step groups of 72 since the end of round 4, 64 before;
+# MS-MARCO 64 sessions in 2 groups of 32; the whole SIFT1M shape:
+# tests/test_gpu_headline.py)
 # ---------------------------------------------------------------------------
 def test_search_sift1m_bench_group_shape(ctx, oracle):
     """configs[1] at the bench's launch shapes: 64 sessions in ONE lock-step
