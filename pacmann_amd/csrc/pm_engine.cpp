@@ -187,6 +187,14 @@ struct pm_ctx {
   bool debug_cache = false;
   bool log_steps = false;    // PM_LOG_STEPS=1: one stderr line per sub-query per step  // PM_DEBUG_CACHE=1: check cached answers against the slot's first answer  // PM_VERIFY_ROWS=1: re-read each step's results after the stream drains     // PM_NO_GUESS=1: k_step answers do not start before their resolution
   bool debug_sync = false;   // PM_DEBUG_SYNC=1: synchronise after every launch (fault triage)
+  // Maintenance: the replacement rows (HBM copies, independent of the PRF
+  // tables and the fold) run on a side stream beside k_prep_offsets
+  // (PM_REPL_SIDE=0: after the fold on the one stream; timed runs keep that
+  // order so every launch carries its own events)
+  bool repl_side = true;
+  hipStream_t side = nullptr;
+  hipEvent_t side_ev[2] = {};
+  std::mutex side_mu;
   // Result rows vs their header checksum when the token is first seen
   // (PmOutHdr::csum): 0 = no check, 1 = count a mismatch ("host_rows_torn")
   // and fail the step, 2 = count it and wait for the row to match (PM_ROWS_CHECK)
@@ -266,6 +274,8 @@ struct pm_ctx {
     for (auto& t : launches) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
     for (auto e : pool) (void)hipEventDestroy(e);
     for (auto e : done_ring) if (e) (void)hipEventDestroy(e);
+    for (auto e : side_ev) if (e) (void)hipEventDestroy(e);
+    if (side) (void)hipStreamDestroy(side);
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -307,6 +317,7 @@ extern "C" int pm_ctx_create(int device, pm_ctx** out) {
       }
     c->done_ev = c->done_ring[0];
   }
+  if (const char* rs = getenv("PM_REPL_SIDE")) c->repl_side = rs[0] != '0';
   const char* ng = getenv("PM_NO_GUESS");
   c->no_guess = ng && ng[0] == '1';
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
@@ -767,6 +778,20 @@ static int engine_prep_launch(pm_ctx* c, const Engine* g, const PmPart* dp, int 
     fold += ((double)d.PH + (double)(d.SS - 1) * d.Qpc) * d.SS * (double)g->E * 8;
     repl += (double)d.SS * d.Qpc * g->E * 8 * 2;
   }
+  // the replacement rows beside the PRF tables (after prep_init, which they follow on st)
+  const bool side = !g->skipPrep && c->repl_side && !c->timing && !c->debug_sync;
+  std::unique_lock<std::mutex> side_lk(c->side_mu, std::defer_lock);
+  if (side) {
+    side_lk.lock();
+    if (!c->side) {
+      HIPCHK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+      for (auto& e : c->side_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    HIPCHK(hipEventRecord(c->side_ev[0], st));
+    HIPCHK(hipStreamWaitEvent(c->side, c->side_ev[0], 0));
+    pmk::prep_repl(c->side, dp, np, g->maxRepl, g->db->as<uint64_t>(), (uint32_t)g->E);
+    HIPCHK(hipEventRecord(c->side_ev[1], c->side));
+  }
   // the PRF table is built even by DummyPreprocessing: queries still evaluate the PRF
   c->timed("prep_offsets", aes, [&] { pmk::prep_offsets(st, dp, np, g->maxH, g->maxSS); });
   if (g->skipPrep) {   // DummyPreprocessing (pir.go:520-523): zero hints
@@ -778,7 +803,8 @@ static int engine_prep_launch(pm_ctx* c, const Engine* g, const PmPart* dp, int 
   } else {
     c->timed("prep_fold", fold, [&] { pmk::prep_fold(st, dp, np, g->maxH, g->db->as<uint64_t>(), (uint32_t)g->E, g->minCS, g->maxCS,
                                                g->zero16.as<uint64_t>(), clients, g->img->p != nullptr, minH); });
-    c->timed("prep_repl", repl, [&] { pmk::prep_repl(st, dp, np, g->maxRepl, g->db->as<uint64_t>(), (uint32_t)g->E); });
+    if (side) HIPCHK(hipStreamWaitEvent(st, c->side_ev[1], 0));
+    else c->timed("prep_repl", repl, [&] { pmk::prep_repl(st, dp, np, g->maxRepl, g->db->as<uint64_t>(), (uint32_t)g->E); });
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(st));
