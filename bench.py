@@ -392,7 +392,10 @@ def client_bytes(sub: dict, E: int) -> int:
             + (SS + 7) // 8 * 8 * H * 2 + PH * SS * 2)
 
 
-def bigann_search(key, name, n_entries, layout, rank, ws, local, dist, comb_group, args):
+def bigann_search(key, name, n_entries, layout, rank, ws, local, dist, comb_group, args, nccl_group_fn=None):
+    """comb_group: the preferred combine when the layout spans the ranks
+    ("native" RCCL inside the library, "torch-rccl" or "gloo"); nccl_group_fn()
+    gives the torch RCCL group (probed and agreed) or None."""
     import gc
 
     import torch
@@ -432,14 +435,13 @@ def bigann_search(key, name, n_entries, layout, rank, ws, local, dist, comb_grou
     ctxs = [x.ctx for x in sess]
     nq = BIG_SEARCH_WARMUP + BIG_SEARCH_Q
     qs = np.random.default_rng(63).random((S, nq, BIG_DIM), dtype=np.float32)   # genRandomMatrix queries
-    if not combine:
-        comb = None
-    elif comb_group == "native":   # the library's own RCCL communicators (pm_rccl_combine)
-        from pacmann_amd.shard import RcclCombiner
-        comb = RcclCombiner(group=None, device=local)
-    else:
-        comb = RecordCombiner(group=comb_group, device=local)
     groups = min(args.big_groups or BIG_GROUPS, S)
+    comb, comb_path, comb_note = None, None, None
+    if combine:   # agreed by every rank, bounded, with fallbacks (shard.combiner_with_fallback)
+        from pacmann_amd.shard import combiner_with_fallback
+        words = [int(pm.lib().pm_sharded_record_words(sess[0].h, n, PARALLEL)) for n in pm.team_sizes(S, groups)]
+        comb, comb_path, comb_note = combiner_with_fallback(words, local, prefer=comb_group, nccl_group_fn=nccl_group_fn)
+        progress(f"  {key}: combine path {comb_path}" + (f" ({comb_note})" if comb_note else ""))
     # the warm-up queries with every record checked on the host (pm_set_option
     # "verify_records": answered records against the graph's spec and the
     # reference-order L2, unanswered ids against their explanation); off in the
@@ -532,11 +534,12 @@ def bigann_search(key, name, n_entries, layout, rank, ws, local, dist, comb_grou
         "peers": ("modelled: the other shards' answers generated from the graph's spec on the device "
                   f"({layout} shards, {ws} GPU(s); their PIR work is not measured)" if modelled else
                   "RCCL all-reduce of the team's records per shared step, inside libpacmann.so (pm_rccl_combine)"
-                  if combine and comb_group == "native" else
+                  if comb_path == "native" else
                   "RCCL all-reduce of the team's records per shared step (torch.distributed callback)"
-                  if combine and comb_group is not None else
-                  "gloo all-reduce of the team's records per shared step" if combine else
+                  if comb_path == "torch-rccl" else
+                  "gloo all-reduce of the team's records per shared step" if comb_path == "gloo" else
                   "none (one rank holds every partition)"),
+        "combine_path": comb_path, "combine_fallback": comb_note,
         "sessions": S, "lockstep_groups": groups, "queries_per_session": BIG_SEARCH_Q,
         "private_queries_per_s": round(S * BIG_SEARCH_Q / elapsed, 2), "wall_s": round(elapsed, 4),
         "ms_per_round": round(elapsed / (BIG_SEARCH_Q * STEP) * 1e3, 4),
@@ -741,6 +744,49 @@ def rccl_group(dist, local, out):
     return grp
 
 
+class Watchdog:
+    """Ends the run with the line written if the multi-rank blocks overrun
+    `budget_s` (a peer stuck in a collective, a bounded init that still
+    fails to return): rank 0 writes the one JSON line with the unfinished
+    blocks marked, every rank exits.  fire() is called by the main thread when
+    the blocks finished: False if the watchdog got there first."""
+
+    def __init__(self, out, rank, line_fd, budget_s):
+        import threading
+        self.out, self.rank, self.line_fd = out, rank, line_fd
+        self.lock = threading.Lock()
+        self.done = False
+        self.timer = threading.Timer(budget_s, self._expire) if budget_s > 0 else None
+        if self.timer:
+            self.timer.daemon = True
+            self.timer.start()
+
+    def _expire(self):
+        with self.lock:
+            if self.done:
+                return
+            self.done = True
+        for key in ("config3_bigann_100m", "config4_bigann_1b"):
+            self.out.setdefault(key, {"error": "unfinished: the run's multi-rank budget expired (watchdog)"})
+        if self.rank == 0:
+            os.write(self.line_fd, (json.dumps(self.out) + "\n").encode())
+        progress("watchdog: multi-rank blocks over budget; line written, exiting")
+        os._exit(0)
+
+    def fire(self) -> bool:
+        with self.lock:
+            if self.done:
+                return False
+            self.done = True
+        if self.timer:
+            self.timer.cancel()
+        return True
+
+
+def start_watchdog(out, rank, line_fd, budget_s):
+    return Watchdog(out, rank, line_fd, budget_s)
+
+
 def cpu_baseline(v, g, q0, warmup, answers0, ctx, pir_seed, search_seed, k=K_TOP):
     """The oracle (single-thread C++ restatement of the Go/AVX path; its hint
     fold on one thread like the reference's ThreadNum = 1) replaying session
@@ -841,6 +887,8 @@ def main():
                     help="collective of the sharded BIGANN rounds: rccl = the library's own RCCL communicators "
                          "(pm_rccl_combine), torch-rccl = torch.distributed's nccl group through a callback, "
                          "gloo = host tensors (e.g. ranks sharing one GPU)")
+    ap.add_argument("--bigann-budget-s", type=float, default=400.0,
+                    help="wall-clock budget of the BIGANN blocks; past it the line is written and the run ends")
     ap.add_argument("--no-combine-probe", action="store_true",
                     help="skip the world-1 comparison of the two RCCL combine paths (BIGANN-100M block)")
     ap.add_argument("--kernel-timing-sample", action="store_true",
@@ -1207,21 +1255,33 @@ def main():
     # BASELINE.json configs[3] (BIGANN-100M, sharded over the ranks) and
     # configs[4] (BIGANN-1B in 8 shards): every rank takes part
     if not args.no_bigann:
-        nccl_group = None
-        if dist and args.combine == "torch-rccl":
-            nccl_group = rccl_group(dist, local, out)
-        elif dist and args.combine == "rccl":
-            nccl_group = "native"
+        # The headline and the single-GPU blocks are complete: their line goes to
+        # stderr now, and a watchdog writes the full line (the BIGANN blocks
+        # marked unfinished) and ends the process if the blocks below overrun
+        # their budget, so a hang in a collective cannot lose the line.
+        if rank == 0:
+            progress("PARTIAL_LINE " + json.dumps(out))
+        wd = start_watchdog(out, rank, line_fd, args.bigann_budget_s)
+        pm.set_option("rccl_timeout_s", 60)   # a peer that never joins costs 60 s, not the run
+        prefer = {"rccl": "native", "torch-rccl": "torch-rccl", "gloo": "gloo"}[args.combine]
+        memo = {}
+
+        def nccl_group_fn():   # the torch RCCL group, probed and agreed once (rccl_group)
+            if "g" not in memo:
+                memo["g"] = rccl_group(dist, local, out)
+            return memo["g"]
         for key, nm, n_entries, layout in (("config3_bigann_100m", "BIGANN-100M-shaped (configs[3])",
                                             100_000_000, ws),
                                            ("config4_bigann_1b", "BIGANN-1B-shaped (configs[4]), 8-way layout",
                                             1_000_000_000, 8)):
             try:
                 progress(key)
-                out[key] = bigann_search(key, nm, n_entries, layout, rank, ws, local, dist,
-                                         nccl_group if nccl_group is not None else None, args)
+                out[key] = bigann_search(key, nm, n_entries, layout, rank, ws, local, dist, prefer, args,
+                                         nccl_group_fn=nccl_group_fn if dist else None)
             except Exception as e:   # recorded, never fatal to the headline line
                 out[key] = {"error": f"{type(e).__name__}: {e}"}
+        if not wd.fire():   # the watchdog already wrote the line and is ending the process
+            return
     if rank == 0:
         sys.stdout.flush()
         os.write(line_fd, (json.dumps(out) + "\n").encode())

@@ -34,6 +34,7 @@ extern "C" {
 #define PM_EINVAL -1   /* bad argument / reference log.Fatalf condition   */
 #define PM_EHIP -2     /* HIP runtime error                              */
 #define PM_ENOMEM -3   /* device allocation failed                       */
+#define PM_ETIMEDOUT -4 /* a bounded wait expired (RCCL peer never joined) */
 
 /* Per-sub-query status codes (pianopir/pir.go:354-471 error returns). */
 #define PM_Q_OK 0          /* answered through PIR                             */
@@ -68,7 +69,10 @@ int         pm_ctx_mem_info(pm_ctx* ctx, uint64_t* free_bytes, uint64_t* total_b
  * "host_step_post", "host_batch_query", "host_gvi_parse", "host_search_knn",
  * "host_knn_init", "host_knn_batch", "host_knn_update", "host_knn_final". */
 int pm_timing_enable(pm_ctx* ctx, int level);
-/* Process-wide choice among equivalent kernel paths (no reference counterpart:
+/* "rccl_timeout_s": the bound (seconds) on RCCL communicator creation and
+ * its probe (pm_rccl_create / pm_rccl_probe); "verify_records" (sharded loop):
+ * check every value-th shared step's records on the host.
+ * Process-wide choice among equivalent kernel paths (no reference counterpart:
  * the same results by every path; tests drive each one).  "match_part": the
  * hint search per (partition, block) instead of per (sub-query, block), -1
  * automatic / 0 / 1; "match_part8": its one-wave-per-block form where PH % 8 ==
@@ -351,6 +355,15 @@ int  pm_rccl_create(int device, int nranks, int rank, const uint8_t* ids /* ntea
                     uint32_t nteams, pm_rccl** out);
 void pm_rccl_destroy(pm_rccl* r);
 int  pm_rccl_combine(void* user, uint32_t team, uint64_t* dev_words, uint64_t nwords, void* stream);
+/* Creation is bounded: the communicators are made nonblocking and polled for
+ * at most pm_set_option("rccl_timeout_s") seconds (else PM_RCCL_TIMEOUT_S,
+ * default 120); a rank whose peer never joins gets PM_ETIMEDOUT, not a hang.
+ * pm_rccl_probe runs one 1-word all-reduce per team within the same bound and
+ * checks that it sums to nranks; on failure the communicators are aborted.
+ * Callers agree on the ranks' outcomes over another channel (a MIN of their
+ * success flags) and fall back to another combine unless every rank
+ * succeeded (pacmann_amd.shard.RcclCombiner.prepare). */
+int  pm_rccl_probe(pm_rccl* r);
 /* pm_search_loop_batched over a sharded graph DB: S sessions (clients of one
  * shard's server DB) in ngroups lock-step teams; every round of a team is one
  * shared step over this shard's partitions followed by ONE combine of the

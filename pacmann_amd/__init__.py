@@ -136,6 +136,7 @@ SIGNATURES = {
     "pm_rccl_create": (C.c_int, [C.c_int, C.c_int, C.c_int, u8p, C.c_uint32, C.POINTER(vp)]),
     "pm_rccl_destroy": (None, [vp]),
     "pm_rccl_combine": (C.c_int, [vp, C.c_uint32, vp, u64, vp]),
+    "pm_rccl_probe": (C.c_int, [vp]),
 }
 RCCL_ID_BYTES = 128   # PM_RCCL_ID_BYTES
 

@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <chrono>
+#include <condition_variable>
 #include <cmath>
 #include <cstring>
 #include <memory>
@@ -167,8 +168,10 @@ struct HostBuf {
 // and the reference-order L2 (verified) or not (bad); unanswered ids explained
 // by the batch layer's overflow drop (dropped), by a failed sub-query of this
 // rank (failed), by another rank's sub-query (peer), or not at all (unexplained).
-enum HostTimer : int { HT_STEP_LAUNCH, HT_STEP_WAIT, HT_STEP_POST, HT_BATCH_QUERY, HT_GVI_PARSE, HT_SEARCH_KNN, HT_KNN_INIT, HT_KNN_BATCH, HT_KNN_UPDATE, HT_KNN_FINAL, HT_WAIT_FIRST, HT_WAIT_ALL, HT_ROWS_SEEN, HT_ROWS_TORN, HT_WAIT_DONE, HT_COMBINE, HT_COMBINE_TURN, HT_PATH_MATCH, HT_PATH_MATCH_PART, HT_PATH_MATCH_PART8, HT_PREP_SETS, HT_REC_VERIFIED, HT_REC_BAD, HT_REC_DROPPED, HT_REC_FAILED, HT_REC_PEER, HT_REC_UNEXPLAINED, HT_COUNT };
-static const char* const kHostTimerName[HT_COUNT] = {"host_step_launch", "host_step_wait", "host_step_post", "host_batch_query", "host_gvi_parse", "host_search_knn", "host_knn_init", "host_knn_batch", "host_knn_update", "host_knn_final", "host_wait_first_token", "host_wait_all_tokens", "host_rows_seen", "host_rows_torn", "host_wait_done", "host_combine", "host_combine_turn", "host_path_match", "host_path_match_part", "host_path_match_part8", "host_prep_sets", "host_records_verified", "host_records_bad", "host_records_dropped", "host_records_failed", "host_records_peer", "host_records_unexplained"};
+// "host_fold_*" count the maintenance fold launches by kernel (k_prep_fold_rot
+// at CS 512 / 1,024, or another form).
+enum HostTimer : int { HT_STEP_LAUNCH, HT_STEP_WAIT, HT_STEP_POST, HT_BATCH_QUERY, HT_GVI_PARSE, HT_SEARCH_KNN, HT_KNN_INIT, HT_KNN_BATCH, HT_KNN_UPDATE, HT_KNN_FINAL, HT_WAIT_FIRST, HT_WAIT_ALL, HT_ROWS_SEEN, HT_ROWS_TORN, HT_WAIT_DONE, HT_COMBINE, HT_COMBINE_TURN, HT_PATH_MATCH, HT_PATH_MATCH_PART, HT_PATH_MATCH_PART8, HT_PREP_SETS, HT_REC_VERIFIED, HT_REC_BAD, HT_REC_DROPPED, HT_REC_FAILED, HT_REC_PEER, HT_REC_UNEXPLAINED, HT_FOLD_ROT512, HT_FOLD_ROT1024, HT_FOLD_OTHER, HT_COUNT };
+static const char* const kHostTimerName[HT_COUNT] = {"host_step_launch", "host_step_wait", "host_step_post", "host_batch_query", "host_gvi_parse", "host_search_knn", "host_knn_init", "host_knn_batch", "host_knn_update", "host_knn_final", "host_wait_first_token", "host_wait_all_tokens", "host_rows_seen", "host_rows_torn", "host_wait_done", "host_combine", "host_combine_turn", "host_path_match", "host_path_match_part", "host_path_match_part8", "host_prep_sets", "host_records_verified", "host_records_bad", "host_records_dropped", "host_records_failed", "host_records_peer", "host_records_unexplained", "host_fold_rot512", "host_fold_rot1024", "host_fold_other"};
 
 struct TimedLaunch { std::string name; hipEvent_t a, b; double bytes; };
 
@@ -373,9 +376,14 @@ extern "C" int pm_timing_timeline(pm_ctx* c, const char* path) {
 // "verify_records" (sharded loop): check the records of every value-th shared
 // step of each team on the host (0: off); read when a loop starts
 static std::atomic<int> g_verify_records{0};
+// Bound on the communicators' creation and on the probe (pm_set_option
+// "rccl_timeout_s", else PM_RCCL_TIMEOUT_S, default 120 s): a rank whose peer
+// never joins returns PM_ETIMEDOUT instead of blocking inside RCCL.
+static std::atomic<int> g_rccl_timeout_s{-1};
 extern "C" int pm_set_option(const char* name, int value) {
   if (!name) return fail(PM_EINVAL, "NULL argument");
   if (!strcmp(name, "verify_records")) { g_verify_records.store(value < 0 ? 0 : value); return 0; }
+  if (!strcmp(name, "rccl_timeout_s")) { g_rccl_timeout_s.store(value); return 0; }
   if (pmk::set_option(name, value)) return fail(PM_EINVAL, std::string("unknown option ") + name);
   return 0;
 }
@@ -801,8 +809,10 @@ static int engine_prep_launch(pm_ctx* c, const Engine* g, const PmPart* dp, int 
       HIPCHK(hipMemsetAsync(d.rval, 0, (uint64_t)d.SS * d.Qpc * g->E * 8, st));
     }
   } else {
-    c->timed("prep_fold", fold, [&] { pmk::prep_fold(st, dp, np, g->maxH, g->db->as<uint64_t>(), (uint32_t)g->E, g->minCS, g->maxCS,
-                                               g->zero16.as<uint64_t>(), clients, g->img->p != nullptr, minH); });
+    int kind = pmk::FOLD_OTHER;
+    c->timed("prep_fold", fold, [&] { kind = pmk::prep_fold(st, dp, np, g->maxH, g->db->as<uint64_t>(), (uint32_t)g->E, g->minCS,
+                                                      g->maxCS, g->zero16.as<uint64_t>(), clients, g->img->p != nullptr, minH); });
+    c->host_add(kind == pmk::FOLD_ROT512 ? HT_FOLD_ROT512 : kind == pmk::FOLD_ROT1024 ? HT_FOLD_ROT1024 : HT_FOLD_OTHER, 0.0);
     if (side) HIPCHK(hipStreamWaitEvent(st, c->side_ev[1], 0));
     else c->timed("prep_repl", repl, [&] { pmk::prep_repl(st, dp, np, g->maxRepl, g->db->as<uint64_t>(), (uint32_t)g->E); });
   }
@@ -3888,6 +3898,11 @@ struct RcclApi {
   decltype(&ncclAllReduce) all_reduce = nullptr;
   decltype(&ncclCommDestroy) comm_destroy = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
+  // the nonblocking forms (optional: an RCCL without them gets a watched blocking init)
+  decltype(&ncclCommInitRankConfig) comm_init_rank_config = nullptr;
+  decltype(&ncclCommGetAsyncError) get_async_error = nullptr;
+  decltype(&ncclCommAbort) comm_abort = nullptr;
+  bool nonblocking() const { return comm_init_rank_config && get_async_error && comm_abort; }
 };
 static const RcclApi& rccl_api() {
   static const RcclApi api = [] {
@@ -3901,6 +3916,9 @@ static const RcclApi& rccl_api() {
     a.all_reduce = (decltype(a.all_reduce))dlsym(a.h, "ncclAllReduce");
     a.comm_destroy = (decltype(a.comm_destroy))dlsym(a.h, "ncclCommDestroy");
     a.error_string = (decltype(a.error_string))dlsym(a.h, "ncclGetErrorString");
+    a.comm_init_rank_config = (decltype(a.comm_init_rank_config))dlsym(a.h, "ncclCommInitRankConfig");
+    a.get_async_error = (decltype(a.get_async_error))dlsym(a.h, "ncclCommGetAsyncError");
+    a.comm_abort = (decltype(a.comm_abort))dlsym(a.h, "ncclCommAbort");
     if (!a.get_unique_id || !a.comm_init_rank || !a.all_reduce || !a.comm_destroy || !a.error_string)
       a.err = "librccl.so.1 lacks an NCCL entry point";
     return a;
@@ -3913,14 +3931,41 @@ static const RcclApi& rccl_api() {
     if (r_ != ncclSuccess) return fail(PM_EHIP, std::string(#call ": ") + rccl_api().error_string(r_)); \
   } while (0)
 
+// (rccl_timeout_s: g_rccl_timeout_s, with pm_set_option)
+static double rccl_timeout_s() {
+  const int o = g_rccl_timeout_s.load();
+  if (o > 0) return o;
+  const char* e = getenv("PM_RCCL_TIMEOUT_S");
+  return e && atof(e) > 0 ? atof(e) : 120.0;
+}
+
 struct pm_rccl {
   int device = 0, nranks = 1, rank = 0;
+  bool nonblocking = false;        // communicators made with config.blocking = 0: calls may return ncclInProgress
   std::vector<ncclComm_t> comms;   // one per lock-step team: a team's collectives never wait for another's
+  bool aborted = false;
+  void abort_all() {
+    for (ncclComm_t& c : comms)
+      if (c) { (void)(rccl_api().comm_abort ? rccl_api().comm_abort(c) : rccl_api().comm_destroy(c)); c = nullptr; }
+    aborted = true;
+  }
   ~pm_rccl() {
     for (ncclComm_t c : comms)
       if (c) (void)rccl_api().comm_destroy(c);
   }
 };
+// A call on a nonblocking communicator: ncclInProgress means "issued, not yet
+// complete" -- poll the communicator's state until it settles (or the bound).
+static ncclResult_t rccl_settle(const pm_rccl* r, ncclComm_t c, ncclResult_t res, double limit_s) {
+  if (res != ncclInProgress || !r->nonblocking) return res;
+  const auto t0 = Clock::now();
+  ncclResult_t st = ncclInProgress;
+  while (st == ncclInProgress) {
+    if (rccl_api().get_async_error(c, &st) != ncclSuccess) return ncclInternalError;
+    if (st == ncclInProgress && std::chrono::duration<double>(Clock::now() - t0).count() > limit_s) return ncclInProgress;
+  }
+  return st;
+}
 
 extern "C" int pm_rccl_unique_id(uint8_t id[PM_RCCL_ID_BYTES]) {
   if (!id) return fail(PM_EINVAL, "NULL argument");
@@ -3933,18 +3978,78 @@ extern "C" int pm_rccl_unique_id(uint8_t id[PM_RCCL_ID_BYTES]) {
   return 0;
 }
 
+// The teams' communicators, created nonblocking (ncclCommInitRankConfig with
+// config.blocking = 0) and polled to completion within rccl_timeout_s(); on an
+// error or the bound every communicator made so far is aborted, so a rank
+// whose peer failed (never joined) gets a status instead of a hang.  An RCCL
+// without the nonblocking entry points is initialised blocking on a watched
+// helper thread, with the same bound.
 extern "C" int pm_rccl_create(int device, int nranks, int rank, const uint8_t* ids, uint32_t nteams, pm_rccl** out) {
   if (!ids || !out || nteams == 0 || nranks < 1 || rank < 0 || rank >= nranks) return fail(PM_EINVAL, "bad argument");
+  *out = nullptr;
   const RcclApi& a = rccl_api();
   if (!a.err.empty()) return fail(PM_EHIP, "RCCL unavailable: " + a.err);
+  static const int fault = [] { const char* e = getenv("PM_FAULT_RCCL_CREATE"); return e ? atoi(e) : -1; }();
+  if (fault == rank) return fail(PM_EHIP, "injected fault (PM_FAULT_RCCL_CREATE)");   // tests: this rank never joins
   HIPCHK(hipSetDevice(device));
   std::unique_ptr<pm_rccl> r(new pm_rccl());
   r->device = device; r->nranks = nranks; r->rank = rank;
   r->comms.assign(nteams, nullptr);
-  for (uint32_t t = 0; t < nteams; ++t) {   // every rank creates the teams' communicators in the same order
-    ncclUniqueId u;
-    memcpy(&u, ids + (size_t)t * PM_RCCL_ID_BYTES, sizeof u);
-    RCCLCHK(a.comm_init_rank(&r->comms[t], nranks, u, rank));
+  const double limit = rccl_timeout_s();
+  if (a.nonblocking()) {
+    r->nonblocking = true;
+    for (uint32_t t = 0; t < nteams; ++t) {   // every rank issues the teams' inits in the same order
+      ncclUniqueId u;
+      memcpy(&u, ids + (size_t)t * PM_RCCL_ID_BYTES, sizeof u);
+      ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+      cfg.blocking = 0;
+      const ncclResult_t res = a.comm_init_rank_config(&r->comms[t], nranks, u, rank, &cfg);
+      if (res != ncclSuccess && res != ncclInProgress) {
+        r->abort_all();
+        return fail(PM_EHIP, std::string("ncclCommInitRankConfig: ") + a.error_string(res));
+      }
+    }
+    const auto t0 = Clock::now();
+    for (uint32_t t = 0; t < nteams; ++t) {
+      const double left = limit - std::chrono::duration<double>(Clock::now() - t0).count();
+      const ncclResult_t st = rccl_settle(r.get(), r->comms[t], ncclInProgress, std::max(0.0, left));
+      if (st == ncclInProgress) {
+        r->abort_all();
+        return fail(PM_ETIMEDOUT, "RCCL communicator " + std::to_string(t) + " not ready after " +
+                                      std::to_string((int)limit) + " s (a peer rank did not join)");
+      }
+      if (st != ncclSuccess) {
+        r->abort_all();
+        return fail(PM_EHIP, std::string("RCCL communicator init: ") + a.error_string(st));
+      }
+    }
+  } else {
+    struct Init { std::mutex mu; std::condition_variable cv; bool done = false; ncclResult_t res = ncclSuccess; };
+    auto st = std::make_shared<Init>();
+    std::vector<ncclComm_t>* comms = &r->comms;
+    std::vector<uint8_t> idv(ids, ids + (size_t)nteams * PM_RCCL_ID_BYTES);
+    std::thread th([st, comms, idv, nranks, rank, nteams, device] {
+      ncclResult_t res = hipSetDevice(device) == hipSuccess ? ncclSuccess : ncclUnhandledCudaError;
+      for (uint32_t t = 0; t < nteams && res == ncclSuccess; ++t) {
+        ncclUniqueId u;
+        memcpy(&u, idv.data() + (size_t)t * PM_RCCL_ID_BYTES, sizeof u);
+        res = rccl_api().comm_init_rank(&(*comms)[t], nranks, u, rank);
+      }
+      std::lock_guard<std::mutex> lk(st->mu);
+      st->done = true; st->res = res;
+      st->cv.notify_all();
+    });
+    std::unique_lock<std::mutex> lk(st->mu);
+    if (!st->cv.wait_for(lk, std::chrono::duration<double>(limit), [&] { return st->done; })) {
+      // the init thread stays blocked inside RCCL: it owns the handle from now on (leaked, never used)
+      th.detach();
+      (void)r.release();
+      return fail(PM_ETIMEDOUT, "RCCL communicator init not complete after " + std::to_string((int)limit) +
+                                    " s (a peer rank did not join)");
+    }
+    lk.unlock();
+    th.join();
+    if (st->res != ncclSuccess) return fail(PM_EHIP, std::string("ncclCommInitRank: ") + a.error_string(st->res));
   }
   *out = r.release();
   return 0;
@@ -3959,9 +4064,57 @@ extern "C" void pm_rccl_destroy(pm_rccl* r) {
 extern "C" int pm_rccl_combine(void* user, uint32_t team, uint64_t* dev_words, uint64_t nwords, void* stream) {
   pm_rccl* r = (pm_rccl*)user;
   if (!r || r->comms.empty() || !dev_words) return fail(PM_EINVAL, "bad argument");
+  if (r->aborted) return fail(PM_EHIP, "RCCL communicators were aborted");
   // in place, on the team's stream: ordered after the records' pack and before their read-back
-  RCCLCHK(rccl_api().all_reduce(dev_words, dev_words, nwords, ncclUint64, ncclSum, r->comms[team % r->comms.size()],
-                                (hipStream_t)stream));
+  ncclComm_t c = r->comms[team % r->comms.size()];
+  const ncclResult_t res = rccl_settle(r, c, rccl_api().all_reduce(dev_words, dev_words, nwords, ncclUint64, ncclSum, c,
+                                                                   (hipStream_t)stream), rccl_timeout_s());
+  if (res == ncclInProgress) return fail(PM_ETIMEDOUT, "ncclAllReduce not issued within the RCCL timeout");
+  if (res != ncclSuccess) return fail(PM_EHIP, std::string("ncclAllReduce: ") + rccl_api().error_string(res));
+  return 0;
+}
+
+// One 1-word all-reduce per team over the fresh communicators, on a private
+// stream, completed within rccl_timeout_s(): every rank must see the sum
+// nranks.  On a timeout or a wrong sum the communicators are aborted (their
+// kernels return) and the handle refuses further combines.  Callers agree on
+// the outcome over another channel (a MIN of the ranks' flags) before use.
+extern "C" int pm_rccl_probe(pm_rccl* r) {
+  if (!r || r->comms.empty()) return fail(PM_EINVAL, "bad argument");
+  if (r->aborted) return fail(PM_EHIP, "RCCL communicators were aborted");
+  HIPCHK(hipSetDevice(r->device));
+  const uint32_t nt = (uint32_t)r->comms.size();
+  DevBuf buf;
+  CHK(buf.reserve(nt * 8));
+  std::vector<uint64_t> one(nt, 1), got(nt, 0);
+  hipStream_t st = nullptr;
+  HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  struct Stream { hipStream_t s; ~Stream() { (void)hipStreamDestroy(s); } } guard{st};
+  HIPCHK(hipMemcpyAsync(buf.p, one.data(), nt * 8, hipMemcpyHostToDevice, st));
+  const double limit = rccl_timeout_s();
+  for (uint32_t t = 0; t < nt; ++t) {
+    const int rc = pm_rccl_combine(r, t, buf.as<uint64_t>() + t, 1, st);
+    if (rc) { r->abort_all(); return rc; }
+  }
+  const auto t0 = Clock::now();
+  for (;;) {
+    const hipError_t e = hipStreamQuery(st);
+    if (e == hipSuccess) break;
+    if (e != hipErrorNotReady) { r->abort_all(); return fail(PM_EHIP, std::string("RCCL probe: ") + hipGetErrorString(e)); }
+    if (std::chrono::duration<double>(Clock::now() - t0).count() > limit) {
+      r->abort_all();
+      (void)hipStreamSynchronize(st);   // the aborted communicators' kernels return
+      return fail(PM_ETIMEDOUT, "RCCL probe all-reduce not complete after " + std::to_string((int)limit) + " s");
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+  HIPCHK(hipMemcpy(got.data(), buf.p, nt * 8, hipMemcpyDeviceToHost));
+  for (uint32_t t = 0; t < nt; ++t)
+    if (got[t] != (uint64_t)r->nranks) {
+      r->abort_all();
+      return fail(PM_EHIP, "RCCL probe: team " + std::to_string(t) + " summed " + std::to_string(got[t]) + ", want " +
+                               std::to_string(r->nranks));
+    }
   return 0;
 }
 

@@ -226,9 +226,11 @@ void prep_init(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxH, 
                uint32_t E, bool zero_state);
 void prep_offsets(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxH, uint32_t maxSS);
 // dparts: `clients` clients of each partition, partition-major (nparts = partitions x clients)
-void prep_fold(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxH, const uint64_t* db,
-               uint32_t E, uint32_t minCS, uint32_t maxCS, const uint64_t* zero16, uint32_t clients = 1,
-               bool have_img = false, uint32_t minH = 0);
+// returns the fold kernel launched (FOLD_*)
+enum : int { FOLD_OTHER = 0, FOLD_ROT512 = 1, FOLD_ROT1024 = 2 };
+int prep_fold(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxH, const uint64_t* db,
+              uint32_t E, uint32_t minCS, uint32_t maxCS, const uint64_t* zero16, uint32_t clients = 1,
+              bool have_img = false, uint32_t minH = 0);
 void prep_repl(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxRepl,
                const uint64_t* db, uint32_t E);
 // The bank-rotated fold's DB image (CS 512, even E, E >= 4): whether it applies,

@@ -1061,14 +1061,14 @@ void fold_image(hipStream_t st, uint64_t* img, const uint64_t* rows, uint64_t N,
   hipLaunchKernelGGL(k_fold_image, dim3(grid), dim3(kBlock), 0, st, (uint4*)img, rows, N, SS / rot_nch(CS), E, nitems,
                      CS);
 }
-void prep_fold(hipStream_t st, const PmPart* d, int np, uint32_t maxH, const uint64_t* db, uint32_t E,
-               uint32_t minCS, uint32_t maxCS, const uint64_t* zero16, uint32_t clients, bool have_img,
+int prep_fold(hipStream_t st, const PmPart* d, int np, uint32_t maxH, const uint64_t* db, uint32_t E,
+              uint32_t minCS, uint32_t maxCS, const uint64_t* zero16, uint32_t clients, bool have_img,
                uint32_t minH) {
   const uint32_t EX = E & ~3u;
   if (EX == 0) {
     hipLaunchKernelGGL(k_prep_fold<2>, dim3(cdiv((uint64_t)maxH * E, kBlock), np), dim3(kBlock), 0,
                        st, d, db, E);
-    return;
+    return FOLD_OTHER;
   }
   // column-slice width: the widest whose double-buffered chunk fits in LDS and
   // whose staging fits kFoldMaxItems 16-B items per thread
@@ -1105,11 +1105,12 @@ void prep_fold(hipStream_t st, const PmPart* d, int np, uint32_t maxH, const uin
       const uint32_t grid = PM_ROT_ORDER == 1
                                 ? 8 * cdiv((uint64_t)cdiv(npv, PM_ROT_GB) * cdiv(nsl, PM_ROT_SB), 8) * PM_ROT_GB * PM_ROT_SB
                                 : 8 * M * cdiv(nsl, PM_ROT_LW) * PM_ROT_LW;
-      if (maxCS == 512)
+      if (maxCS == 512) {
         hipLaunchKernelGGL(k_prep_fold_rot<512>, dim3(grid), dim3(kFoldThreads), 0, st, d, E, nvg, nsl, npv, M, K, ngc);
-      else
-        hipLaunchKernelGGL(k_prep_fold_rot<1024>, dim3(grid), dim3(kFoldThreads), 0, st, d, E, nvg, nsl, npv, M, K, ngc);
-      return;
+        return FOLD_ROT512;
+      }
+      hipLaunchKernelGGL(k_prep_fold_rot<1024>, dim3(grid), dim3(kFoldThreads), 0, st, d, E, nvg, nsl, npv, M, K, ngc);
+      return FOLD_ROT1024;
     }
     const uint32_t nb = maxCS == 512 ? PM_FOLD_NB512 : 3;   // LDS buffers: <= 150 KB
     const size_t lds = (size_t)nb * ((maxCS + 1) * psw + kPipeTabWords) * 8;
@@ -1121,7 +1122,7 @@ void prep_fold(hipStream_t st, const PmPart* d, int np, uint32_t maxH, const uin
       hipLaunchKernelGGL((k_prep_fold_pipe<4, 2, 3>), grid, blk, lds, st, d, db, zero16, E, ng, nsl, npg, K);
     else
       hipLaunchKernelGGL((k_prep_fold_pipe<2, 2, 3>), grid, blk, lds, st, d, db, zero16, E, ng, nsl, npg, K);
-    return;
+    return FOLD_OTHER;
   }
   uint32_t sw = 8;
   while (sw > 2 && !fits(sw)) sw /= 2;
@@ -1132,11 +1133,12 @@ void prep_fold(hipStream_t st, const PmPart* d, int np, uint32_t maxH, const uin
     else
       hipLaunchKernelGGL(k_prep_fold<1>, dim3(cdiv((uint64_t)maxH * EX, kBlock), np), dim3(kBlock), 0,
                          st, d, db, E);
-    return;
+    return FOLD_OTHER;
   }
   const uint32_t nfull = EX / sw, rem = EX % sw;   // EX is a multiple of 4
   if (nfull) launch(sw, 0, nfull);
   if (rem) launch(rem, nfull * sw, 1);
+  return FOLD_OTHER;
 }
 void prep_repl(hipStream_t st, const PmPart* d, int np, uint32_t maxRepl, const uint64_t* db,
                uint32_t E) {

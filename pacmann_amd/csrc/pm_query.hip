@@ -2671,8 +2671,11 @@ void step_answer(hipStream_t st, const PmStep& S, uint32_t maxSS, PmEvents ev) {
   // the pipelined pair form (k_answer_p) where its shapes hold: pre-expanded
   // query sets, one gather segment per thread slice (E & ~3 <= 2 * 128 words)
   static const int pair = [] { const char* e = getenv("PM_ANSWER_PAIR"); return e ? atoi(e) : 1; }();
-  if (pair && S.qset && S.nsplit <= 1 && maxSS <= kSmallSS && S.E % 2 == 0 && (S.E & ~3u) <= 2u * kAnsPNT &&
-      S.nsub >= 2 * 256) {
+  // the pair form's decoded row lives in RowBufT<kSmallE>: E itself (not only
+  // its gather part E & ~3) must fit, or the epilogue's tail words overrun it
+  static_assert(2u * kAnsPNT >= kSmallE, "k_answer_p's gather slices must cover a kSmallE row");
+  if (pair && S.qset && S.nsplit <= 1 && maxSS <= kSmallSS && S.E % 2 == 0 && S.E <= kSmallE &&
+      (S.E & ~3u) <= 2u * kAnsPNT && S.nsub >= 2 * 256) {
     PM_LAUNCH(ev, (k_answer_p<2, kAnsPNT>), dim3((S.nsub + 1) / 2), dim3(kAnsPNT), st, S);
     return;
   }

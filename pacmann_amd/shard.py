@@ -193,6 +193,43 @@ class RecordCombiner:
             raise self.error
 
 
+class RcclUnavailable(RuntimeError):
+    """The library-native RCCL combine could not be set up on every rank; the
+    ranks agreed on it, so each may fall back to another combine."""
+
+
+def agree(ok: bool, group=None) -> bool:
+    """True iff every rank of `group` passed ok=True (a MIN of the ranks'
+    flags over a host collective: gloo, or whatever the group's backend is)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return int(t.item()) == 1
+
+
+def agreed_setup(setup, teardown=None, group=None):
+    """Run setup() on every rank and agree on the outcome: returns setup()'s
+    result when every rank succeeded; otherwise every rank tears its own
+    result down (teardown(result), if it got one) and raises RcclUnavailable
+    with its own error or "another rank failed".  setup() must be bounded
+    (pm_rccl_create / pm_rccl_probe are: PM_ETIMEDOUT), so every rank reaches
+    the agreement even when a peer never joins the collective part."""
+    res, err = None, None
+    try:
+        res = setup()
+    except Exception as e:   # recorded; the agreement decides for every rank alike
+        err = e
+    if agree(err is None, group):
+        return res
+    if res is not None and teardown is not None:
+        try:
+            teardown(res)
+        except Exception:
+            pass
+    raise RcclUnavailable(f"{type(err).__name__}: {err}" if err is not None else "another rank failed its setup")
+
+
 class RcclCombiner:
     """The library-native combine of pm_search_loop_sharded: RCCL
     communicators over xGMI inside libpacmann.so (pm_rccl_create), one per
@@ -200,9 +237,14 @@ class RcclCombiner:
     pm_combine_fn, so no Python and no GIL sit on the per-step path (the
     RecordCombiner's callback is the alternative through torch.distributed).
 
-    `group`: any torch.distributed group of the ranks (gloo is enough): it only
-    carries rank 0's ncclUniqueIds to the others, once per team count.  The
-    records live in the library's own device buffers."""
+    `group`: any torch.distributed group of the ranks (gloo is enough): it
+    carries rank 0's ncclUniqueIds to the others, once per team count, and the
+    agreement.  prepare() is bounded and agreed: the communicators' creation
+    (nonblocking, polled) and a 1-word probe all-reduce per team each finish
+    within pm_set_option("rccl_timeout_s") seconds, then the ranks take a MIN of
+    their success flags; unless every rank succeeded, every rank drops its
+    communicators and raises RcclUnavailable (the caller falls back to
+    RecordCombiner).  The records live in the library's own device buffers."""
 
     native = True
 
@@ -220,7 +262,8 @@ class RcclCombiner:
 
     def prepare(self, words_per_team):
         """Communicators for len(words_per_team) teams (created collectively on
-        first use or when the team count changes); returns the pm_rccl handle."""
+        first use or when the team count changes); returns the pm_rccl handle
+        or raises RcclUnavailable on every rank alike."""
         import ctypes as C
 
         import torch
@@ -230,19 +273,37 @@ class RcclCombiner:
         if self.h is not None and self.nteams == n:
             return self.h
         self.close()
-        ids = np.zeros(n * RCCL_ID_BYTES, dtype=np.uint8)
+        # word 0: rank 0 could make the ids (1) or not (0); the ids follow
+        buf = np.zeros(8 + n * RCCL_ID_BYTES, dtype=np.uint8)
+        err0 = None
         if self.rank == 0:
-            for t in range(n):
-                _check(lib().pm_rccl_unique_id(ids[t * RCCL_ID_BYTES:].ctypes.data_as(C.POINTER(C.c_uint8))))
-        t_ids = torch.from_numpy(ids.view(np.int64).copy())
+            try:
+                for t in range(n):
+                    _check(lib().pm_rccl_unique_id(buf[8 + t * RCCL_ID_BYTES:].ctypes.data_as(C.POINTER(C.c_uint8))))
+                buf[0] = 1
+            except Exception as e:
+                err0 = e
+        t_ids = torch.from_numpy(buf.view(np.int64).copy())
         self._dist.broadcast(t_ids, src=self._dist.get_global_rank(self.group, 0) if self.group else 0,
                              group=self.group)
-        ids = t_ids.numpy().view(np.uint8).copy()
-        h = C.c_void_p()
-        _check(lib().pm_rccl_create(self.device, self.world, self.rank, ids.ctypes.data_as(C.POINTER(C.c_uint8)), n,
-                                    C.byref(h)))
-        self.h, self.nteams = h, n
-        return h
+        buf = t_ids.numpy().view(np.uint8).copy()
+
+        def setup():
+            if buf[0] != 1:
+                raise RcclUnavailable(f"rank 0 could not make RCCL ids: {err0}" if err0 else
+                                      "rank 0 could not make RCCL ids")
+            h = C.c_void_p()
+            _check(lib().pm_rccl_create(self.device, self.world, self.rank,
+                                        buf[8:].ctypes.data_as(C.POINTER(C.c_uint8)), n, C.byref(h)))
+            try:
+                _check(lib().pm_rccl_probe(h))   # one 1-word all-reduce per team, bounded
+            except Exception:
+                lib().pm_rccl_destroy(h)
+                raise
+            return h
+        self.h = agreed_setup(setup, lambda h: lib().pm_rccl_destroy(h), self.group)
+        self.nteams = n
+        return self.h
 
     def finish(self):
         pass
@@ -258,3 +319,28 @@ class RcclCombiner:
             self.close()
         except Exception:
             pass
+
+
+def combiner_with_fallback(words_per_team, device: int, prefer: str = "native", nccl_group_fn=None,
+                           gloo_group=None):
+    """The sharded loop's combine, agreed by every rank and never left half-set-up:
+    the library-native RCCL communicators (RcclCombiner, bounded and probed);
+    unless every rank got them, a torch.distributed RCCL group from
+    nccl_group_fn() (which must itself probe and agree, returning None on
+    failure); else the gloo group through the host.  Returns (combiner, path,
+    note) with path "native" | "torch-rccl" | "gloo" and note the reason for a
+    fallback (None when the preferred path was taken)."""
+    note = None
+    if prefer == "native":
+        c = RcclCombiner(group=gloo_group, device=device)
+        try:
+            c.prepare(words_per_team)
+            return c, "native", None
+        except RcclUnavailable as e:
+            note = f"native RCCL combine unavailable ({e}); fell back"
+    if prefer in ("native", "torch-rccl") and nccl_group_fn is not None:
+        g = nccl_group_fn()
+        if g is not None:
+            return RecordCombiner(group=g, device=device), "torch-rccl", note
+        note = (note + "; " if note else "") + "torch RCCL group unavailable; fell back to gloo"
+    return RecordCombiner(group=gloo_group, device=device), "gloo", note

@@ -380,6 +380,130 @@ def test_search_msmarco_bench_group_shape(ctx, oracle):
 
 
 # ---------------------------------------------------------------------------
+# configs[2]: the MS-MARCO private-search block EXACTLY as bench.py serves it
+# ---------------------------------------------------------------------------
+def test_search_msmarco_bench_exact_shape(oracle):
+    """bench.py private_search_msmarco, unchanged: the bench's data
+    (msmarco_like_vectors(3,201,821, 192, seed=501)) and its GPU-built graph
+    (pm.build_graph(v, 32, 1.2, seed=502): kNN + robustPrune), its queries
+    (rng 503, 2 warm-up + 48 timed per session), 64 sessions (seeds 601 + i,
+    602 + i), each on its own context, in 2 lock-step teams of 32 with 16
+    pooled workers, k = 100, step 20, parallel 3, and the bench's two calls
+    of the serving loop.  Every session reaches its maintenance after query
+    44 (window 45, private-search.go:226-232) and the 64 clients are
+    re-preprocessed as ONE launch set whose fold is ONE k_prep_fold_rot<1024>
+    launch (CS 1,024: two chunks per staged block, 7 hints per lane) over all
+    64 clients' virtual hint groups.  Eight sessions from both teams are
+    replayed by independent oracle clients over all 50 queries
+    (pir.go:303-352, 354-471; search.go:114-234): answers, graph counts and
+    FinishedBatchNum / QueriesMadeInPartition / PrepCount equal."""
+    import pacmann_amd as pm
+    from pacmann_amd.synth import msmarco_like_vectors
+    N, DIM, K, S, G, NQ, WARM = 3_201_821, 192, 100, 64, 2, 50, 2
+    ctx0 = pm.Context(0)
+    v = msmarco_like_vectors(N, DIM, seed=501)
+    g, _ = pm.build_graph(v, 32, 1.2, seed=502, ctx=ctx0)
+    rng = np.random.default_rng(503)
+    qs = (v[rng.integers(0, N, S * NQ)] + rng.normal(0, 0.1, (S * NQ, DIM))).astype(np.float32).reshape(S, NQ, DIM)
+    base = pm.PIRGraphInfo(v, g, pir_seed=601, search_seed=602, ctx=ctx0)
+    base.Preprocess()
+    sess = [base] + [base.Session(601 + i, 602 + i, pm.Context(0)) for i in range(1, S)]
+    for x in sess[1:]:
+        x.Preprocess()
+    ctxs = [x.ctx for x in sess]
+    a0, _, _, _ = pm.search_loop_batched(sess, qs[:, :WARM], K, 20, 3, G, 16)
+    for c in ctxs:
+        c.sync()
+        c.timing_reset()
+        c.timing(2)
+    a1, _, _, mt = pm.search_loop_batched(sess, qs[:, WARM:], K, 20, 3, G, 16)
+    for c in ctxs:
+        c.sync()
+        c.timing(False)
+    ans = np.concatenate([a0, a1], axis=1)
+
+    def tsum(name):
+        r = [c.timing_get(name) for c in ctxs]
+        return tuple(sum(x[i] for x in r) for i in range(3))
+    n_ans = tsum("answer")[0]
+    assert n_ans == G * (NQ - WARM) * 20 and tsum("match_resolve")[0] == n_ans, n_ans
+    assert tsum("host_prep_sets")[:2] == (1, S), tsum("host_prep_sets")
+    n_fold, _, fby = tsum("prep_fold")
+    sc = base.PIR.SubConfig(0)
+    assert (sc["ChunkSize"], sc["SetSize"]) == (1024, 196)
+    one = sum((base.PIR.SubConfig(p)["PrimaryHintNum"] + (base.PIR.SubConfig(p)["SetSize"] - 1) *
+               base.PIR.SubConfig(p)["MaxQueryPerChunk"]) * base.PIR.SubConfig(p)["SetSize"] * 112 * 8
+              for p in range(16))
+    assert n_fold == 1 and abs(fby / one - S) < 0.5, (n_fold, fby / one)
+    assert tsum("host_fold_rot1024")[0] == 1 and tsum("host_fold_other")[0] == 0
+    assert (mt > 0).all()
+    check = [0, 1, 17, 31, 32, 33, 50, 63]   # team 0: sessions 0-31, team 1: 32-63
+    got = {i: (sess[i].counts(), sess[i].PIR.stats()) for i in check}
+    del sess, base, ctxs
+
+    def run_oracle(i):
+        o = oracle.Graph(v, g, pir_seed=601 + i, search_seed=602 + i)
+        o.Preprocess()
+        oa, _, _ = o.SearchLoop(qs[i], K, 20, 3)
+        res = (oa, o.counts(), o.pir().stats())
+        del o
+        return res
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=8) as ex:
+        for i, (oa, oc, po) in zip(check, ex.map(run_oracle, check)):
+            bad = np.where((ans[i] != oa).any(axis=1))[0]
+            assert len(bad) == 0, (i, bad[:5].tolist())
+            assert got[i][0] == oc, i
+            for key in ("FinishedBatchNum", "QueriesMadeInPartition", "PrepCount"):
+                assert got[i][1][key] == po[key], (i, key)
+            assert got[i][1]["PrepCount"] == 2, i
+
+
+def test_group_preprocessing_msmarco_64_clients(ctx, oracle):
+    """pm_batchpir_group_preprocessing at the MS-MARCO bench's maintenance
+    shape: 64 clients of the 3,201,821 x 896 B server (CS 1,024 / SS 196)
+    folded in ONE k_prep_fold_rot<1024> launch (virtual hint groups mixing the
+    clients) give, for every client and sampled partitions, exactly the state
+    of that client's own Preprocessing, through two epochs; clients 0 and 63
+    also equal independent oracle clients after the first grouped epoch."""
+    import pacmann_amd as pm
+    N, E, B, K = 3_201_821, 112, 32, 64
+    db = rand_db(N, E, seed=65)
+    server = pm.SimpleBatchPianoPIR(N, E * 8, B, db, 8, seed=SEED, ctx=ctx)
+    server.Preprocessing()
+    cg, ci = pm.Context(0), pm.Context(0)
+    seeds = [3000 + i for i in range(K)]
+    grouped = [server.Client(sd, cg) for sd in seeds]
+    alone = [server.Client(sd, ci) for sd in seeds]
+    for c in grouped + alone:
+        c.Preprocessing()   # epoch 0, one client at a time
+    grp = pm.BatchPIRGroup(grouped)
+    for epoch in (1, 2):
+        cg.timing_reset()
+        cg.timing(1)
+        grp.Preprocessing()
+        cg.sync()
+        cg.timing(False)
+        assert cg.timing_get("host_fold_rot1024")[0] == 1 and cg.timing_get("prep_fold")[0] == 1, epoch
+        for c in alone:
+            c.Preprocessing()
+        for i in range(K):   # one partition per client (all 16 covered), four for every 8th
+            for p in ((i % 16,) if i % 8 else (0, 5, 10, 15)):
+                diff = state_diff(grouped[i].export_state(p), alone[i].export_state(p))
+                assert not diff, (epoch, i, p, diff)
+        assert grouped[0].stats()["PrepCount"] == alone[0].stats()["PrepCount"] == epoch + 1
+        if epoch == 1:
+            for i in (0, K - 1):
+                o = oracle.SimpleBatchPianoPIR(N, E * 8, B, db, 8, seed=seeds[i])
+                o.Preprocessing()   # epoch 0
+                o.Preprocessing()   # epoch 1
+                for p in (0, 7, 15):
+                    diff = state_diff(grouped[i].export_state(p), o.sub(p).export_state())
+                    assert not diff, (i, p, diff)
+                del o
+
+
+# ---------------------------------------------------------------------------
 # configs[1]: the serving loop's maintenance fold of 64 clients in one launch
 # ---------------------------------------------------------------------------
 def test_group_preprocessing_sift1m_64_clients(ctx):

@@ -461,6 +461,39 @@ def test_search_sessions_batched(ctx, oracle, ngroups, nthreads):
         assert sess[i].PIR.stats()["PrepCount"] == o.pir().stats()["PrepCount"] > 1, i
 
 
+def test_search_sessions_batched_wide_entries(ctx, oracle):
+    """Entries wider than the answer kernels' small row buffer: dim 500, m 16
+    gives E = (2000 + 64) / 8 = 258 words, which passes k_answer_p's even-E
+    and gather-slice tests but not its RowBufT<kSmallE = 256> row.  Twelve
+    sessions in one lock-step group (12 x 48 = 576 sub-queries per shared
+    step, above k_answer_p's 512 threshold, with pre-expanded query sets) must
+    take a kernel whose row holds all 258 words and equal independent oracle
+    runs (answers, counts, batch-PIR counters through maintenance)."""
+    import pacmann_amd as pm
+    from pacmann_amd.synth import random_graph, sift_like_vectors
+    n, dim, m = 4096, 500, 16
+    v = sift_like_vectors(n, dim, seed=41)
+    graph = random_graph(n, m, seed=42)
+    base = pm.PIRGraphInfo(v, graph, pir_seed=43, search_seed=44, ctx=ctx)
+    base.Preprocess()
+    assert base.PIR.Config()["DBEntryByteNum"] == (dim + m) * 4
+    seeds = [(50 + i, 60 + i) for i in range(12)]
+    sess = [base.Session(p, s) for p, s in seeds]
+    for s in sess:
+        s.Preprocess()
+    rng = np.random.default_rng(45)
+    qs = np.stack([np.clip(np.rint(v[rng.integers(0, n, 12)] + rng.normal(0, 8, (12, dim))), 0, 255)
+                   .astype(np.float32) for _ in seeds])
+    ans, wall, on, mt = pm.search_loop_batched(sess, qs, 10, 20, 3, 1, 4)
+    for i, (p, s) in enumerate(seeds):
+        o = oracle.Graph(v, graph, pir_seed=p, search_seed=s)
+        o.Preprocess()
+        oa, _, _ = o.SearchLoop(qs[i], 10, 20, 3)
+        assert np.array_equal(ans[i], oa), i
+        assert sess[i].counts() == o.counts(), i
+        assert sess[i].PIR.stats()["PrepCount"] == o.pir().stats()["PrepCount"] > 1, i
+
+
 def test_batch_pir_group(ctx, oracle):
     """pm_batchpir_group_query: five clients of one server answered with one
     shared step per call; every client's entries, success flags, counters and
