@@ -1,0 +1,370 @@
+// pm_drl.hip — the device-resident team round of the batched serving loop
+// (pm_search_loop_batched's device loop).
+//
+// The host round of a lock-step team (pm_engine.cpp run_batched_pool: per
+// session the results' post-processing, GetVertexInfo's decode and success
+// count, SearchKNN's update and next batch, SimpleBatchPianoPIR.Query's
+// bucketing) as ONE launch of one 64-lane workgroup per session, so a team's
+// 20 rounds chain on its stream as [match + resolve, answer, round] with no
+// host round trip.  Same operations in the same order as the host restatement
+// (and the oracle), with Go's tie rules:
+//   * results (pm_engine.cpp post_results / bq_emit_fast, batch-pir.go:216-236):
+//     an ST_OK sub-query's row enters the localCache (pir.go:468-470); each id
+//     takes the LAST sub-query made for it; an in-step duplicate (ST_DUP) reads
+//     the row and distance of the sub-query it repeats; ids dropped by the
+//     overflow get the zero entry;
+//   * GetVertexInfo (private-search.go:441-506): the neighbour list of each
+//     entry, the success count against the true graph;
+//   * SearchKNN's update (graphann/search.go:185-207): positions in order; an
+//     id already known, or with an all-zero neighbour list, is skipped; the
+//     rest become known and are pushed on the min-heap -- container/heap's
+//     exact Push (up) and Pop (swap, down), so equal distances pop in Go's
+//     order;
+//   * the next batch (search.go:153-171): `parallel` pops, each one's m
+//     neighbours, or m ids of the SplitMix stream when the heap is empty;
+//   * the bucketing (batch-pir.go:175-200, pm_engine.cpp bq_prepare/add_sub):
+//     ids per partition in order, the first queryNumToMake kept, the rest
+//     dropped, the partition padded with dummy queries; a localCache hit is a
+//     HOSTCACHE sub-query.
+// The query's start (search.go:129-148: the first `parallel` start vertices
+// by (distance, position)) and end (search.go:211-233: top k by (distance,
+// id)) are the kernel's BEGIN and END modes.  The caller guarantees that no
+// partition reaches its query budget during the rounds it chains (the gate in
+// pm_engine.cpp drl_schedule), i.e. that the host would take the one-step path.
+#include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
+
+#include <algorithm>
+
+#include "pm_internal.h"
+
+namespace pm {
+
+struct HeapE { float d; uint32_t slot; };
+
+// Open-addressing tables of u64 entries {key + 1 | value << 32} (0 = empty),
+// probed with device-scope atomics (they bypass the CU's L1, so a lane sees
+// the entries other lanes inserted earlier in the same launch).
+__device__ __forceinline__ bool tab_find(const uint64_t* t, uint32_t mask, uint32_t key, uint32_t* val) {
+  for (uint32_t i = drl_hash(key) & mask;; i = (i + 1) & mask) {
+    const uint64_t e = __hip_atomic_load(const_cast<uint64_t*>(t) + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (e == 0) return false;
+    if ((uint32_t)e == key + 1u) { *val = (uint32_t)(e >> 32); return true; }
+  }
+}
+__device__ __forceinline__ void tab_put(uint64_t* t, uint32_t mask, uint32_t key, uint32_t val) {
+  const uint64_t ne = ((uint64_t)val << 32) | (uint64_t)(key + 1u);
+  for (uint32_t i = drl_hash(key) & mask;; i = (i + 1) & mask) {
+    uint64_t e = 0;
+    if (__hip_atomic_compare_exchange_strong(t + i, &e, ne, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT))
+      return;
+    if ((uint32_t)e == key + 1u) {   // insert or overwrite (FlatMap::put)
+      __hip_atomic_store(t + i, ne, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+  }
+}
+
+// container/heap.Push: append, then up().  up() swaps the new element with its
+// parent while it is strictly Less (dist <); the ancestors on its path are
+// non-increasing upward (heap order), so the elements it passes are exactly the
+// c nearest ancestors with dist > x.  Lane l >= 1 holds the ancestor l levels
+// up (0-based index ((n + 1) >> l) - 1): one LDS read per lane, one ballot, and
+// the c passed ancestors move one level down while x lands at ancestor c.
+__device__ __forceinline__ void heap_push(HeapE* hp, uint32_t& nh, HeapE x, uint32_t lane) {
+  const uint32_t j1 = nh + 1;   // 1-based position of the new element
+  const bool valid = lane >= 1 && lane < 32 && (j1 >> lane) >= 1u;
+  HeapE a{0.0f, 0u};
+  if (valid) a = hp[(j1 >> lane) - 1];
+  const uint64_t b = __ballot(valid && x.d < a.d);
+  const uint32_t c = (uint32_t)__builtin_ctzll(~(b >> 1));   // consecutive passed ancestors from lane 1
+  if (lane >= 1 && lane <= c) hp[(j1 >> (lane - 1)) - 1] = a;
+  if (lane == c) hp[(j1 >> c) - 1] = x;
+  nh = j1;   // (one wave: its LDS operations complete in order, so the next push reads these stores)
+}
+// container/heap.Pop: swap(0, n-1), down(0, n-1), remove the last.  down()
+// moves the larger-index child only when strictly Less than the smaller-index
+// one, and stops when the chosen child is not Less than the element.
+__device__ __forceinline__ HeapE heap_pop(HeapE* hp, uint32_t& nh, uint32_t lane) {
+  const uint32_t n1 = nh - 1;
+  const HeapE top = hp[0];
+  const HeapE x = hp[n1];
+  uint32_t i = 0;
+  for (;;) {
+    const uint32_t j1 = 2 * i + 1;
+    if (j1 >= n1) break;
+    uint32_t j = j1;
+    HeapE e = hp[j1];
+    if (j1 + 1 < n1) {
+      const HeapE e2 = hp[j1 + 1];
+      if (e2.d < e.d) { j = j1 + 1; e = e2; }
+    }
+    if (!(e.d < x.d)) break;
+    if (lane == 0) hp[i] = e;
+    i = j;
+  }
+  if (lane == 0) hp[i] = x;
+  nh = n1;
+  return top;
+}
+
+// wave-wide lexicographic minimum of (d, id)
+__device__ __forceinline__ void wave_min2(float& d, uint32_t& id) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float od = __shfl_xor(d, o);
+    const uint32_t oi = __shfl_xor(id, o);
+    if (od < d || (od == d && oi < id)) { d = od; id = oi; }
+  }
+}
+__device__ __forceinline__ uint64_t wave_sum(uint64_t x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+  return x;
+}
+__device__ __forceinline__ double wave_sumd(double x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+  return x;
+}
+
+__global__ void __launch_bounds__(64) k_team_round(const DrlArgs A) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const uint32_t s = blockIdx.x, lane = threadIdx.x;
+  const uint32_t n = A.n, m = A.m, kcap = A.kcap, P = A.P, qn = A.qn;
+  HeapE* hp = (HeapE*)lds;                                   // [kcap]
+  uint32_t* nbuf = (uint32_t*)(lds + (size_t)kcap * 8);     // [n][m] the round's neighbour lists
+  uint32_t* bat = nbuf + (size_t)n * m;                      // [n] the round's ids
+  float* dbuf = (float*)(bat + n);                           // [n] their distances
+  uint32_t* pbuf = (uint32_t*)(dbuf + n);                    // [n] their partitions (bucketing)
+
+  DrlSess* SS = A.sess + s;
+  uint64_t rng = SS->rng;
+  uint32_t nknown = SS->nknown, nheap = SS->nheap;
+  HeapE* gheap = (HeapE*)(A.heap + (uint64_t)s * kcap);
+  uint64_t* ktab = A.ktab + (uint64_t)s * 2 * kcap;
+  const uint32_t kmask = 2 * kcap - 1;
+  uint32_t* knb = A.knb + (uint64_t)s * kcap * m;
+  float* kdist = A.kdist + (uint64_t)s * kcap;
+  uint32_t* kid = A.kid + (uint64_t)s * kcap;
+  uint32_t* gbat = A.batch + (uint64_t)s * n;
+  const uint32_t base = s * P * qn;   // this session's first sub-query of the shared step
+
+  if (A.mode == DRL_BEGIN) {
+    // knn_reset: an empty known set and heap
+    for (uint32_t i = lane; i < 2 * kcap; i += 64) ktab[i] = 0;
+    nknown = 0;
+    nheap = 0;
+    __threadfence();
+    // knn_begin_finish (search.go:130-146): the first `parallel` start
+    // vertices in (distance, position) order become known (with their true
+    // neighbour lists: GetStartVertex is non-private) and go on the heap
+    const float* sd = A.start_dist + (uint64_t)s * A.ns;
+    const uint32_t* sid = A.start_ids + (uint64_t)s * A.ns;
+    const uint32_t take = min(A.parallel, A.ns);
+    float pd = 0.0f;
+    uint32_t ppos = 0;
+    for (uint32_t t = 0; t < take; ++t) {
+      float bd = __builtin_inff();
+      uint32_t bp = 0xffffffffu;
+      for (uint32_t j = lane; j < A.ns; j += 64) {
+        const float d = sd[j];
+        const bool after = t == 0 || d > pd || (d == pd && j > ppos);
+        if (after && (d < bd || (d == bd && j < bp))) { bd = d; bp = j; }
+      }
+      wave_min2(bd, bp);
+      pd = bd; ppos = bp;
+      const uint32_t id = sid[bp], slot = nknown++;
+      if (lane < m) knb[(uint64_t)slot * m + lane] = A.graph[(uint64_t)id * m + lane];
+      if (lane == 0) {
+        kdist[slot] = bd;
+        kid[slot] = id;
+        tab_put(ktab, kmask, id, slot);
+      }
+      heap_push(hp, nheap, HeapE{bd, slot}, lane);
+    }
+    __threadfence();
+  } else {
+    for (uint32_t i = lane; i < nheap; i += 64) hp[i] = gheap[i];
+    for (uint32_t i = lane; i < n; i += 64) bat[i] = gbat[i];
+    __syncthreads();
+    // ---- the last shared step's results (post_results): localCache entries
+    for (uint32_t j = lane; j < P * qn; j += 64) {
+      const PmOutHdr h = A.hdr[base + j];
+      if (h.status == ST_OK) {
+        const PmSub sub = A.subs[base + j];
+        const uint32_t p = sub.part - s * P;
+        tab_put(A.ctab[s] + (uint64_t)p * (A.cmask + 1), A.cmask, (uint32_t)sub.idx, h.ref);
+      }
+    }
+    // ---- each position's response (bq_emit_fast) and GetVertexInfo's decode
+    const uint32_t* rows32 = (const uint32_t*)A.rows;
+    uint64_t succ = 0;
+    for (uint32_t i = lane; i < n; i += 64) {
+      const uint32_t id = bat[i];
+      const uint32_t p = (uint32_t)(id / A.PS);
+      const uint32_t b0 = base + p * qn;
+      int32_t src = -1;
+      for (uint32_t j = 0; j < qn; ++j)
+        if (A.gid[b0 + j] == (uint64_t)id) src = (int32_t)(b0 + j);   // last wins
+      float d = 0.0f;
+      for (int hop = 0; src >= 0 && A.hdr[src].status == ST_DUP && hop < 2; ++hop) src = (int32_t)A.hdr[src].ref;
+      if (src >= 0) d = A.hdr[src].dist;
+      const uint32_t* r = rows32 + (uint64_t)(src >= 0 ? src : 0) * 2 * A.E + A.dim;
+      const uint32_t* tg = A.graph + (uint64_t)id * m;
+      bool same = true;
+      for (uint32_t k = 0; k < m; ++k) {
+        const uint32_t v = src >= 0 ? r[k] : 0u;
+        nbuf[(size_t)i * m + k] = v;
+        same &= v == tg[k];
+      }
+      dbuf[i] = d;
+      succ += same;
+    }
+    succ = wave_sum(succ);
+    if (lane == 0) SS->succ += succ;
+    __syncthreads();
+    // ---- SearchKNN's update (search.go:185-207): in position order, ids not
+    // yet known with a non-empty neighbour list become known and are pushed
+    for (uint32_t c0 = 0; c0 < n; c0 += 64) {
+      const uint32_t i = c0 + lane;
+      bool nw = false;
+      if (i < n) {
+        const uint32_t id = bat[i];
+        bool nz = false;
+        for (uint32_t k = 0; k < m; ++k) nz |= nbuf[(size_t)i * m + k] != 0;
+        bool dup = false;
+        for (uint32_t j = 0; j < i && !dup; ++j) dup = bat[j] == id;   // an earlier position: known by then
+        uint32_t v;
+        nw = nz && !dup && !tab_find(ktab, kmask, id, &v);
+      }
+      const uint64_t b = __ballot(nw);
+      const uint32_t slot = nknown + (uint32_t)__builtin_popcountll(b & ((1ull << lane) - 1ull));
+      if (nw) {
+        const uint32_t id = bat[i];
+        for (uint32_t k = 0; k < m; ++k) knb[(uint64_t)slot * m + k] = nbuf[(size_t)i * m + k];
+        kdist[slot] = dbuf[i];
+        kid[slot] = id;
+        tab_put(ktab, kmask, id, slot);
+      }
+      for (uint64_t bb = b; bb; bb &= bb - 1) {   // the pushes, in position order
+        const uint32_t l = (uint32_t)__builtin_ctzll(bb);
+        const uint32_t ps = nknown + (uint32_t)__builtin_popcountll(b & ((1ull << l) - 1ull));
+        heap_push(hp, nheap, HeapE{dbuf[c0 + l], ps}, lane);
+      }
+      nknown += (uint32_t)__builtin_popcountll(b);
+    }
+    __threadfence();   // the new known rows are read back by this launch's pops
+  }
+
+  if (A.mode != DRL_END) {
+    // ---- the next batch (search.go:153-171)
+    for (uint32_t r = 0; r < A.parallel; ++r) {
+      if (nheap == 0) {   // rng.Intn(n) for each of the m positions (SplitMix::next: state += gamma, then mix)
+        if (lane < m) bat[r * m + lane] = (uint32_t)(sm64(rng + (uint64_t)lane * 0x9e3779b97f4a7c15ULL) % A.N);
+        rng += (uint64_t)m * 0x9e3779b97f4a7c15ULL;
+      } else {
+        const HeapE e = heap_pop(hp, nheap, lane);
+        if (lane < m) bat[r * m + lane] = knb[(uint64_t)e.slot * m + lane];
+      }
+    }
+    __syncthreads();
+    // ---- SimpleBatchPianoPIR.Query's bucketing into the next shared step
+    for (uint32_t i = lane; i < n; i += 64) pbuf[i] = (uint32_t)(bat[i] / A.PS);
+    __syncthreads();
+    double bytes = 0.0;
+    uint32_t nreal = 0;
+    for (uint32_t i = lane; i < n; i += 64) {
+      const uint32_t id = bat[i], p = pbuf[i];
+      uint32_t rank = 0;
+      for (uint32_t j = 0; j < i; ++j) rank += pbuf[j] == p;
+      if (rank < qn) {   // the first queryNumToMake ids of a partition; the rest are dropped
+        const uint32_t j = base + p * qn + rank;
+        const uint32_t local = (uint32_t)(id - (uint64_t)p * A.PS);
+        uint32_t slot;
+        PmSub sub{s * P + p, SUB_REAL, local};
+        if (tab_find(A.ctab[s] + (uint64_t)p * (A.cmask + 1), A.cmask, local, &slot)) {
+          sub.kind = SUB_HOSTCACHE;
+          sub.idx = slot;
+        } else {
+          bytes += A.part_bytes[p];
+          nreal++;
+        }
+        A.subs[j] = sub;
+        A.gid[j] = id;
+      }
+    }
+    for (uint32_t p = lane; p < P; p += 64) {   // dummy padding (batch-pir.go:182-190)
+      uint32_t cnt = 0;
+      for (uint32_t i = 0; i < n; ++i) cnt += pbuf[i] == p;
+      uint64_t dc = A.dummy[(uint64_t)s * P + p];
+      for (uint32_t j = cnt; j < qn; ++j) {
+        A.subs[base + p * qn + j] = PmSub{s * P + p, SUB_DUMMY, dc++};
+        A.gid[base + p * qn + j] = ~0ull;
+        bytes += A.part_bytes[p];
+      }
+      A.dummy[(uint64_t)s * P + p] = dc;
+    }
+    if (A.step_bytes) {
+      bytes = wave_sumd(bytes);
+      const uint64_t nr = wave_sum(nreal);
+      if (lane == 0) {
+        A.step_bytes[(uint64_t)A.seq * A.S + s] = bytes;
+        A.step_real[(uint64_t)A.seq * A.S + s] = (uint32_t)nr;
+      }
+    }
+    for (uint32_t i = lane; i < n; i += 64) gbat[i] = bat[i];
+    for (uint32_t i = lane; i < nheap; i += 64) gheap[i] = hp[i];
+  } else {
+    // ---- the top k by (distance, id) (search.go:211-233), -1 padded
+    float* ld = (float*)lds;                          // the heap's LDS, no longer needed
+    uint32_t* li = (uint32_t*)(lds + (size_t)kcap * 4);
+    for (uint32_t j = lane; j < nknown; j += 64) { ld[j] = kdist[j]; li[j] = kid[j]; }
+    __syncthreads();
+    int64_t* out = A.answers + ((uint64_t)s * A.q + A.qi) * A.k;
+    float pd = 0.0f;
+    uint32_t pi = 0;
+    for (uint32_t t = 0; t < A.k; ++t) {
+      float bd = __builtin_inff();
+      uint32_t bi = 0xffffffffu;
+      bool any = false;
+      for (uint32_t j = lane; j < nknown; j += 64) {
+        const float d = ld[j];
+        const uint32_t id = li[j];
+        const bool after = t == 0 || d > pd || (d == pd && id > pi);
+        if (after && (!any || d < bd || (d == bd && id < bi))) { bd = d; bi = id; any = true; }
+      }
+      const bool found = __ballot(any) != 0;
+      wave_min2(bd, bi);   // lanes without a candidate hold (inf, ~0): never below a real one
+      if (lane == 0) out[t] = found ? (int64_t)bi : -1;
+      if (!found) {
+        for (uint32_t u = t + 1 + lane; u < A.k; u += 64) out[u] = -1;
+        break;
+      }
+      pd = bd; pi = bi;
+    }
+  }
+  if (lane == 0) {
+    SS->rng = rng;
+    SS->nknown = nknown;
+    SS->nheap = A.mode == DRL_END ? 0u : nheap;
+  }
+}
+
+static uint32_t team_round_lds_impl(uint32_t kcap, uint32_t n, uint32_t m) {
+  return kcap * 8 + n * m * 4 + 3 * n * 4;
+}
+
+static void team_round_impl(hipStream_t st, const DrlArgs& A, hipEvent_t a, hipEvent_t b) {
+  const uint32_t lds = team_round_lds_impl(A.kcap, A.n, A.m);
+  if (a) hipExtLaunchKernelGGL(k_team_round, dim3(A.S), dim3(64), lds, st, a, b, 0, A);
+  else hipLaunchKernelGGL(k_team_round, dim3(A.S), dim3(64), lds, st, A);
+}
+
+}  // namespace pm
+
+namespace pmk {
+void team_round(hipStream_t st, const DrlArgs& A, PmEvents ev) { pm::team_round_impl(st, A, ev.a, ev.b); }
+uint32_t team_round_lds(uint32_t kcap, uint32_t n, uint32_t m) { return pm::team_round_lds_impl(kcap, n, m); }
+}  // namespace pmk

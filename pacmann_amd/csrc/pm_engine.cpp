@@ -73,6 +73,9 @@ struct FlatMap {
     put(k, v);
     return true;
   }
+  template <class F> void for_each(F&& f) const {
+    for (const Slot& x : slot) if (x.gen == cur) f(x.key, x.val);
+  }
 };
 
 // ---------------------------------------------------------------------------
@@ -169,9 +172,10 @@ struct HostBuf {
 // by the batch layer's overflow drop (dropped), by a failed sub-query of this
 // rank (failed), by another rank's sub-query (peer), or not at all (unexplained).
 // "host_fold_*" count the maintenance fold launches by kernel (k_prep_fold_rot
-// at CS 512 / 1,024, or another form).
-enum HostTimer : int { HT_STEP_LAUNCH, HT_STEP_WAIT, HT_STEP_POST, HT_BATCH_QUERY, HT_GVI_PARSE, HT_SEARCH_KNN, HT_KNN_INIT, HT_KNN_BATCH, HT_KNN_UPDATE, HT_KNN_FINAL, HT_WAIT_FIRST, HT_WAIT_ALL, HT_ROWS_SEEN, HT_ROWS_TORN, HT_WAIT_DONE, HT_COMBINE, HT_COMBINE_TURN, HT_PATH_MATCH, HT_PATH_MATCH_PART, HT_PATH_MATCH_PART8, HT_PREP_SETS, HT_REC_VERIFIED, HT_REC_BAD, HT_REC_DROPPED, HT_REC_FAILED, HT_REC_PEER, HT_REC_UNEXPLAINED, HT_FOLD_ROT512, HT_FOLD_ROT1024, HT_FOLD_OTHER, HT_COUNT };
-static const char* const kHostTimerName[HT_COUNT] = {"host_step_launch", "host_step_wait", "host_step_post", "host_batch_query", "host_gvi_parse", "host_search_knn", "host_knn_init", "host_knn_batch", "host_knn_update", "host_knn_final", "host_wait_first_token", "host_wait_all_tokens", "host_rows_seen", "host_rows_torn", "host_wait_done", "host_combine", "host_combine_turn", "host_path_match", "host_path_match_part", "host_path_match_part8", "host_prep_sets", "host_records_verified", "host_records_bad", "host_records_dropped", "host_records_failed", "host_records_peer", "host_records_unexplained", "host_fold_rot512", "host_fold_rot1024", "host_fold_other"};
+// at CS 512 / 1,024, or another form); "host_dev_steps" / "host_dev_queries"
+// the shared steps and session queries the device loop served (pm_drl.hip).
+enum HostTimer : int { HT_STEP_LAUNCH, HT_STEP_WAIT, HT_STEP_POST, HT_BATCH_QUERY, HT_GVI_PARSE, HT_SEARCH_KNN, HT_KNN_INIT, HT_KNN_BATCH, HT_KNN_UPDATE, HT_KNN_FINAL, HT_WAIT_FIRST, HT_WAIT_ALL, HT_ROWS_SEEN, HT_ROWS_TORN, HT_WAIT_DONE, HT_COMBINE, HT_COMBINE_TURN, HT_PATH_MATCH, HT_PATH_MATCH_PART, HT_PATH_MATCH_PART8, HT_PREP_SETS, HT_REC_VERIFIED, HT_REC_BAD, HT_REC_DROPPED, HT_REC_FAILED, HT_REC_PEER, HT_REC_UNEXPLAINED, HT_FOLD_ROT512, HT_FOLD_ROT1024, HT_FOLD_OTHER, HT_DEV_STEPS, HT_DEV_QUERIES, HT_COUNT };
+static const char* const kHostTimerName[HT_COUNT] = {"host_step_launch", "host_step_wait", "host_step_post", "host_batch_query", "host_gvi_parse", "host_search_knn", "host_knn_init", "host_knn_batch", "host_knn_update", "host_knn_final", "host_wait_first_token", "host_wait_all_tokens", "host_rows_seen", "host_rows_torn", "host_wait_done", "host_combine", "host_combine_turn", "host_path_match", "host_path_match_part", "host_path_match_part8", "host_prep_sets", "host_records_verified", "host_records_bad", "host_records_dropped", "host_records_failed", "host_records_peer", "host_records_unexplained", "host_fold_rot512", "host_fold_rot1024", "host_fold_other", "host_dev_steps", "host_dev_queries"};
 
 struct TimedLaunch { std::string name; hipEvent_t a, b; double bytes; };
 
@@ -376,6 +380,9 @@ extern "C" int pm_timing_timeline(pm_ctx* c, const char* path) {
 // "verify_records" (sharded loop): check the records of every value-th shared
 // step of each team on the host (0: off); read when a loop starts
 static std::atomic<int> g_verify_records{0};
+// "device_loop": pm_search_loop_batched's device loop (run_batched_dev) 1 / 0;
+// -1: the environment's choice (PM_DEVICE_LOOP, default 1)
+static std::atomic<int> g_device_loop{-1};
 // Bound on the communicators' creation and on the probe (pm_set_option
 // "rccl_timeout_s", else PM_RCCL_TIMEOUT_S, default 120 s): a rank whose peer
 // never joins returns PM_ETIMEDOUT instead of blocking inside RCCL.
@@ -384,6 +391,7 @@ extern "C" int pm_set_option(const char* name, int value) {
   if (!name) return fail(PM_EINVAL, "NULL argument");
   if (!strcmp(name, "verify_records")) { g_verify_records.store(value < 0 ? 0 : value); return 0; }
   if (!strcmp(name, "rccl_timeout_s")) { g_rccl_timeout_s.store(value); return 0; }
+  if (!strcmp(name, "device_loop")) { g_device_loop.store(value < 0 ? -1 : value); return 0; }
   if (pmk::set_option(name, value)) return fail(PM_EINVAL, std::string("unknown option ") + name);
   return 0;
 }
@@ -485,6 +493,13 @@ struct Engine {
   uint64_t qn = 0;                  // queryNumToMake of the batch being served
   uint64_t prep_gen = 0;            // preprocessings run (any range): a shared step re-copies the parts
   std::vector<uint64_t> zero_row;   // response of dropped / failed ids (batch-pir.go:229-236)
+  // The device loop's copy of the localCache indexes (pm_drl.hip): [P][cmask + 1]
+  // entries {local idx + 1 | arena slot << 32}.  cache_on_dev: the device copy
+  // is the truth and the host FlatMaps are stale (ensure_host_cache brings them
+  // back); dcache_valid: the device copy equals the host's.
+  DevBuf dcache;
+  uint32_t dcache_cmask = 0;
+  bool cache_on_dev = false, dcache_valid = false;
 };
 
 // NewPianoPIR parameterisation (pir.go:479-514) + NewPianoPIRClient (:130-175)
@@ -747,10 +762,34 @@ static int upload_parts_async(Engine* g, hipStream_t st) {
 // (pir.go:203-255: new key from the next epoch, reset counters and cache);
 // uploads the parts (on `st` without synchronising when given).  Fills `todo`
 // with the partitions to fold.
+// The localCache indexes back from the device loop's copy (pm_drl.hip) before
+// a host-side use: the FlatMaps are rebuilt from the device table, which is
+// then stale (the host path owns the index until the next device loop).
+// Callers have synchronised the loop's streams (it ends with them drained).
+static int ensure_host_cache(Engine* g) {
+  if (!g->cache_on_dev) return 0;
+  const uint64_t cap = (uint64_t)g->dcache_cmask + 1;
+  std::vector<uint64_t> t(g->P * cap);
+  HIPCHK(hipSetDevice(g->ctx->device));
+  HIPCHK(hipMemcpy(t.data(), g->dcache.p, t.size() * 8, hipMemcpyDeviceToHost));
+  for (uint64_t p = 0; p < g->P; ++p) {
+    FlatMap& c = g->parts[p].cache;
+    c.clear();
+    for (uint64_t i = 0; i < cap; ++i)
+      if (const uint64_t e = t[p * cap + i]) c.put((uint32_t)e - 1u, (uint32_t)(e >> 32));
+  }
+  g->cache_on_dev = false;
+  g->dcache_valid = false;
+  return 0;
+}
+
 static int engine_prep_host(Engine* g, uint64_t p0, uint64_t p1, std::vector<uint64_t>& todo,
                             hipStream_t st = nullptr) {
   // the owned partitions in [p0, p1): all of them (owned_d) or a single one
   if (p1 - p0 > 1 && !(p0 == 0 && p1 == g->P)) return fail(PM_EINVAL, "engine_prep: unsupported range");
+  const bool all = p0 == 0 && p1 == g->P;
+  if (g->cache_on_dev && !all) CHK(ensure_host_cache(g));   // one partition's prep keeps the others' entries
+  if (all) { g->cache_on_dev = false; g->dcache_valid = false; }   // every index cleared below: the host's (empty) is the truth
   todo.clear();
   for (uint64_t i = p0; i < p1; ++i)
     if (g->parts[i].owned) todo.push_back(i);
@@ -1481,6 +1520,7 @@ static inline bool status_ok(uint32_t st) { return st == ST_OK || st == ST_CACHE
 //                re-preprocessing trigger (:238-247).
 static int bq_prepare(Engine* g, const uint64_t* idx, uint64_t n, bool* fast) {
   const uint64_t E = g->E, P = g->P;
+  CHK(ensure_host_cache(g));
   if (g->zero_row.size() != E) g->zero_row.assign(E, 0);
   for (uint64_t i = 0; i < n; ++i)
     if (idx[i] >= g->N) return fail(PM_EINVAL, "id " + std::to_string(idx[i]) + " >= DBSize");
@@ -1827,6 +1867,7 @@ struct pm_graph {
   const float* vectors = nullptr;
   const uint32_t* graph = nullptr;
   std::shared_ptr<DevBuf> dvec = std::make_shared<DevBuf>();
+  std::shared_ptr<DevBuf> dgraph = std::make_shared<DevBuf>();   // [n][m] on the device (device loop), made on first use
   // Sharded / synthetic graphs (pm_graph_create_shard / _synth): the batch
   // PIR holds the partitions p % nshards == shard only, and there is no device
   // copy of all vectors (dvec stays empty): the start set's vectors, fetched
@@ -1966,6 +2007,7 @@ extern "C" int pm_graph_create_session(pm_ctx* ctx, pm_graph* base, uint64_t pir
   g->vec_own = base->vec_own; g->graph_own = base->graph_own;
   g->vectors = base->vectors; g->graph = base->graph;
   g->dvec = base->dvec;
+  g->dgraph = base->dgraph;
   g->shard = base->shard; g->nshards = base->nshards;
   g->synth = base->synth; g->data_seed = base->data_seed;
   g->server = base->pir;
@@ -2617,6 +2659,97 @@ static void group_stage_session(StepGroup& G, uint32_t s) {
   ss.ok = true;
 }
 
+// The kernels of one shared step whose descriptor S is complete: the hint
+// search + resolution (k_match_resolve_s where the shapes hold), the split
+// gather for wide sets, the answer; the completion event unless the records
+// go to a combine.  (group_step; the device loop's steps, run_batched_dev.)
+static int group_step_launch(StepGroup& G, PmStep& S, uint32_t max_per_part, uint32_t nreal, double ans_bytes) {
+  pm_ctx* c = G.c;
+  hipStream_t st = c->stream;
+  const uint32_t nsub = S.nsub, np = S.np;
+  (void)np;
+  auto t0 = Clock::now();
+  const bool lds = pmk::step_resolve_lds_ok(G.maxPH, max_per_part);
+  S.nsplit = c->no_split ? 1 : pmk::step_gather_split(G.maxSS, nsub);
+  const pmk::StepOpts opts = pmk::step_opts();   // one snapshot: np_live, the qset and the kernels agree
+  if (pmk::step_qset_ok(S, opts, lds, G.ph8, G.maxPH, max_per_part, G.maxSS)) {
+    S.qw = (G.maxSS + 7) & ~7u;
+    CHK(G.qset.reserve((uint64_t)nsub * S.qw * 2));
+    S.qset = G.qset.as<uint16_t>();
+  }
+  if (pmk::step_match_resolve_ok(S, opts, lds)) {   // one launch: match + resolve per partition
+    if (pmk::step_match_resolve_small(opts, G.ph8, G.maxPH, max_per_part)) S.np_live = 0;   // resolvers do not count in
+#ifdef PM_MR_STAMPS
+    static const char* mr_file = getenv("PM_MR_STAMPS");   // append {np} + np x 8 stamps per step
+    static std::atomic<int> mr_steps{0};   // the first 40 steps of the run
+    const bool mr_this = mr_file && mr_steps.fetch_add(1) < 40;
+    if (mr_this) {
+      CHK(G.stamps.reserve((uint64_t)np * 8 * 8));
+      HIPCHK(hipMemsetAsync(G.stamps.p, 0, (uint64_t)np * 8 * 8, st));
+      S.stamps = G.stamps.as<uint64_t>();
+    }
+#endif
+    c->timed_ext("match_resolve", (double)nreal * G.maxPH, [&](pmk::PmEvents ev) { pmk::step_match_resolve(st, S, opts, G.ph8, G.maxPH, max_per_part, ev); }, 2);
+#ifdef PM_MR_STAMPS
+    if (mr_this) {
+      HIPCHK(hipStreamSynchronize(st));
+      std::vector<uint64_t> t((uint64_t)np * 8);
+      HIPCHK(hipMemcpy(t.data(), G.stamps.p, t.size() * 8, hipMemcpyDeviceToHost));
+      static std::mutex mu;
+      std::lock_guard<std::mutex> lk(mu);
+      if (FILE* f = fopen(mr_file, "ab")) {
+        const uint64_t h = np;
+        fwrite(&h, 8, 1, f);
+        fwrite(t.data(), 8, t.size(), f);
+        fclose(f);
+      }
+      S.stamps = nullptr;
+    }
+#endif
+  } else {
+    int path = 0;
+    c->timed_ext("hint_match", (double)nreal * G.maxPH, [&](pmk::PmEvents ev) { path = pmk::step_match(st, S, opts, G.ph8, G.maxPH, max_per_part, ev); }, 2);
+    c->count_match_path(path);
+    c->timed_ext("resolve", 0, [&](pmk::PmEvents ev) { pmk::step_resolve(st, S, lds, ev); }, 2);
+  }
+  if (S.nsplit > 1) {
+    CHK(G.part_x.reserve((uint64_t)nsub * S.nsplit * (G.E & ~3u) * 8));
+    S.part_x = G.part_x.as<uint64_t>();
+    c->timed_ext("gather", ans_bytes, [&](pmk::PmEvents ev) { pmk::step_gather(st, S, ev); }, 2);
+  }
+#ifdef PM_ANSWER_STAMPS
+  static const char* stamp_file = getenv("PM_ANSWER_STAMPS");   // append {nsub} + nsub x 8 stamps per step
+  static std::atomic<int> stamp_steps{0};   // the first 40 steps of the run (file size)
+  const bool stamp_this = stamp_file && stamp_steps.fetch_add(1) < 40;
+  if (stamp_this) {
+    CHK(G.stamps.reserve((uint64_t)nsub * 8 * 8));
+    HIPCHK(hipMemsetAsync(G.stamps.p, 0, (uint64_t)nsub * 8 * 8, st));
+    S.stamps = G.stamps.as<uint64_t>();
+  }
+#endif
+  c->timed_ext("answer", S.nsplit > 1 ? 0 : ans_bytes, [&](pmk::PmEvents ev) { pmk::step_answer(st, S, G.maxSS, ev); }, 2);
+  if (!G.comb) G.seq = c->record_done(st);   // sharded: group_exchange publishes the records
+  HIPCHK(hipGetLastError());
+#ifdef PM_ANSWER_STAMPS
+  if (stamp_this) {
+    HIPCHK(hipStreamSynchronize(st));
+    std::vector<uint64_t> t((uint64_t)nsub * 8);
+    HIPCHK(hipMemcpy(t.data(), G.stamps.p, t.size() * 8, hipMemcpyDeviceToHost));
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lk(mu);
+    if (FILE* f = fopen(stamp_file, "ab")) {
+      const uint64_t h = nsub;
+      fwrite(&h, 8, 1, f);
+      fwrite(t.data(), 8, t.size(), f);
+      fclose(f);
+    }
+  }
+#endif
+  c->host_add(HT_STEP_LAUNCH, ms_since(t0));
+  G.pf_w0 = S.pf_w0; G.pf_w1 = S.pf_w1;
+  return 0;
+}
+
 // One shared step over the clients whose sub-queries are ready (in[s]).
 static int group_step(StepGroup& G, const std::vector<char>& in) {
   pm_ctx* c = G.c;
@@ -2770,86 +2903,7 @@ static int group_step(StepGroup& G, const std::vector<char>& in) {
     S.pf_w1 = (uint32_t)((end + 7) / 8);
     S.rows_partial = G.rows_partial && !c->verify_rows && !c->debug_cache ? 1u : 0u;
   }
-  auto t0 = Clock::now();
-  const bool lds = pmk::step_resolve_lds_ok(G.maxPH, max_per_part);
-  S.nsplit = c->no_split ? 1 : pmk::step_gather_split(G.maxSS, nsub);
-  const pmk::StepOpts opts = pmk::step_opts();   // one snapshot: np_live, the qset and the kernels agree
-  if (pmk::step_qset_ok(S, opts, lds, G.ph8, G.maxPH, max_per_part, G.maxSS)) {
-    S.qw = (G.maxSS + 7) & ~7u;
-    CHK(G.qset.reserve((uint64_t)nsub * S.qw * 2));
-    S.qset = G.qset.as<uint16_t>();
-  }
-  if (pmk::step_match_resolve_ok(S, opts, lds)) {   // one launch: match + resolve per partition
-    if (pmk::step_match_resolve_small(opts, G.ph8, G.maxPH, max_per_part)) S.np_live = 0;   // resolvers do not count in
-#ifdef PM_MR_STAMPS
-    static const char* mr_file = getenv("PM_MR_STAMPS");   // append {np} + np x 8 stamps per step
-    static std::atomic<int> mr_steps{0};   // the first 40 steps of the run
-    const bool mr_this = mr_file && mr_steps.fetch_add(1) < 40;
-    if (mr_this) {
-      CHK(G.stamps.reserve((uint64_t)np * 8 * 8));
-      HIPCHK(hipMemsetAsync(G.stamps.p, 0, (uint64_t)np * 8 * 8, st));
-      S.stamps = G.stamps.as<uint64_t>();
-    }
-#endif
-    c->timed_ext("match_resolve", (double)nreal * G.maxPH, [&](pmk::PmEvents ev) { pmk::step_match_resolve(st, S, opts, G.ph8, G.maxPH, max_per_part, ev); }, 2);
-#ifdef PM_MR_STAMPS
-    if (mr_this) {
-      HIPCHK(hipStreamSynchronize(st));
-      std::vector<uint64_t> t((uint64_t)np * 8);
-      HIPCHK(hipMemcpy(t.data(), G.stamps.p, t.size() * 8, hipMemcpyDeviceToHost));
-      static std::mutex mu;
-      std::lock_guard<std::mutex> lk(mu);
-      if (FILE* f = fopen(mr_file, "ab")) {
-        const uint64_t h = np;
-        fwrite(&h, 8, 1, f);
-        fwrite(t.data(), 8, t.size(), f);
-        fclose(f);
-      }
-      S.stamps = nullptr;
-    }
-#endif
-  } else {
-    int path = 0;
-    c->timed_ext("hint_match", (double)nreal * G.maxPH, [&](pmk::PmEvents ev) { path = pmk::step_match(st, S, opts, G.ph8, G.maxPH, max_per_part, ev); }, 2);
-    c->count_match_path(path);
-    c->timed_ext("resolve", 0, [&](pmk::PmEvents ev) { pmk::step_resolve(st, S, lds, ev); }, 2);
-  }
-  if (S.nsplit > 1) {
-    CHK(G.part_x.reserve((uint64_t)nsub * S.nsplit * (G.E & ~3u) * 8));
-    S.part_x = G.part_x.as<uint64_t>();
-    c->timed_ext("gather", ans_bytes, [&](pmk::PmEvents ev) { pmk::step_gather(st, S, ev); }, 2);
-  }
-#ifdef PM_ANSWER_STAMPS
-  static const char* stamp_file = getenv("PM_ANSWER_STAMPS");   // append {nsub} + nsub x 8 stamps per step
-  static std::atomic<int> stamp_steps{0};   // the first 40 steps of the run (file size)
-  const bool stamp_this = stamp_file && stamp_steps.fetch_add(1) < 40;
-  if (stamp_this) {
-    CHK(G.stamps.reserve((uint64_t)nsub * 8 * 8));
-    HIPCHK(hipMemsetAsync(G.stamps.p, 0, (uint64_t)nsub * 8 * 8, st));
-    S.stamps = G.stamps.as<uint64_t>();
-  }
-#endif
-  c->timed_ext("answer", S.nsplit > 1 ? 0 : ans_bytes, [&](pmk::PmEvents ev) { pmk::step_answer(st, S, G.maxSS, ev); }, 2);
-  if (!G.comb) G.seq = c->record_done(st);   // sharded: group_exchange publishes the records
-  HIPCHK(hipGetLastError());
-#ifdef PM_ANSWER_STAMPS
-  if (stamp_this) {
-    HIPCHK(hipStreamSynchronize(st));
-    std::vector<uint64_t> t((uint64_t)nsub * 8);
-    HIPCHK(hipMemcpy(t.data(), G.stamps.p, t.size() * 8, hipMemcpyDeviceToHost));
-    static std::mutex mu;
-    std::lock_guard<std::mutex> lk(mu);
-    if (FILE* f = fopen(stamp_file, "ab")) {
-      const uint64_t h = nsub;
-      fwrite(&h, 8, 1, f);
-      fwrite(t.data(), 8, t.size(), f);
-      fclose(f);
-    }
-  }
-#endif
-  c->host_add(HT_STEP_LAUNCH, ms_since(t0));
-  G.pf_w0 = S.pf_w0; G.pf_w1 = S.pf_w1;
-  return 0;
+  return group_step_launch(G, S, max_per_part, nreal, ans_bytes);
 }
 
 // The lines session s's collect will read (its result headers and the row
@@ -3828,6 +3882,371 @@ static int run_batched_pool(pm_graph** gs, uint32_t S, const float* queries, uin
   return 0;
 }
 
+// ---- the device loop (pm_drl.hip) -------------------------
+// The batched serving loop with each team's rounds chained on the GPU: per
+// query and team, [queries -> qbuf, start-set L2, k_team_round BEGIN], then per
+// round [k_match_resolve_s, k_answer_p, k_team_round MID / END] on the team's
+// stream, enqueued ahead; the host only decides the maintenance between
+// queries (its schedule is a function of the counters alone) and runs it as
+// one launch set of every triggered client, like run_batched_pool.  Taken when
+// drl_plan shows that every round of the call would take the host's one-step
+// path (no partition at its query budget, no batch-layer re-preprocessing);
+// otherwise, or with pm_set_option("device_loop", 0) / PM_DEVICE_LOOP=0, the
+// host loop serves the call.  Every session's answers, counters and state
+// equal the host loop's (tests/test_gpu_parity.py, test_gpu_headline.py).
+static bool device_loop_on() {
+  const int o = g_device_loop.load();
+  if (o >= 0) return o != 0;
+  static const int env = [] { const char* e = getenv("PM_DEVICE_LOOP"); return e ? atoi(e) : 1; }();
+  return env != 0;
+}
+static uint32_t pow2_at_least(uint64_t x) { uint32_t c = 1; while (c < x) c *= 2; return c; }
+
+struct DrlShape { uint32_t n = 0, qn = 0, kcap = 0, cmask = 0; };
+// Whether the device loop can serve the call, and its shape.  The counters
+// FinishedBatchNum / QueriesMadeInPartition advance by fixed amounts per round
+// (n / B, queryNumToMake) and reset at the harness's maintenance
+// (private-search.go:226-232), so the whole call's schedule is known here: a
+// query is chained on the device only if no round of it can reach a
+// partition's budget (FinishedQueryNum + real sub-queries >= MaxQueryNum:
+// bq_prepare's slow path; FinishedQueryNum <= QueriesMadeInPartition always)
+// or the batch layer's trigger (QueriesMadeInPartition >= MaxQueryNum - 2).
+static bool drl_plan(pm_graph** gs, uint32_t S, uint64_t q, int k, int step, int parallel, DrlShape* sh) {
+  if (!device_loop_on() || S == 0 || step <= 0 || parallel <= 0 || k <= 0) return false;
+  const pm_graph* g0 = gs[0];
+  const Engine& e0 = g0->pir->e;
+  const uint64_t m = g0->m, n = (uint64_t)parallel * m, P = e0.P;
+  if (m == 0 || m > 64 || n > pmk::kDrlMaxN || n * m > pmk::kDrlMaxNM || P == 0 || P > 64) return false;
+  const uint64_t qn = n / P;
+  if (qn == 0 || qn > pmk::step_max_sub_per_part() || e0.B == 0) return false;
+  const uint64_t kcap = pow2_at_least((uint64_t)parallel + (uint64_t)step * n);
+  if (kcap > pmk::kDrlMaxKcap || (uint64_t)k > kcap || pmk::team_round_lds(kcap, n, m) > 64 * 1024) return false;
+  uint64_t maxq = ~0ull;
+  for (uint32_t i = 0; i < S; ++i) {
+    const pm_graph* g = gs[i];
+    const Engine& e = g->pir->e;
+    if (g->nonprivate || g->synth || !g->graph || !g->dvec->p || e.nshards != 1 || e.P != P || e.B != e0.B ||
+        e.pf_off != g->dim * 4 || g->dim > 0xffffffffull || g->n >= 0xffffffffull || e.PS >= 0xffffffffull)
+      return false;
+    uint64_t mq = ~0ull;
+    for (const PartHost& ph : e.parts) {
+      mq = std::min(mq, ph.maxq64);
+      maxq = std::max<uint64_t>(maxq == ~0ull ? 0 : maxq, ph.maxq64);   // localCache entries per partition <= MaxQueryNum
+      if (ph.fqn > e.QMIP) return false;   // the bound below needs FinishedQueryNum <= QueriesMadeInPartition
+    }
+    uint64_t fbn = e.FBN, qmip = e.QMIP;
+    for (uint64_t qi = 0; qi < q; ++qi) {
+      if (qmip + (uint64_t)step * qn >= mq || qmip + (uint64_t)(step - 1) * qn + 2 >= e.parts[0].maxq64) return false;
+      fbn += (uint64_t)step * (n / e.B);
+      qmip += (uint64_t)step * qn;
+      if (fbn + (uint64_t)step * (uint64_t)parallel + 10 >= e.Support) fbn = qmip = 0;
+    }
+  }
+  sh->n = (uint32_t)n; sh->qn = (uint32_t)qn; sh->kcap = (uint32_t)kcap;
+  sh->cmask = pow2_at_least(2 * std::max<uint64_t>(maxq, 1)) - 1;
+  return true;
+}
+
+// The localCache indexes on the device for the loop: the device copy is made
+// from the host's FlatMaps where it is not current (empty after a
+// maintenance: a memset), and from then on the device copy is the truth.
+static int ensure_dev_cache(Engine* e, uint32_t cmask, hipStream_t st) {
+  const uint64_t cap = (uint64_t)cmask + 1, words = e->P * cap;
+  if (e->dcache_cmask != cmask || !e->dcache.p) {
+    if (e->cache_on_dev) CHK(ensure_host_cache(e));
+    CHK(e->dcache.reserve(words * 8));
+    e->dcache_cmask = cmask;
+    e->dcache_valid = false;
+  }
+  if (!e->dcache_valid) {
+    bool any = false;
+    for (const PartHost& ph : e->parts) any |= ph.cache.count > 0;
+    if (!any) {
+      HIPCHK(hipMemsetAsync(e->dcache.p, 0, words * 8, st));
+    } else {
+      std::vector<uint64_t> t(words, 0);
+      for (uint64_t p = 0; p < e->P; ++p)
+        e->parts[p].cache.for_each([&](uint64_t key, uint32_t val) {
+          uint64_t* tp = &t[p * cap];
+          for (uint32_t i = pm::drl_hash((uint32_t)key) & cmask;; i = (i + 1) & cmask)
+            if (!tp[i]) { tp[i] = ((uint64_t)val << 32) | (uint64_t)((uint32_t)key + 1u); break; }
+        });
+      HIPCHK(hipStreamSynchronize(st));
+      HIPCHK(hipMemcpy(e->dcache.p, t.data(), words * 8, hipMemcpyHostToDevice));
+    }
+    e->dcache_valid = true;
+  }
+  e->cache_on_dev = true;
+  return 0;
+}
+
+struct DrlTeam {
+  StepGroup G;
+  pm_graph** gs = nullptr;
+  uint32_t S = 0, s0 = 0, nsub = 0;
+  DevBuf sess, dummy, batch, heap, ktab, knb, kdist, kid, ctabp, answers, subs, gid, sb, out, allq, part_bytes,
+      step_bytes, step_real;
+  DrlArgs A{};
+  hipEvent_t ev_end = nullptr;
+  uint32_t seq = 0;                              // shared steps built so far (step_bytes rows)
+  std::vector<std::pair<size_t, uint32_t>> tl;   // timed "answer" / "match_resolve" launches: (index, step)
+  std::vector<char> need;
+  std::vector<double> mt;
+  ~DrlTeam() { if (ev_end) (void)hipEventDestroy(ev_end); }
+};
+
+static int drl_team_init(DrlTeam& T, pm_graph** gs, uint32_t S, uint32_t s0, const float* queries, uint64_t q, int k,
+                         int step, int parallel, const DrlShape& sh) {
+  T.gs = gs; T.S = S; T.s0 = s0;
+  StepGroup& G = T.G;
+  CHK(team_init(G, gs, S));
+  hipStream_t st = G.c->stream;
+  const pm_graph* g0 = gs[0];
+  const Engine& e0 = g0->pir->e;
+  const uint32_t P = (uint32_t)e0.P, m = (uint32_t)g0->m, n = sh.n, kcap = sh.kcap, dim = (uint32_t)g0->dim;
+  T.nsub = S * P * sh.qn;
+  if (!g0->dgraph->p) {   // the true neighbour lists (success count, start set) on the device, once per graph
+    CHK(g0->dgraph->reserve(g0->n * m * 4));
+    HIPCHK(hipMemcpy(g0->dgraph->p, g0->graph, g0->n * m * 4, hipMemcpyHostToDevice));
+  }
+  CHK(T.sess.reserve(S * sizeof(DrlSess)));
+  CHK(T.dummy.reserve((uint64_t)S * P * 8));
+  CHK(T.batch.reserve((uint64_t)S * n * 4));
+  CHK(T.heap.reserve((uint64_t)S * kcap * 8));
+  CHK(T.ktab.reserve((uint64_t)S * 2 * kcap * 8));
+  CHK(T.knb.reserve((uint64_t)S * kcap * m * 4));
+  CHK(T.kdist.reserve((uint64_t)S * kcap * 4));
+  CHK(T.kid.reserve((uint64_t)S * kcap * 4));
+  CHK(T.ctabp.reserve(S * 8));
+  CHK(T.answers.reserve(std::max<uint64_t>(8, (uint64_t)S * q * k * 8)));
+  CHK(T.subs.reserve((uint64_t)T.nsub * sizeof(PmSub)));
+  CHK(T.gid.reserve((uint64_t)T.nsub * 8));
+  CHK(T.sb.reserve((uint64_t)(S * P + 1) * 4));
+  CHK(T.out.reserve((uint64_t)T.nsub * sizeof(PmOutHdr) + (uint64_t)T.nsub * G.E * 8));
+  CHK(T.allq.reserve(std::max<uint64_t>(4, (uint64_t)S * q * dim * 4)));
+  CHK(T.part_bytes.reserve(P * 8));
+  // host state -> device: search streams and counters, dummy counters, localCache indexes
+  std::vector<DrlSess> hs(S);
+  std::vector<uint64_t> dmy((uint64_t)S * P), ctp(S);
+  for (uint32_t i = 0; i < S; ++i) {
+    pm_graph* g = gs[i];
+    Engine* e = &g->pir->e;
+    hs[i] = DrlSess{g->rng.s, g->succ, 0, 0, 0, 0};
+    for (uint32_t p = 0; p < P; ++p) dmy[(uint64_t)i * P + p] = e->parts[p].dummy_ctr;
+    CHK(ensure_dev_cache(e, sh.cmask, st));
+    ctp[i] = (uint64_t)(uintptr_t)e->dcache.p;
+  }
+  std::vector<uint32_t> sbv(S * P + 1);
+  for (uint32_t j = 0; j <= S * P; ++j) sbv[j] = j * sh.qn;
+  std::vector<double> pb(P);
+  for (uint32_t p = 0; p < P; ++p) pb[p] = answer_bytes(e0.parts[p].d, G.E);
+  HIPCHK(hipStreamSynchronize(st));
+  HIPCHK(hipMemcpy(T.sess.p, hs.data(), S * sizeof(DrlSess), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(T.dummy.p, dmy.data(), dmy.size() * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(T.ctabp.p, ctp.data(), S * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(T.sb.p, sbv.data(), sbv.size() * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(T.part_bytes.p, pb.data(), P * 8, hipMemcpyHostToDevice));
+  if (q) HIPCHK(hipMemcpy(T.allq.p, queries + (uint64_t)s0 * q * dim, (uint64_t)S * q * dim * 4, hipMemcpyHostToDevice));
+  if (G.c->timing >= 2) {   // each step's answer bytes and real sub-queries, counted by the round that builds it
+    const uint64_t steps = q * (uint64_t)step;
+    CHK(T.step_bytes.reserve(std::max<uint64_t>(8, steps * S * 8)));
+    CHK(T.step_real.reserve(std::max<uint64_t>(4, steps * S * 4)));
+  }
+  HIPCHK(hipEventCreateWithFlags(&T.ev_end, hipEventDisableTiming));
+  // the step buffers of group_step for nsub sub-queries
+  const uint32_t words = (G.maxPH + 63) / 64, cblk = pmk::step_match_blocks(G.maxPH);
+  CHK(G.bits.reserve((uint64_t)T.nsub * words * 8));
+  CHK(G.cand.reserve((uint64_t)T.nsub * cblk * 6 * 4));
+  CHK(G.meta.reserve((uint64_t)T.nsub * 2 * 4));
+  CHK(G.spec.reserve((uint64_t)T.nsub * 64 * 4));
+  CHK(G.res_d.reserve(T.nsub * sizeof(PmRes)));
+  CHK(G.ans.reserve((uint64_t)T.nsub * G.E * 8));
+  DrlArgs& A = T.A;
+  A.S = S; A.P = P; A.qn = sh.qn; A.n = n; A.m = m; A.parallel = (uint32_t)parallel; A.k = (uint32_t)k;
+  A.E = G.E; A.dim = dim; A.kcap = kcap; A.cmask = sh.cmask; A.ns = G.ns; A.q = (uint32_t)q;
+  A.N = g0->n; A.PS = e0.PS;
+  A.hdr = T.out.as<PmOutHdr>();
+  A.rows = (const uint64_t*)(T.out.as<char>() + (uint64_t)T.nsub * sizeof(PmOutHdr));
+  A.subs = T.subs.as<PmSub>(); A.gid = T.gid.as<uint64_t>();
+  A.graph = g0->dgraph->as<uint32_t>();
+  A.start_dist = G.start_dist.as<float>(); A.start_ids = G.start_ids.as<uint32_t>();
+  A.sess = T.sess.as<DrlSess>(); A.dummy = T.dummy.as<uint64_t>(); A.batch = T.batch.as<uint32_t>();
+  A.heap = T.heap.as<uint64_t>(); A.ktab = T.ktab.as<uint64_t>(); A.knb = T.knb.as<uint32_t>();
+  A.kdist = T.kdist.as<float>(); A.kid = T.kid.as<uint32_t>(); A.ctab = T.ctabp.as<uint64_t*>();
+  A.answers = T.answers.as<int64_t>(); A.part_bytes = T.part_bytes.as<double>();
+  A.step_bytes = T.step_bytes.p ? T.step_bytes.as<double>() : nullptr;
+  A.step_real = T.step_real.p ? T.step_real.as<uint32_t>() : nullptr;
+  T.need.assign(S, 0);
+  T.mt.assign(S, 0.0);
+  return 0;
+}
+
+// One shared step of the device loop: the descriptor the last round kernel
+// built, results into device memory.
+static int drl_step(DrlTeam& T, const DrlShape& sh) {
+  StepGroup& G = T.G;
+  pm_ctx* c = G.c;
+  const Engine* e0 = G.es[0];
+  c->sample_now = c->sample_ctr++ % 7 == 0;   // timing level 3: group_step's sample
+  PmStep S{};
+  S.parts = G.parts_d.as<PmPart>();
+  S.subs_h = S.subs = T.subs.as<PmSub>();
+  S.sb_h = S.sb = T.sb.as<uint32_t>();
+  S.bits = G.bits.as<uint64_t>(); S.cand = G.cand.as<uint32_t>(); S.meta = G.meta.as<uint32_t>();
+  S.spec = G.spec.as<uint32_t>(); S.cblk = pmk::step_match_blocks(G.maxPH);
+  S.res = G.res_d.as<PmRes>(); S.ans = G.ans.as<uint64_t>(); S.done = G.done.as<uint32_t>();
+  S.db = e0->db->as<uint64_t>();
+  S.q = nullptr;   // each partition's PmPart::qv
+  S.hdr_h = T.out.as<PmOutHdr>();
+  S.rows_h = (uint64_t*)(T.out.as<char>() + (uint64_t)T.nsub * sizeof(PmOutHdr));
+  S.words = (G.maxPH + 63) / 64; S.E = G.E; S.dim = G.dim; S.nsub = T.nsub; S.np = T.S * G.Pl;
+  S.np_live = S.np;
+  S.args_valid = 0;
+  if (++G.token == 0) ++G.token;
+  S.token = G.token;
+  const size_t off = std::min<size_t>(e0->pf_off, G.E * 8);
+  const size_t end = std::min<size_t>(G.E * 8, off + std::min<size_t>(e0->pf_len, G.E * 8));
+  S.pf_w0 = (uint32_t)(off / 8);
+  S.pf_w1 = (uint32_t)((end + 7) / 8);
+  S.rows_partial = 1;
+  const size_t before = c->launches.size();
+  // bytes: every sub-query answered (patched with the round's exact count in timing runs)
+  double ans_bytes = 0;
+  for (uint32_t li = 0; li < G.Pl; ++li) ans_bytes += answer_bytes(e0->parts[G.lp[li]].d, G.E) * sh.qn * T.S;
+  CHK(group_step_launch(G, S, sh.qn, T.nsub, ans_bytes));
+  for (size_t i = before; i < c->launches.size(); ++i)
+    if (c->launches[i].name == "answer" || c->launches[i].name == "match_resolve" || c->launches[i].name == "hint_match")
+      T.tl.emplace_back(i, T.seq);
+  c->host_add(HT_DEV_STEPS, 0.0);
+  return 0;
+}
+
+static void drl_round(DrlTeam& T, uint32_t mode, uint64_t qi) {
+  pm_ctx* c = T.G.c;
+  DrlArgs A = T.A;
+  A.mode = mode;
+  A.qi = (uint32_t)qi;
+  A.seq = T.seq;   // the step this round builds (BEGIN / MID)
+  if (mode != DRL_END) T.seq++;
+  c->timed_ext("team_round", 0, [&](pmk::PmEvents ev) { pmk::team_round(c->stream, A, ev); }, 2);
+}
+
+// A query of team T enqueued on its stream: the queries into qbuf, the start
+// set's distances, BEGIN, then the rounds.
+static int drl_query(DrlTeam& T, const DrlShape& sh, uint64_t qi, uint64_t q, int step) {
+  StepGroup& G = T.G;
+  hipStream_t st = G.c->stream;
+  const uint32_t dim = G.dim;
+  HIPCHK(hipMemcpy2DAsync(G.qbuf.p, (size_t)dim * 4, T.allq.as<float>() + qi * dim, (size_t)q * dim * 4,
+                          (size_t)dim * 4, T.S, hipMemcpyDeviceToDevice, st));
+  const uint64_t nrows = (uint64_t)T.S * G.ns;
+  if (nrows)
+    G.c->timed("l2_rows", (double)nrows * G.dim * 4, [&] {
+      pmk::l2_rows(st, T.gs[0]->dvec->as<float>(), G.dim, nrows, G.start_ids.as<uint32_t>(), G.qbuf.as<float>(), G.dim,
+                   G.start_dist.as<float>(), G.ns);
+    });
+  drl_round(T, DRL_BEGIN, qi);
+  for (int r = 0; r < step; ++r) {
+    CHK(drl_step(T, sh));
+    drl_round(T, r + 1 == step ? DRL_END : DRL_MID, qi);
+  }
+  HIPCHK(hipGetLastError());
+  for (uint32_t i = 0; i < T.S; ++i) {   // the host's deterministic mirrors of the rounds (bq_tail, gvi_pre)
+    pm_graph* g = T.gs[i];
+    Engine* e = &g->pir->e;
+    e->FBN += (uint64_t)step * (sh.n / e->B);
+    e->QMIP += (uint64_t)step * sh.qn;
+    g->total += (uint64_t)step * sh.n;
+  }
+  G.c->host_add(HT_DEV_QUERIES, (double)T.S);
+  return 0;
+}
+
+// Device state -> host at the end of the call: answers, search streams and
+// counters, dummy counters, FinishedQueryNum; the timed launches' bytes.
+static int drl_team_finish(DrlTeam& T, uint64_t q, int k, int64_t* answers) {
+  StepGroup& G = T.G;
+  HIPCHK(hipStreamSynchronize(G.c->stream));
+  const uint32_t S = T.S, P = (uint32_t)G.es[0]->P;
+  if (q) HIPCHK(hipMemcpy(answers + (uint64_t)T.s0 * q * k, T.answers.p, (uint64_t)S * q * k * 8, hipMemcpyDeviceToHost));
+  std::vector<DrlSess> hs(S);
+  std::vector<uint64_t> dmy((uint64_t)S * P);
+  HIPCHK(hipMemcpy(hs.data(), T.sess.p, S * sizeof(DrlSess), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(dmy.data(), T.dummy.p, dmy.size() * 8, hipMemcpyDeviceToHost));
+  std::vector<uint32_t> fq(P);
+  for (uint32_t i = 0; i < S; ++i) {
+    pm_graph* g = T.gs[i];
+    Engine* e = &g->pir->e;
+    g->rng.s = hs[i].rng;
+    g->succ = hs[i].succ;
+    HIPCHK(hipMemcpy(fq.data(), e->fqn.p, P * 4, hipMemcpyDeviceToHost));
+    for (uint32_t p = 0; p < P; ++p) {
+      e->parts[p].dummy_ctr = dmy[(uint64_t)i * P + p];
+      e->parts[p].fqn = fq[p];
+    }
+  }
+  pm_ctx* c = G.c;
+  if (!T.tl.empty() && T.step_bytes.p) {   // the timed steps' exact answer bytes / real sub-queries
+    std::vector<double> by((uint64_t)T.seq * S);
+    std::vector<uint32_t> nr((uint64_t)T.seq * S);
+    HIPCHK(hipMemcpy(by.data(), T.step_bytes.p, by.size() * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(nr.data(), T.step_real.p, nr.size() * 4, hipMemcpyDeviceToHost));
+    for (auto& [idx, sq] : T.tl) {
+      if (idx >= c->launches.size() || sq >= T.seq) continue;
+      double b = 0, r = 0;
+      for (uint32_t i = 0; i < S; ++i) { b += by[(uint64_t)sq * S + i]; r += nr[(uint64_t)sq * S + i]; }
+      if (c->launches[idx].name == "answer") c->launches[idx].bytes = b;
+      else c->launches[idx].bytes = r * G.maxPH;
+    }
+  }
+  return 0;
+}
+
+static int run_batched_dev(pm_graph** gs, uint32_t S, const float* queries, uint64_t q, int k, int step, int parallel,
+                           uint32_t NG, int64_t* answers, double* mt_out, const DrlShape& sh) {
+  std::vector<std::unique_ptr<DrlTeam>> teams;
+  struct Release {
+    std::vector<std::unique_ptr<DrlTeam>>& t;
+    ~Release() { for (auto& x : t) if (x->gs) team_release(x->gs, x->S); }
+  } release{teams};
+  for (uint32_t g = 0; g < NG; ++g) {
+    const uint32_t s0 = (uint32_t)((uint64_t)S * g / NG), s1 = (uint32_t)((uint64_t)S * (g + 1) / NG);
+    teams.emplace_back(new DrlTeam());
+    CHK(drl_team_init(*teams.back(), gs + s0, s1 - s0, s0, queries, q, k, step, parallel, sh));
+  }
+  DevBuf prep_buf;
+  for (uint64_t qi = 0; qi < q; ++qi) {
+    for (auto& t : teams) CHK(drl_query(*t, sh, qi, q, step));
+    // the harness's maintenance trigger (private-search.go:226-232) per session:
+    // the triggered clients of every team as ONE launch set after the query
+    std::vector<Engine*> who;
+    std::vector<double*> mts;
+    std::vector<DrlTeam*> involved;
+    for (auto& t : teams) {
+      bool any = false;
+      for (uint32_t i = 0; i < t->S; ++i) {
+        Engine* e = &t->gs[i]->pir->e;
+        t->need[i] = e->FBN + (uint64_t)step * (uint64_t)parallel + 10 >= e->Support;
+        if (t->need[i]) { who.push_back(e); mts.push_back(&t->mt[i]); any = true; }
+      }
+      if (any) involved.push_back(t.get());
+    }
+    if (who.empty()) continue;
+    for (DrlTeam* t : involved) HIPCHK(hipStreamSynchronize(t->G.c->stream));   // the query's rounds are done
+    CHK(prep_clients(involved[0]->G.c, prep_buf, involved[0]->G.lp, who, &mts));
+    for (DrlTeam* t : involved) {   // the new keys into the team's parts; the emptied localCache indexes
+      CHK(group_upload_parts(t->G));
+      for (uint32_t i = 0; i < t->S; ++i)
+        if (t->need[i]) CHK(ensure_dev_cache(&t->gs[i]->pir->e, sh.cmask, t->G.c->stream));
+    }
+  }
+  for (auto& t : teams) {
+    CHK(drl_team_finish(*t, q, k, answers));
+    for (uint32_t i = 0; i < t->S; ++i) mt_out[t->s0 + i] = t->mt[i];
+  }
+  return 0;
+}
+
 extern "C" int pm_search_loop_batched(pm_graph** gs, uint32_t S, const float* queries, uint64_t q, int k, int step,
                                       int parallel, uint32_t ngroups, uint32_t nthreads, int64_t* answers,
                                       double* wall_s, double* online_s, double* maint_s) {
@@ -3853,6 +4272,17 @@ extern "C" int pm_search_loop_batched(pm_graph** gs, uint32_t S, const float* qu
   std::vector<std::thread> teams;
   const float* qbase = queries;
   auto t0 = Clock::now();
+  DrlShape sh;
+  if (drl_plan(gs, S, q, k, step, parallel, &sh)) {   // every round on the GPU (run_batched_dev)
+    CHK(run_batched_dev(gs, S, queries, q, k, step, parallel, NG, answers, mt.data(), sh));
+    const double wall = std::chrono::duration<double>(Clock::now() - t0).count();
+    if (wall_s) *wall_s = wall;
+    for (uint32_t s = 0; s < S; ++s) {
+      if (online_s) online_s[s] = wall - mt[s];
+      if (maint_s) maint_s[s] = mt[s];
+    }
+    return 0;
+  }
   static const int pool = [] { const char* e = getenv("PM_BATCH_POOL"); return e ? atoi(e) : 1; }();
   if (pool && NG > 1) {   // the pooled workers (run_batched_pool); one team: the workers serve it alone anyway
     CHK(run_batched_pool(gs, S, queries, q, k, step, parallel, NG, TT, answers, mt.data()));

@@ -217,6 +217,49 @@ struct PmStep {
   PmSub subs_a[kArgSubs];
 };
 
+// ---- the device-resident team round (pm_drl.hip; pm_search_loop_batched's
+// device loop): a lock-step team's 20 rounds of SearchKNN +
+// SimpleBatchPianoPIR.Query bucketing run on the GPU, chained on the team's
+// stream, with the host touching only a query's start and end.
+// the device loop's open-addressing tables (pm_drl.hip; the host builds the
+// localCache table with the same probe sequence)
+__host__ __device__ inline uint32_t drl_hash(uint32_t k) {
+  uint64_t x = k;
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33;
+  return (uint32_t)x;
+}
+struct DrlSess {          // one session's search state between launches
+  uint64_t rng;           // SplitMix state (the host's id stream, SplitMix::next)
+  uint64_t succ;          // successQueryNum (private-search.go:483-497)
+  uint32_t nknown, nheap; // knownVertices / the min-heap's sizes
+  uint32_t pad0, pad1;
+};
+enum : uint32_t { DRL_BEGIN = 0, DRL_MID = 1, DRL_END = 2 };
+struct DrlArgs {
+  uint32_t S, P, qn, n, m, parallel, k, E, dim, kcap, cmask, ns, mode, q, qi, seq;
+  uint64_t N, PS;
+  const PmOutHdr* hdr;            // the last shared step's results [nsub] (device)
+  const uint64_t* rows;           // ... and rows [nsub][E] (the neighbour words only)
+  PmSub* subs;                    // the next shared step's descriptor [S][P][qn]
+  uint64_t* gid;                  // ... each sub-query's global id (~0: dummy)
+  const uint32_t* graph;          // [N][m] the true neighbour lists (success check, start set)
+  const float* start_dist;        // [S][ns] the start set's L2 distances to the query
+  const uint32_t* start_ids;      // [S][ns]
+  DrlSess* sess;                  // [S]
+  uint64_t* dummy;                // [S][P] dummy-query counters (PartHost::dummy_ctr)
+  uint32_t* batch;                // [S][n] the round's ids
+  uint64_t* heap;                 // [S][kcap] {dist f32 bits | known slot << 32}
+  uint64_t* ktab;                 // [S][2 kcap] knownVertices: {id + 1 | slot << 32}, 0 empty
+  uint32_t* knb;                  // [S][kcap][m] known vertices' neighbour lists
+  float* kdist;                   // [S][kcap]
+  uint32_t* kid;                  // [S][kcap]
+  uint64_t* const* ctab;          // [S] -> [P][cmask + 1] localCache: {local idx + 1 | arena slot << 32}
+  int64_t* answers;               // [S][q][k]
+  const double* part_bytes;       // [P] algorithmic answer bytes of one sub-query
+  double* step_bytes;             // [launch seq][S] (timing runs; null: not counted)
+  uint32_t* step_real;            // [launch seq][S] real sub-queries (timing runs)
+};
+
 }  // namespace pm
 
 // Kernel launchers (pm_kernels.hip).  All asynchronous on `st`.
@@ -319,6 +362,10 @@ void synth_records(hipStream_t st, const int32_t* map, const uint64_t* ids, uint
                    uint64_t* rec);
 void prf_batch(hipStream_t st, const uint32_t* rk, const uint64_t* tags, const uint64_t* xs,
                uint64_t n, uint64_t* out);
+// the device-resident team round (pm_drl.hip): one 64-lane workgroup per session
+void team_round(hipStream_t st, const DrlArgs& A, PmEvents ev = {});
+uint32_t team_round_lds(uint32_t kcap, uint32_t n, uint32_t m);   // bytes of dynamic LDS
+constexpr uint32_t kDrlMaxKcap = 4096, kDrlMaxN = 256, kDrlMaxNM = 8192;
 // graph construction and ground truth (pm_graph.hip)
 uint32_t knn_pad_dim(uint32_t dim);   // bf16 row width for the prefilter (0: unsupported)
 uint32_t knn_top();                   // prefilter candidates per query row

@@ -461,6 +461,67 @@ def test_search_sessions_batched(ctx, oracle, ngroups, nthreads):
         assert sess[i].PIR.stats()["PrepCount"] == o.pir().stats()["PrepCount"] > 1, i
 
 
+@pytest.mark.parametrize("ngroups", [1, 2, 3])
+def test_search_device_loop_vs_host_loop(ctx, oracle, ngroups):
+    """pm_search_loop_batched's device loop (pm_drl.hip: every round's results,
+    GetVertexInfo decode, SearchKNN update / next batch and the batch-PIR
+    bucketing on the GPU, chained per team) against the host loop
+    (pm_set_option("device_loop", 0)) on fresh sessions with the same seeds,
+    and against independent oracle runs: answers, graph counts, batch-PIR
+    counters, the id stream's position and the localCache index (a host-path
+    batch query after the loop reads it back) all equal.  16,384 vertices
+    (PartitionSize 1,024, MaxQueryNum 221): the harness re-preprocesses every
+    session after each query, so maintenance runs between the chained queries."""
+    import pacmann_amd as pm
+    from pacmann_amd.synth import random_graph, sift_like_vectors
+    n = 16384
+    v = sift_like_vectors(n, 128, seed=71)
+    graph = random_graph(n, 32, seed=72)
+    seeds = [(80 + i, 90 + i) for i in range(6)]
+    rng = np.random.default_rng(73)
+    qs = np.stack([np.clip(np.rint(v[rng.integers(0, n, 9)] + rng.normal(0, 8, (9, 128))), 0, 255)
+                   .astype(np.float32) for _ in seeds])
+    out = {}
+    for mode in (1, 0):
+        pm.set_option("device_loop", mode)
+        try:
+            base = pm.PIRGraphInfo(v, graph, pir_seed=1, search_seed=2, ctx=pm.Context(0))
+            base.Preprocess()
+            sess = [base.Session(p, s) for p, s in seeds]
+            for x in sess:
+                x.Preprocess()
+            for x in sess:
+                x.ctx.timing_reset()
+            ans, _, _, mt = pm.search_loop_batched(sess, qs, 10, 20, 3, ngroups, 4)
+            dev_steps = sum(x.ctx.timing_get("host_dev_steps")[0] for x in sess)
+            dev_q = sum(x.ctx.timing_get("host_dev_queries")[1] for x in sess)
+            # after the loop, one host-path batch query per session (reads the localCache back)
+            probe = np.random.default_rng(74).integers(0, n, size=96).astype(np.uint64)
+            extra = [x.PIR.QueryWithMask(probe) for x in sess]
+            out[mode] = (ans, [x.counts() for x in sess], [x.PIR.stats() for x in sess], dev_steps, dev_q, extra,
+                         (mt > 0).all())
+        finally:
+            pm.set_option("device_loop", -1)
+    (a1, c1, s1, st1, q1, x1, m1), (a0, c0, s0, st0, q0, x0, m0) = out[1], out[0]
+    assert st1 == 9 * 20 * ngroups and q1 == 6 * 9, (st1, q1)   # every step of the device run on the GPU loop
+    assert st0 == 0
+    assert m1 and m0
+    assert np.array_equal(a1, a0)
+    assert c1 == c0
+    for a, b in zip(s1, s0):
+        for key in ("FinishedBatchNum", "QueriesMadeInPartition", "PrepCount"):
+            assert a[key] == b[key], key
+        assert a["PrepCount"] > 2
+    for (ra, oa), (rb, ob) in zip(x1, x0):
+        assert np.array_equal(ra, rb) and np.array_equal(oa, ob)
+    for i, (p, s) in enumerate(seeds):
+        o = oracle.Graph(v, graph, pir_seed=p, search_seed=s)
+        o.Preprocess()
+        oa, _, _ = o.SearchLoop(qs[i], 10, 20, 3)
+        assert np.array_equal(a1[i], oa), i
+        assert c1[i] == o.counts(), i
+
+
 def test_search_sessions_batched_wide_entries(ctx, oracle):
     """Entries wider than the answer kernels' small row buffer: dim 500, m 16
     gives E = (2000 + 64) / 8 = 258 words, which passes k_answer_p's even-E
