@@ -69,7 +69,8 @@ def prf_peak_g(lookups: float) -> float:
 PRF_PEAK_G = prf_peak_g(AES_LOOKUPS_PER_PRF)   # ~153 G PRF/s
 METRIC = "private queries/sec + PIR-scan HBM GB/s, SIFT1M d=128 at 1/2/4/8 GPUs"
 PREP_KERNELS = ["prep_offsets", "prep_fold", "prep_repl", "l2_rows"]
-STEP_KERNELS = ["step", "hint_match", "resolve", "match_resolve", "gather", "answer"]   # timed in the measured region too
+STEP_KERNELS = ["step", "hint_match", "resolve", "match_resolve", "gather", "answer",
+                "team_round"]   # timed in the measured region too (team_round: the device loop's round, pm_drl.hip)
 KERNELS = PREP_KERNELS + STEP_KERNELS
 PROFILE_QUERIES = 8
 # the kernel-timing pass after the timed region (same sessions, teams and
@@ -714,6 +715,44 @@ def prf_roofline(entry, note, set_size=None):
                     "~2 VALU per lookup put the vector-issue ceiling at about the same rate"}
 
 
+def composite_floor(ktime, S, queries_per_session, pir, value_per_gpu, ss_r2=None):
+    """The whole private query's GPU floor: per session
+    query, its answer bytes at HBM peak + its share of the maintenance fold's
+    entry reads at the LDS ds_read_b128 aggregate + its share of the PRFs at the
+    AES T-table ceiling, the shares over the harness's actual maintenance
+    cadence (private-search.go:226-232: FinishedBatchNum + step*parallel + 10 >=
+    SupportBatchNum, FinishedBatchNum advancing step*(parallel*m/BatchSize) per
+    query).  `frac` = value per GPU / the floor's q/s.  From the kernel-timing
+    pass, which holds one maintenance of every session."""
+    na, _, ab = ktime["answer"]
+    nf, _, fb = ktime["prep_fold"]
+    npf, _, prfs = ktime["prep_offsets"]
+    if not (na and ab and nf and fb and npf and prfs):
+        return None
+    st = pir.stats()
+    fbn_per_q = STEP * (PARALLEL * M // st["BatchSize"])
+    cadence = -(-(st["SupportBatchNum"] - STEP * PARALLEL - 10) // fbn_per_q)   # queries between maintenances
+    clients = max(1, round(fb / sum(((c["PrimaryHintNum"] + (c["SetSize"] - 1) * c["MaxQueryPerChunk"]) * c["SetSize"]
+                                      * ((DIM + M) // 2) * 8)
+                                     for c in (pir.SubConfig(p) for p in range(st["PartitionNum"])))))
+    ans_q = ab / (S * queries_per_session)
+    fold_q = fb / clients / cadence
+    prf_q = prfs / clients / cadence
+    lk = AES_LOOKUPS_PER_PRF_R2 if ss_r2 is not None and ss_r2 <= 256 else AES_LOOKUPS_PER_PRF
+    t_ans = ans_q / (HBM_PEAK_GBS * 1e9)
+    t_fold = fold_q / (LDS_B128_PEAK_GBS * 1e9)
+    t_prf = prf_q / (prf_peak_g(lk) * 1e9)
+    floor = t_ans + t_fold + t_prf
+    return {"unit": "us per private query", "answer_us": round(t_ans * 1e6, 3), "fold_us": round(t_fold * 1e6, 3),
+            "prf_us": round(t_prf * 1e6, 3), "floor_us": round(floor * 1e6, 3),
+            "floor_queries_per_s": round(1 / floor, 1), "frac": round(value_per_gpu * floor, 4),
+            "maintenance_cadence_queries": cadence, "clients_per_maintenance": clients,
+            "per_query": {"answer_bytes": ans_q, "fold_bytes": fold_q, "prfs": prf_q},
+            "note": "answer bytes at HBM peak + the fold's entry reads at the LDS ds_read_b128 aggregate + the "
+                    "PRFs at the T-table lookup ceiling, per private query (maintenance amortised over its actual "
+                    "cadence); frac = value per GPU x floor"}
+
+
 def rccl_group(dist, local, out):
     """An RCCL (nccl backend) group over all ranks for the sharded blocks'
     combine, or None (the shards then combine over the gloo group).  RCCL
@@ -1053,7 +1092,7 @@ def main():
         one.PIR.Preprocessing()
         one.ctx.timing(False)
         isolated = {"sessions": gsz, "queries_each": PROFILE_QUERIES, "kernel_avg_us": {}}
-        for k in ("hint_match", "resolve", "match_resolve", "answer"):
+        for k in ("hint_match", "resolve", "match_resolve", "answer", "team_round"):
             n, ms, by = grp[0].ctx.timing_get(k)
             if n:
                 isolated["kernel_avg_us"][k] = round(ms / n * 1e3, 3)
@@ -1169,6 +1208,9 @@ def main():
                                   "note": "answer bytes of every step of the kernel-timing pass / its wall time"
                                           if kt_pass else "answer bytes of every step in the timed region / its "
                                           "wall time"}
+    if main_roof and not args.no_kernel_timing:
+        main_roof["composite"] = composite_floor(ktime, S, kt_pass["queries_per_session"] if kt_pass else args.steps,
+                                                 base.PIR, value / ws, ss_r2=base.PIR.SubConfig(0)["SetSize"])
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "queries/s", "n_gpus": ws,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),

@@ -129,15 +129,39 @@ __device__ __forceinline__ double wave_sumd(double x) {
   return x;
 }
 
-__global__ void __launch_bounds__(64) k_team_round(const DrlArgs A) {
+// One workgroup of kDrlThreads per session.  The per-position and per-sub-
+// query work is spread over all its lanes in a few phases whose global loads
+// are all in flight together (a handful of round trips per round); wave 0
+// alone runs the order-dependent part (the heap's pushes and pops).
+constexpr uint32_t kDrlThreads = 256;
+__device__ __forceinline__ void block_sync() { __syncthreads(); }
+
+__global__ void __launch_bounds__(kDrlThreads) k_team_round(const DrlArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const uint32_t s = blockIdx.x, lane = threadIdx.x;
-  const uint32_t n = A.n, m = A.m, kcap = A.kcap, P = A.P, qn = A.qn;
-  HeapE* hp = (HeapE*)lds;                                   // [kcap]
+  uint64_t t_prev = A.stamps ? __builtin_amdgcn_s_memtime() : 0;
+  auto stamp = [&](int k) {   // diagnostics: phase k's shader clocks (thread 0, MID rounds)
+    if (!A.stamps || A.mode != DRL_MID) return;
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    if (threadIdx.x == 0) atomicAdd((unsigned long long*)&A.stamps[k], (unsigned long long)(t - t_prev));
+    t_prev = t;
+  };
+  const uint32_t s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t n = A.n, m = A.m, kcap = A.kcap, P = A.P, qn = A.qn, nsq = P * qn;
+  HeapE* hp = (HeapE*)lds;                                   // [kcap] the heap
   uint32_t* nbuf = (uint32_t*)(lds + (size_t)kcap * 8);     // [n][m] the round's neighbour lists
   uint32_t* bat = nbuf + (size_t)n * m;                      // [n] the round's ids
   float* dbuf = (float*)(bat + n);                           // [n] their distances
-  uint32_t* pbuf = (uint32_t*)(dbuf + n);                    // [n] their partitions (bucketing)
+  uint32_t* pbuf = bat + 2 * n;                              // [n] partitions; then slots of new vertices
+  uint32_t* flg = bat + 3 * n;                               // [n] bit 0 mismatch, 1 non-zero, 2 new, 3 success
+  int32_t* srcj = (int32_t*)(bat + 4 * n);                   // [n] the answering sub-query (session-local) or -1
+  uint32_t* sst = bat + 5 * n;                               // [nsq] status of the session's sub-queries
+  uint32_t* sref = sst + nsq;                                // [nsq] DUP: the repeated sub-query (session-local)
+  float* sdist = (float*)(sref + nsq);                       // [nsq]
+  uint32_t* sgid = sref + 2 * nsq;                           // [nsq] global id (~0: dummy)
+  __shared__ uint32_t s_wcnt[kDrlThreads / 64];
+  __shared__ uint64_t s_wmask[kDrlThreads / 64];
+  __shared__ uint32_t s_pop[64];
+  __shared__ uint32_t s_nknown, s_nheap;
 
   DrlSess* SS = A.sess + s;
   uint64_t rng = SS->rng;
@@ -149,142 +173,192 @@ __global__ void __launch_bounds__(64) k_team_round(const DrlArgs A) {
   float* kdist = A.kdist + (uint64_t)s * kcap;
   uint32_t* kid = A.kid + (uint64_t)s * kcap;
   uint32_t* gbat = A.batch + (uint64_t)s * n;
-  const uint32_t base = s * P * qn;   // this session's first sub-query of the shared step
+  uint64_t* ctab = A.ctab[s];
+  const uint32_t cap = A.cmask + 1;
+  const uint32_t base = s * nsq;   // this session's first sub-query of the shared step
+  const uint32_t PS = (uint32_t)A.PS;
 
   if (A.mode == DRL_BEGIN) {
     // knn_reset: an empty known set and heap
-    for (uint32_t i = lane; i < 2 * kcap; i += 64) ktab[i] = 0;
-    nknown = 0;
-    nheap = 0;
+    for (uint32_t i = tid; i < 2 * kcap; i += kDrlThreads) ktab[i] = 0;
     __threadfence();
-    // knn_begin_finish (search.go:130-146): the first `parallel` start
-    // vertices in (distance, position) order become known (with their true
-    // neighbour lists: GetStartVertex is non-private) and go on the heap
-    const float* sd = A.start_dist + (uint64_t)s * A.ns;
-    const uint32_t* sid = A.start_ids + (uint64_t)s * A.ns;
-    const uint32_t take = min(A.parallel, A.ns);
-    float pd = 0.0f;
-    uint32_t ppos = 0;
-    for (uint32_t t = 0; t < take; ++t) {
-      float bd = __builtin_inff();
-      uint32_t bp = 0xffffffffu;
-      for (uint32_t j = lane; j < A.ns; j += 64) {
-        const float d = sd[j];
-        const bool after = t == 0 || d > pd || (d == pd && j > ppos);
-        if (after && (d < bd || (d == bd && j < bp))) { bd = d; bp = j; }
+    block_sync();
+    if (wave == 0) {
+      // knn_begin_finish (search.go:130-146): the first `parallel` start
+      // vertices in (distance, position) order become known (with their true
+      // neighbour lists: GetStartVertex is non-private) and go on the heap
+      nknown = 0;
+      nheap = 0;
+      const float* sd = A.start_dist + (uint64_t)s * A.ns;
+      const uint32_t* sid = A.start_ids + (uint64_t)s * A.ns;
+      const uint32_t take = min(A.parallel, A.ns);
+      float pd = 0.0f;
+      uint32_t ppos = 0;
+      for (uint32_t t = 0; t < take; ++t) {
+        float bd = __builtin_inff();
+        uint32_t bp = 0xffffffffu;
+        for (uint32_t j = lane; j < A.ns; j += 64) {
+          const float d = sd[j];
+          const bool after = t == 0 || d > pd || (d == pd && j > ppos);
+          if (after && (d < bd || (d == bd && j < bp))) { bd = d; bp = j; }
+        }
+        wave_min2(bd, bp);
+        pd = bd; ppos = bp;
+        const uint32_t id = sid[bp], slot = nknown++;
+        if (lane < m) knb[(uint64_t)slot * m + lane] = A.graph[(uint64_t)id * m + lane];
+        if (lane == 0) {
+          kdist[slot] = bd;
+          kid[slot] = id;
+          tab_put(ktab, kmask, id, slot);
+        }
+        heap_push(hp, nheap, HeapE{bd, slot}, lane);
       }
-      wave_min2(bd, bp);
-      pd = bd; ppos = bp;
-      const uint32_t id = sid[bp], slot = nknown++;
-      if (lane < m) knb[(uint64_t)slot * m + lane] = A.graph[(uint64_t)id * m + lane];
-      if (lane == 0) {
-        kdist[slot] = bd;
-        kid[slot] = id;
-        tab_put(ktab, kmask, id, slot);
-      }
-      heap_push(hp, nheap, HeapE{bd, slot}, lane);
+      if (lane == 0) { s_nknown = nknown; s_nheap = nheap; }
     }
     __threadfence();
+    block_sync();
+    nknown = s_nknown;
+    nheap = s_nheap;
   } else {
-    for (uint32_t i = lane; i < nheap; i += 64) hp[i] = gheap[i];
-    for (uint32_t i = lane; i < n; i += 64) bat[i] = gbat[i];
-    __syncthreads();
-    // ---- the last shared step's results (post_results): localCache entries
-    for (uint32_t j = lane; j < P * qn; j += 64) {
+    // ---- phase 1: the heap, the ids, the session's sub-query results; the
+    // localCache entries of its ST_OK answers (post_results, pir.go:468-470)
+    for (uint32_t i = tid; i < nheap; i += kDrlThreads) hp[i] = gheap[i];
+    for (uint32_t i = tid; i < n; i += kDrlThreads) { bat[i] = gbat[i]; flg[i] = 0; }
+    for (uint32_t j = tid; j < nsq; j += kDrlThreads) {
       const PmOutHdr h = A.hdr[base + j];
+      const uint64_t g = A.gid[base + j];
+      sst[j] = h.status;
+      sref[j] = h.ref - base;
+      sdist[j] = h.dist;
+      sgid[j] = g == ~0ull ? 0xffffffffu : (uint32_t)g;
       if (h.status == ST_OK) {
-        const PmSub sub = A.subs[base + j];
-        const uint32_t p = sub.part - s * P;
-        tab_put(A.ctab[s] + (uint64_t)p * (A.cmask + 1), A.cmask, (uint32_t)sub.idx, h.ref);
+        const uint32_t p = j / qn;
+        tab_put(ctab + (uint64_t)p * cap, A.cmask, (uint32_t)A.subs[base + j].idx, h.ref);
       }
     }
-    // ---- each position's response (bq_emit_fast) and GetVertexInfo's decode
-    const uint32_t* rows32 = (const uint32_t*)A.rows;
-    uint64_t succ = 0;
-    for (uint32_t i = lane; i < n; i += 64) {
+    block_sync();
+    stamp(1);
+    // ---- phase 2: each position's response (bq_emit_fast: the last sub-query
+    // made for its id; an in-step duplicate follows the one it repeats), its
+    // distance, whether the id is known, whether an earlier position has it
+    for (uint32_t i = tid; i < n; i += kDrlThreads) {
       const uint32_t id = bat[i];
-      const uint32_t p = (uint32_t)(id / A.PS);
-      const uint32_t b0 = base + p * qn;
+      const uint32_t p = id / PS;
       int32_t src = -1;
       for (uint32_t j = 0; j < qn; ++j)
-        if (A.gid[b0 + j] == (uint64_t)id) src = (int32_t)(b0 + j);   // last wins
-      float d = 0.0f;
-      for (int hop = 0; src >= 0 && A.hdr[src].status == ST_DUP && hop < 2; ++hop) src = (int32_t)A.hdr[src].ref;
-      if (src >= 0) d = A.hdr[src].dist;
-      const uint32_t* r = rows32 + (uint64_t)(src >= 0 ? src : 0) * 2 * A.E + A.dim;
-      const uint32_t* tg = A.graph + (uint64_t)id * m;
-      bool same = true;
-      for (uint32_t k = 0; k < m; ++k) {
-        const uint32_t v = src >= 0 ? r[k] : 0u;
-        nbuf[(size_t)i * m + k] = v;
-        same &= v == tg[k];
-      }
-      dbuf[i] = d;
-      succ += same;
+        if (sgid[p * qn + j] == id) src = (int32_t)(p * qn + j);   // last wins
+      for (int hop = 0; src >= 0 && sst[src] == ST_DUP && hop < 2; ++hop) src = (int32_t)sref[src];
+      srcj[i] = src;
+      dbuf[i] = src >= 0 ? sdist[src] : 0.0f;
+      bool dup = false;
+      for (uint32_t j = 0; j < i && !dup; ++j) dup = bat[j] == id;   // an earlier position: known by then
+      uint32_t v;
+      const bool known = dup || tab_find(ktab, kmask, id, &v);
+      if (known) atomicOr(&flg[i], 4u);   // bit 2 here: not new
     }
+    block_sync();
+    stamp(2);
+    // ---- phase 3: GetVertexInfo's decode (Entry2VectorAndNeighbors) and the
+    // success check against the true neighbour list, one element per lane
+    const uint32_t* rows32 = (const uint32_t*)A.rows;
+    for (uint32_t e = tid; e < n * m; e += kDrlThreads) {
+      const uint32_t i = e / m, k = e - i * m;
+      const int32_t src = srcj[i];
+      const uint32_t v = src >= 0 ? rows32[(uint64_t)(base + src) * 2 * A.E + A.dim + k] : 0u;
+      const uint32_t t = A.graph[(uint64_t)bat[i] * m + k];
+      nbuf[e] = v;
+      if (v != t) atomicOr(&flg[i], 1u);
+      if (v != 0) atomicOr(&flg[i], 2u);
+    }
+    block_sync();
+    stamp(3);
+    // ---- phase 4: the new vertices in position order (SearchKNN's update,
+    // search.go:185-207): known slots, rows, the known table
+    uint64_t succ = 0;
+    bool nw = false;
+    uint32_t i4 = tid;
+    if (tid < n) {
+      const uint32_t f = flg[tid];
+      succ = (f & 1u) == 0;
+      nw = (f & 2u) && !(f & 4u);
+    }
+    const uint64_t bal = __ballot(nw);
+    if (lane == 0 && wave < kDrlThreads / 64) { s_wcnt[wave] = (uint32_t)__builtin_popcountll(bal); s_wmask[wave] = bal; }
     succ = wave_sum(succ);
-    if (lane == 0) SS->succ += succ;
-    __syncthreads();
-    // ---- SearchKNN's update (search.go:185-207): in position order, ids not
-    // yet known with a non-empty neighbour list become known and are pushed
-    for (uint32_t c0 = 0; c0 < n; c0 += 64) {
-      const uint32_t i = c0 + lane;
-      bool nw = false;
-      if (i < n) {
-        const uint32_t id = bat[i];
-        bool nz = false;
-        for (uint32_t k = 0; k < m; ++k) nz |= nbuf[(size_t)i * m + k] != 0;
-        bool dup = false;
-        for (uint32_t j = 0; j < i && !dup; ++j) dup = bat[j] == id;   // an earlier position: known by then
-        uint32_t v;
-        nw = nz && !dup && !tab_find(ktab, kmask, id, &v);
-      }
-      const uint64_t b = __ballot(nw);
-      const uint32_t slot = nknown + (uint32_t)__builtin_popcountll(b & ((1ull << lane) - 1ull));
-      if (nw) {
-        const uint32_t id = bat[i];
-        for (uint32_t k = 0; k < m; ++k) knb[(uint64_t)slot * m + k] = nbuf[(size_t)i * m + k];
-        kdist[slot] = dbuf[i];
-        kid[slot] = id;
-        tab_put(ktab, kmask, id, slot);
-      }
-      for (uint64_t bb = b; bb; bb &= bb - 1) {   // the pushes, in position order
-        const uint32_t l = (uint32_t)__builtin_ctzll(bb);
-        const uint32_t ps = nknown + (uint32_t)__builtin_popcountll(b & ((1ull << l) - 1ull));
-        heap_push(hp, nheap, HeapE{dbuf[c0 + l], ps}, lane);
-      }
-      nknown += (uint32_t)__builtin_popcountll(b);
+    if (lane == 0 && succ) atomicAdd((unsigned long long*)&SS->succ, (unsigned long long)succ);
+    block_sync();
+    uint32_t before = nknown;
+    for (uint32_t w = 0; w < wave; ++w) before += s_wcnt[w];
+    uint32_t total_new = 0;
+    for (uint32_t w = 0; w < kDrlThreads / 64; ++w) total_new += s_wcnt[w];
+    if (nw) {
+      const uint32_t slot = before + (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
+      pbuf[i4] = slot;
+      kdist[slot] = dbuf[i4];
+      kid[slot] = bat[i4];
+      tab_put(ktab, kmask, bat[i4], slot);
     }
+    block_sync();
+    for (uint32_t e = tid; e < n * m; e += kDrlThreads) {   // the new vertices' neighbour lists
+      const uint32_t i = e / m;
+      if ((s_wmask[i >> 6] >> (i & 63)) & 1ull) knb[(uint64_t)pbuf[i] * m + (e - i * m)] = nbuf[e];
+    }
+    // ---- the heap pushes, in position order (wave 0)
+    if (wave == 0) {
+      for (uint32_t w = 0; w < kDrlThreads / 64; ++w)
+        for (uint64_t bb = s_wmask[w]; bb; bb &= bb - 1) {
+          const uint32_t i = w * 64 + (uint32_t)__builtin_ctzll(bb);
+          heap_push(hp, nheap, HeapE{dbuf[i], pbuf[i]}, lane);
+        }
+    }
+    nknown += total_new;
     __threadfence();   // the new known rows are read back by this launch's pops
+    block_sync();
+    stamp(4);
   }
 
   if (A.mode != DRL_END) {
-    // ---- the next batch (search.go:153-171)
-    for (uint32_t r = 0; r < A.parallel; ++r) {
-      if (nheap == 0) {   // rng.Intn(n) for each of the m positions (SplitMix::next: state += gamma, then mix)
-        if (lane < m) bat[r * m + lane] = (uint32_t)(sm64(rng + (uint64_t)lane * 0x9e3779b97f4a7c15ULL) % A.N);
-        rng += (uint64_t)m * 0x9e3779b97f4a7c15ULL;
-      } else {
-        const HeapE e = heap_pop(hp, nheap, lane);
-        if (lane < m) bat[r * m + lane] = knb[(uint64_t)e.slot * m + lane];
+    // ---- the next batch (search.go:153-171): wave 0 pops, then every lane
+    // gathers the popped vertices' neighbours (or the SplitMix ids)
+    if (wave == 0) {
+      for (uint32_t r = 0; r < A.parallel; ++r) {
+        uint32_t slot = 0xffffffffu;
+        if (nheap) slot = heap_pop(hp, nheap, lane).slot;
+        if (lane == 0) s_pop[r] = slot;
       }
+      if (lane == 0) s_nheap = nheap;
     }
-    __syncthreads();
+    block_sync();
+    nheap = s_nheap;
+    {
+      uint64_t r0 = rng;   // the id stream consumed by the empty-heap positions in order
+      for (uint32_t r = 0; r < A.parallel; ++r) {
+        const uint32_t slot = s_pop[r];
+        for (uint32_t k = tid; k < m; k += kDrlThreads) {
+          if (slot == 0xffffffffu) bat[r * m + k] = (uint32_t)(sm64(r0 + (uint64_t)k * 0x9e3779b97f4a7c15ULL) % A.N);
+          else bat[r * m + k] = knb[(uint64_t)slot * m + k];
+        }
+        if (slot == 0xffffffffu) r0 += (uint64_t)m * 0x9e3779b97f4a7c15ULL;
+      }
+      rng = r0;
+    }
+    block_sync();
+    stamp(5);
     // ---- SimpleBatchPianoPIR.Query's bucketing into the next shared step
-    for (uint32_t i = lane; i < n; i += 64) pbuf[i] = (uint32_t)(bat[i] / A.PS);
-    __syncthreads();
+    for (uint32_t i = tid; i < n; i += kDrlThreads) pbuf[i] = bat[i] / PS;
+    block_sync();
     double bytes = 0.0;
     uint32_t nreal = 0;
-    for (uint32_t i = lane; i < n; i += 64) {
+    for (uint32_t i = tid; i < n; i += kDrlThreads) {
       const uint32_t id = bat[i], p = pbuf[i];
       uint32_t rank = 0;
       for (uint32_t j = 0; j < i; ++j) rank += pbuf[j] == p;
       if (rank < qn) {   // the first queryNumToMake ids of a partition; the rest are dropped
         const uint32_t j = base + p * qn + rank;
-        const uint32_t local = (uint32_t)(id - (uint64_t)p * A.PS);
+        const uint32_t local = id - p * PS;
         uint32_t slot;
         PmSub sub{s * P + p, SUB_REAL, local};
-        if (tab_find(A.ctab[s] + (uint64_t)p * (A.cmask + 1), A.cmask, local, &slot)) {
+        if (tab_find(ctab + (uint64_t)p * cap, A.cmask, local, &slot)) {
           sub.kind = SUB_HOSTCACHE;
           sub.idx = slot;
         } else {
@@ -295,7 +369,7 @@ __global__ void __launch_bounds__(64) k_team_round(const DrlArgs A) {
         A.gid[j] = id;
       }
     }
-    for (uint32_t p = lane; p < P; p += 64) {   // dummy padding (batch-pir.go:182-190)
+    for (uint32_t p = tid; p < P; p += kDrlThreads) {   // dummy padding (batch-pir.go:182-190)
       uint32_t cnt = 0;
       for (uint32_t i = 0; i < n; ++i) cnt += pbuf[i] == p;
       uint64_t dc = A.dummy[(uint64_t)s * P + p];
@@ -306,46 +380,51 @@ __global__ void __launch_bounds__(64) k_team_round(const DrlArgs A) {
       }
       A.dummy[(uint64_t)s * P + p] = dc;
     }
-    if (A.step_bytes) {
+    if (A.step_bytes) {   // (timing runs) the step's exact answer bytes and real sub-queries
       bytes = wave_sumd(bytes);
       const uint64_t nr = wave_sum(nreal);
       if (lane == 0) {
-        A.step_bytes[(uint64_t)A.seq * A.S + s] = bytes;
-        A.step_real[(uint64_t)A.seq * A.S + s] = (uint32_t)nr;
+        atomicAdd(&A.step_bytes[(uint64_t)A.seq * A.S + s], bytes);
+        atomicAdd(&A.step_real[(uint64_t)A.seq * A.S + s], (uint32_t)nr);
       }
     }
-    for (uint32_t i = lane; i < n; i += 64) gbat[i] = bat[i];
-    for (uint32_t i = lane; i < nheap; i += 64) gheap[i] = hp[i];
+    stamp(6);
+    for (uint32_t i = tid; i < n; i += kDrlThreads) gbat[i] = bat[i];
+    for (uint32_t i = tid; i < nheap; i += kDrlThreads) gheap[i] = hp[i];
+    stamp(7);
+    if (A.stamps && A.mode == DRL_MID && threadIdx.x == 0) atomicAdd((unsigned long long*)&A.stamps[15], 1ull);
   } else {
     // ---- the top k by (distance, id) (search.go:211-233), -1 padded
     float* ld = (float*)lds;                          // the heap's LDS, no longer needed
     uint32_t* li = (uint32_t*)(lds + (size_t)kcap * 4);
-    for (uint32_t j = lane; j < nknown; j += 64) { ld[j] = kdist[j]; li[j] = kid[j]; }
-    __syncthreads();
-    int64_t* out = A.answers + ((uint64_t)s * A.q + A.qi) * A.k;
-    float pd = 0.0f;
-    uint32_t pi = 0;
-    for (uint32_t t = 0; t < A.k; ++t) {
-      float bd = __builtin_inff();
-      uint32_t bi = 0xffffffffu;
-      bool any = false;
-      for (uint32_t j = lane; j < nknown; j += 64) {
-        const float d = ld[j];
-        const uint32_t id = li[j];
-        const bool after = t == 0 || d > pd || (d == pd && id > pi);
-        if (after && (!any || d < bd || (d == bd && id < bi))) { bd = d; bi = id; any = true; }
+    for (uint32_t j = tid; j < nknown; j += kDrlThreads) { ld[j] = kdist[j]; li[j] = kid[j]; }
+    block_sync();
+    if (wave == 0) {
+      int64_t* out = A.answers + ((uint64_t)s * A.q + A.qi) * A.k;
+      float pd = 0.0f;
+      uint32_t pi = 0;
+      for (uint32_t t = 0; t < A.k; ++t) {
+        float bd = __builtin_inff();
+        uint32_t bi = 0xffffffffu;
+        bool any = false;
+        for (uint32_t j = lane; j < nknown; j += 64) {
+          const float d = ld[j];
+          const uint32_t id = li[j];
+          const bool after = t == 0 || d > pd || (d == pd && id > pi);
+          if (after && (!any || d < bd || (d == bd && id < bi))) { bd = d; bi = id; any = true; }
+        }
+        const bool found = __ballot(any) != 0;
+        wave_min2(bd, bi);   // lanes without a candidate hold (inf, ~0): never below a real one
+        if (lane == 0) out[t] = found ? (int64_t)bi : -1;
+        if (!found) {
+          for (uint32_t u = t + 1 + lane; u < A.k; u += 64) out[u] = -1;
+          break;
+        }
+        pd = bd; pi = bi;
       }
-      const bool found = __ballot(any) != 0;
-      wave_min2(bd, bi);   // lanes without a candidate hold (inf, ~0): never below a real one
-      if (lane == 0) out[t] = found ? (int64_t)bi : -1;
-      if (!found) {
-        for (uint32_t u = t + 1 + lane; u < A.k; u += 64) out[u] = -1;
-        break;
-      }
-      pd = bd; pi = bi;
     }
   }
-  if (lane == 0) {
+  if (tid == 0) {
     SS->rng = rng;
     SS->nknown = nknown;
     SS->nheap = A.mode == DRL_END ? 0u : nheap;
@@ -353,13 +432,13 @@ __global__ void __launch_bounds__(64) k_team_round(const DrlArgs A) {
 }
 
 static uint32_t team_round_lds_impl(uint32_t kcap, uint32_t n, uint32_t m) {
-  return kcap * 8 + n * m * 4 + 3 * n * 4;
+  return kcap * 8 + n * m * 4 + 5 * n * 4 + 4 * n * 4;   // heap, rows, per-position arrays, per-sub-query arrays (<= n)
 }
 
 static void team_round_impl(hipStream_t st, const DrlArgs& A, hipEvent_t a, hipEvent_t b) {
   const uint32_t lds = team_round_lds_impl(A.kcap, A.n, A.m);
-  if (a) hipExtLaunchKernelGGL(k_team_round, dim3(A.S), dim3(64), lds, st, a, b, 0, A);
-  else hipLaunchKernelGGL(k_team_round, dim3(A.S), dim3(64), lds, st, A);
+  if (a) hipExtLaunchKernelGGL(k_team_round, dim3(A.S), dim3(kDrlThreads), lds, st, a, b, 0, A);
+  else hipLaunchKernelGGL(k_team_round, dim3(A.S), dim3(kDrlThreads), lds, st, A);
 }
 
 }  // namespace pm

@@ -3610,8 +3610,50 @@ struct PoolTeam {
   double launched_us = 0;
   uint32_t id = 0;
 };
+// Streams of the lock-step teams.  A team's steps ran on its first session's
+// context stream, and every session context creates its stream when it is
+// made: HIP maps streams onto the process's GPU_MAX_HW_QUEUES (4) hardware
+// queues in creation order, so with 72 sessions per team the four teams'
+// streams (sessions 0, 72, 144, 216) could all land on ONE hardware queue,
+// whose in-order packets serialise the teams' kernels.  The teams get streams
+// of their own instead, created back to back once per device (so they take
+// distinct hardware queues), swapped into the team's context for the loop
+// (PM_TEAM_STREAMS=0: the context streams).
+static hipStream_t team_stream(int dev, uint32_t t) {
+  static std::mutex mu;
+  static std::vector<hipStream_t> pool[64];
+  static const int on = [] { const char* e = getenv("PM_TEAM_STREAMS"); return e ? atoi(e) : 1; }();
+  if (!on || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  std::vector<hipStream_t>& v = pool[dev];
+  if (v.empty()) {
+    for (int i = 0; i < 8; ++i) {
+      hipStream_t st = nullptr;
+      if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) break;
+      v.push_back(st);
+    }
+  }
+  return v.empty() ? nullptr : v[t % v.size()];
+}
+struct StreamSwap {   // a team context's stream replaced for the loop's duration (restored drained)
+  pm_ctx* c = nullptr;
+  hipStream_t old = nullptr;
+  void swap_in(pm_ctx* ctx, hipStream_t st) {
+    if (!st) return;
+    c = ctx; old = ctx->stream;
+    (void)hipStreamSynchronize(old);
+    ctx->stream = st;
+  }
+  ~StreamSwap() {
+    if (!c) return;
+    (void)hipStreamSynchronize(c->stream);
+    c->stream = old;
+  }
+};
+
 static int run_batched_pool(pm_graph** gs, uint32_t S, const float* queries, uint64_t q, int k, int step, int parallel,
                             uint32_t NG, uint32_t T, int64_t* answers, double* mt_out) {
+  std::vector<StreamSwap> swaps(NG);   // destroyed after `teams` (declared first): streams drained, restored
   std::vector<std::unique_ptr<PoolTeam>> teams;
   DevBuf prep_buf;   // the merged maintenance's parts
   std::mutex prep_mu;
@@ -3641,6 +3683,7 @@ static int run_batched_pool(pm_graph** gs, uint32_t S, const float* queries, uin
     t.lane.reset(new std::atomic<uint32_t>[T]);
     for (uint32_t w = 0; w < T; ++w) t.lane[w].store(0);
     CHK(team_init(t.G, t.gs, t.S));
+    swaps[g].swap_in(t.G.c, team_stream(t.G.c->device, g));
     static const int stage = [] { const char* e = getenv("PM_DESC_STAGE"); return e ? atoi(e) : 1; }();
     t.G.stage_on = stage != 0;
     t.G.stg.resize(t.S);
@@ -3985,7 +4028,7 @@ struct DrlTeam {
   pm_graph** gs = nullptr;
   uint32_t S = 0, s0 = 0, nsub = 0;
   DevBuf sess, dummy, batch, heap, ktab, knb, kdist, kid, ctabp, answers, subs, gid, sb, out, allq, part_bytes,
-      step_bytes, step_real;
+      step_bytes, step_real, stamps;
   DrlArgs A{};
   hipEvent_t ev_end = nullptr;
   uint32_t seq = 0;                              // shared steps built so far (step_bytes rows)
@@ -4051,8 +4094,14 @@ static int drl_team_init(DrlTeam& T, pm_graph** gs, uint32_t S, uint32_t s0, con
     const uint64_t steps = q * (uint64_t)step;
     CHK(T.step_bytes.reserve(std::max<uint64_t>(8, steps * S * 8)));
     CHK(T.step_real.reserve(std::max<uint64_t>(4, steps * S * 4)));
+    HIPCHK(hipMemsetAsync(T.step_bytes.p, 0, std::max<uint64_t>(8, steps * S * 8), st));   // accumulated by the rounds
+    HIPCHK(hipMemsetAsync(T.step_real.p, 0, std::max<uint64_t>(4, steps * S * 4), st));
   }
   HIPCHK(hipEventCreateWithFlags(&T.ev_end, hipEventDisableTiming));
+  if (getenv("PM_DRL_STAMPS")) {   // diagnostics: per-phase shader clocks of the MID rounds (printed at the end)
+    CHK(T.stamps.reserve(16 * 8));
+    HIPCHK(hipMemset(T.stamps.p, 0, 16 * 8));
+  }
   // the step buffers of group_step for nsub sub-queries
   const uint32_t words = (G.maxPH + 63) / 64, cblk = pmk::step_match_blocks(G.maxPH);
   CHK(G.bits.reserve((uint64_t)T.nsub * words * 8));
@@ -4076,6 +4125,7 @@ static int drl_team_init(DrlTeam& T, pm_graph** gs, uint32_t S, uint32_t s0, con
   A.answers = T.answers.as<int64_t>(); A.part_bytes = T.part_bytes.as<double>();
   A.step_bytes = T.step_bytes.p ? T.step_bytes.as<double>() : nullptr;
   A.step_real = T.step_real.p ? T.step_real.as<uint32_t>() : nullptr;
+  A.stamps = T.stamps.p ? T.stamps.as<uint64_t>() : nullptr;
   T.need.assign(S, 0);
   T.mt.assign(S, 0.0);
   return 0;
@@ -4131,9 +4181,11 @@ static void drl_round(DrlTeam& T, uint32_t mode, uint64_t qi) {
   c->timed_ext("team_round", 0, [&](pmk::PmEvents ev) { pmk::team_round(c->stream, A, ev); }, 2);
 }
 
-// A query of team T enqueued on its stream: the queries into qbuf, the start
-// set's distances, BEGIN, then the rounds.
-static int drl_query(DrlTeam& T, const DrlShape& sh, uint64_t qi, uint64_t q, int step) {
+// Query qi of every team, enqueued round by round across the teams (so that
+// teams whose streams share a hardware queue still interleave their rounds):
+// per team the queries into qbuf, the start set's distances and BEGIN, then
+// per round the shared step and the round kernel (MID, END after the last).
+static int drl_begin(DrlTeam& T, uint64_t qi, uint64_t q) {
   StepGroup& G = T.G;
   hipStream_t st = G.c->stream;
   const uint32_t dim = G.dim;
@@ -4146,19 +4198,27 @@ static int drl_query(DrlTeam& T, const DrlShape& sh, uint64_t qi, uint64_t q, in
                    G.start_dist.as<float>(), G.ns);
     });
   drl_round(T, DRL_BEGIN, qi);
-  for (int r = 0; r < step; ++r) {
-    CHK(drl_step(T, sh));
-    drl_round(T, r + 1 == step ? DRL_END : DRL_MID, qi);
-  }
+  return 0;
+}
+static int drl_query_all(std::vector<std::unique_ptr<DrlTeam>>& teams, const DrlShape& sh, uint64_t qi, uint64_t q,
+                         int step) {
+  for (auto& t : teams) CHK(drl_begin(*t, qi, q));
+  for (int r = 0; r < step; ++r)
+    for (auto& t : teams) {
+      CHK(drl_step(*t, sh));
+      drl_round(*t, r + 1 == step ? DRL_END : DRL_MID, qi);
+    }
   HIPCHK(hipGetLastError());
-  for (uint32_t i = 0; i < T.S; ++i) {   // the host's deterministic mirrors of the rounds (bq_tail, gvi_pre)
-    pm_graph* g = T.gs[i];
-    Engine* e = &g->pir->e;
-    e->FBN += (uint64_t)step * (sh.n / e->B);
-    e->QMIP += (uint64_t)step * sh.qn;
-    g->total += (uint64_t)step * sh.n;
+  for (auto& t : teams) {
+    for (uint32_t i = 0; i < t->S; ++i) {   // the host's deterministic mirrors of the rounds (bq_tail, gvi_pre)
+      pm_graph* g = t->gs[i];
+      Engine* e = &g->pir->e;
+      e->FBN += (uint64_t)step * (sh.n / e->B);
+      e->QMIP += (uint64_t)step * sh.qn;
+      g->total += (uint64_t)step * sh.n;
+    }
+    t->G.c->host_add(HT_DEV_QUERIES, (double)t->S);
   }
-  G.c->host_add(HT_DEV_QUERIES, (double)T.S);
   return 0;
 }
 
@@ -4185,6 +4245,15 @@ static int drl_team_finish(DrlTeam& T, uint64_t q, int k, int64_t* answers) {
       e->parts[p].fqn = fq[p];
     }
   }
+  if (T.stamps.p) {
+    uint64_t st[16];
+    HIPCHK(hipMemcpy(st, T.stamps.p, sizeof st, hipMemcpyDeviceToHost));
+    if (st[15])
+      fprintf(stderr, "[pm] team_round MID phases (shader clocks per launch, %lu launches): load %.0f respond %.0f decode %.0f "
+              "update+push %.0f pop+gather %.0f bucket %.0f store %.0f\n", (unsigned long)st[15], st[1] / (double)st[15],
+              st[2] / (double)st[15], st[3] / (double)st[15], st[4] / (double)st[15], st[5] / (double)st[15],
+              st[6] / (double)st[15], st[7] / (double)st[15]);
+  }
   pm_ctx* c = G.c;
   if (!T.tl.empty() && T.step_bytes.p) {   // the timed steps' exact answer bytes / real sub-queries
     std::vector<double> by((uint64_t)T.seq * S);
@@ -4204,6 +4273,7 @@ static int drl_team_finish(DrlTeam& T, uint64_t q, int k, int64_t* answers) {
 
 static int run_batched_dev(pm_graph** gs, uint32_t S, const float* queries, uint64_t q, int k, int step, int parallel,
                            uint32_t NG, int64_t* answers, double* mt_out, const DrlShape& sh) {
+  std::vector<StreamSwap> swaps(NG);   // (destroyed after the teams: drained, restored)
   std::vector<std::unique_ptr<DrlTeam>> teams;
   struct Release {
     std::vector<std::unique_ptr<DrlTeam>>& t;
@@ -4213,10 +4283,11 @@ static int run_batched_dev(pm_graph** gs, uint32_t S, const float* queries, uint
     const uint32_t s0 = (uint32_t)((uint64_t)S * g / NG), s1 = (uint32_t)((uint64_t)S * (g + 1) / NG);
     teams.emplace_back(new DrlTeam());
     CHK(drl_team_init(*teams.back(), gs + s0, s1 - s0, s0, queries, q, k, step, parallel, sh));
+    swaps[g].swap_in(teams.back()->G.c, team_stream(teams.back()->G.c->device, g));
   }
   DevBuf prep_buf;
   for (uint64_t qi = 0; qi < q; ++qi) {
-    for (auto& t : teams) CHK(drl_query(*t, sh, qi, q, step));
+    CHK(drl_query_all(teams, sh, qi, q, step));
     // the harness's maintenance trigger (private-search.go:226-232) per session:
     // the triggered clients of every team as ONE launch set after the query
     std::vector<Engine*> who;

@@ -258,6 +258,7 @@ struct DrlArgs {
   const double* part_bytes;       // [P] algorithmic answer bytes of one sub-query
   double* step_bytes;             // [launch seq][S] (timing runs; null: not counted)
   uint32_t* step_real;            // [launch seq][S] real sub-queries (timing runs)
+  uint64_t* stamps;               // diagnostics (PM_DRL_STAMPS): [16] summed shader clocks per phase of MID rounds
 };
 
 }  // namespace pm

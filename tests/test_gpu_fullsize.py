@@ -427,6 +427,7 @@ def test_search_msmarco_bench_exact_shape(oracle):
         return tuple(sum(x[i] for x in r) for i in range(3))
     n_ans = tsum("answer")[0]
     assert n_ans == G * (NQ - WARM) * 20 and tsum("match_resolve")[0] == n_ans, n_ans
+    assert tsum("host_dev_steps")[0] == n_ans   # the device loop chained every step (pm_drl.hip)
     assert tsum("host_prep_sets")[:2] == (1, S), tsum("host_prep_sets")
     n_fold, _, fby = tsum("prep_fold")
     sc = base.PIR.SubConfig(0)

@@ -3,9 +3,10 @@
 
   * the bench's data: `sift_like_vectors(1e6, 128, seed=100)` and the graph
     `pm.build_graph(v, 32, 1.2, seed=7)` built on the GPU (kNN + robustPrune);
-  * the bench's serving shape: 288 sessions in 4 lock-step teams of 72 with 16
-    pooled host workers (pm_search_loop_batched -> run_batched_pool), every
-    round of a team ONE shared step over 72 x 16 partitions;
+  * the bench's serving shape: 288 sessions in 4 lock-step teams of 72
+    (pm_search_loop_batched -> run_batched_dev: each team's rounds chained on
+    its stream by the device loop, pm_drl.hip), every round of a team ONE
+    shared step over 72 x 16 partitions;
   * the merged maintenance: the 288 sessions reach their re-preprocessing at
     the same query (window 23, private-search.go:226-232), and the waiting
     teams' clients are re-preprocessed as ONE launch set (one k_prep_fold_rot
@@ -59,6 +60,8 @@ def test_headline_bench_sessions_4_teams_vs_oracle(oracle):
     assert n_ans == TEAMS * QUERIES * STEP, n_ans
     assert tsum("match_resolve")[0] == n_ans
     assert by / n_ans > 330e6   # ~6,912 sub-queries x ~80.5 KB per step (minus cache hits)
+    # ... every one of them chained on the GPU by the device loop (pm_drl.hip)
+    assert tsum("host_dev_steps")[0] == n_ans and tsum("host_dev_queries")[1] == S * QUERIES
     # ... and the maintenance ran ONCE, merged: one launch set of all 288
     # clients, one fold launch over all their hints
     sets, clients, _ = tsum("host_prep_sets")
