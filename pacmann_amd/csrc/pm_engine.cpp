@@ -3955,7 +3955,8 @@ struct DrlShape { uint32_t n = 0, qn = 0, kcap = 0, cmask = 0; };
 // bq_prepare's slow path; FinishedQueryNum <= QueriesMadeInPartition always)
 // or the batch layer's trigger (QueriesMadeInPartition >= MaxQueryNum - 2).
 static bool drl_plan(pm_graph** gs, uint32_t S, uint64_t q, int k, int step, int parallel, DrlShape* sh) {
-  if (!device_loop_on() || S == 0 || step <= 0 || parallel <= 0 || k <= 0) return false;
+  if (!device_loop_on() || S == 0 || step <= 0 || parallel <= 0 || k <= 0 || (uint32_t)parallel > pmk::kDrlMaxParallel)
+    return false;
   const pm_graph* g0 = gs[0];
   const Engine& e0 = g0->pir->e;
   const uint64_t m = g0->m, n = (uint64_t)parallel * m, P = e0.P;
@@ -4114,6 +4115,7 @@ static int drl_team_init(DrlTeam& T, pm_graph** gs, uint32_t S, uint32_t s0, con
   A.S = S; A.P = P; A.qn = sh.qn; A.n = n; A.m = m; A.parallel = (uint32_t)parallel; A.k = (uint32_t)k;
   A.E = G.E; A.dim = dim; A.kcap = kcap; A.cmask = sh.cmask; A.ns = G.ns; A.q = (uint32_t)q;
   A.N = g0->n; A.PS = e0.PS;
+  A.vec16 = (G.E % 2 == 0 && dim % 4 == 0 && m % 4 == 0 && ((m / 4) & (m / 4 - 1)) == 0) ? 1u : 0u;
   A.hdr = T.out.as<PmOutHdr>();
   A.rows = (const uint64_t*)(T.out.as<char>() + (uint64_t)T.nsub * sizeof(PmOutHdr));
   A.subs = T.subs.as<PmSub>(); A.gid = T.gid.as<uint64_t>();
@@ -4250,9 +4252,10 @@ static int drl_team_finish(DrlTeam& T, uint64_t q, int k, int64_t* answers) {
     HIPCHK(hipMemcpy(st, T.stamps.p, sizeof st, hipMemcpyDeviceToHost));
     if (st[15])
       fprintf(stderr, "[pm] team_round MID phases (shader clocks per launch, %lu launches): load %.0f respond %.0f decode %.0f "
-              "update+push %.0f pop+gather %.0f bucket %.0f store %.0f\n", (unsigned long)st[15], st[1] / (double)st[15],
-              st[2] / (double)st[15], st[3] / (double)st[15], st[4] / (double)st[15], st[5] / (double)st[15],
-              st[6] / (double)st[15], st[7] / (double)st[15]);
+              "[ballot %.0f known %.0f rows %.0f push %.0f fence %.0f] pop+gather %.0f bucket %.0f store %.0f\n",
+              (unsigned long)st[15], st[1] / (double)st[15], st[2] / (double)st[15], st[3] / (double)st[15],
+              st[8] / (double)st[15], st[9] / (double)st[15], st[10] / (double)st[15], st[11] / (double)st[15],
+              st[4] / (double)st[15], st[5] / (double)st[15], st[6] / (double)st[15], st[7] / (double)st[15]);
   }
   pm_ctx* c = G.c;
   if (!T.tl.empty() && T.step_bytes.p) {   // the timed steps' exact answer bytes / real sub-queries

@@ -237,6 +237,7 @@ struct DrlSess {          // one session's search state between launches
 enum : uint32_t { DRL_BEGIN = 0, DRL_MID = 1, DRL_END = 2 };
 struct DrlArgs {
   uint32_t S, P, qn, n, m, parallel, k, E, dim, kcap, cmask, ns, mode, q, qi, seq;
+  uint32_t vec16;                 // rows and neighbour lists 16-B aligned, m / 4 a power of two (vector decode)
   uint64_t N, PS;
   const PmOutHdr* hdr;            // the last shared step's results [nsub] (device)
   const uint64_t* rows;           // ... and rows [nsub][E] (the neighbour words only)
@@ -366,7 +367,7 @@ void prf_batch(hipStream_t st, const uint32_t* rk, const uint64_t* tags, const u
 // the device-resident team round (pm_drl.hip): one 64-lane workgroup per session
 void team_round(hipStream_t st, const DrlArgs& A, PmEvents ev = {});
 uint32_t team_round_lds(uint32_t kcap, uint32_t n, uint32_t m);   // bytes of dynamic LDS
-constexpr uint32_t kDrlMaxKcap = 4096, kDrlMaxN = 256, kDrlMaxNM = 8192;
+constexpr uint32_t kDrlMaxKcap = 4096, kDrlMaxN = 256, kDrlMaxNM = 8192, kDrlMaxParallel = 8;
 // graph construction and ground truth (pm_graph.hip)
 uint32_t knn_pad_dim(uint32_t dim);   // bf16 row width for the prefilter (0: unsupported)
 uint32_t knn_top();                   // prefilter candidates per query row

@@ -1419,8 +1419,12 @@ __global__ void __launch_bounds__(kResolveBlockG) k_match_resolve(PmStep S) {
 #ifndef PM_MR_G
 #define PM_MR_G 8       // search rows of 8 / NU sub-queries per round trip (0: see above)
 #endif
+#ifndef PM_CHAIN_PRIO
+#define PM_CHAIN_PRIO 0   // s_setprio of the device loop's chain kernels (match + resolve, the team round)
+#endif
 template <int NU, int NT>
 __global__ void __launch_bounds__(NT) k_match_resolve_s(PmStep S) {
+  if (PM_CHAIN_PRIO) __builtin_amdgcn_s_setprio(PM_CHAIN_PRIO);
   // G sub-queries' search rows in flight together (the usual 6 per partition:
   // one round trip); 2 * G * NU <= 64 candidates per wave, one per lane
   constexpr int NW = NT / 64, G = PM_MR_G ? PM_MR_G / NU : NU <= 2 ? 8 : NU == 4 ? 6 : 8 / NU;
