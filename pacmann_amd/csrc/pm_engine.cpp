@@ -459,6 +459,7 @@ struct Engine {
   std::shared_ptr<DevBuf> img = std::make_shared<DevBuf>();  // the DB's fold image (pmk::fold_image), shared likewise
   DevBuf zero16, parts_d, owned_d, tag, pp, parity, ridx, rval, hist, fqn, arena, tab, tabT, cur, done, gran;
   HostBuf parts_stage;   // pinned copy of [parts | owned parts] for the asynchronous upload (upload_parts_async)
+  hipEvent_t stage_ev = nullptr;   // the last upload from parts_stage (the stage is rewritten only after it)
   uint32_t gran_words = 0;
   std::vector<uint32_t> owned_list;   // owned partitions in order (owned_d holds their PmPart)
   DevBuf qoffs, ans_srv;
@@ -472,7 +473,10 @@ struct Engine {
   HostBuf desc_h, out_h, err_h, src_h;   // src_h: pm_batchpir_query_dev's row pointers
   HostBuf stage_h;                       // ... and its rows of a multi-step query (pinned staging)
   hipEvent_t dev_ev = nullptr;           // ... its completion, for the consumer's stream
-  ~Engine() { if (dev_ev) (void)hipEventDestroy(dev_ev); }
+  ~Engine() {
+    if (dev_ev) (void)hipEventDestroy(dev_ev);
+    if (stage_ev) (void)hipEventDestroy(stage_ev);
+  }
   std::vector<PartHost> parts;
   uint32_t maxH = 0, maxPH = 0, maxSS = 0, maxRepl = 0, maxCS = 0, minCS = ~0u;
   bool ph8 = true;   // every owned partition's PH is a multiple of 8 (16-B hint search rows)
@@ -747,12 +751,15 @@ static int upload_parts_async(Engine* g, hipStream_t st) {
   // queued there finishes first (idle in batched serving: no wait)
   if (g->ctx->stream != st && hipStreamQuery(g->ctx->stream) != hipSuccess) HIPCHK(hipStreamSynchronize(g->ctx->stream));
   const size_t no = g->owned_list.size();
+  if (g->stage_ev) HIPCHK(hipEventSynchronize(g->stage_ev));   // the previous upload has left the stage
+  else HIPCHK(hipEventCreateWithFlags(&g->stage_ev, hipEventDisableTiming));
   CHK(g->parts_stage.reserve((g->P + no) * sizeof(PmPart)));
   PmPart* h = g->parts_stage.as<PmPart>();
   for (uint64_t i = 0; i < g->P; ++i) h[i] = g->parts[i].d;
   for (size_t i = 0; i < no; ++i) h[g->P + i] = g->parts[g->owned_list[i]].d;
   HIPCHK(hipMemcpyAsync(g->parts_d.p, h, g->P * sizeof(PmPart), hipMemcpyHostToDevice, st));
   if (no) HIPCHK(hipMemcpyAsync(g->owned_d.p, h + g->P, no * sizeof(PmPart), hipMemcpyHostToDevice, st));
+  HIPCHK(hipEventRecord(g->stage_ev, st));
   return 0;
 }
 
@@ -812,7 +819,7 @@ static int engine_prep_host(Engine* g, uint64_t p0, uint64_t p1, std::vector<uin
 // one server: same parameters and DB): PRF tables, then the hint fold and
 // the replacement rows, or zero hints for DummyPreprocessing.  Synchronous.
 static int engine_prep_launch(pm_ctx* c, const Engine* g, const PmPart* dp, int np, const PmPart* host_parts,
-                              uint32_t clients = 1) {
+                              uint32_t clients = 1, bool sync = true) {
   hipStream_t st = c->stream;
   c->timed("prep_init", 0, [&] { pmk::prep_init(st, dp, np, g->maxH, g->maxRepl, (uint32_t)g->E, g->skipPrep); });
   double aes = 0, fold = 0, repl = 0;
@@ -856,7 +863,7 @@ static int engine_prep_launch(pm_ctx* c, const Engine* g, const PmPart* dp, int 
     else c->timed("prep_repl", repl, [&] { pmk::prep_repl(st, dp, np, g->maxRepl, g->db->as<uint64_t>(), (uint32_t)g->E); });
   }
   HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(st));
+  if (sync) HIPCHK(hipStreamSynchronize(st));
   return 0;
 }
 static int engine_prep(Engine* g, uint64_t p0, uint64_t p1) {
@@ -2971,8 +2978,11 @@ static int group_start_dist(StepGroup& G, pm_graph** gs) {
 // lp), as ONE launch set over all their partitions on c's stream, with its
 // parts staged in pbuf.  Each client's maintenance time is the set's wall time
 // (added to *mt[i] when given).
+// Async form (stage non-null): the parts go up from the pinned `stage` (its
+// previous copy waited for through *stage_ev), nothing waits for the launch
+// set, and the caller times it with events (mt unused).
 static int prep_clients(pm_ctx* c, DevBuf& pbuf, const std::vector<uint32_t>& lp, const std::vector<Engine*>& who,
-                        const std::vector<double*>* mt) {
+                        const std::vector<double*>* mt, HostBuf* stage = nullptr, hipEvent_t* stage_ev = nullptr) {
   if (who.empty()) return 0;
   auto t0 = Clock::now();
   std::vector<PmPart> hp;
@@ -2990,8 +3000,17 @@ static int prep_clients(pm_ctx* c, DevBuf& pbuf, const std::vector<uint32_t>& lp
   for (Engine* e : who) skip |= e->skipPrep != e0->skipPrep;
   if (skip) return fail(PM_EINVAL, "batched sessions mix Preprocessing and DummyPreprocessing");
   CHK(pbuf.reserve(hp.size() * sizeof(PmPart)));
-  HIPCHK(hipMemcpyAsync(pbuf.p, hp.data(), hp.size() * sizeof(PmPart), hipMemcpyHostToDevice, c->stream));
-  CHK(engine_prep_launch(c, e0, pbuf.as<PmPart>(), (int)hp.size(), hp.data(), (uint32_t)who.size()));
+  if (stage) {
+    if (*stage_ev) HIPCHK(hipEventSynchronize(*stage_ev));
+    else HIPCHK(hipEventCreateWithFlags(stage_ev, hipEventDisableTiming));
+    CHK(stage->reserve(hp.size() * sizeof(PmPart)));
+    memcpy(stage->p, hp.data(), hp.size() * sizeof(PmPart));
+    HIPCHK(hipMemcpyAsync(pbuf.p, stage->p, hp.size() * sizeof(PmPart), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipEventRecord(*stage_ev, c->stream));
+  } else {
+    HIPCHK(hipMemcpyAsync(pbuf.p, hp.data(), hp.size() * sizeof(PmPart), hipMemcpyHostToDevice, c->stream));
+  }
+  CHK(engine_prep_launch(c, e0, pbuf.as<PmPart>(), (int)hp.size(), hp.data(), (uint32_t)who.size(), !stage));
   c->host_add(HT_PREP_SETS, (double)who.size());
   const double t = std::chrono::duration<double>(Clock::now() - t0).count();
   for (size_t i = 0; i < who.size(); ++i) {
@@ -4032,12 +4051,39 @@ struct DrlTeam {
       step_bytes, step_real, stamps;
   DrlArgs A{};
   hipEvent_t ev_end = nullptr;
+  HostBuf prep_stage, parts_stage;               // pinned stages of the asynchronous maintenance (run_batched_dev)
+  hipEvent_t prep_stage_ev = nullptr, parts_stage_ev = nullptr;
+  DevBuf prep_buf;
   uint32_t seq = 0;                              // shared steps built so far (step_bytes rows)
   std::vector<std::pair<size_t, uint32_t>> tl;   // timed "answer" / "match_resolve" launches: (index, step)
   std::vector<char> need;
   std::vector<double> mt;
-  ~DrlTeam() { if (ev_end) (void)hipEventDestroy(ev_end); }
+  ~DrlTeam() {
+    for (hipEvent_t e : {ev_end, prep_stage_ev, parts_stage_ev})
+      if (e) (void)hipEventDestroy(e);
+  }
 };
+
+// The team's parts (new keys after a maintenance) up from a pinned stage on
+// stream st, nothing waiting (the stage's previous copy is waited for first).
+static int group_upload_parts_async(StepGroup& G, hipStream_t st, HostBuf& stage, hipEvent_t& ev) {
+  if (ev) HIPCHK(hipEventSynchronize(ev));
+  else HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  const size_t np = (size_t)G.S * G.Pl;
+  CHK(stage.reserve(std::max<size_t>(1, np) * sizeof(PmPart)));
+  PmPart* v = stage.as<PmPart>();
+  for (uint32_t s = 0; s < G.S; ++s)
+    for (uint32_t li = 0; li < G.Pl; ++li) {
+      PmPart d = G.es[s]->parts[G.lp[li]].d;
+      d.qv = G.qv.empty() ? nullptr : G.qv[s];
+      v[(size_t)s * G.Pl + li] = d;
+    }
+  HIPCHK(hipMemcpyAsync(G.parts_d.p, v, np * sizeof(PmPart), hipMemcpyHostToDevice, st));
+  HIPCHK(hipEventRecord(ev, st));
+  G.gen.resize(G.S);
+  for (uint32_t s = 0; s < G.S; ++s) G.gen[s] = G.es[s]->prep_gen;
+  return 0;
+}
 
 static int drl_team_init(DrlTeam& T, pm_graph** gs, uint32_t S, uint32_t s0, const float* queries, uint64_t q, int k,
                          int step, int parallel, const DrlShape& sh) {
@@ -4288,7 +4334,13 @@ static int run_batched_dev(pm_graph** gs, uint32_t S, const float* queries, uint
     CHK(drl_team_init(*teams.back(), gs + s0, s1 - s0, s0, queries, q, k, step, parallel, sh));
     swaps[g].swap_in(teams.back()->G.c, team_stream(teams.back()->G.c->device, g));
   }
-  DevBuf prep_buf;
+  // Maintenance launch sets, timed by events around them on the leader's stream
+  struct PrepSet { hipEvent_t a = nullptr, b = nullptr; std::vector<std::pair<DrlTeam*, uint32_t>> members; };
+  std::vector<PrepSet> sets;
+  struct SetsRelease {
+    std::vector<PrepSet>& v;
+    ~SetsRelease() { for (auto& x : v) { if (x.a) (void)hipEventDestroy(x.a); if (x.b) (void)hipEventDestroy(x.b); } }
+  } sets_release{sets};
   for (uint64_t qi = 0; qi < q; ++qi) {
     CHK(drl_query_all(teams, sh, qi, q, step));
     // the harness's maintenance trigger (private-search.go:226-232) per session:
@@ -4306,18 +4358,46 @@ static int run_batched_dev(pm_graph** gs, uint32_t S, const float* queries, uint
       if (any) involved.push_back(t.get());
     }
     if (who.empty()) continue;
-    for (DrlTeam* t : involved) HIPCHK(hipStreamSynchronize(t->G.c->stream));   // the query's rounds are done
-    CHK(prep_clients(involved[0]->G.c, prep_buf, involved[0]->G.lp, who, &mts));
+    // ONE launch set of every triggered client, on the first involved team's
+    // stream after every involved team's query; nothing on the host waits for
+    // it (the other teams keep running what is queued), and the involved
+    // teams' next rounds wait for it on the device
+    DrlTeam* L = involved[0];
+    hipStream_t sl = L->G.c->stream;
+    for (DrlTeam* t : involved)
+      if (t != L) {
+        HIPCHK(hipEventRecord(t->ev_end, t->G.c->stream));
+        HIPCHK(hipStreamWaitEvent(sl, t->ev_end, 0));
+      }
+    sets.emplace_back();
+    PrepSet& ps = sets.back();
+    HIPCHK(hipEventCreate(&ps.a));
+    HIPCHK(hipEventCreate(&ps.b));
+    HIPCHK(hipEventRecord(ps.a, sl));
+    CHK(prep_clients(L->G.c, L->prep_buf, L->G.lp, who, nullptr, &L->prep_stage, &L->prep_stage_ev));
     for (DrlTeam* t : involved) {   // the new keys into the team's parts; the emptied localCache indexes
-      CHK(group_upload_parts(t->G));
+      CHK(group_upload_parts_async(t->G, sl, t->parts_stage, t->parts_stage_ev));
       for (uint32_t i = 0; i < t->S; ++i)
-        if (t->need[i]) CHK(ensure_dev_cache(&t->gs[i]->pir->e, sh.cmask, t->G.c->stream));
+        if (t->need[i]) {
+          CHK(ensure_dev_cache(&t->gs[i]->pir->e, sh.cmask, sl));
+          ps.members.emplace_back(t, i);
+        }
+    }
+    HIPCHK(hipEventRecord(ps.b, sl));
+    for (DrlTeam* t : involved)
+      if (t != L) HIPCHK(hipStreamWaitEvent(t->G.c->stream, ps.b, 0));
+  }
+  for (auto& t : teams) CHK(drl_team_finish(*t, q, k, answers));
+  for (PrepSet& ps : sets) {   // each triggered client's maintenance time: its launch set's span on the GPU
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, ps.a, ps.b));
+    for (auto& [t, i] : ps.members) {
+      t->mt[i] += ms / 1e3;
+      record_stats(&t->gs[i]->pir->e, ms / 1e3);   // PreprocessingTime: the set's GPU span
     }
   }
-  for (auto& t : teams) {
-    CHK(drl_team_finish(*t, q, k, answers));
+  for (auto& t : teams)
     for (uint32_t i = 0; i < t->S; ++i) mt_out[t->s0 + i] = t->mt[i];
-  }
   return 0;
 }
 
