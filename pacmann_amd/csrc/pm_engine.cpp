@@ -2670,7 +2670,13 @@ static void group_stage_session(StepGroup& G, uint32_t s) {
 // search + resolution (k_match_resolve_s where the shapes hold), the split
 // gather for wide sets, the answer; the completion event unless the records
 // go to a combine.  (group_step; the device loop's steps, run_batched_dev.)
-static int group_step_launch(StepGroup& G, PmStep& S, uint32_t max_per_part, uint32_t nreal, double ans_bytes) {
+// ans_st (device loop, PM_ANSWER_STREAM): the answer runs on that stream, one
+// shared by every team, between two events (after this step's match + resolve,
+// before the team's next kernel): the teams' answers, which all read HBM, run
+// one at a time at the full gather rate while the teams' latency-bound chain
+// kernels run beside them.
+static int group_step_launch(StepGroup& G, PmStep& S, uint32_t max_per_part, uint32_t nreal, double ans_bytes,
+                             hipStream_t ans_st = nullptr, hipEvent_t* ans_ev = nullptr) {
   pm_ctx* c = G.c;
   hipStream_t st = c->stream;
   const uint32_t nsub = S.nsub, np = S.np;
@@ -2734,7 +2740,15 @@ static int group_step_launch(StepGroup& G, PmStep& S, uint32_t max_per_part, uin
     S.stamps = G.stamps.as<uint64_t>();
   }
 #endif
-  c->timed_ext("answer", S.nsplit > 1 ? 0 : ans_bytes, [&](pmk::PmEvents ev) { pmk::step_answer(st, S, G.maxSS, ev); }, 2);
+  if (ans_st) {
+    HIPCHK(hipEventRecord(ans_ev[0], st));
+    HIPCHK(hipStreamWaitEvent(ans_st, ans_ev[0], 0));
+    c->timed_ext("answer", S.nsplit > 1 ? 0 : ans_bytes, [&](pmk::PmEvents ev) { pmk::step_answer(ans_st, S, G.maxSS, ev); }, 2);
+    HIPCHK(hipEventRecord(ans_ev[1], ans_st));
+    HIPCHK(hipStreamWaitEvent(st, ans_ev[1], 0));
+  } else {
+    c->timed_ext("answer", S.nsplit > 1 ? 0 : ans_bytes, [&](pmk::PmEvents ev) { pmk::step_answer(st, S, G.maxSS, ev); }, 2);
+  }
   if (!G.comb) G.seq = c->record_done(st);   // sharded: group_exchange publishes the records
   HIPCHK(hipGetLastError());
 #ifdef PM_ANSWER_STAMPS
@@ -2925,8 +2939,8 @@ static void prefetch_session(StepGroup& G, uint32_t s, const pm_graph* g) {
   for (uint32_t j = 0; j < n; j += 2) __builtin_prefetch(hdr + j);
   for (uint32_t j = 0; j < n; ++j)
     for (uint32_t w = G.pf_w0; w < G.pf_w1; w += 8) __builtin_prefetch(rows + ((size_t)j * G.E + w) * 8);
-  for (uint32_t j = 0; j < n; ++j)
-    if (e->subs[j].kind == SUB_REAL) e->parts[e->subs[j].part].cache.prefetch(e->subs[j].idx);
+  // (not its localCache slots: that session's collect may be rehashing its
+  // FlatMap on another worker right now; group_collect prefetches them itself)
   if (g->graph)
     for (size_t b = 0; b < g->batch.size(); ++b) __builtin_prefetch(&g->graph[(uint64_t)g->batch[b] * g->m]);
 }
@@ -3116,34 +3130,57 @@ static int gvi_pre_sharded(pm_graph* g, StepGroup& G, uint32_t s, bool* fast) {
 static int group_exchange(StepGroup& G, const std::vector<char>& in, bool poison) {
   pm_ctx* c = G.c;
   hipStream_t st = c->stream;
-  const uint32_t nrec = G.S * G.npos, nsub = poison ? 0u : G.nsub;
+  const uint32_t nrec = G.S * G.npos;
   const uint64_t nw = (uint64_t)nrec * G.W;
-  int32_t* map = G.map_h.as<int32_t>();
-  for (uint32_t s = 0; s < G.S; ++s)   // client-local sub-query indices -> the shared step's
-    for (uint32_t i = 0; i < G.npos; ++i) {
-      int32_t& v = map[(uint64_t)s * G.npos + i];
-      if (poison) v = -1;
-      else if (v >= 0) v = in[s] ? v + (int32_t)G.base[s] : -1;
-    }
-  HIPCHK(hipMemcpyAsync(G.map_d.p, map, (uint64_t)nrec * 4, hipMemcpyHostToDevice, st));
   uint32_t* st2 = G.st_d.as<uint32_t>();
-  const PmOutHdr* hdr = G.out_d.as<PmOutHdr>();
-  const uint64_t* rows = (const uint64_t*)(G.out_d.as<char>() + (uint64_t)G.nsub * sizeof(PmOutHdr));
-  c->timed("pack_records", (double)nw * 8, [&] {
-    pmk::pack_records(st, G.map_d.as<int32_t>(), nrec, hdr, rows, G.E, G.w0, G.W, G.rec_d, nsub, st2,
-                      poison ? 1u : 0u); });
-  for (uint32_t s = 0; s < G.S && !poison; ++s)
-    if (G.slow[s])
-      HIPCHK(hipMemcpyAsync(G.rec_d + (uint64_t)s * G.npos * G.W, G.slow_h.as<uint64_t>() + (uint64_t)s * G.npos * G.W,
-                            (uint64_t)G.npos * G.W * 8, hipMemcpyHostToDevice, st));
-  if (G.comb->model_peers && !poison) {
-    HIPCHK(hipMemcpyAsync(G.ids_d.p, G.ids_h.p, (uint64_t)nrec * 8, hipMemcpyHostToDevice, st));
-    const pm_graph* g0 = G.gs[0];
-    c->timed("synth_records", 0, [&] {
-      pmk::synth_records(st, G.map_d.as<int32_t>(), G.ids_d.as<uint64_t>(), nrec, G.npos, G.qbuf.as<float>(), G.dim,
-                         (uint32_t)g0->m, g0->n, g0->data_seed, G.w0, G.W, G.rec_d); });
+  uint32_t nsub = poison ? 0u : G.nsub;
+  // this rank's records (map, pack, multi-step sessions, modelled peers)
+  auto pack = [&]() -> int {
+    int32_t* map = G.map_h.as<int32_t>();
+    for (uint32_t s = 0; s < G.S; ++s)   // client-local sub-query indices -> the shared step's
+      for (uint32_t i = 0; i < G.npos; ++i) {
+        int32_t& v = map[(uint64_t)s * G.npos + i];
+        if (poison) v = -1;
+        else if (v >= 0) v = in[s] ? v + (int32_t)G.base[s] : -1;
+      }
+    HIPCHK(hipMemcpyAsync(G.map_d.p, map, (uint64_t)nrec * 4, hipMemcpyHostToDevice, st));
+    const PmOutHdr* hdr = G.out_d.as<PmOutHdr>();
+    const uint64_t* rows = (const uint64_t*)(G.out_d.as<char>() + (uint64_t)G.nsub * sizeof(PmOutHdr));
+    c->timed("pack_records", (double)nw * 8, [&] {
+      pmk::pack_records(st, G.map_d.as<int32_t>(), nrec, hdr, rows, G.E, G.w0, G.W, G.rec_d, nsub, st2,
+                        poison ? 1u : 0u); });
+    for (uint32_t s = 0; s < G.S && !poison; ++s)
+      if (G.slow[s])
+        HIPCHK(hipMemcpyAsync(G.rec_d + (uint64_t)s * G.npos * G.W, G.slow_h.as<uint64_t>() + (uint64_t)s * G.npos * G.W,
+                              (uint64_t)G.npos * G.W * 8, hipMemcpyHostToDevice, st));
+    if (G.comb->model_peers && !poison) {
+      HIPCHK(hipMemcpyAsync(G.ids_d.p, G.ids_h.p, (uint64_t)nrec * 8, hipMemcpyHostToDevice, st));
+      const pm_graph* g0 = G.gs[0];
+      c->timed("synth_records", 0, [&] {
+        pmk::synth_records(st, G.map_d.as<int32_t>(), G.ids_d.as<uint64_t>(), nrec, G.npos, G.qbuf.as<float>(), G.dim,
+                           (uint32_t)g0->m, g0->n, g0->data_seed, G.w0, G.W, G.rec_d); });
+    }
+    HIPCHK(hipGetLastError());
+    return 0;
+  };
+  const int pre = pack();
+  std::string pre_msg;
+  if (pre) {
+    // a failure before the collective: the turn is still owed to the peers.
+    // Take it poisoned (zero records, error word 1) if the device still
+    // accepts work; otherwise no further turn can match the peers' (they are
+    // then bounded by their own RCCL / torch.distributed timeout).
+    pre_msg = pm_last_error();
+    poison = true;
+    nsub = 0;
+    const uint64_t one = 1;
+    if (!G.comb->fn || hipMemsetAsync(G.rec_d, 0, nw * 8, st) != hipSuccess ||
+        hipMemcpyAsync(G.rec_d + nw, &one, 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) {
+      G.combine_dead = true;
+      return fail(pre, pre_msg);
+    }
   }
-  HIPCHK(hipGetLastError());
   if (G.comb->fn) {   // the collective, in the global (round, team) order on every rank
     ShardComb* cb = G.comb;
     const uint64_t turn = G.round * cb->NG + G.team;
@@ -3171,6 +3208,7 @@ static int group_exchange(StepGroup& G, const std::vector<char>& in, bool poison
       G.combine_dead = true;
       return fail(PM_EHIP, "sharded search: the combine callback failed (" + std::to_string(rc) + ")");
     }
+    if (pre) { G.peer_failed.store(true); return fail(pre, pre_msg); }   // the turn taken poisoned; this team stops
   } else {
     G.round++;
   }
@@ -3687,8 +3725,14 @@ static int run_batched_pool(pm_graph** gs, uint32_t S, const float* queries, uin
   // Q.  The maintenance kernels fill the GPU, so teams' maintenances run one
   // after another either way; merged, the teams also resume together instead
   // of finishing the timed work one after another with the GPU partly idle.
-  // PM_PREP_WAIT_MS=0: each team alone.
-  static const double prep_wait = [] { const char* e = getenv("PM_PREP_WAIT_MS"); return e ? atof(e) : 1.0; }();
+  // PM_PREP_MERGE=0 (or the former name PM_PREP_WAIT_MS=0): each team's
+  // maintenance alone, when it reaches it; otherwise merged as above.  (Not a
+  // time: a team waits for the others' query Q only, never longer.)
+  static const double prep_wait = [] {
+    const char* e = getenv("PM_PREP_MERGE");
+    if (!e) e = getenv("PM_PREP_WAIT_MS");
+    return e ? atof(e) : 1.0;
+  }();
   struct Release {
     std::vector<std::unique_ptr<PoolTeam>>& t;
     ~Release() { for (auto& x : t) team_release(x->gs, x->S); }
@@ -4051,6 +4095,8 @@ struct DrlTeam {
       step_bytes, step_real, stamps;
   DrlArgs A{};
   hipEvent_t ev_end = nullptr;
+  hipStream_t ans_st = nullptr;                  // the shared answer stream (null: the team's own)
+  hipEvent_t ans_ev[2] = {};
   HostBuf prep_stage, parts_stage;               // pinned stages of the asynchronous maintenance (run_batched_dev)
   hipEvent_t prep_stage_ev = nullptr, parts_stage_ev = nullptr;
   DevBuf prep_buf;
@@ -4059,7 +4105,7 @@ struct DrlTeam {
   std::vector<char> need;
   std::vector<double> mt;
   ~DrlTeam() {
-    for (hipEvent_t e : {ev_end, prep_stage_ev, parts_stage_ev})
+    for (hipEvent_t e : {ev_end, prep_stage_ev, parts_stage_ev, ans_ev[0], ans_ev[1]})
       if (e) (void)hipEventDestroy(e);
   }
 };
@@ -4211,7 +4257,7 @@ static int drl_step(DrlTeam& T, const DrlShape& sh) {
   // bytes: every sub-query answered (patched with the round's exact count in timing runs)
   double ans_bytes = 0;
   for (uint32_t li = 0; li < G.Pl; ++li) ans_bytes += answer_bytes(e0->parts[G.lp[li]].d, G.E) * sh.qn * T.S;
-  CHK(group_step_launch(G, S, sh.qn, T.nsub, ans_bytes));
+  CHK(group_step_launch(G, S, sh.qn, T.nsub, ans_bytes, T.ans_st, T.ans_ev));
   for (size_t i = before; i < c->launches.size(); ++i)
     if (c->launches[i].name == "answer" || c->launches[i].name == "match_resolve" || c->launches[i].name == "hint_match")
       T.tl.emplace_back(i, T.seq);
@@ -4334,6 +4380,14 @@ static int run_batched_dev(pm_graph** gs, uint32_t S, const float* queries, uint
     CHK(drl_team_init(*teams.back(), gs + s0, s1 - s0, s0, queries, q, k, step, parallel, sh));
     swaps[g].swap_in(teams.back()->G.c, team_stream(teams.back()->G.c->device, g));
   }
+  static const int ans_stream = [] { const char* e = getenv("PM_ANSWER_STREAM"); return e ? atoi(e) : 0; }();
+  if (ans_stream && NG > 1) {   // the last stream of the pool (created first-to-last: its own hardware queue)
+    hipStream_t as = team_stream(teams[0]->G.c->device, 7);
+    for (auto& t : teams) {
+      t->ans_st = as;
+      for (auto& e : t->ans_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+  }
   // Maintenance launch sets, timed by events around them on the leader's stream
   struct PrepSet { hipEvent_t a = nullptr, b = nullptr; std::vector<std::pair<DrlTeam*, uint32_t>> members; };
   std::vector<PrepSet> sets;
@@ -4387,6 +4441,7 @@ static int run_batched_dev(pm_graph** gs, uint32_t S, const float* queries, uint
     for (DrlTeam* t : involved)
       if (t != L) HIPCHK(hipStreamWaitEvent(t->G.c->stream, ps.b, 0));
   }
+  if (!teams.empty() && teams[0]->ans_st) HIPCHK(hipStreamSynchronize(teams[0]->ans_st));
   for (auto& t : teams) CHK(drl_team_finish(*t, q, k, answers));
   for (PrepSet& ps : sets) {   // each triggered client's maintenance time: its launch set's span on the GPU
     float ms = 0;
