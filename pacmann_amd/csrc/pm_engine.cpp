@@ -4617,12 +4617,16 @@ extern "C" int pm_rccl_unique_id(uint8_t id[PM_RCCL_ID_BYTES]) {
   return 0;
 }
 
-// The teams' communicators, created nonblocking (ncclCommInitRankConfig with
-// config.blocking = 0) and polled to completion within rccl_timeout_s(); on an
-// error or the bound every communicator made so far is aborted, so a rank
-// whose peer failed (never joined) gets a status instead of a hang.  An RCCL
-// without the nonblocking entry points is initialised blocking on a watched
-// helper thread, with the same bound.
+// The teams' communicators, created within rccl_timeout_s(): the blocking
+// init runs on a helper thread the caller waits for with that bound, so a
+// rank whose peer failed (never joined) gets PM_ETIMEDOUT instead of a hang
+// (the helper stays blocked in RCCL and its handle is leaked, never used).
+// PM_RCCL_NONBLOCKING=1: ncclCommInitRankConfig with blocking = 0, polled, and
+// aborted on an error or the bound.
+static bool rccl_debug() {
+  static const bool on = [] { const char* e = getenv("PM_RCCL_DEBUG"); return e && e[0] == '1'; }();
+  return on;
+}
 extern "C" int pm_rccl_create(int device, int nranks, int rank, const uint8_t* ids, uint32_t nteams, pm_rccl** out) {
   if (!ids || !out || nteams == 0 || nranks < 1 || rank < 0 || rank >= nranks) return fail(PM_EINVAL, "bad argument");
   *out = nullptr;
@@ -4635,7 +4639,13 @@ extern "C" int pm_rccl_create(int device, int nranks, int rank, const uint8_t* i
   r->device = device; r->nranks = nranks; r->rank = rank;
   r->comms.assign(nteams, nullptr);
   const double limit = rccl_timeout_s();
-  if (a.nonblocking()) {
+  if (rccl_debug()) fprintf(stderr, "[pm] rccl_create rank %d/%d teams %u nonblocking %d\n", rank, nranks, nteams, (int)a.nonblocking());
+  // The nonblocking form (ncclCommInitRankConfig, blocking = 0) is opt-in
+  // (PM_RCCL_NONBLOCKING=1): with the RCCL torch ships (2.26.6) polling a
+  // nonblocking communicator's state did not return on the GPU box; the
+  // default is the blocking init on a watched helper thread.
+  static const bool want_nb = [] { const char* e = getenv("PM_RCCL_NONBLOCKING"); return e && e[0] == '1'; }();
+  if (want_nb && a.nonblocking()) {
     r->nonblocking = true;
     for (uint32_t t = 0; t < nteams; ++t) {   // every rank issues the teams' inits in the same order
       ncclUniqueId u;
@@ -4648,6 +4658,7 @@ extern "C" int pm_rccl_create(int device, int nranks, int rank, const uint8_t* i
         return fail(PM_EHIP, std::string("ncclCommInitRankConfig: ") + a.error_string(res));
       }
     }
+    if (rccl_debug()) fprintf(stderr, "[pm] rccl_create: inits issued\n");
     const auto t0 = Clock::now();
     for (uint32_t t = 0; t < nteams; ++t) {
       const double left = limit - std::chrono::duration<double>(Clock::now() - t0).count();
@@ -4731,10 +4742,12 @@ extern "C" int pm_rccl_probe(pm_rccl* r) {
   struct Stream { hipStream_t s; ~Stream() { (void)hipStreamDestroy(s); } } guard{st};
   HIPCHK(hipMemcpyAsync(buf.p, one.data(), nt * 8, hipMemcpyHostToDevice, st));
   const double limit = rccl_timeout_s();
+  if (rccl_debug()) fprintf(stderr, "[pm] rccl_probe: %u teams\n", nt);
   for (uint32_t t = 0; t < nt; ++t) {
     const int rc = pm_rccl_combine(r, t, buf.as<uint64_t>() + t, 1, st);
     if (rc) { r->abort_all(); return rc; }
   }
+  if (rccl_debug()) fprintf(stderr, "[pm] rccl_probe: all-reduces issued\n");
   const auto t0 = Clock::now();
   for (;;) {
     const hipError_t e = hipStreamQuery(st);

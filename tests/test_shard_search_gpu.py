@@ -104,6 +104,10 @@ def _run(world, backend, oracle):
     import torch.multiprocessing as mp
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_rank, args=(world, _free_port(), d, backend), nprocs=world, join=True)
+        for r in range(world):   # a rank whose loop raised left its message instead of its answers
+            e = os.path.join(d, f"err{r}.txt")
+            if os.path.exists(e):
+                pytest.fail(f"rank {r}: {open(e).read()}")
         ans = [np.load(os.path.join(d, f"ans{r}.npy")) for r in range(world)]
         st = [np.load(os.path.join(d, f"st{r}.npy")) for r in range(world)]
     for r in range(1, world):   # every rank continued the identical searches
