@@ -38,6 +38,9 @@
 namespace pm {
 
 constexpr int kAnsBlock = 512;
+#ifndef PM_ANSWER_NTLOAD
+#define PM_ANSWER_NTLOAD 0   // k_answer_p's row gather with nontemporal loads (streamed past the caches)
+#endif
 #ifndef PM_ANSWER_KG
 #define PM_ANSWER_KG 6   // k_answer gather: rows per thread in flight together (no VGPR spill at 8 waves;
                          // alone 76.0-76.7 us vs 77.3 at 8 and 81-82 at 10, which spills 9 VGPRs)
@@ -2224,8 +2227,13 @@ struct AnsGather {   // one thread's share of a sub-query's XOR gather (HOT LOOP
       x[u] = u64x2{0, 0};
       if (rr[u] < P.N) {
         const PM_G uint64_t* q = base + (uint64_t)rr[u] * S.E + (uint64_t)seg * W;
+#if PM_ANSWER_NTLOAD
+        if (W == 2) x[u] = __builtin_nontemporal_load(reinterpret_cast<const PM_G u64x2*>(q));
+        else x[u].x = __builtin_nontemporal_load(q);
+#else
         if (W == 2) x[u] = *reinterpret_cast<const PM_G u64x2*>(q);
         else x[u].x = *q;
+#endif
       }
     }
   }
@@ -2329,79 +2337,101 @@ __device__ __forceinline__ void ansp_epilogue(const PmStep& S, const AnsQ& a, LD
   }
   __syncthreads();   // row and red are the next sub-query's
 }
+template <int W, int NT>
+__device__ __forceinline__ void ansp_record(const PmStep& S, uint32_t s, AnsQ& a, uint4& qpv) {
+  const uint32_t tid = threadIdx.x;
+  a.s = s;
+  const PmSub sub = step_sub(S, s);
+  a.part = sub.part;
+  a.idx = sub.idx;
+  a.r = S.res[s];
+  qpv = make_uint4(0, 0, 0, 0);
+  if (tid < S.qw / 8) qpv = *reinterpret_cast<const PM_G uint4*>(S.qset + (uint64_t)s * S.qw + 8 * tid);
+  const PmPart& P = S.parts[a.part];
+  const float* const qq = P.qv ? P.qv : S.q;
+  a.q0 = a.q1 = 0.0f;
+  if (qq && S.dim <= 2 * NT) {
+    if (tid < S.dim) a.q0 = qq[tid];
+    if (tid + NT < S.dim) a.q1 = qq[tid + NT];
+  }
+}
+__device__ __forceinline__ bool ansp_gathers(const AnsQ& a) {
+  return a.mode == A_FINAL || a.mode == A_CHAINED || a.mode == A_DUMMY;
+}
+// A workgroup owns sub-queries s_k = blockIdx.x + k * gridDim.x (grid =
+// nsub / PM_ANSWER_PK on the host, 2 by default) in two operand slots: while
+// slot c gathers, slot c ^ 1 holds the next sub-query's record and query set;
+// the next one's first row batch is issued before slot c's reduction, decode
+// and publication, and slot c is refilled (record + query set of s_{k+2})
+// while that batch is in flight.
+template <int W, int NT, int KG, int C>
+__device__ __forceinline__ bool ansp_turn(const PmStep& S, AnswerPLds<NT>& L, AnsQ (&q)[2], uint4 (&qpv)[2],
+                                          AnsGather<W, NT, KG> (&g)[2], uint32_t k, bool first) {
+  constexpr int N = C ^ 1;
+  const uint32_t ns = S.nsub, G = gridDim.x;
+  const bool hasN = blockIdx.x + (k + 1) * G < ns;
+  if (ansp_gathers(q[C])) {
+    const PmPart& P = S.parts[q[C].part];
+    const uint32_t nb = g[C].batches(P);
+    uint32_t b = 0;
+    if (!first) { g[C].fold(); b = 1; }   // batch 0 was issued under the previous turn's epilogue
+    for (; b < nb; ++b) {
+      g[C].load(S, P, L.qo[C], b);
+      g[C].fold();
+    }
+  }
+  const bool gathN = hasN && ansp_gathers(q[N]);
+  if (gathN) {
+    g[N].a0 = g[N].a1 = 0;
+    g[N].load(S, S.parts[q[N].part], L.qo[N], 0);
+  }
+  if (ansp_gathers(q[C])) g[C].reduce(L, S.E);
+  ansp_epilogue<W, NT>(S, q[C], L);   // ends with a barrier: L.qo[C] is free
+  if (!hasN) return false;
+  if (blockIdx.x + (k + 2) * G < ns) {
+    ansp_record<W, NT>(S, blockIdx.x + (k + 2) * G, q[C], qpv[C]);
+    q[C].mode = answer_mode(q[C].r);
+    ansp_set(S, q[C], qpv[C], L.qo[C]);
+    __syncthreads();   // L.qo[C] is read by the next turn's first batch of it
+  }
+  ansp_decode_ops<W, NT>(S, q[N]);
+  return true;
+}
+#ifndef PM_ANSWER_PK_MAX
+#define PM_ANSWER_PK_MAX 2   // sub-queries per k_answer_p workgroup the kernel is built for (the host's PM_ANSWER_PK is
+                             // clamped to it); 3 spills ~150 VGPRs at 80
+#endif
 #ifndef PM_ANSWER_P_WAVES
-#define PM_ANSWER_P_WAVES 6   // min waves per SIMD: <= 80 VGPRs (B's row batch stays live through A's epilogue);
-                              // 12 two-wave workgroups per CU = the 3,072 of a 6,144-sub-query step, all resident
+#define PM_ANSWER_P_WAVES 6   // min waves per SIMD: <= 80 VGPRs (the next sub-query's row batch stays live through
+                              // an epilogue); 12 two-wave workgroups per CU = the 3,072 of a 6,144-sub-query step
 #endif
 template <int W, int NT>
 __global__ void __launch_bounds__(NT, PM_ANSWER_P_WAVES) k_answer_p(PmStep S) {
   __shared__ AnswerPLds<NT> L;
   constexpr int KG = PM_ANSWER_KG;
-  const uint32_t tid = threadIdx.x;
   AnsQ q[2];
   uint4 qpv[2];
-  const uint32_t ns = S.nsub;
-  const bool hasB = blockIdx.x + gridDim.x < ns;
-  // ---- prologue: both records, both query sets and A's query vector, one round trip
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    q[k].s = blockIdx.x + k * gridDim.x;
-    const uint32_t sk = k == 0 || hasB ? q[k].s : q[0].s;
-    const PmSub sub = step_sub(S, sk);
-    q[k].part = sub.part;
-    q[k].idx = sub.idx;
-    q[k].r = S.res[sk];
-    qpv[k] = make_uint4(0, 0, 0, 0);
-    if (tid < S.qw / 8) qpv[k] = *reinterpret_cast<const PM_G uint4*>(S.qset + (uint64_t)sk * S.qw + 8 * tid);
-  }
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const PmPart& P = S.parts[q[k].part];
-    const float* const qq = P.qv ? P.qv : S.q;
-    q[k].q0 = q[k].q1 = 0.0f;
-    if (qq && S.dim <= 2 * NT) {
-      if (tid < S.dim) q[k].q0 = qq[tid];
-      if (tid + NT < S.dim) q[k].q1 = qq[tid + NT];
-    }
-  }
+  const uint32_t ns = S.nsub, G = gridDim.x;
+  const bool has1 = blockIdx.x + G < ns;
+  // ---- prologue: the first two records and query sets, one round trip
+  ansp_record<W, NT>(S, blockIdx.x, q[0], qpv[0]);
+  ansp_record<W, NT>(S, has1 ? blockIdx.x + G : blockIdx.x, q[1], qpv[1]);
   q[0].mode = answer_mode(q[0].r);
   q[1].mode = answer_mode(q[1].r);
   ansp_decode_ops<W, NT>(S, q[0]);
   ansp_set(S, q[0], qpv[0], L.qo[0]);
-  if (hasB) ansp_set(S, q[1], qpv[1], L.qo[1]);
+  if (has1) ansp_set(S, q[1], qpv[1], L.qo[1]);
   __syncthreads();
-  // ---- A's gather
-  AnsGather<W, NT, KG> gA;
-  gA.init(S.E);
-  const bool gathA = q[0].mode == A_FINAL || q[0].mode == A_CHAINED || q[0].mode == A_DUMMY;
-  const bool gathB = hasB && (q[1].mode == A_FINAL || q[1].mode == A_CHAINED || q[1].mode == A_DUMMY);
-  if (gathA) {
-    const PmPart& P = S.parts[q[0].part];
-    const uint32_t nb = gA.batches(P);
-    for (uint32_t b = 0; b < nb; ++b) {
-      gA.load(S, P, L.qo[0], b);
-      gA.fold();
-    }
-  }
-  // ---- B's first row batch in flight, then A's epilogue under it
-  AnsGather<W, NT, KG> gB;
-  gB.init(S.E);
-  if (gathB) gB.load(S, S.parts[q[1].part], L.qo[1], 0);
-  if (gathA) gA.reduce(L, S.E);
-  ansp_epilogue<W, NT>(S, q[0], L);
-  if (!hasB) return;
-  ansp_decode_ops<W, NT>(S, q[1]);
-  if (gathB) {
-    const PmPart& P = S.parts[q[1].part];
-    gB.fold();
-    const uint32_t nb = gB.batches(P);
-    for (uint32_t b = 1; b < nb; ++b) {
-      gB.load(S, P, L.qo[1], b);
-      gB.fold();
-    }
-    gB.reduce(L, S.E);
-  }
-  ansp_epilogue<W, NT>(S, q[1], L);
+  AnsGather<W, NT, KG> g[2];
+  g[0].init(S.E);
+  g[1].init(S.E);
+  // straight-line turns (a loop keeps every slot's state live across its
+  // back edge and spills): at most PM_ANSWER_PK_MAX sub-queries per workgroup
+  static_assert(PM_ANSWER_PK_MAX >= 2 && PM_ANSWER_PK_MAX <= 4, "k_answer_p turns");
+  if (!ansp_turn<W, NT, KG, 0>(S, L, q, qpv, g, 0, true)) return;
+  if (!ansp_turn<W, NT, KG, 1>(S, L, q, qpv, g, 1, false)) return;
+  if (PM_ANSWER_PK_MAX > 2 && !ansp_turn<W, NT, KG, 0>(S, L, q, qpv, g, 2, false)) return;
+  if (PM_ANSWER_PK_MAX > 3) ansp_turn<W, NT, KG, 1>(S, L, q, qpv, g, 3, false);
 }
 
 // ---- k_gather: the server's XOR gather of wide sets, split ----------------
@@ -2680,7 +2710,10 @@ void step_answer(hipStream_t st, const PmStep& S, uint32_t maxSS, PmEvents ev) {
   static_assert(2u * kAnsPNT >= kSmallE, "k_answer_p's gather slices must cover a kSmallE row");
   if (pair && S.qset && S.nsplit <= 1 && maxSS <= kSmallSS && S.E % 2 == 0 && S.E <= kSmallE &&
       (S.E & ~3u) <= 2u * kAnsPNT && S.nsub >= 2 * 256) {
-    PM_LAUNCH(ev, (k_answer_p<2, kAnsPNT>), dim3((S.nsub + 1) / 2), dim3(kAnsPNT), st, S);
+    // sub-queries per workgroup (the grid is nsub / pk; 2: every workgroup of a
+    // 6,144-sub-query step resident at once)
+    static const uint32_t pk = [] { const char* e = getenv("PM_ANSWER_PK"); return e && atoi(e) > 1 ? std::min((uint32_t)atoi(e), (uint32_t)PM_ANSWER_PK_MAX) : 2u; }();
+    PM_LAUNCH(ev, (k_answer_p<2, kAnsPNT>), dim3((S.nsub + pk - 1) / pk), dim3(kAnsPNT), st, S);
     return;
   }
   if (nt && S.nsplit <= 1 && maxSS <= kSmallSS && S.E <= kSmallE) {

@@ -5,6 +5,8 @@
 //   W  whole sub-query staged by LDS-DMA (79 KB), then XORed
 // Each prints the average kernel time over its launches and the result hash.
 //   hipcc -O3 --offload-arch=gfx950 -o build/gather_bench tools/gather_bench.hip
+//   build/gather_bench [sub-queries] [table copies]: copies > 1 spreads the rows over
+//   that many 640 MB tables (16 copies = 10 GB: the Infinity Cache holds ~2.5 % of it)
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
@@ -18,17 +20,18 @@ typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
 constexpr uint32_t E = 80, SS = 124, CS = 512, PS = 62500, NPART = 16;
 constexpr uint64_t NROWS = 1000000;
+static uint32_t g_copies = 1;   // argv[2]: the table is this many 640 MB copies; sub-query s reads copy (s / NPART) % copies
 constexpr uint32_t SEGS = E / 2;   // 16-B pieces per row
 
 template <int NT, int KG, bool NTL = false>
 __global__ void __launch_bounds__(NT) k_reg(const uint64_t* __restrict__ db, const uint16_t* __restrict__ offs,
-                                            uint64_t* __restrict__ out) {
+                                            uint64_t* __restrict__ out, uint32_t copies) {
   __shared__ uint16_t qo[SS];
   __shared__ u64x2 red[NT];
   const uint32_t s = blockIdx.x, tid = threadIdx.x, p = s % NPART;
   for (uint32_t i = tid; i < SS; i += NT) qo[i] = offs[(uint64_t)s * SS + i];
   __syncthreads();
-  const uint64_t* base = db + (uint64_t)p * PS * E;
+  const uint64_t* base = db + ((uint64_t)(s / NPART % copies) * NROWS + (uint64_t)p * PS) * E;
   const uint32_t nsl = NT / SEGS, sl = tid / SEGS, seg = tid % SEGS;
   u64x2 a = {0, 0};
   if (sl < nsl) {
@@ -59,12 +62,62 @@ __global__ void __launch_bounds__(NT) k_reg(const uint64_t* __restrict__ db, con
   }
 }
 
+// k_reg with the next batch in flight while the current one folds (2 x KG rows per lane)
+template <int NT, int KG>
+__global__ void __launch_bounds__(NT) k_regp(const uint64_t* __restrict__ db, const uint16_t* __restrict__ offs,
+                                             uint64_t* __restrict__ out, uint32_t copies) {
+  __shared__ uint16_t qo[SS];
+  __shared__ u64x2 red[NT];
+  const uint32_t s = blockIdx.x, tid = threadIdx.x, p = s % NPART;
+  for (uint32_t i = tid; i < SS; i += NT) qo[i] = offs[(uint64_t)s * SS + i];
+  __syncthreads();
+  const uint64_t* base = db + ((uint64_t)(s / NPART % copies) * NROWS + (uint64_t)p * PS) * E;
+  const uint32_t nsl = NT / SEGS, sl = tid / SEGS, seg = tid % SEGS;
+  u64x2 a = {0, 0};
+  auto ld = [&](uint32_t i0, u64x2* x) {
+#pragma unroll
+    for (int u = 0; u < KG; ++u) {
+      const uint32_t i = i0 + u * nsl;
+      const uint32_t r = i < SS ? i * CS + qo[i] : ~0u;
+      x[u] = u64x2{0, 0};
+      if (r < PS) x[u] = *reinterpret_cast<const u64x2*>(base + (uint64_t)r * E + seg * 2);
+    }
+  };
+  if (sl < nsl) {
+    u64x2 x[KG], y[KG];
+    uint32_t i0 = sl;
+    ld(i0, x);
+    for (;;) {
+      const uint32_t i1 = i0 + KG * nsl;
+      if (i1 >= SS) {
+#pragma unroll
+        for (int u = 0; u < KG; ++u) a ^= x[u];
+        break;
+      }
+      ld(i1, y);
+#pragma unroll
+      for (int u = 0; u < KG; ++u) a ^= x[u];
+#pragma unroll
+      for (int u = 0; u < KG; ++u) x[u] = y[u];
+      i0 = i1;
+    }
+  }
+  red[tid] = a;
+  __syncthreads();
+  if (tid < SEGS) {
+    u64x2 x = {0, 0};
+    for (uint32_t k = 0; k < nsl; ++k) x ^= red[k * SEGS + tid];
+    out[(uint64_t)s * E + tid * 2] = x.x;
+    out[(uint64_t)s * E + tid * 2 + 1] = x.y;
+  }
+}
+
 // LDS-DMA ring: B rows per stage, NB stages in flight.  Piece q of a stage =
 // row q / 40, 16-B segment q % 40; wave-instruction k of the stage moves pieces
 // 64k .. 64k + 63 (whole 128-B lines: rows are 5 lines).
 template <int NT, int B, int NB>
 __global__ void __launch_bounds__(NT) k_dma(const uint64_t* __restrict__ db, const uint16_t* __restrict__ offs,
-                                            uint64_t* __restrict__ out) {
+                                            uint64_t* __restrict__ out, uint32_t copies) {
   constexpr uint32_t PIECES = B * SEGS, INSTR = (PIECES + 63) / 64, NW = NT / 64;
   __shared__ __attribute__((aligned(16))) u64x2 ring[NB][INSTR * 64];
   __shared__ uint32_t rows[SS];
@@ -75,7 +128,7 @@ __global__ void __launch_bounds__(NT) k_dma(const uint64_t* __restrict__ db, con
     rows[i] = r < PS ? r : PS;   // PS: a zero row (the table has one past every partition? use row 0 masked below)
   }
   __syncthreads();
-  const char* base = reinterpret_cast<const char*>(db + (uint64_t)p * PS * E);
+  const char* base = reinterpret_cast<const char*>(db + ((uint64_t)(s / NPART % copies) * NROWS + (uint64_t)p * PS) * E);
   constexpr uint32_t NST = (SS + B - 1) / B;
   auto issue = [&](uint32_t st) {
     for (uint32_t k = wave; k < INSTR; k += NW) {
@@ -147,12 +200,13 @@ static void run(const char* name, F launch, uint64_t* d_out, uint32_t ns, int re
 
 int main(int argc, char** argv) {
   const uint32_t ns = argc > 1 ? atoi(argv[1]) : 6144;
+  g_copies = argc > 2 ? atoi(argv[2]) : 1;
   const int reps = 50;
   uint64_t *db, *out; uint16_t* offs;
-  CK(hipMalloc(&db, NROWS * E * 8));
+  CK(hipMalloc(&db, g_copies * NROWS * E * 8));
   CK(hipMalloc(&out, (size_t)ns * E * 8));
   CK(hipMalloc(&offs, (size_t)ns * SS * 2));
-  k_fill<<<4096, 256>>>(db, NROWS * E);
+  k_fill<<<4096, 256>>>(db, g_copies * NROWS * E);
   std::vector<uint16_t> ho((size_t)ns * SS);
   uint64_t x = 88172645463325252ull, inrange = 0;
   for (auto& o : ho) { x ^= x << 13; x ^= x >> 7; x ^= x << 17; o = x % CS; }
@@ -160,6 +214,7 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(offs, ho.data(), ho.size() * 2, hipMemcpyHostToDevice));
   const double bytes = inrange * 640.0;
   g_bytes = bytes;
+  printf("table copies %u (%.1f GB)\n", g_copies, g_copies * NROWS * E * 8 / 1e9);
   printf("sub-queries %u, in-range rows %llu, %.1f MB per launch\n", ns, (unsigned long long)inrange, bytes / 1e6);
   // NSETS different offset sets, cycled launch by launch (every launch gathers
   // new rows, as the serving steps do; one set repeated back to back keeps
@@ -174,10 +229,13 @@ int main(int argc, char** argv) {
   int launch_no = 0;
   auto R = [&](const char* nm, auto kern, int nt) {
     run(nm, [&] {
-      hipLaunchKernelGGL(kern, dim3(ns), dim3(nt), 0, 0, db, offs_all + (size_t)(launch_no++ % NSETS) * ns * SS, out);
+      hipLaunchKernelGGL(kern, dim3(ns), dim3(nt), 0, 0, db, offs_all + (size_t)(launch_no++ % NSETS) * ns * SS, out, g_copies);
     }, out, ns, reps);
   };
   R("reg128k6", (k_reg<128, 6>), 128);
+  R("regp128k6", (k_regp<128, 6>), 128);
+  R("regp128k4", (k_regp<128, 4>), 128);
+  R("regp128k8", (k_regp<128, 8>), 128);
   R("reg128k6nt", (k_reg<128, 6, true>), 128);
   R("reg128k8nt", (k_reg<128, 8, true>), 128);
   R("reg256k8nt", (k_reg<256, 8, true>), 256);
