@@ -97,11 +97,12 @@ struct PmPart {
   PM_G uint16_t* tab;
   PM_G uint16_t* tabT;    // the same table tag-major in tiles of 8 chunks (tabT_at): set expansion
                           // reads one tag's row; k_prep_offsets writes whole 16-B tiles
-  // The hint search's row: cur[c*PH + h] = PRF(current tag of primary hint h,
-  // chunk c) & (CS-1), i.e. tab[c][tag[h]] kept in hint order, so matching a
-  // (chunk, offset) streams PH contiguous u16 instead of gathering through
-  // the tags.  k_prep_offsets seeds it (tags are h); the final refresh of a
-  // hint in a step rewrites its column from tabT[new tag] (pm_query.hip refresh_cur).
+  // The hint search's table: entry (c, h) = PRF(current tag of primary hint
+  // h, chunk c) & (CS-1), i.e. tab[c][tag[h]] kept in hint order, so matching
+  // a (chunk, offset) streams chunk c's row of PH u16 instead of gathering
+  // through the tags.  k_prep_offsets seeds it (tags are h); the final refresh
+  // of a hint in a step rewrites its column from tabT[new tag] (pm_query.hip
+  // refresh_cur).  Layout cur_index: chunk pairs interleaved in 16-B blocks.
   PM_G uint16_t* cur;
   // the search query this client's decoded rows are scored against (L2) when
   // several clients' steps share one launch (pm_search_loop_batched); null:
@@ -122,6 +123,22 @@ __host__ __device__ inline uint64_t tabT_index(uint32_t H, uint32_t t, uint32_t 
   return ((uint64_t)(c >> 3) * H + t) * 8 + (c & 7);
 }
 __host__ __device__ inline uint64_t tabT_words(uint32_t H, uint32_t SS) { return (uint64_t)((SS + 7) / 8) * 8 * H; }
+
+// Hint-search table layout: [SS / 2][PH8 / 8][2][8] u16 (PH8 = PH rounded up
+// to 8): block b of chunk c's row (hints 8b .. 8b + 7, one 16-B load) sits
+// beside the same block of chunk c ^ 1.  A refresh writes a hint's entry of
+// every chunk, i.e. one column: paired, its SS entries touch SS / 2 cache lines
+// instead of SS (random line writes cost ~2.6 random line reads on MI355X:
+// tools/gather_bench.hip regw_*), while a row's reads stay whole 16-B blocks
+// (every other one: twice the row's bytes through L2).
+__host__ __device__ inline uint32_t cur_blocks(uint32_t PH) { return (PH + 7) >> 3; }
+__host__ __device__ inline uint64_t cur_index(uint32_t PH, uint32_t c, uint32_t h) {
+  return (((uint64_t)(c >> 1) * cur_blocks(PH) + (h >> 3)) * 2 + (c & 1)) * 8 + (h & 7);
+}
+// chunk c's row: hint h at row[cur_row_off(h)], block b (8 hints) at row + 16 b
+__host__ __device__ inline uint64_t cur_row(uint32_t PH, uint32_t c) { return cur_index(PH, c, 0); }
+__host__ __device__ inline uint32_t cur_row_off(uint32_t h) { return ((h >> 3) << 4) | (h & 7); }
+__host__ __device__ inline uint64_t cur_words(uint32_t PH, uint32_t SS) { return (uint64_t)((SS + 1) / 2) * cur_blocks(PH) * 16; }
 
 // Sub-query kinds / statuses for one batched step.
 enum : uint32_t { SUB_NONE = 0, SUB_REAL = 1, SUB_DUMMY = 2, SUB_HOSTCACHE = 3 };

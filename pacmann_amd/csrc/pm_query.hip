@@ -276,7 +276,7 @@ __device__ __forceinline__ void match_role(const PmStep& S, uint32_t s, uint32_t
   STAMP_AT(stamp_wg, 42);
   const uint32_t mask = P.CS - 1, chunk = (uint32_t)(sub.idx >> P.log2CS),
                  offset = (uint32_t)(sub.idx & mask);
-  const PM_G uint16_t* crow = P.cur + (uint64_t)chunk * P.PH;   // the hint search row of this chunk
+  const PM_G uint16_t* crow = P.cur + cur_row(P.PH, chunk);   // the hint search row of this chunk
   const bool live = sub.idx < P.N;
   // Block 0 of a sub-query also prepares k_resolve's prediction: its chunk's
   // QueryHistogram now, the rest below (loads overlap the match loads).
@@ -291,7 +291,7 @@ __device__ __forceinline__ void match_role(const PmStep& S, uint32_t s, uint32_t
 #pragma unroll
   for (int u = 0; u < kMatchHPT; ++u) {
     const uint32_t h = base + u * NT + threadIdx.x;
-    rv[u] = (live && h < P.PH) ? crow[h] : kSkip;
+    rv[u] = (live && h < P.PH) ? crow[cur_row_off(h)] : kSkip;
   }
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (meta_wg && wave == 0) {
@@ -475,11 +475,11 @@ __device__ __forceinline__ void match_part_block(const PmStep& S, const PmPart& 
       const bool lv = act && kind[g] == SUB_REAL && idx < P.N;
       const uint32_t chk = (uint32_t)(idx >> lg);
       off[g] = (uint32_t)(idx & mask);
-      const PM_G uint16_t* crow = P.cur + (uint64_t)chk * P.PH;
+      const PM_G uint16_t* crow = P.cur + cur_row(P.PH, chk);
 #pragma unroll
       for (int u = 0; u < HPT; ++u) {
         const uint32_t h = base + u * NT + tid;
-        rv[g][u] = (lv && h < P.PH) ? crow[h] : kSkip;
+        rv[g][u] = (lv && h < P.PH) ? crow[cur_row_off(h)] : kSkip;
       }
     }
 #pragma unroll
@@ -624,13 +624,14 @@ __global__ void __launch_bounds__(64 * NW, PM_MATCHPART8_WAVES) k_match_part8(Pm
                            __builtin_amdgcn_readfirstlane((uint32_t)sub.idx);
       const bool lv = kind[g] == SUB_REAL && idx < P.N;
       off[g] = (uint32_t)(idx & mask);
-      const PM_G uint4* crow = reinterpret_cast<const PM_G uint4*>(P.cur + (uint64_t)(uint32_t)(idx >> lg) * P.PH);
+      // (16-B blocks of the row are 32 B apart: cur_index)
+      const PM_G uint4* crow = reinterpret_cast<const PM_G uint4*>(P.cur + cur_row(P.PH, (uint32_t)(idx >> lg)));
       // unconditional 16-B loads (a dead lane reads the partition's first
       // vector), then kSkip x 8 by value: a select of the loaded VALUE keeps
       // them global_load_dwordx4
       const bool okA = lv && hA < P.PH, okB = lv && hB < P.PH;
-      const uint4 a = okA ? crow[hA >> 3] : *reinterpret_cast<const PM_G uint4*>(P.cur);
-      const uint4 b = okB ? crow[hB >> 3] : *reinterpret_cast<const PM_G uint4*>(P.cur);
+      const uint4 a = okA ? crow[(hA >> 3) * 2] : *reinterpret_cast<const PM_G uint4*>(P.cur);
+      const uint4 b = okB ? crow[(hB >> 3) * 2] : *reinterpret_cast<const PM_G uint4*>(P.cur);
       rv[g][0] = okA ? a : make_uint4(~0u, ~0u, ~0u, ~0u);
       rv[g][1] = okB ? b : make_uint4(~0u, ~0u, ~0u, ~0u);
     }
@@ -721,12 +722,12 @@ __device__ __forceinline__ uint32_t find_next_g(const PmStep& S, uint64_t sub, u
 // before the step's k_answer).  One wave, 8 hints per lane (PH % 8 == 0).
 __device__ __forceinline__ uint32_t find_cur(const PmPart& P, uint32_t chunk, uint32_t off, uint32_t start) {
   const uint32_t lane = threadIdx.x & 63;
-  const PM_G uint16_t* row = P.cur + (uint64_t)chunk * P.PH;
+  const PM_G uint16_t* row = P.cur + cur_row(P.PH, chunk);
   for (uint32_t h0 = start & ~7u; h0 < P.PH; h0 += 512) {
     const uint32_t h = h0 + lane * 8;
     uint32_t f = kNone;
     if (h < P.PH) {
-      const uint4 v = *reinterpret_cast<const PM_G uint4*>(row + h);
+      const uint4 v = *reinterpret_cast<const PM_G uint4*>(row + cur_row_off(h));
       const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int e = 7; e >= 0; --e) {
@@ -1503,12 +1504,12 @@ __global__ void __launch_bounds__(NT) k_match_resolve_s(PmStep S) {
                            (uint32_t)__builtin_amdgcn_readlane((uint32_t)mine.idx, jj);
       const bool lv = kind == SUB_REAL && idx < P.N;
       off[g] = lv ? (uint32_t)(idx & mask) : kNone;
-      const PM_G uint16_t* crow = P.cur + (uint64_t)(lv ? (uint32_t)(idx >> lg) : 0u) * P.PH;
+      const PM_G uint16_t* crow = P.cur + cur_row(P.PH, lv ? (uint32_t)(idx >> lg) : 0u);
 #pragma unroll
       for (int u = 0; u < NU; ++u) {
         const uint32_t h = (u * NT + tid) * 8;
         v[g][u] = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);   // kSkip x 8
-        if (lv && h < P.PH) v[g][u] = *reinterpret_cast<const PM_G uint4*>(crow + h);
+        if (lv && h < P.PH) v[g][u] = *reinterpret_cast<const PM_G uint4*>(crow + cur_row_off(h));
       }
     }
 #pragma unroll
@@ -1737,7 +1738,7 @@ enum : uint32_t { A_ZERO = 0, A_FINAL = 1, A_CHAINED = 2, A_CACHED = 3, A_DUMMY 
 // clear); read by the next step's hint search, after this launch ends.
 __device__ __forceinline__ void refresh_cur(const PmPart& P, const PmRes& r, uint32_t tid, uint32_t nt) {
   const uint32_t ntag = P.PH + r.chunk * P.Qpc + r.ing;
-  for (uint32_t c = tid; c < P.SS; c += nt) P.cur[(uint64_t)c * P.PH + r.hit] = P.tabT[tabT_index(P.H, ntag, c)];
+  for (uint32_t c = tid; c < P.SS; c += nt) P.cur[cur_index(P.PH, c, r.hit)] = P.tabT[tabT_index(P.H, ntag, c)];
 }
 
 // Decode one chained sub-query (its hint was refreshed earlier in this step)
@@ -1987,9 +1988,9 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, LDS& L)
       const uint32_t ch = (uint32_t)(sub.idx >> lg), off = (uint32_t)(sub.idx & mask);
       const uint32_t wave = tid >> 6, lane = tid & 63;
       uint32_t rv[HPT];
-      const PM_G uint16_t* crow = P.cur + (uint64_t)ch * P.PH;   // match: value == offset (see match_role)
+      const PM_G uint16_t* crow = P.cur + cur_row(P.PH, ch);   // match: value == offset (see match_role)
 #pragma unroll
-      for (int u = 0; u < HPT; ++u) rv[u] = u * NT + tid < P.PH ? crow[u * NT + tid] : kNone;
+      for (int u = 0; u < HPT; ++u) rv[u] = u * NT + tid < P.PH ? crow[cur_row_off(u * NT + tid)] : kNone;
       const uint32_t h0k = wave == 0 ? P.hist[ch] : 0;
       // per wave the lowest matching hint (lower u first: hints u*NT + tid)
       uint32_t wh = kNone, wt = 0, wp = 0;
@@ -2049,7 +2050,7 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, LDS& L)
   // ---- decode + refresh, or the cached row -----------------------------
   if (mode == A_FINAL) {
     if (!(r.flags & 2u)) {   // refresh_cur with the row prefetched with the decode operands
-      if (tid < P.SS) P.cur[(uint64_t)tid * P.PH + r.hit] = (uint16_t)e_cur;
+      if (tid < P.SS) P.cur[cur_index(P.PH, tid, r.hit)] = (uint16_t)e_cur;
       if (P.SS > NT) refresh_cur(P, r, tid + NT, NT);   // SetSize > workgroup (BIGANN): the rest
     }
     for (uint32_t w = tid; w < E; w += NT) {
@@ -2273,7 +2274,7 @@ __device__ __forceinline__ void ansp_epilogue(const PmStep& S, const AnsQ& a, LD
   uint64_t* pp = P.parity + (uint64_t)r.hit * E;
   if (mode == A_FINAL) {   // pir.go:450-468
     if (!(r.flags & 2u)) {
-      if (tid < P.SS) P.cur[(uint64_t)tid * P.PH + r.hit] = (uint16_t)a.e_cur;
+      if (tid < P.SS) P.cur[cur_index(P.PH, tid, r.hit)] = (uint16_t)a.e_cur;
       if (P.SS > NT) refresh_cur(P, r, tid + NT, NT);
     }
     const uint64_t* rv = P.rval + dslot * E;
@@ -2401,6 +2402,10 @@ __device__ __forceinline__ bool ansp_turn(const PmStep& S, AnswerPLds<NT>& L, An
 #define PM_ANSWER_PK_MAX 2   // sub-queries per k_answer_p workgroup the kernel is built for (the host's PM_ANSWER_PK is
                              // clamped to it); 3 spills ~150 VGPRs at 80
 #endif
+#ifndef PM_ANSWER_P_TAIL
+#define PM_ANSWER_P_TAIL 0   // k_answer_p's grid capped at PM_ANSWER_P_TAIL workgroups; the sub-queries past two
+                             // per workgroup are answered one at a time at the end (diagnostic build)
+#endif
 #ifndef PM_ANSWER_P_WAVES
 #define PM_ANSWER_P_WAVES 6   // min waves per SIMD: <= 80 VGPRs (the next sub-query's row batch stays live through
                               // an epilogue); 12 two-wave workgroups per CU = the 3,072 of a 6,144-sub-query step
@@ -2432,6 +2437,31 @@ __global__ void __launch_bounds__(NT, PM_ANSWER_P_WAVES) k_answer_p(PmStep S) {
   if (!ansp_turn<W, NT, KG, 1>(S, L, q, qpv, g, 1, false)) return;
   if (PM_ANSWER_PK_MAX > 2 && !ansp_turn<W, NT, KG, 0>(S, L, q, qpv, g, 2, false)) return;
   if (PM_ANSWER_PK_MAX > 3) ansp_turn<W, NT, KG, 1>(S, L, q, qpv, g, 3, false);
+#if PM_ANSWER_P_TAIL
+  // a grid of fewer workgroups than sub-query pairs (PM_ANSWER_P_TAIL: the
+  // host caps it at the resident slots): the rest, one at a time, unpipelined
+  for (uint32_t s = blockIdx.x + 2 * G; s < ns; s += G) {
+    AnsQ t;
+    uint4 tq;
+    ansp_record<W, NT>(S, s, t, tq);
+    t.mode = answer_mode(t.r);
+    ansp_decode_ops<W, NT>(S, t);
+    ansp_set(S, t, tq, L.qo[0]);
+    __syncthreads();
+    AnsGather<W, NT, KG> gt;
+    gt.init(S.E);
+    if (ansp_gathers(t)) {
+      const PmPart& P = S.parts[t.part];
+      const uint32_t nb = gt.batches(P);
+      for (uint32_t b = 0; b < nb; ++b) {
+        gt.load(S, P, L.qo[0], b);
+        gt.fold();
+      }
+      gt.reduce(L, S.E);
+    }
+    ansp_epilogue<W, NT>(S, t, L);
+  }
+#endif
 }
 
 // ---- k_gather: the server's XOR gather of wide sets, split ----------------
@@ -2712,8 +2742,10 @@ void step_answer(hipStream_t st, const PmStep& S, uint32_t maxSS, PmEvents ev) {
       (S.E & ~3u) <= 2u * kAnsPNT && S.nsub >= 2 * 256) {
     // sub-queries per workgroup (the grid is nsub / pk; 2: every workgroup of a
     // 6,144-sub-query step resident at once)
-    static const uint32_t pk = [] { const char* e = getenv("PM_ANSWER_PK"); return e && atoi(e) > 1 ? std::min((uint32_t)atoi(e), (uint32_t)PM_ANSWER_PK_MAX) : 2u; }();
-    PM_LAUNCH(ev, (k_answer_p<2, kAnsPNT>), dim3((S.nsub + pk - 1) / pk), dim3(kAnsPNT), st, S);
+    static const uint32_t pk = [] { const char* e = getenv("PM_ANSWER_PK"); return std::min(e && atoi(e) > 1 ? (uint32_t)atoi(e) : (uint32_t)PM_ANSWER_PK_MAX, (uint32_t)PM_ANSWER_PK_MAX); }();
+    uint32_t grid = (S.nsub + pk - 1) / pk;
+    if (PM_ANSWER_P_TAIL) grid = std::min(grid, (uint32_t)PM_ANSWER_P_TAIL);
+    PM_LAUNCH(ev, (k_answer_p<2, kAnsPNT>), dim3(grid), dim3(kAnsPNT), st, S);
     return;
   }
   if (nt && S.nsplit <= 1 && maxSS <= kSmallSS && S.E <= kSmallE) {

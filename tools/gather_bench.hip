@@ -112,6 +112,97 @@ __global__ void __launch_bounds__(NT) k_regp(const uint64_t* __restrict__ db, co
   }
 }
 
+
+// k_reg + the answer's hint refresh: 124 scattered 2-B stores per sub-query
+// (cur[c][hit] for every chunk c of a [SS][PH] u16 table, one table per
+// (client, partition)), to price the refresh's partial-line writes
+constexpr uint32_t PH = 3584;
+// MODE 0: plain 2-B stores; 1: the target's word loaded first (before the
+// gather: the line is in L2 when the store lands); 2: a 4-B atomic OR per
+// entry (done in L2); 3: nontemporal 2-B stores
+template <int NT, int KG, int MODE = 0>
+__global__ void __launch_bounds__(NT) k_regw(const uint64_t* __restrict__ db, const uint16_t* __restrict__ offs,
+                                             uint64_t* __restrict__ out, uint32_t copies, uint16_t* __restrict__ cur,
+                                             uint32_t ntab, uint32_t salt) {
+  __shared__ uint16_t qo[SS];
+  __shared__ u64x2 red[NT];
+  const uint32_t s = blockIdx.x, tid = threadIdx.x, p = s % NPART;
+  const uint32_t hit = ((s + salt * 7919u) * 2654435761u >> 7) % PH;   // salt: new hints every launch
+  // layouts of the [SS][PH] table: 0-3 row-major (chunk rows of PH hints);
+  // 4: [PH / 64][SS][64] (a hint group's 124 chunk lines contiguous, 15.9 KB);
+  // 5: [SS / 16][PH / 64][16][64] (2-KB tiles of 16 chunk lines x 64 hints)
+  uint64_t off;
+  if (MODE == 4) off = ((uint64_t)(hit / 64) * SS + tid) * 64 + hit % 64;
+  else if (MODE == 5) off = (((uint64_t)(tid / 16) * (PH / 64) + hit / 64) * 16 + tid % 16) * 64 + hit % 64;
+  else off = (uint64_t)tid * PH + hit;
+  uint16_t* const cw = cur + (uint64_t)(s % ntab) * SS * PH + off;
+  uint16_t pre = 0;
+  if (MODE == 1 && tid < SS) pre = *reinterpret_cast<volatile uint16_t*>(cw);
+  if (MODE == 6 && tid < SS) *cw = (uint16_t)(s + tid);   // the refresh issued before the gather
+  for (uint32_t i = tid; i < SS; i += NT) qo[i] = offs[(uint64_t)s * SS + i];
+  __syncthreads();
+  const uint64_t* base = db + ((uint64_t)(s / NPART % copies) * NROWS + (uint64_t)p * PS) * E;
+  const uint32_t nsl = NT / SEGS, sl = tid / SEGS, seg = tid % SEGS;
+  u64x2 a = {0, 0};
+  if (sl < nsl) {
+    for (uint32_t i0 = sl; i0 < SS; i0 += KG * nsl) {
+      uint32_t rr[KG];
+#pragma unroll
+      for (int u = 0; u < KG; ++u) { const uint32_t i = i0 + u * nsl; rr[u] = i < SS ? i * CS + qo[i] : ~0u; }
+      u64x2 x[KG];
+#pragma unroll
+      for (int u = 0; u < KG; ++u) {
+        x[u] = u64x2{0, 0};
+        if (rr[u] < PS) x[u] = *reinterpret_cast<const u64x2*>(base + (uint64_t)rr[u] * E + seg * 2);
+      }
+#pragma unroll
+      for (int u = 0; u < KG; ++u) a ^= x[u];
+    }
+  }
+  red[tid] = a;
+  __syncthreads();
+  if (tid < SEGS) {
+    u64x2 x = {0, 0};
+    for (uint32_t k = 0; k < nsl; ++k) x ^= red[k * SEGS + tid];
+    out[(uint64_t)s * E + tid * 2] = x.x;
+    out[(uint64_t)s * E + tid * 2 + 1] = x.y;
+  }
+  if (MODE == 7 || MODE == 8) {   // chunk-pair / chunk-quad tiles: SS / 2 (4) stores of 4 (8) B
+    constexpr uint32_t K = MODE == 7 ? 2 : 4;
+    if (tid < SS / K) {
+      uint16_t* t = cur + (uint64_t)(s % ntab) * SS * PH + ((uint64_t)tid * PH + hit) * K;
+      if (K == 2) *reinterpret_cast<uint32_t*>(t) = qo[tid] | (uint32_t)qo[tid + 1] << 16;
+      else *reinterpret_cast<uint2*>(t) = make_uint2(qo[tid], qo[tid + 1]);
+    }
+  } else if (MODE != 6 && tid < SS) {
+    if (MODE == 2) atomicOr(reinterpret_cast<uint32_t*>((uintptr_t)cw & ~(uintptr_t)3), (uint32_t)qo[tid] << (((uintptr_t)cw & 2) * 8));
+    else if (MODE == 3) __builtin_nontemporal_store((uint16_t)(qo[tid] ^ pre), cw);
+    else *cw = (uint16_t)(qo[tid] ^ pre);
+  }
+}
+
+// MODE 0 / 1: 2-B stores (plain / nontemporal); 2: aligned 4-B; 3: aligned
+// 32-B (a full sector: two 16-B stores); 4: aligned 128-B (a full line: 8 lanes)
+template <int MODE>
+__global__ void __launch_bounds__(128) k_wonly(uint16_t* __restrict__ cur, uint32_t ntab, uint32_t salt) {
+  const uint32_t s = blockIdx.x, tid = threadIdx.x;
+  const uint32_t hit = ((s + salt * 7919u) * 2654435761u >> 7) % PH;
+  if (tid < SS) {
+    uint16_t* cw = cur + (uint64_t)(s % ntab) * SS * PH + (uint64_t)tid * PH + hit;
+    if (MODE == 1) __builtin_nontemporal_store((uint16_t)(s + tid), cw);
+    else if (MODE == 2) *reinterpret_cast<uint32_t*>((uintptr_t)cw & ~(uintptr_t)3) = s + tid;
+    else if (MODE == 3) {
+      uint4* q = reinterpret_cast<uint4*>((uintptr_t)cw & ~(uintptr_t)31);
+      q[0] = make_uint4(s, tid, 1, 2);
+      q[1] = make_uint4(s, tid, 3, 4);
+    } else if (MODE == 4) {
+      uint4* q = reinterpret_cast<uint4*>((uintptr_t)cw & ~(uintptr_t)127);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) q[k] = make_uint4(s, tid, k, 2);
+    } else *cw = (uint16_t)(s + tid);
+  }
+}
+
 // LDS-DMA ring: B rows per stage, NB stages in flight.  Piece q of a stage =
 // row q / 40, 16-B segment q % 40; wave-instruction k of the stage moves pieces
 // 64k .. 64k + 63 (whole 128-B lines: rows are 5 lines).
@@ -233,6 +324,42 @@ int main(int argc, char** argv) {
     }, out, ns, reps);
   };
   R("reg128k6", (k_reg<128, 6>), 128);
+  {   // the refresh's scattered writes beside the gather: 4,608 tables = 288 clients x 16 partitions (4.1 GB)
+    const uint32_t ntab = 4608;
+    const bool salt_on = getenv("GB_SALT") != nullptr;   // new hints every launch (the serving pattern)
+    uint16_t* cur;
+    CK(hipMalloc(&cur, (size_t)ntab * SS * PH * 2));
+    CK(hipMemset(cur, 0, (size_t)ntab * SS * PH * 2));
+    run("reg128k6", [&] {
+      hipLaunchKernelGGL((k_reg<128, 6>), dim3(ns), dim3(128), 0, 0, db, offs_all + (size_t)(launch_no++ % NSETS) * ns * SS, out, g_copies);
+    }, out, ns, reps);
+    auto W = [&](const char* nm, auto kern) {
+      run(nm, [&] {
+        const uint32_t ln = launch_no++;
+        hipLaunchKernelGGL(kern, dim3(ns), dim3(128), 0, 0, db, offs_all + (size_t)(ln % NSETS) * ns * SS, out,
+                           g_copies, cur, ntab, salt_on ? ln : 0u);
+      }, out, ns, reps);
+    };
+    W("regw_plain", (k_regw<128, 6, 0>));
+    W("regw_pair", (k_regw<128, 6, 7>));
+    W("regw_quad", (k_regw<128, 6, 8>));
+    W("regw_plain", (k_regw<128, 6, 0>));
+    W("regw_pair", (k_regw<128, 6, 7>));
+    W("regw_quad", (k_regw<128, 6, 8>));
+    W("regw_plain", (k_regw<128, 6, 0>));
+    W("regw_nt", (k_regw<128, 6, 3>));
+    auto WO = [&](const char* nm, auto kern) {
+      run(nm, [&] { hipLaunchKernelGGL(kern, dim3(ns), dim3(128), 0, 0, cur, ntab, salt_on ? launch_no++ : 0u); }, out, ns, reps);
+    };
+    WO("wonly_2B", k_wonly<0>);
+    WO("wonly_2B_nt", k_wonly<1>);
+    WO("wonly_4B", k_wonly<2>);
+    WO("wonly_32B", k_wonly<3>);
+    WO("wonly_128B", k_wonly<4>);
+    WO("wonly_2B", k_wonly<0>);
+    CK(hipFree(cur));
+  }
+  if (getenv("GB_ONLY_W")) return 0;
   R("regp128k6", (k_regp<128, 6>), 128);
   R("regp128k4", (k_regp<128, 4>), 128);
   R("regp128k8", (k_regp<128, 8>), 128);

@@ -5,7 +5,10 @@ t=$1; shift
 for i in 1 2 3 4 5 6 7 8; do
   out=$(/usr/local/graft/bin/gpurun --timeout "$t" -- "$@" 2>&1); rc=$?
   echo "$out" | tail -n 6
-  if echo "$out" | grep -q "status=transient\|backing off\|no box or slot"; then sleep 90; continue; fi
+  # retry only when the call's own status line says nothing ran (a finished
+  # call's tail can quote such words from earlier attempts)
+  if echo "$out" | grep -q "^\[gpurun\] status=transient" && ! echo "$out" | grep -q "^\[gpurun\] status=ok"; then sleep 90; continue; fi
+  if [ $rc -eq 3 ]; then sleep 90; continue; fi
   exit $rc
 done
 exit $rc
