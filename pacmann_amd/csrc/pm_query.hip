@@ -1423,6 +1423,17 @@ __global__ void __launch_bounds__(kResolveBlockG) k_match_resolve(PmStep S) {
 #ifndef PM_MR_G
 #define PM_MR_G 8       // search rows of 8 / NU sub-queries per round trip (0: see above)
 #endif
+#ifndef PM_MR_NT
+#define PM_MR_NT 1   // k_match_resolve_s' search-row loads nontemporal: streamed, not kept in the Infinity Cache
+                     // the answer's DB rows reuse (with PM_REFRESH_NT +2.0 %, ABBA, profiles/r05/ab/nontemporal_*)
+#endif
+#ifndef PM_REFRESH_NT
+#define PM_REFRESH_NT 1   // k_answer_p's refresh stores nontemporal (the same reason)
+#endif
+#ifndef PM_EPI_NT
+#define PM_EPI_NT 1   // k_answer_p's parity and localCache stores nontemporal (+0.5 %, within noise; written
+                      // once per refresh, read back rounds later if at all)
+#endif
 #ifndef PM_CHAIN_PRIO
 #define PM_CHAIN_PRIO 0   // s_setprio of the device loop's chain kernels (match + resolve, the team round)
 #endif
@@ -1509,7 +1520,12 @@ __global__ void __launch_bounds__(NT) k_match_resolve_s(PmStep S) {
       for (int u = 0; u < NU; ++u) {
         const uint32_t h = (u * NT + tid) * 8;
         v[g][u] = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);   // kSkip x 8
-        if (lv && h < P.PH) v[g][u] = *reinterpret_cast<const PM_G uint4*>(crow + cur_row_off(h));
+        if (lv && h < P.PH) {
+          typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+          const PM_G u32x4* src = reinterpret_cast<const PM_G u32x4*>(crow + cur_row_off(h));
+          const u32x4 x = PM_MR_NT ? __builtin_nontemporal_load(src) : *src;
+          v[g][u] = make_uint4(x.x, x.y, x.z, x.w);
+        }
       }
     }
 #pragma unroll
@@ -2057,12 +2073,10 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, LDS& L)
       const uint64_t rvw = w < NT ? e_rv : rv[w], bpw = w < NT ? e_bp : bp[w],
                      ppw = w < NT ? e_pp : pp[w];
       uint64_t v = 0;
-      if (w < EX) {
-        v = row.w[w] ^ rvw ^ ppw;
-        pp[w] = bpw ^ v;
-      } else {
-        pp[w] = bpw;
-      }
+      if (w < EX) v = row.w[w] ^ rvw ^ ppw;
+      const uint64_t nw = w < EX ? bpw ^ v : bpw;
+      if (PM_EPI_NT) __builtin_nontemporal_store(nw, pp + w);
+      else pp[w] = nw;
       row.w[w] = v;
     }
   } else if (mode == A_CHAINED) {
@@ -2088,7 +2102,10 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, LDS& L)
       row_store(orow + w, has_row ? row.w[w] : 0);
     if (mode == A_FINAL) {
       uint64_t* ar = P.arena + (uint64_t)r.slot * E;
-      for (uint32_t w = tid; w < E; w += NT) ar[w] = row.w[w];
+      for (uint32_t w = tid; w < E; w += NT) {
+        if (PM_EPI_NT) __builtin_nontemporal_store(row.w[w], ar + w);
+        else ar[w] = row.w[w];
+      }
     }
     float d = 0.0f;
     if (has_row && qq && tid < 8) d = l2_lds(row.f, q_lds ? qf : qq, S.dim);
@@ -2274,7 +2291,11 @@ __device__ __forceinline__ void ansp_epilogue(const PmStep& S, const AnsQ& a, LD
   uint64_t* pp = P.parity + (uint64_t)r.hit * E;
   if (mode == A_FINAL) {   // pir.go:450-468
     if (!(r.flags & 2u)) {
-      if (tid < P.SS) P.cur[cur_index(P.PH, tid, r.hit)] = (uint16_t)a.e_cur;
+      if (tid < P.SS) {
+        PM_G uint16_t* dst = P.cur + cur_index(P.PH, tid, r.hit);
+        if (PM_REFRESH_NT) __builtin_nontemporal_store((uint16_t)a.e_cur, dst);
+        else *dst = (uint16_t)a.e_cur;
+      }
       if (P.SS > NT) refresh_cur(P, r, tid + NT, NT);
     }
     const uint64_t* rv = P.rval + dslot * E;
@@ -2282,12 +2303,10 @@ __device__ __forceinline__ void ansp_epilogue(const PmStep& S, const AnsQ& a, LD
     for (uint32_t w = tid; w < E; w += NT) {
       const uint64_t rvw = w < NT ? a.e_rv : rv[w], bpw = w < NT ? a.e_bp : bp[w], ppw = w < NT ? a.e_pp : pp[w];
       uint64_t v = 0;
-      if (w < EX) {
-        v = row.w[w] ^ rvw ^ ppw;
-        pp[w] = bpw ^ v;
-      } else {
-        pp[w] = bpw;
-      }
+      if (w < EX) v = row.w[w] ^ rvw ^ ppw;
+      const uint64_t nw = w < EX ? bpw ^ v : bpw;
+      if (PM_EPI_NT) __builtin_nontemporal_store(nw, pp + w);
+      else pp[w] = nw;
       row.w[w] = v;
     }
   } else if (mode == A_CHAINED) {
@@ -2311,7 +2330,10 @@ __device__ __forceinline__ void ansp_epilogue(const PmStep& S, const AnsQ& a, LD
       row_store(orow + w, has_row ? row.w[w] : 0);
     if (mode == A_FINAL) {
       uint64_t* ar = P.arena + (uint64_t)r.slot * E;
-      for (uint32_t w = tid; w < E; w += NT) ar[w] = row.w[w];
+      for (uint32_t w = tid; w < E; w += NT) {
+        if (PM_EPI_NT) __builtin_nontemporal_store(row.w[w], ar + w);
+        else ar[w] = row.w[w];
+      }
     }
     float d = 0.0f;
     if (has_row && qq && tid < 8) d = l2_lds(row.f, q_lds ? qf : qq, S.dim);
