@@ -131,14 +131,21 @@ __host__ __device__ inline uint64_t tabT_words(uint32_t H, uint32_t SS) { return
 // instead of SS (random line writes cost ~2.6 random line reads on MI355X:
 // tools/gather_bench.hip regw_*), while a row's reads stay whole 16-B blocks
 // (every other one: twice the row's bytes through L2).
+#ifndef PM_CUR_K
+#define PM_CUR_K 2   // chunks interleaved per 16-B hint block (1: round 4's row-major table)
+#endif
+constexpr uint32_t kCurK = PM_CUR_K;
+static_assert(kCurK == 1 || kCurK == 2 || kCurK == 4, "chunk group of the hint-search table");
 __host__ __device__ inline uint32_t cur_blocks(uint32_t PH) { return (PH + 7) >> 3; }
 __host__ __device__ inline uint64_t cur_index(uint32_t PH, uint32_t c, uint32_t h) {
-  return (((uint64_t)(c >> 1) * cur_blocks(PH) + (h >> 3)) * 2 + (c & 1)) * 8 + (h & 7);
+  return (((uint64_t)(c / kCurK) * cur_blocks(PH) + (h >> 3)) * kCurK + (c % kCurK)) * 8 + (h & 7);
 }
-// chunk c's row: hint h at row[cur_row_off(h)], block b (8 hints) at row + 16 b
+// chunk c's row: hint h at row[cur_row_off(h)], block b (8 hints) at row + 8 K b
 __host__ __device__ inline uint64_t cur_row(uint32_t PH, uint32_t c) { return cur_index(PH, c, 0); }
-__host__ __device__ inline uint32_t cur_row_off(uint32_t h) { return ((h >> 3) << 4) | (h & 7); }
-__host__ __device__ inline uint64_t cur_words(uint32_t PH, uint32_t SS) { return (uint64_t)((SS + 1) / 2) * cur_blocks(PH) * 16; }
+__host__ __device__ inline uint32_t cur_row_off(uint32_t h) { return (h >> 3) * 8 * kCurK + (h & 7); }
+__host__ __device__ inline uint64_t cur_words(uint32_t PH, uint32_t SS) {
+  return (uint64_t)((SS + kCurK - 1) / kCurK) * cur_blocks(PH) * 8 * kCurK;
+}
 
 // Sub-query kinds / statuses for one batched step.
 enum : uint32_t { SUB_NONE = 0, SUB_REAL = 1, SUB_DUMMY = 2, SUB_HOSTCACHE = 3 };

@@ -630,8 +630,8 @@ __global__ void __launch_bounds__(64 * NW, PM_MATCHPART8_WAVES) k_match_part8(Pm
       // vector), then kSkip x 8 by value: a select of the loaded VALUE keeps
       // them global_load_dwordx4
       const bool okA = lv && hA < P.PH, okB = lv && hB < P.PH;
-      const uint4 a = okA ? crow[(hA >> 3) * 2] : *reinterpret_cast<const PM_G uint4*>(P.cur);
-      const uint4 b = okB ? crow[(hB >> 3) * 2] : *reinterpret_cast<const PM_G uint4*>(P.cur);
+      const uint4 a = okA ? crow[(hA >> 3) * kCurK] : *reinterpret_cast<const PM_G uint4*>(P.cur);
+      const uint4 b = okB ? crow[(hB >> 3) * kCurK] : *reinterpret_cast<const PM_G uint4*>(P.cur);
       rv[g][0] = okA ? a : make_uint4(~0u, ~0u, ~0u, ~0u);
       rv[g][1] = okB ? b : make_uint4(~0u, ~0u, ~0u, ~0u);
     }
@@ -1430,6 +1430,9 @@ __global__ void __launch_bounds__(kResolveBlockG) k_match_resolve(PmStep S) {
 #ifndef PM_REFRESH_NT
 #define PM_REFRESH_NT 1   // k_answer_p's refresh stores nontemporal (the same reason)
 #endif
+#ifndef PM_DEC_NT
+#define PM_DEC_NT 0   // k_answer_p's decode operands (replacement row, parities, the new tag's offsets) nontemporal
+#endif
 #ifndef PM_EPI_NT
 #define PM_EPI_NT 1   // k_answer_p's parity and localCache stores nontemporal (+0.5 %, within noise; written
                       // once per refresh, read back rounds later if at all)
@@ -2198,6 +2201,16 @@ __device__ __forceinline__ void ansp_decode_ops(const PmStep& S, AnsQ& a) {
   if (a.mode != A_FINAL) return;
   const PmRes& r = a.r;
   const uint64_t dslot = (uint64_t)r.chunk * P.Qpc + r.ing;
+  if (PM_DEC_NT) {
+    if (!(r.flags & 2u) && tid < P.SS)
+      a.e_cur = __builtin_nontemporal_load(P.tabT + tabT_index(P.H, P.PH + r.chunk * P.Qpc + r.ing, tid));
+    if (tid < E) {
+      a.e_rv = __builtin_nontemporal_load(P.rval + dslot * E + tid);
+      a.e_bp = __builtin_nontemporal_load(P.parity + ((uint64_t)P.PH + dslot) * E + tid);
+      a.e_pp = __builtin_nontemporal_load(P.parity + (uint64_t)r.hit * E + tid);
+    }
+    return;
+  }
   if (!(r.flags & 2u) && tid < P.SS) a.e_cur = P.tabT[tabT_index(P.H, P.PH + r.chunk * P.Qpc + r.ing, tid)];
   if (tid < E) {
     a.e_rv = P.rval[dslot * E + tid];
