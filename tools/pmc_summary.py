@@ -7,6 +7,7 @@ taken as is.  Both counters are in KB.
 usage: python tools/pmc_summary.py FETCH.csv WRITE.csv OUT.json "command run"
 """
 import csv
+import gzip
 import json
 import sys
 from collections import defaultdict
@@ -14,7 +15,7 @@ from collections import defaultdict
 
 def per_kernel(path, counter, by_grid=False):
     acc = defaultdict(lambda: [0, 0.0])
-    for r in csv.DictReader(open(path)):
+    for r in csv.DictReader(gzip.open(path, 'rt') if path.endswith('.gz') else open(path)):
         if r["Counter_Name"] != counter:
             continue
         k = acc[(r["Kernel_Name"], int(r["Grid_Size"])) if by_grid else r["Kernel_Name"]]
