@@ -3676,21 +3676,62 @@ struct PoolTeam {
 // of their own instead, created back to back once per device (so they take
 // distinct hardware queues), swapped into the team's context for the loop
 // (PM_TEAM_STREAMS=0: the context streams).
+// PM_PREP_CUS=X (the device loop): the maintenance runs on a stream limited to
+// X CUs and the teams on the other ones, so one team's maintenance (the fold
+// and the AES tables: LDS-bound, a workgroup filling its CU) runs beside the
+// other teams' queries (HBM-bound answers) instead of taking the whole GPU in
+// turn.  Meant with the teams' maintenance windows staggered (bench.py
+// --stagger-teams).  0: off.  PM_CU_MAP: how mask bits map to XCDs (0: 32
+// consecutive bits per XCD, 1: bit i on XCD i % 8); X / 8 CUs are taken from
+// every XCD either way.
+static int prep_cus() {
+  static const int v = [] { const char* e = getenv("PM_PREP_CUS"); return e ? std::max(0, atoi(e)) : 0; }();
+  return v;
+}
+static std::vector<uint32_t> cu_mask(int dev, uint32_t n, bool complement) {
+  static const int map = [] { const char* e = getenv("PM_CU_MAP"); return e ? atoi(e) : 0; }();
+  int ncu = 256;
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  const uint32_t per = (uint32_t)ncu / 8, take = std::min(per, n / 8);
+  std::vector<uint32_t> m(((uint32_t)ncu + 31) / 32, 0);
+  for (uint32_t i = 0; i < (uint32_t)ncu; ++i) {
+    const uint32_t j = map == 1 ? i / 8 : i % per;   // index of CU i inside its XCD
+    const bool on = (j < take) != complement;
+    if (on) m[i / 32] |= 1u << (i % 32);
+  }
+  return m;
+}
+static hipStream_t masked_stream(int dev, uint32_t n, bool complement) {
+  std::vector<uint32_t> m = cu_mask(dev, n, complement);
+  hipStream_t st = nullptr;
+  if (hipExtStreamCreateWithCUMask(&st, (uint32_t)m.size(), m.data()) != hipSuccess) return nullptr;
+  return st;
+}
 static hipStream_t team_stream(int dev, uint32_t t) {
   static std::mutex mu;
   static std::vector<hipStream_t> pool[64];
   static const int on = [] { const char* e = getenv("PM_TEAM_STREAMS"); return e ? atoi(e) : 1; }();
-  if (!on || dev < 0 || dev >= 64) return nullptr;
+  if ((!on && !prep_cus()) || dev < 0 || dev >= 64) return nullptr;
   std::lock_guard<std::mutex> lk(mu);
   std::vector<hipStream_t>& v = pool[dev];
   if (v.empty()) {
     for (int i = 0; i < 8; ++i) {
       hipStream_t st = nullptr;
-      if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) break;
+      if (prep_cus()) st = masked_stream(dev, (uint32_t)prep_cus(), true);
+      else if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) st = nullptr;
+      if (!st) break;
       v.push_back(st);
     }
   }
   return v.empty() ? nullptr : v[t % v.size()];
+}
+static hipStream_t prep_stream(int dev) {
+  static std::mutex mu;
+  static hipStream_t st[64] = {};
+  if (!prep_cus() || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  if (!st[dev]) st[dev] = masked_stream(dev, (uint32_t)prep_cus(), false);
+  return st[dev];
 }
 struct StreamSwap {   // a team context's stream replaced for the loop's duration (restored drained)
   pm_ctx* c = nullptr;
@@ -4416,10 +4457,12 @@ static int run_batched_dev(pm_graph** gs, uint32_t S, const float* queries, uint
     // stream after every involved team's query; nothing on the host waits for
     // it (the other teams keep running what is queued), and the involved
     // teams' next rounds wait for it on the device
+    // (PM_PREP_CUS: on the maintenance stream's CUs, beside the other teams)
     DrlTeam* L = involved[0];
-    hipStream_t sl = L->G.c->stream;
+    hipStream_t const pst = prep_stream(L->G.c->device);
+    hipStream_t sl = pst ? pst : L->G.c->stream;
     for (DrlTeam* t : involved)
-      if (t != L) {
+      if (t != L || pst) {
         HIPCHK(hipEventRecord(t->ev_end, t->G.c->stream));
         HIPCHK(hipStreamWaitEvent(sl, t->ev_end, 0));
       }
@@ -4428,6 +4471,11 @@ static int run_batched_dev(pm_graph** gs, uint32_t S, const float* queries, uint
     HIPCHK(hipEventCreate(&ps.a));
     HIPCHK(hipEventCreate(&ps.b));
     HIPCHK(hipEventRecord(ps.a, sl));
+    struct OnStream {   // the leader's context launches on sl for the set
+      pm_ctx* c; hipStream_t old;
+      OnStream(pm_ctx* cc, hipStream_t st) : c(cc), old(cc->stream) { c->stream = st; }
+      ~OnStream() { c->stream = old; }
+    } on_sl(L->G.c, sl);
     CHK(prep_clients(L->G.c, L->prep_buf, L->G.lp, who, nullptr, &L->prep_stage, &L->prep_stage_ev));
     for (DrlTeam* t : involved) {   // the new keys into the team's parts; the emptied localCache indexes
       CHK(group_upload_parts_async(t->G, sl, t->parts_stage, t->parts_stage_ev));
@@ -4439,7 +4487,7 @@ static int run_batched_dev(pm_graph** gs, uint32_t S, const float* queries, uint
     }
     HIPCHK(hipEventRecord(ps.b, sl));
     for (DrlTeam* t : involved)
-      if (t != L) HIPCHK(hipStreamWaitEvent(t->G.c->stream, ps.b, 0));
+      if (t != L || pst) HIPCHK(hipStreamWaitEvent(t == L ? on_sl.old : t->G.c->stream, ps.b, 0));
   }
   if (!teams.empty() && teams[0]->ans_st) HIPCHK(hipStreamSynchronize(teams[0]->ans_st));
   for (auto& t : teams) CHK(drl_team_finish(*t, q, k, answers));
