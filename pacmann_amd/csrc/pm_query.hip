@@ -1423,6 +1423,10 @@ __global__ void __launch_bounds__(kResolveBlockG) k_match_resolve(PmStep S) {
 #ifndef PM_MR_G
 #define PM_MR_G 8       // search rows of 8 / NU sub-queries per round trip (0: see above)
 #endif
+#ifndef PM_MR_EARLY
+#define PM_MR_EARLY 1   // k_match_resolve_s: row block 0 first, the rest only where fewer than two matches
+                        // (+0.6 %, ABBA, profiles/r05/ab/match_early_exit.log)
+#endif
 #ifndef PM_MR_NT
 #define PM_MR_NT 1   // k_match_resolve_s' search-row loads nontemporal: streamed, not kept in the Infinity Cache
                      // the answer's DB rows reuse (with PM_REFRESH_NT +2.0 %, ABBA, profiles/r05/ab/nontemporal_*)
@@ -1505,7 +1509,9 @@ __global__ void __launch_bounds__(NT) k_match_resolve_s(PmStep S) {
   // the batch's loads were serialised.)
   PmSub mine{0, SUB_NONE, 0};
   if (lane < n) mine = step_sub(S, b0 + lane);
-  // the match: sub-queries j0 .. j0 + G - 1 at a time
+  // the match: sub-queries j0 .. j0 + G - 1 at a time, over the row blocks u
+  // in umask of the sub-queries in jmask (bit j)
+  auto match_pass = [&](uint32_t umask, uint64_t jmask) {
   for (uint32_t j0 = 0; j0 < n; j0 += G) {
     uint32_t cand = kNone;   // lane q: candidate i = q % 2 of (g, u) = (q / (2 NU), (q / 2) % NU)
     uint32_t off[G];
@@ -1516,14 +1522,14 @@ __global__ void __launch_bounds__(NT) k_match_resolve_s(PmStep S) {
       const uint32_t kind = j0 + g < n ? (uint32_t)__builtin_amdgcn_readlane(mine.kind, jj) : (uint32_t)SUB_NONE;
       const uint64_t idx = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(mine.idx >> 32), jj) << 32) |
                            (uint32_t)__builtin_amdgcn_readlane((uint32_t)mine.idx, jj);
-      const bool lv = kind == SUB_REAL && idx < P.N;
+      const bool lv = kind == SUB_REAL && idx < P.N && j0 + g < 64 && ((jmask >> (j0 + g)) & 1);
       off[g] = lv ? (uint32_t)(idx & mask) : kNone;
       const PM_G uint16_t* crow = P.cur + cur_row(P.PH, lv ? (uint32_t)(idx >> lg) : 0u);
 #pragma unroll
       for (int u = 0; u < NU; ++u) {
         const uint32_t h = (u * NT + tid) * 8;
         v[g][u] = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);   // kSkip x 8
-        if (lv && h < P.PH) {
+        if (lv && ((umask >> u) & 1) && h < P.PH) {
           typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
           const PM_G u32x4* src = reinterpret_cast<const PM_G u32x4*>(crow + cur_row_off(h));
           const u32x4 x = PM_MR_NT ? __builtin_nontemporal_load(src) : *src;
@@ -1568,11 +1574,35 @@ __global__ void __launch_bounds__(NT) k_match_resolve_s(PmStep S) {
     uint32_t ct = 0, cp = 0;
     if (PM_MR_TAGPF && cand != kNone) { ct = P.tag[cand]; cp = P.pp[cand]; }
     const uint32_t qg = lane / (2 * NU), qu = (lane / 2) % NU, qi = lane % 2;
-    if (lane < 2 * G * NU && j0 + qg < n) {
+    if (lane < 2 * G * NU && j0 + qg < n && ((umask >> qu) & 1) && ((jmask >> (j0 + qg)) & 1)) {
       s_m[j0 + qg][qu][wave][qi] = cand;
       if (PM_MR_TAGPF) { s_mt[j0 + qg][qu][wave][qi % 2] = ct; s_mp[j0 + qg][qu][wave][qi % 2] = cp; }
     }
   }
+  };
+#if PM_MR_EARLY
+  // Row block 0 first (hints 0 .. 8 NT - 1); the other blocks only for the
+  // sub-queries with fewer than two matches there (the candidates are the
+  // first two in hint order): ~9 % of them at SIFT1M's PH, and ~40 % fewer
+  // search-row bytes per step for one more round trip where any needs them
+  match_pass(1u, ~0ull);
+  if (NU > 1) {
+    for (uint32_t x = tid; x < n * (NU - 1) * NW * 2; x += NT) {   // the other blocks' slots: none yet
+      const uint32_t j = x / ((NU - 1) * NW * 2), r = x % ((NU - 1) * NW * 2);
+      s_m[j][1 + r / (NW * 2)][(r / 2) % NW][r % 2] = kNone;
+    }
+    __syncthreads();
+    uint64_t need = 0;
+    for (uint32_t j = 0; j < n && j < 64; ++j) {
+      uint32_t c = 0;
+      for (int w = 0; w < NW; ++w) c += (s_m[j][0][w][0] != kNone) + (s_m[j][0][w][1] != kNone);
+      if (L.s_kind[j] == SUB_REAL && c < 2) need |= 1ull << j;
+    }
+    if (need) match_pass(((1u << NU) - 1) & ~1u, need);   // block-uniform (from LDS)
+  }
+#else
+  match_pass((1u << NU) - 1, ~0ull);
+#endif
   MRST(2);
   __syncthreads();
   MRST(3);
