@@ -36,6 +36,7 @@ import argparse
 import json
 import os
 import sys
+import tempfile
 import time
 from pathlib import Path
 
@@ -753,6 +754,45 @@ def composite_floor(ktime, S, queries_per_session, pir, value_per_gpu, ss_r2=Non
                     "cadence); frac = value per GPU x floor"}
 
 
+def read_timeline(path):
+    """Per kernel of a pm_timing_timeline file: launches, summed and union
+    milliseconds; "query_phase": the span before the first maintenance kernel
+    and the share of it with any kernel running."""
+    rows = []
+    with open(path) as f:
+        for ln in f:
+            n, a, b, _ = ln.strip().split(",")
+            rows.append((float(a), float(b), n))
+    if not rows:
+        return {}
+
+    def union(iv):
+        tot, cs, ce = 0.0, None, None
+        for a, b in sorted(iv):
+            if ce is None or a > ce:
+                if ce is not None:
+                    tot += ce - cs
+                cs, ce = a, b
+            else:
+                ce = max(ce, b)
+        return tot + (ce - cs if ce is not None else 0.0)
+
+    out = {}
+    for n in sorted({r[2] for r in rows}):
+        iv = [(a, b) for a, b, m in rows if m == n]
+        out[n] = {"launches": len(iv), "sum_ms": round(sum(b - a for a, b in iv) / 1e3, 3),
+                  "union_ms": round(union(iv) / 1e3, 3)}
+    t0 = min(r[0] for r in rows)
+    prep = [a for a, b, n in rows if n.startswith("prep_")]
+    if prep:
+        t1 = min(prep)
+        q = [(a, min(b, t1)) for a, b, n in rows if a < t1]
+        out["query_phase"] = {"ms": round((t1 - t0) / 1e3, 3),
+                              "busy_frac": round(union(q) / max(t1 - t0, 1e-9), 4),
+                              "note": "kernel-timing pass before its maintenance: share with any kernel running"}
+    return out
+
+
 def rccl_group(dist, local, out):
     """An RCCL (nccl backend) group over all ranks for the sharded blocks'
     combine, or None (the shards then combine over the gloo group).  RCCL
@@ -940,7 +980,7 @@ def main():
     ap.add_argument("--no-msmarco-search", action="store_true", help="skip the MS-MARCO d=192 private-search block")
     ap.add_argument("--ms-sessions", type=int, default=0, help="MS-MARCO private-search sessions (0: MS_SESSIONS)")
     ap.add_argument("--ms-groups", type=int, default=0, help="MS-MARCO private-search lock-step teams (0: MS_GROUPS)")
-    ap.add_argument("--stagger-teams", action="store_true",
+    ap.add_argument("--stagger-teams", action="store_true", default=os.environ.get("PM_BENCH_STAGGER") == "1",
                     help="desynchronise the teams' maintenance windows (extra warm-up queries per team)")
     ap.add_argument("--graph", choices=["built", "random"], default="built",
                     help="GPU-built kNN+robustPrune graph (default) or the reference's synthetic random graph")
@@ -1033,6 +1073,7 @@ def main():
     ktime = {k: tsum(k) for k in KERNELS}
     kt_wall = elapsed   # the wall time the kernels were timed over
     kt_pass = None
+    kt_timeline = None
     if not in_value and not args.no_kernel_timing:
         # the kernel-timing pass: KT_QUERIES more queries of every session with
         # events on every launch (one maintenance of every session inside)
@@ -1050,9 +1091,19 @@ def main():
         tk = time.perf_counter() - tk
         for c in ctxs:
             c.timing(False)
-        if os.environ.get("PM_TIMELINE"):   # diagnostics: the pass's GPU timeline (tools/timeline.py)
+        # the pass's GPU timeline (every timed launch's start / end: the
+        # answers' union time and the query phase's busy share, below;
+        # PM_TIMELINE=<file> keeps it for tools/timeline.py)
+        tl_path = os.environ.get("PM_TIMELINE") or os.path.join(
+            tempfile.gettempdir(), f"pm_timeline_{os.getpid()}.csv")
+        try:
             for c in ctxs:
-                c.timing_timeline(os.environ["PM_TIMELINE"])
+                c.timing_timeline(tl_path)
+            kt_timeline = read_timeline(tl_path)
+        except Exception as e:   # diagnostics only
+            kt_timeline = {"error": f"{type(e).__name__}: {e}"}
+        if not os.environ.get("PM_TIMELINE") and os.path.exists(tl_path):
+            os.remove(tl_path)
         ktime = {k: tsum(k) for k in KERNELS}
         kt_pass = {"queries_per_session": KT_QUERIES, "wall_s": round(tk, 4),
                    "private_queries_per_s": round(S * KT_QUERIES / tk, 2),
@@ -1208,6 +1259,19 @@ def main():
                                   "note": "answer bytes of every step of the kernel-timing pass / its wall time"
                                           if kt_pass else "answer bytes of every step in the timed region / its "
                                           "wall time"}
+    if main_roof and main_roof["kernel"] == ans_k and isinstance(kt_timeline, dict) and "answer" in kt_timeline:
+        # The device loop overlaps the teams' answers (1-2 in flight most of the
+        # query phase), so a launch's own duration overstates its cost: the
+        # answers' union time is what they take of the GPU
+        u = kt_timeline["answer"]
+        if u["union_ms"] > 0:
+            ach = u["launches"] * main_roof["alg_bytes_per_launch"] / (u["union_ms"] / 1e3) / 1e9
+            main_roof["union"] = {
+                "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
+                "effective_us_per_launch": round(u["union_ms"] * 1e3 / u["launches"], 2),
+                "launches": u["launches"], "union_ms": u["union_ms"],
+                "note": "answer bytes of the kernel-timing pass over the union of its answer launches' "
+                        "[start, end] intervals (the GPU time during which any answer ran)"}
     if main_roof and not args.no_kernel_timing:
         main_roof["composite"] = composite_floor(ktime, S, kt_pass["queries_per_session"] if kt_pass else args.steps,
                                                  base.PIR, value / ws, ss_r2=base.PIR.SubConfig(0)["SetSize"])
@@ -1252,6 +1316,9 @@ def main():
                                           "steady state's (steps shorter than a window)"
                                           if prep_in_region < S else "at least one per session"},
         "kernel_timing_pass": kt_pass,
+        "kernel_timing_timeline": ({k: v for k, v in kt_timeline.items()
+                                    if k in ("answer", "match_resolve", "team_round", "query_phase", "error")}
+                                   if isinstance(kt_timeline, dict) else None),
         "maintenance_stagger": stagger,
         # result rows the host read at token time vs those whose bytes did not yet
         # match their header hash then; results are taken only after the step's

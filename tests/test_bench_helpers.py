@@ -1,0 +1,36 @@
+"""CPU checks of bench.py's own arithmetic: the timeline reader behind the
+answer roofline's `union` figure and the query phase's busy share."""
+import importlib.util
+import pathlib
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+
+
+def _bench():
+    spec = importlib.util.spec_from_file_location("pm_bench", ROOT / "bench.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_read_timeline_union_and_busy(tmp_path):
+    f = tmp_path / "tl.csv"
+    # two overlapping answers (union 150 us of 200 summed), a gap, maintenance after 300 us
+    f.write_text("answer,0,100,0x1\n"
+                 "answer,50,150,0x2\n"
+                 "match_resolve,150,170,0x1\n"
+                 "team_round,170,200,0x1\n"
+                 "prep_offsets,300,400,0x1\n"
+                 "prep_fold,400,600,0x1\n")
+    t = _bench().read_timeline(str(f))
+    assert t["answer"] == {"launches": 2, "sum_ms": 0.2, "union_ms": 0.15}
+    assert t["prep_fold"]["union_ms"] == 0.2
+    qp = t["query_phase"]
+    assert qp["ms"] == 0.3 and abs(qp["busy_frac"] - 200 / 300) < 1e-3
+
+
+def test_read_timeline_no_maintenance(tmp_path):
+    f = tmp_path / "tl.csv"
+    f.write_text("answer,10,20,0x1\nanswer,30,40,0x1\n")
+    t = _bench().read_timeline(str(f))
+    assert t["answer"]["union_ms"] == 0.02 and "query_phase" not in t
