@@ -3711,13 +3711,17 @@ static hipStream_t team_stream(int dev, uint32_t t) {
   static std::mutex mu;
   static std::vector<hipStream_t> pool[64];
   static const int on = [] { const char* e = getenv("PM_TEAM_STREAMS"); return e ? atoi(e) : 1; }();
-  if ((!on && !prep_cus()) || dev < 0 || dev >= 64) return nullptr;
+  // PM_TEAM_CUS=1: the teams on the complement of the maintenance's CUs
+  // (a static split; default: the teams keep every CU)
+  static const int split = [] { const char* e = getenv("PM_TEAM_CUS"); return e ? atoi(e) : 0; }();
+  if ((!on && !(prep_cus() && split)) || dev < 0 || dev >= 64) return nullptr;
   std::lock_guard<std::mutex> lk(mu);
   std::vector<hipStream_t>& v = pool[dev];
   if (v.empty()) {
     for (int i = 0; i < 8; ++i) {
       hipStream_t st = nullptr;
-      if (prep_cus()) st = masked_stream(dev, (uint32_t)prep_cus(), true);
+      if (prep_cus() && split) st = masked_stream(dev, (uint32_t)prep_cus(), true);
+      else if (on == 2) st = masked_stream(dev, 1u << 16, false);   // every CU: a CU-masked stream's own queue
       else if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) st = nullptr;
       if (!st) break;
       v.push_back(st);
