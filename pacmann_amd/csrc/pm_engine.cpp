@@ -619,7 +619,8 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
     ph.d.hist = (uint32_t*)(uintptr_t)off_hist; off_hist += ph.d.SS;
     ph.d.arena = (uint64_t*)(uintptr_t)off_ar; off_ar += (uint64_t)ph.d.MaxQ * g->E;
     ph.d.tab = (uint16_t*)(uintptr_t)off_tab; off_tab += (uint64_t)ph.d.H * ph.d.SS;
-    ph.d.cur = (uint16_t*)(uintptr_t)off_cur; off_cur += cur_words(ph.d.PH, ph.d.SS);
+    ph.d.curk = cur_k(ph.d.PH, ph.d.SS);
+    ph.d.cur = (uint16_t*)(uintptr_t)off_cur; off_cur += cur_words(ph.d.PH, ph.d.SS, ph.d.curk);
     ph.d.tabT = (uint16_t*)(uintptr_t)off_tabT; off_tabT += tabT_words(ph.d.H, ph.d.SS);
     ph.cache.reserve(ph.d.MaxQ);
   }

@@ -77,7 +77,7 @@ struct PmPart {
   uint64_t seed;     // randomness seed (keys, replacement, dummy)
   uint64_t epoch;    // preprocessing epoch in use
   uint64_t idx;      // partition index (stream domain)
-  uint32_t CS, log2CS, SS, PH, Qpc, H, MaxQ, pad;
+  uint32_t CS, log2CS, SS, PH, Qpc, H, MaxQ, curk;   // curk: chunks per hint-search block (cur_index)
   uint32_t rk[44];   // expanded AES-128 key (expandKeyAsm layout)
   // client state, device-resident
   PM_G uint32_t* tag;     // [H]   short tags (primary tags mutate on refresh)
@@ -132,19 +132,25 @@ __host__ __device__ inline uint64_t tabT_words(uint32_t H, uint32_t SS) { return
 // tools/gather_bench.hip regw_*), while a row's reads stay whole 16-B blocks
 // (every other one: twice the row's bytes through L2).
 #ifndef PM_CUR_K
-#define PM_CUR_K 2   // chunks interleaved per 16-B hint block (1: round 4's row-major table)
+#define PM_CUR_K 0   // chunks interleaved per 16-B hint block: 0 = chosen per partition (cur_k), else forced
 #endif
-constexpr uint32_t kCurK = PM_CUR_K;
-static_assert(kCurK == 1 || kCurK == 2 || kCurK == 4, "chunk group of the hint-search table");
-__host__ __device__ inline uint32_t cur_blocks(uint32_t PH) { return (PH + 7) >> 3; }
-__host__ __device__ inline uint64_t cur_index(uint32_t PH, uint32_t c, uint32_t h) {
-  return (((uint64_t)(c / kCurK) * cur_blocks(PH) + (h >> 3)) * kCurK + (c % kCurK)) * 8 + (h & 7);
+// K chunks interleaved: a refresh writes SS / K lines, a search reads K x its
+// row.  K = 2 unless the row (PH x 2 B) outweighs the column's lines (SS x
+// 128 B): BIGANN-100M's 57,344-hint rows read twice cost the hint search more
+// than the halved refresh saves (k_match_part8 34 -> 55 us per team step)
+__host__ __device__ inline uint32_t cur_k(uint32_t PH, uint32_t SS) {
+  return PM_CUR_K ? PM_CUR_K : ((uint64_t)PH * 2 > (uint64_t)SS * 128 ? 1u : 2u);
 }
-// chunk c's row: hint h at row[cur_row_off(h)], block b (8 hints) at row + 8 K b
-__host__ __device__ inline uint64_t cur_row(uint32_t PH, uint32_t c) { return cur_index(PH, c, 0); }
-__host__ __device__ inline uint32_t cur_row_off(uint32_t h) { return (h >> 3) * 8 * kCurK + (h & 7); }
-__host__ __device__ inline uint64_t cur_words(uint32_t PH, uint32_t SS) {
-  return (uint64_t)((SS + kCurK - 1) / kCurK) * cur_blocks(PH) * 8 * kCurK;
+__host__ __device__ inline uint32_t cur_blocks(uint32_t PH) { return (PH + 7) >> 3; }
+__host__ __device__ inline uint64_t cur_index(uint32_t PH, uint32_t K, uint32_t c, uint32_t h) {
+  return K == 2 ? (((uint64_t)(c >> 1) * cur_blocks(PH) + (h >> 3)) * 2 + (c & 1)) * 8 + (h & 7)
+                : (((uint64_t)(c / K) * cur_blocks(PH) + (h >> 3)) * K + (c % K)) * 8 + (h & 7);
+}
+// chunk c's row: hint h at row[cur_row_off(K, h)], block b (8 hints) at row + 8 K b
+__host__ __device__ inline uint64_t cur_row(uint32_t PH, uint32_t K, uint32_t c) { return cur_index(PH, K, c, 0); }
+__host__ __device__ inline uint32_t cur_row_off(uint32_t K, uint32_t h) { return (h >> 3) * 8 * K + (h & 7); }
+__host__ __device__ inline uint64_t cur_words(uint32_t PH, uint32_t SS, uint32_t K) {
+  return (uint64_t)((SS + K - 1) / K) * cur_blocks(PH) * 8 * K;
 }
 
 // Sub-query kinds / statuses for one batched step.

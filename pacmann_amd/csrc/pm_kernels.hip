@@ -80,7 +80,7 @@ __global__ void __launch_bounds__(kOffsBlock) k_prep_offsets(const PmPart* __res
       v = (c == own) ? kSkip : v;
       if (o) o[(uint64_t)c * H + h] = v;   // chunk-major (only the folds that stage it read it)
       tile[c - c0] = v;
-      if (h < P.PH) P.cur[cur_index(P.PH, c, h)] = v;   // hint search (tags start at h)
+      if (h < P.PH) P.cur[cur_index(P.PH, P.curk, c, h)] = v;   // hint search (tags start at h)
     }
     uint4 t4;   // tag-major tile (set expansion): one 16-B store
     t4.x = tile[0] | ((uint32_t)tile[1] << 16); t4.y = tile[2] | ((uint32_t)tile[3] << 16);

@@ -276,7 +276,7 @@ __device__ __forceinline__ void match_role(const PmStep& S, uint32_t s, uint32_t
   STAMP_AT(stamp_wg, 42);
   const uint32_t mask = P.CS - 1, chunk = (uint32_t)(sub.idx >> P.log2CS),
                  offset = (uint32_t)(sub.idx & mask);
-  const PM_G uint16_t* crow = P.cur + cur_row(P.PH, chunk);   // the hint search row of this chunk
+  const PM_G uint16_t* crow = P.cur + cur_row(P.PH, P.curk, chunk);   // the hint search row of this chunk
   const bool live = sub.idx < P.N;
   // Block 0 of a sub-query also prepares k_resolve's prediction: its chunk's
   // QueryHistogram now, the rest below (loads overlap the match loads).
@@ -291,7 +291,7 @@ __device__ __forceinline__ void match_role(const PmStep& S, uint32_t s, uint32_t
 #pragma unroll
   for (int u = 0; u < kMatchHPT; ++u) {
     const uint32_t h = base + u * NT + threadIdx.x;
-    rv[u] = (live && h < P.PH) ? crow[cur_row_off(h)] : kSkip;
+    rv[u] = (live && h < P.PH) ? crow[cur_row_off(P.curk, h)] : kSkip;
   }
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (meta_wg && wave == 0) {
@@ -475,11 +475,11 @@ __device__ __forceinline__ void match_part_block(const PmStep& S, const PmPart& 
       const bool lv = act && kind[g] == SUB_REAL && idx < P.N;
       const uint32_t chk = (uint32_t)(idx >> lg);
       off[g] = (uint32_t)(idx & mask);
-      const PM_G uint16_t* crow = P.cur + cur_row(P.PH, chk);
+      const PM_G uint16_t* crow = P.cur + cur_row(P.PH, P.curk, chk);
 #pragma unroll
       for (int u = 0; u < HPT; ++u) {
         const uint32_t h = base + u * NT + tid;
-        rv[g][u] = (lv && h < P.PH) ? crow[cur_row_off(h)] : kSkip;
+        rv[g][u] = (lv && h < P.PH) ? crow[cur_row_off(P.curk, h)] : kSkip;
       }
     }
 #pragma unroll
@@ -624,14 +624,14 @@ __global__ void __launch_bounds__(64 * NW, PM_MATCHPART8_WAVES) k_match_part8(Pm
                            __builtin_amdgcn_readfirstlane((uint32_t)sub.idx);
       const bool lv = kind[g] == SUB_REAL && idx < P.N;
       off[g] = (uint32_t)(idx & mask);
-      // (16-B blocks of the row are 32 B apart: cur_index)
-      const PM_G uint4* crow = reinterpret_cast<const PM_G uint4*>(P.cur + cur_row(P.PH, (uint32_t)(idx >> lg)));
+      // (16-B blocks of the row are 16 curk B apart: cur_index)
+      const PM_G uint4* crow = reinterpret_cast<const PM_G uint4*>(P.cur + cur_row(P.PH, P.curk, (uint32_t)(idx >> lg)));
       // unconditional 16-B loads (a dead lane reads the partition's first
       // vector), then kSkip x 8 by value: a select of the loaded VALUE keeps
       // them global_load_dwordx4
       const bool okA = lv && hA < P.PH, okB = lv && hB < P.PH;
-      const uint4 a = okA ? crow[(hA >> 3) * kCurK] : *reinterpret_cast<const PM_G uint4*>(P.cur);
-      const uint4 b = okB ? crow[(hB >> 3) * kCurK] : *reinterpret_cast<const PM_G uint4*>(P.cur);
+      const uint4 a = okA ? crow[(hA >> 3) * P.curk] : *reinterpret_cast<const PM_G uint4*>(P.cur);
+      const uint4 b = okB ? crow[(hB >> 3) * P.curk] : *reinterpret_cast<const PM_G uint4*>(P.cur);
       rv[g][0] = okA ? a : make_uint4(~0u, ~0u, ~0u, ~0u);
       rv[g][1] = okB ? b : make_uint4(~0u, ~0u, ~0u, ~0u);
     }
@@ -722,12 +722,12 @@ __device__ __forceinline__ uint32_t find_next_g(const PmStep& S, uint64_t sub, u
 // before the step's k_answer).  One wave, 8 hints per lane (PH % 8 == 0).
 __device__ __forceinline__ uint32_t find_cur(const PmPart& P, uint32_t chunk, uint32_t off, uint32_t start) {
   const uint32_t lane = threadIdx.x & 63;
-  const PM_G uint16_t* row = P.cur + cur_row(P.PH, chunk);
+  const PM_G uint16_t* row = P.cur + cur_row(P.PH, P.curk, chunk);
   for (uint32_t h0 = start & ~7u; h0 < P.PH; h0 += 512) {
     const uint32_t h = h0 + lane * 8;
     uint32_t f = kNone;
     if (h < P.PH) {
-      const uint4 v = *reinterpret_cast<const PM_G uint4*>(row + cur_row_off(h));
+      const uint4 v = *reinterpret_cast<const PM_G uint4*>(row + cur_row_off(P.curk, h));
       const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int e = 7; e >= 0; --e) {
@@ -1524,14 +1524,14 @@ __global__ void __launch_bounds__(NT) k_match_resolve_s(PmStep S) {
                            (uint32_t)__builtin_amdgcn_readlane((uint32_t)mine.idx, jj);
       const bool lv = kind == SUB_REAL && idx < P.N && j0 + g < 64 && ((jmask >> (j0 + g)) & 1);
       off[g] = lv ? (uint32_t)(idx & mask) : kNone;
-      const PM_G uint16_t* crow = P.cur + cur_row(P.PH, lv ? (uint32_t)(idx >> lg) : 0u);
+      const PM_G uint16_t* crow = P.cur + cur_row(P.PH, P.curk, lv ? (uint32_t)(idx >> lg) : 0u);
 #pragma unroll
       for (int u = 0; u < NU; ++u) {
         const uint32_t h = (u * NT + tid) * 8;
         v[g][u] = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);   // kSkip x 8
         if (lv && ((umask >> u) & 1) && h < P.PH) {
           typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-          const PM_G u32x4* src = reinterpret_cast<const PM_G u32x4*>(crow + cur_row_off(h));
+          const PM_G u32x4* src = reinterpret_cast<const PM_G u32x4*>(crow + cur_row_off(P.curk, h));
           const u32x4 x = PM_MR_NT ? __builtin_nontemporal_load(src) : *src;
           v[g][u] = make_uint4(x.x, x.y, x.z, x.w);
         }
@@ -1787,7 +1787,7 @@ enum : uint32_t { A_ZERO = 0, A_FINAL = 1, A_CHAINED = 2, A_CACHED = 3, A_DUMMY 
 // clear); read by the next step's hint search, after this launch ends.
 __device__ __forceinline__ void refresh_cur(const PmPart& P, const PmRes& r, uint32_t tid, uint32_t nt) {
   const uint32_t ntag = P.PH + r.chunk * P.Qpc + r.ing;
-  for (uint32_t c = tid; c < P.SS; c += nt) P.cur[cur_index(P.PH, c, r.hit)] = P.tabT[tabT_index(P.H, ntag, c)];
+  for (uint32_t c = tid; c < P.SS; c += nt) P.cur[cur_index(P.PH, P.curk, c, r.hit)] = P.tabT[tabT_index(P.H, ntag, c)];
 }
 
 // Decode one chained sub-query (its hint was refreshed earlier in this step)
@@ -2037,9 +2037,9 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, LDS& L)
       const uint32_t ch = (uint32_t)(sub.idx >> lg), off = (uint32_t)(sub.idx & mask);
       const uint32_t wave = tid >> 6, lane = tid & 63;
       uint32_t rv[HPT];
-      const PM_G uint16_t* crow = P.cur + cur_row(P.PH, ch);   // match: value == offset (see match_role)
+      const PM_G uint16_t* crow = P.cur + cur_row(P.PH, P.curk, ch);   // match: value == offset (see match_role)
 #pragma unroll
-      for (int u = 0; u < HPT; ++u) rv[u] = u * NT + tid < P.PH ? crow[cur_row_off(u * NT + tid)] : kNone;
+      for (int u = 0; u < HPT; ++u) rv[u] = u * NT + tid < P.PH ? crow[cur_row_off(P.curk, u * NT + tid)] : kNone;
       const uint32_t h0k = wave == 0 ? P.hist[ch] : 0;
       // per wave the lowest matching hint (lower u first: hints u*NT + tid)
       uint32_t wh = kNone, wt = 0, wp = 0;
@@ -2099,7 +2099,7 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, LDS& L)
   // ---- decode + refresh, or the cached row -----------------------------
   if (mode == A_FINAL) {
     if (!(r.flags & 2u)) {   // refresh_cur with the row prefetched with the decode operands
-      if (tid < P.SS) P.cur[cur_index(P.PH, tid, r.hit)] = (uint16_t)e_cur;
+      if (tid < P.SS) P.cur[cur_index(P.PH, P.curk, tid, r.hit)] = (uint16_t)e_cur;
       if (P.SS > NT) refresh_cur(P, r, tid + NT, NT);   // SetSize > workgroup (BIGANN): the rest
     }
     for (uint32_t w = tid; w < E; w += NT) {
@@ -2335,7 +2335,7 @@ __device__ __forceinline__ void ansp_epilogue(const PmStep& S, const AnsQ& a, LD
   if (mode == A_FINAL) {   // pir.go:450-468
     if (!(r.flags & 2u)) {
       if (tid < P.SS) {
-        PM_G uint16_t* dst = P.cur + cur_index(P.PH, tid, r.hit);
+        PM_G uint16_t* dst = P.cur + cur_index(P.PH, P.curk, tid, r.hit);
         if (PM_REFRESH_NT) __builtin_nontemporal_store((uint16_t)a.e_cur, dst);
         else *dst = (uint16_t)a.e_cur;
       }
