@@ -1427,8 +1427,8 @@ __global__ void __launch_bounds__(kResolveBlockG) k_match_resolve(PmStep S) {
 #define PM_MR_EARLY 1   // k_match_resolve_s: row block 0 first, the rest only where fewer than two matches
                         // (+0.6 %, ABBA, profiles/r05/ab/match_early_exit.log)
 #endif
-#ifndef PM_MR_NT
-#define PM_MR_NT 1   // k_match_resolve_s' search-row loads nontemporal: streamed, not kept in the Infinity Cache
+#ifndef PM_MR_NTLOAD
+#define PM_MR_NTLOAD 1   // k_match_resolve_s' search-row loads nontemporal: streamed, not kept in the Infinity Cache
                      // the answer's DB rows reuse (with PM_REFRESH_NT +2.0 %, ABBA, profiles/r05/ab/nontemporal_*)
 #endif
 #ifndef PM_REFRESH_NT
@@ -1532,7 +1532,7 @@ __global__ void __launch_bounds__(NT) k_match_resolve_s(PmStep S) {
         if (lv && ((umask >> u) & 1) && h < P.PH) {
           typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
           const PM_G u32x4* src = reinterpret_cast<const PM_G u32x4*>(crow + cur_row_off(P.curk, h));
-          const u32x4 x = PM_MR_NT ? __builtin_nontemporal_load(src) : *src;
+          const u32x4 x = PM_MR_NTLOAD ? __builtin_nontemporal_load(src) : *src;
           v[g][u] = make_uint4(x.x, x.y, x.z, x.w);
         }
       }
