@@ -34,3 +34,41 @@ def test_read_timeline_no_maintenance(tmp_path):
     f.write_text("answer,10,20,0x1\nanswer,30,40,0x1\n")
     t = _bench().read_timeline(str(f))
     assert t["answer"]["union_ms"] == 0.02 and "query_phase" not in t
+
+
+def _run_watchdog(body: str):
+    import json
+    import subprocess
+    import sys
+    import time
+    code = ("import importlib.util, sys, time\n"
+            f"spec = importlib.util.spec_from_file_location('pm_bench', {str(ROOT / 'bench.py')!r})\n"
+            "b = importlib.util.module_from_spec(spec); spec.loader.exec_module(b)\n" + body)
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r.returncode, [json.loads(ln) for ln in lines], time.monotonic() - t0
+
+
+def test_watchdog_writes_the_partial_line_and_exits():
+    """A stuck multi-rank block: the watchdog writes the one line (the blocks
+    marked unfinished) and ends the process, instead of a hang."""
+    rc, lines, dt = _run_watchdog(
+        "out = {'metric': 'm', 'value': 1.0}\n"
+        "wd = b.Watchdog(out, 0, 1, 0.3)\n"
+        "time.sleep(30)\n"
+        "print('not reached')\n")
+    assert rc == 0 and len(lines) == 1, (rc, lines)
+    assert lines[0]["value"] == 1.0
+    assert "unfinished" in lines[0]["config3_bigann_100m"]["error"]
+    assert dt < 25
+
+
+def test_watchdog_fire_before_the_budget():
+    rc, lines, _ = _run_watchdog(
+        "out = {'metric': 'm', 'value': 2.0}\n"
+        "wd = b.Watchdog(out, 0, 1, 5.0)\n"
+        "assert wd.fire() is True\n"
+        "assert wd.fire() is False\n"
+        "import json; print(json.dumps({'finished': True}))\n")
+    assert rc == 0 and lines == [{"finished": True}]
