@@ -3684,13 +3684,14 @@ struct PoolTeam {
 // turn.  Meant with the teams' maintenance windows staggered (bench.py
 // --stagger-teams).  0: off.  PM_CU_MAP: how mask bits map to XCDs (0: 32
 // consecutive bits per XCD, 1: bit i on XCD i % 8); X / 8 CUs are taken from
-// every XCD either way.
+// every XCD either way (default 1).
 static int prep_cus() {
   static const int v = [] { const char* e = getenv("PM_PREP_CUS"); return e ? std::max(0, atoi(e)) : 0; }();
   return v;
 }
 static std::vector<uint32_t> cu_mask(int dev, uint32_t n, bool complement) {
-  static const int map = [] { const char* e = getenv("PM_CU_MAP"); return e ? atoi(e) : 0; }();
+  // (profiles/r05/cumask_bench.txt: one 32-bit mask word spans all 8 XCDs, i.e. bit i is on XCD i % 8)
+  static const int map = [] { const char* e = getenv("PM_CU_MAP"); return e ? atoi(e) : 1; }();
   int ncu = 256;
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   const uint32_t per = (uint32_t)ncu / 8, take = std::min(per, n / 8);
@@ -4427,11 +4428,31 @@ static int run_batched_dev(pm_graph** gs, uint32_t S, const float* queries, uint
     swaps[g].swap_in(teams.back()->G.c, team_stream(teams.back()->G.c->device, g));
   }
   static const int ans_stream = [] { const char* e = getenv("PM_ANSWER_STREAM"); return e ? atoi(e) : 0; }();
-  if (ans_stream && NG > 1) {   // the last stream of the pool (created first-to-last: its own hardware queue)
+  if (ans_stream == 1 && NG > 1) {   // the last stream of the pool (created first-to-last: its own hardware queue)
     hipStream_t as = team_stream(teams[0]->G.c->device, 7);
     for (auto& t : teams) {
       t->ans_st = as;
       for (auto& e : t->ans_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+  } else if (ans_stream >= 2) {
+    // PM_ANSWER_STREAM=2: each team's answers on a stream of its own limited to
+    // all CUs but PM_ANSWER_RESERVE_CUS (default 16, 2 per XCD), so the
+    // chain kernels (match + resolve, the team round) always find free slots
+    static const int reserve = [] { const char* e = getenv("PM_ANSWER_RESERVE_CUS"); return e ? atoi(e) : 16; }();
+    static std::vector<hipStream_t> ast[64];
+    const int dev = teams[0]->G.c->device;
+    int ncu = 256;
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (dev >= 0 && dev < 64) {
+      while (ast[dev].size() < teams.size()) {
+        hipStream_t st = masked_stream(dev, (uint32_t)std::max(8, ncu - reserve), false);
+        if (!st) break;
+        ast[dev].push_back(st);
+      }
+      for (size_t i = 0; i < teams.size() && i < ast[dev].size(); ++i) {
+        teams[i]->ans_st = ast[dev][i];
+        for (auto& e : teams[i]->ans_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      }
     }
   }
   // Maintenance launch sets, timed by events around them on the leader's stream
@@ -4494,7 +4515,8 @@ static int run_batched_dev(pm_graph** gs, uint32_t S, const float* queries, uint
     for (DrlTeam* t : involved)
       if (t != L || pst) HIPCHK(hipStreamWaitEvent(t == L ? on_sl.old : t->G.c->stream, ps.b, 0));
   }
-  if (!teams.empty() && teams[0]->ans_st) HIPCHK(hipStreamSynchronize(teams[0]->ans_st));
+  for (auto& t : teams)
+    if (t->ans_st) HIPCHK(hipStreamSynchronize(t->ans_st));
   for (auto& t : teams) CHK(drl_team_finish(*t, q, k, answers));
   for (PrepSet& ps : sets) {   // each triggered client's maintenance time: its launch set's span on the GPU
     float ms = 0;
