@@ -581,6 +581,9 @@ __device__ __forceinline__ uint32_t match8(uint4 v, uint32_t off) {
     m |= (((w[i] & 0xffffu) == off) ? 1u : 0u) << (2 * i) | (((w[i] >> 16) == off) ? 1u : 0u) << (2 * i + 1);
   return m;
 }
+#ifndef PM_MATCH8_NT
+#define PM_MATCH8_NT 0   // k_match_part8's search-row loads nontemporal
+#endif
 template <int NW>
 __global__ void __launch_bounds__(64 * NW, PM_MATCHPART8_WAVES) k_match_part8(PmStep S) {
   constexpr int G = PM_MATCHPART8_G;
@@ -630,8 +633,12 @@ __global__ void __launch_bounds__(64 * NW, PM_MATCHPART8_WAVES) k_match_part8(Pm
       // vector), then kSkip x 8 by value: a select of the loaded VALUE keeps
       // them global_load_dwordx4
       const bool okA = lv && hA < P.PH, okB = lv && hB < P.PH;
-      const uint4 a = okA ? crow[(hA >> 3) * P.curk] : *reinterpret_cast<const PM_G uint4*>(P.cur);
-      const uint4 b = okB ? crow[(hB >> 3) * P.curk] : *reinterpret_cast<const PM_G uint4*>(P.cur);
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      const PM_G u32x4* pa = reinterpret_cast<const PM_G u32x4*>(okA ? crow + (hA >> 3) * P.curk : reinterpret_cast<const PM_G uint4*>(P.cur));
+      const PM_G u32x4* pb = reinterpret_cast<const PM_G u32x4*>(okB ? crow + (hB >> 3) * P.curk : reinterpret_cast<const PM_G uint4*>(P.cur));
+      const u32x4 xa = PM_MATCH8_NT ? __builtin_nontemporal_load(pa) : *pa;
+      const u32x4 xb = PM_MATCH8_NT ? __builtin_nontemporal_load(pb) : *pb;
+      const uint4 a = make_uint4(xa.x, xa.y, xa.z, xa.w), b = make_uint4(xb.x, xb.y, xb.z, xb.w);
       rv[g][0] = okA ? a : make_uint4(~0u, ~0u, ~0u, ~0u);
       rv[g][1] = okB ? b : make_uint4(~0u, ~0u, ~0u, ~0u);
     }
@@ -2538,6 +2545,10 @@ __global__ void __launch_bounds__(NT, PM_ANSWER_P_WAVES) k_answer_p(PmStep S) {
 // rows are read by nsplit CUs instead of one.
 constexpr int kGatherBlock = 256;
 constexpr uint32_t kGatherMaxRange = 4096;   // chunks per workgroup (SetSize / nsplit; BIGANN-1B: 3,816 at nsplit 1)
+#ifndef PM_GATHER_NT
+#define PM_GATHER_NT 1   // k_gather's row loads nontemporal (BIGANN: a 32-64 GB DB, no Infinity Cache reuse):
+                         // 100M +3.2 %, 1B +0.7 % (ABBA, profiles/r05/ab/bigann_gather_nt.log)
+#endif
 #ifndef PM_GATHER_KG
 #define PM_GATHER_KG 8
 #endif
@@ -2601,8 +2612,9 @@ __global__ void __launch_bounds__(kGatherBlock, PM_GATHER_WAVES) k_gather(PmStep
           x[u] = u64x2{0, 0};
           if (rr[u] != ~0u) {
             const PM_G uint64_t* q = base + (uint64_t)rr[u] * E + (uint64_t)seg * W;
-            if (W == 2) x[u] = *reinterpret_cast<const PM_G u64x2*>(q);
-            else x[u].x = *q;
+            if (W == 2) x[u] = PM_GATHER_NT ? __builtin_nontemporal_load(reinterpret_cast<const PM_G u64x2*>(q))
+                                         : *reinterpret_cast<const PM_G u64x2*>(q);
+            else x[u].x = PM_GATHER_NT ? __builtin_nontemporal_load(q) : *q;
           }
         }
 #pragma unroll
