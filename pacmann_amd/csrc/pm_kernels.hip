@@ -89,6 +89,10 @@ __global__ void __launch_bounds__(kOffsBlock) k_prep_offsets(const PmPart* __res
   }
 }
 
+#ifndef PM_FOLD_NT
+#define PM_FOLD_NT 1   // k_prep_fold's (BIGANN's gather fold) row loads nontemporal: 221-222 -> 210-212 ms per
+                       // 100M client = 0.83 of HBM peak (profiles/r05/ab/fold_nt_100m)
+#endif
 template <int W>   // 64-bit words per lane segment: 2 (16-B loads) or 1
 __global__ void __launch_bounds__(kBlock) k_prep_fold(const PmPart* __restrict__ parts,
                                                       const uint64_t* __restrict__ db, uint32_t E) {
@@ -118,11 +122,13 @@ __global__ void __launch_bounds__(kBlock) k_prep_fold(const PmPart* __restrict__
       if (v[u] != kSkip && r < N) {
         const uint64_t* p = base + r * E;
         if (W == 2) {
-          uint4 x = *reinterpret_cast<const uint4*>(p);
+          typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+          const u32x4 x = PM_FOLD_NT ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p))
+                                     : *reinterpret_cast<const u32x4*>(p);
           a0 ^= ((uint64_t)x.y << 32) | x.x;
           a1 ^= ((uint64_t)x.w << 32) | x.z;
         } else {
-          a0 ^= *p;
+          a0 ^= PM_FOLD_NT ? __builtin_nontemporal_load(p) : *p;
         }
       }
     }
