@@ -4,6 +4,9 @@
 #include "pm_internal.h"
 
 namespace pm {
+#ifndef PM_PREP_NT
+#define PM_PREP_NT 0   // the maintenance's bulk stores (tabT tiles, the CS-512 fold's parities) nontemporal
+#endif
 
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
@@ -85,7 +88,12 @@ __global__ void __launch_bounds__(kOffsBlock) k_prep_offsets(const PmPart* __res
     uint4 t4;   // tag-major tile (set expansion): one 16-B store
     t4.x = tile[0] | ((uint32_t)tile[1] << 16); t4.y = tile[2] | ((uint32_t)tile[3] << 16);
     t4.z = tile[4] | ((uint32_t)tile[5] << 16); t4.w = tile[6] | ((uint32_t)tile[7] << 16);
-    *reinterpret_cast<uint4*>(P.tabT + tabT_index(H, h, c0)) = t4;
+    if (PM_PREP_NT) {
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      __builtin_nontemporal_store(u32x4{t4.x, t4.y, t4.z, t4.w}, reinterpret_cast<u32x4*>(P.tabT + tabT_index(H, h, c0)));
+    } else {
+      *reinterpret_cast<uint4*>(P.tabT + tabT_index(H, h, c0)) = t4;
+    }
   }
 }
 
@@ -737,9 +745,12 @@ __global__ void __launch_bounds__(kFoldThreads) k_prep_fold_rot(const PmPart* __
     PM_G uint64_t* const par = (inB ? PB.parity : PA.parity) + (uint64_t)(v - (inB ? vb : hA)) * E;
     PM_G uint32_t* dst = reinterpret_cast<PM_G uint32_t*>(par + w);
 #pragma unroll
-    for (int t = 0; t < 8; ++t)
-      dst[PM_ROT_B128 ? 4 * (j ^ (t >> 2)) + (t & 3)
-                      : PM_ROT_B64 ? 2 * (((j & 3) + t / 2) & 3) + (t & 1) : (j + t) & 7] = acc[k][t];
+    for (int t = 0; t < 8; ++t) {
+      PM_G uint32_t* const d = dst + (PM_ROT_B128 ? 4 * (j ^ (t >> 2)) + (t & 3)
+                                      : PM_ROT_B64 ? 2 * (((j & 3) + t / 2) & 3) + (t & 1) : (j + t) & 7);
+      if (PM_PREP_NT) __builtin_nontemporal_store(acc[k][t], d);
+      else *d = acc[k][t];
+    }
     if (w == 0)   // xorSlices leaves the words past len&~3 zero
       for (uint32_t t = E & ~3u; t < E; ++t) par[t] = 0;
   }
