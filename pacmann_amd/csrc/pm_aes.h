@@ -57,7 +57,11 @@ struct AesTables {
 // that | 0x80.  A lookup address is ONE v_perm_b32 (the state byte into byte
 // 1, the lane offset with the table bit in byte 0), and a ds_read_b32 lane
 // group (32 lanes, bank = (a/4) mod 32) reads 32 distinct banks.  64 KiB.
-constexpr int kTeLdsWords = 256 * 64;
+#ifndef PM_AES_4T
+#define PM_AES_4T 0   // all four T-tables in LDS (Te1 = rotl8 Te0, Te3 = rotl24 Te0 in a second 64 KiB):
+#endif                // no rotation or extra XOR per column, but 128 KiB per workgroup, i.e. 16 waves per CU
+                      // instead of 32: 76 vs 53.6 ms per 288-client launch (profiles/r05/ab/aes_four_tables.log)
+constexpr int kTeLdsWords = 256 * 64 * (PM_AES_4T ? 2 : 1);
 
 // Device copy of the tables (one per translation unit; read only by aes_lds_init).
 static constexpr AesTables kAesTablesHost{};
@@ -71,8 +75,9 @@ __device__ __forceinline__ uint32_t aes_x3(uint32_t a, uint32_t b, uint32_t c) {
 // Fill the replicated table.  Call with the whole block, then __syncthreads().
 __device__ __forceinline__ void aes_lds_init(uint32_t* te, const uint32_t* __restrict__ g_te0) {
   for (int i = threadIdx.x; i < kTeLdsWords; i += blockDim.x) {
-    const uint32_t t = g_te0[i >> 6];
-    te[i] = (i & 32) ? rotl32(t, 16) : t;
+    const uint32_t t = g_te0[(i >> 6) & 255];
+    te[i] = i < 256 * 64 ? ((i & 32) ? rotl32(t, 16) : t)     // Te0 | Te2
+                         : ((i & 32) ? rotl32(t, 24) : rotl32(t, 8));   // Te1 | Te3
   }
 }
 
@@ -92,6 +97,25 @@ struct AesLane {
     return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(te) + a);
   }
   template <int K> __device__ __forceinline__ uint32_t Sk(uint32_t s) const { return (Tk<K>(s) >> 8) & 0xffu; }
+  // PM_AES_4T: Te1 / Te3 [byte k of s] in the second 64 KiB (byte 2 of the
+  // address from the lane word: lane | 0x10000)
+  template <int K> __device__ __forceinline__ uint32_t T1k(uint32_t s) const {
+    const uint32_t a = __builtin_amdgcn_perm(s, lane | 0x10000u, 0x0c020000u | ((4u + K) << 8));
+    return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(te) + a);
+  }
+  template <int K> __device__ __forceinline__ uint32_t T3k(uint32_t s) const {
+    const uint32_t a = __builtin_amdgcn_perm(s, lane2 | 0x10000u, 0x0c020000u | ((4u + K) << 8));
+    return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(te) + a);
+  }
+  // one round column: Te0[a.b0] ^ Te1[b.b1] ^ Te2[c.b2] ^ Te3[d.b3] ^ k
+  __device__ __forceinline__ uint32_t col(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) const {
+#if PM_AES_4T
+    return __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(Tk<0>(a), T1k<1>(b), T2k<2>(c), 0x96), T3k<3>(d), k, 0x96);
+#else
+    return __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(Tk<0>(a), T2k<2>(c), k, 0x96),
+                                       rotl32(Tk<1>(b) ^ T2k<3>(d), 8), 0u, 0x96);
+#endif
+  }
 };
 
 // Full rounds R0..R1-1 on state (s0..s3) with round keys rk[4*R0..4*R1-1].
@@ -103,10 +127,10 @@ __device__ __forceinline__ void aes_rounds(const AesLane& A, const uint32_t* __r
     // Te0[a] ^ rotl8(Te0[b]) ^ rotl16(Te0[c]) ^ rotl24(Te0[d]) ^ rk
     //   = Te0[a] ^ Te2[c] ^ rotl8(Te0[b] ^ Te2[d]) ^ rk
     // (v_bitop3_b32 0x96 = three-input XOR on gfx950: 4 VALU per column instead of 5)
-    uint32_t t0 = aes_x3(aes_x3(A.Tk<0>(s0), A.T2k<2>(s2), rk[4 * r + 0]), rotl32(A.Tk<1>(s1) ^ A.T2k<3>(s3), 8), 0u);
-    uint32_t t1 = aes_x3(aes_x3(A.Tk<0>(s1), A.T2k<2>(s3), rk[4 * r + 1]), rotl32(A.Tk<1>(s2) ^ A.T2k<3>(s0), 8), 0u);
-    uint32_t t2 = aes_x3(aes_x3(A.Tk<0>(s2), A.T2k<2>(s0), rk[4 * r + 2]), rotl32(A.Tk<1>(s3) ^ A.T2k<3>(s1), 8), 0u);
-    uint32_t t3 = aes_x3(aes_x3(A.Tk<0>(s3), A.T2k<2>(s1), rk[4 * r + 3]), rotl32(A.Tk<1>(s0) ^ A.T2k<3>(s2), 8), 0u);
+    uint32_t t0 = A.col(s0, s1, s2, s3, rk[4 * r + 0]);
+    uint32_t t1 = A.col(s1, s2, s3, s0, rk[4 * r + 1]);
+    uint32_t t2 = A.col(s2, s3, s0, s1, rk[4 * r + 2]);
+    uint32_t t3 = A.col(s3, s0, s1, s2, rk[4 * r + 3]);
     s0 = t0; s1 = t1; s2 = t2; s3 = t3;
   }
 }
@@ -171,8 +195,8 @@ __device__ __forceinline__ uint32_t prf_lo16_split(const AesLane& A, const uint3
                                                    const R1Uniform& u, const R1Lane& v, uint32_t x) {
   uint32_t s0 = u.u0 ^ v.v0, s1 = u.u1 ^ v.v1, s2 = u.u2 ^ v.v2, s3 = u.u3 ^ v.v3;
   aes_rounds<2, 9>(A, rk, s0, s1, s2, s3);
-  const uint32_t t0 = aes_x3(aes_x3(A.Tk<0>(s0), A.T2k<2>(s2), rk[36]), rotl32(A.Tk<1>(s1) ^ A.T2k<3>(s3), 8), 0u);
-  const uint32_t t1 = aes_x3(aes_x3(A.Tk<0>(s1), A.T2k<2>(s3), rk[37]), rotl32(A.Tk<1>(s2) ^ A.T2k<3>(s0), 8), 0u);
+  const uint32_t t0 = A.col(s0, s1, s2, s3, rk[36]);
+  const uint32_t t1 = A.col(s1, s2, s3, s0, rk[37]);
   return ((A.Sk<0>(t0) | (A.Sk<1>(t1) << 8)) ^ rk[40] ^ x) & 0xffffu;
 }
 // Chunks x < 256 (SetSize <= 256: SIFT1M's 124, MS-MARCO's 196): after the
@@ -197,11 +221,16 @@ __device__ __forceinline__ R2Hint r2_hint(const AesLane& A, const uint32_t* __re
 __device__ __forceinline__ uint32_t prf_lo16_r2(const AesLane& A, const uint32_t* __restrict__ rk, uint32_t u0,
                                                 const R1Lane& v, const R2Hint& k, uint32_t x) {
   const uint32_t s = u0 ^ v.v0;
+#if PM_AES_4T
+  uint32_t s0 = A.Tk<0>(s) ^ k.k0, s1 = A.T3k<3>(s) ^ k.k1;   // rotl8(Te2) = Te3, rotl8(Te0) = Te1
+  uint32_t s2 = A.T2k<2>(s) ^ k.k2, s3 = A.T1k<1>(s) ^ k.k3;
+#else
   uint32_t s0 = A.Tk<0>(s) ^ k.k0, s1 = rotl32(A.T2k<3>(s), 8) ^ k.k1;
   uint32_t s2 = A.T2k<2>(s) ^ k.k2, s3 = rotl32(A.Tk<1>(s), 8) ^ k.k3;
+#endif
   aes_rounds<3, 9>(A, rk, s0, s1, s2, s3);
-  const uint32_t t0 = aes_x3(aes_x3(A.Tk<0>(s0), A.T2k<2>(s2), rk[36]), rotl32(A.Tk<1>(s1) ^ A.T2k<3>(s3), 8), 0u);
-  const uint32_t t1 = aes_x3(aes_x3(A.Tk<0>(s1), A.T2k<2>(s3), rk[37]), rotl32(A.Tk<1>(s2) ^ A.T2k<3>(s0), 8), 0u);
+  const uint32_t t0 = A.col(s0, s1, s2, s3, rk[36]);
+  const uint32_t t1 = A.col(s1, s2, s3, s0, rk[37]);
   return ((A.Sk<0>(t0) | (A.Sk<1>(t1) << 8)) ^ rk[40] ^ x) & 0xffffu;
 }
 }  // namespace pm
