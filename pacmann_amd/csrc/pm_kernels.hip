@@ -41,11 +41,15 @@ constexpr int kOffsBlock = 1024;   // 64 KiB of replicated table per workgroup: 
 // them the kernel is only 2 % faster).  1,024-thread workgroups share one 64 KiB
 // table copy (the LDS init is 4 B per PRF, not 16) and keep 16 waves per CU
 // for the lookups' latency: 0.370 -> 0.335 ms at SIFT1M shape.
+#ifndef PM_OFFS_PAIR
+#define PM_OFFS_PAIR 0   // k_prep_offsets: two chunks' PRFs per iteration (61 VGPRs at 8 waves: 56.5 vs 54.2 ms
+                         // per 288-client launch, profiles/r05/ab/aes_chunk_pairs.log)
+#endif
 #ifndef PM_OFFS_TILES
 #define PM_OFFS_TILES 1   // 8-chunk tiles per workgroup sharing one 64 KiB table fill (2 and 4 measured no faster: 244 / 268 vs 240 us per client alone)
 #endif
 constexpr int kOffsTiles = PM_OFFS_TILES;
-__global__ void __launch_bounds__(kOffsBlock) k_prep_offsets(const PmPart* __restrict__ parts) {
+__global__ void __launch_bounds__(kOffsBlock, PM_OFFS_PAIR ? 8 : 1) k_prep_offsets(const PmPart* __restrict__ parts) {
   __shared__ uint32_t te[kTeLdsWords];
   __shared__ R1Uniform r1u[kOffsTiles][kOffsChunksPerBlock];
   const PmPart& P = parts[blockIdx.z];
@@ -77,14 +81,33 @@ __global__ void __launch_bounds__(kOffsBlock) k_prep_offsets(const PmPart* __res
     uint16_t tile[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) tile[j] = kSkip;   // chunks past SetSize: padding
-    for (uint32_t c = c0; c < c1; ++c) {
-      uint16_t v = (uint16_t)((r2 ? prf_lo16_r2(A, P.rk, r1u[tl][c - c0].u0, r1v, r2k, c)
-                                  : prf_lo16_split(A, P.rk, r1u[tl][c - c0], r1v, c)) & mask);
+    auto put = [&](uint32_t c, uint32_t prf) {
+      uint16_t v = (uint16_t)(prf & mask);
       v = (c == own) ? kSkip : v;
       if (o) o[(uint64_t)c * H + h] = v;   // chunk-major (only the folds that stage it read it)
       tile[c - c0] = v;
       if (h < P.PH) P.cur[cur_index(P.PH, P.curk, c, h)] = v;   // hint search (tags start at h)
+    };
+#if PM_OFFS_PAIR
+    // two chunks' PRFs as independent chains side by side (twice the lookups in
+    // flight per lane for the LDS latency)
+    for (uint32_t c = c0; c < c1; c += 2) {
+      const uint32_t cB = min(c + 1, c1 - 1);
+      uint32_t pa, pb;
+      if (r2) {
+        pa = prf_lo16_r2(A, P.rk, r1u[tl][c - c0].u0, r1v, r2k, c);
+        pb = prf_lo16_r2(A, P.rk, r1u[tl][cB - c0].u0, r1v, r2k, cB);
+      } else {
+        pa = prf_lo16_split(A, P.rk, r1u[tl][c - c0], r1v, c);
+        pb = prf_lo16_split(A, P.rk, r1u[tl][cB - c0], r1v, cB);
+      }
+      put(c, pa);
+      if (cB != c) put(cB, pb);
     }
+#else
+    for (uint32_t c = c0; c < c1; ++c)
+      put(c, r2 ? prf_lo16_r2(A, P.rk, r1u[tl][c - c0].u0, r1v, r2k, c) : prf_lo16_split(A, P.rk, r1u[tl][c - c0], r1v, c));
+#endif
     uint4 t4;   // tag-major tile (set expansion): one 16-B store
     t4.x = tile[0] | ((uint32_t)tile[1] << 16); t4.y = tile[2] | ((uint32_t)tile[3] << 16);
     t4.z = tile[4] | ((uint32_t)tile[5] << 16); t4.w = tile[6] | ((uint32_t)tile[7] << 16);
