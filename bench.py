@@ -279,7 +279,9 @@ def batch_pir_msmarco(ctx, with_cpu: bool):
 # -m 32 -k 100 -q 1000 -step 20 -parallel 3): synthetic d=192 vectors ~
 # N(0, sigma_j), a degree-32 graph built on the GPU, k = 100,
 # and every session runs past its 45-query maintenance window.
-MS_N, MS_DIM, MS_K, MS_SESSIONS, MS_GROUPS, MS_QUERIES, MS_WARMUP = 3_201_821, 192, 100, 64, 2, 48, 2
+# 128 sessions in 4 teams (round 5, device loop): 8.65K q/s vs 7.2K for 64 in 2
+# (tools/sweep_msmarco.sh, profiles/r05/ab/msmarco_sessions.log; 192 in 4: 8.97K)
+MS_N, MS_DIM, MS_K, MS_SESSIONS, MS_GROUPS, MS_QUERIES, MS_WARMUP = 3_201_821, 192, 100, 128, 4, 48, 2
 
 
 def private_search_msmarco(local, args, with_cpu: bool):

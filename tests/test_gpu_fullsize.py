@@ -386,20 +386,20 @@ def test_search_msmarco_bench_exact_shape(oracle):
     """bench.py private_search_msmarco, unchanged: the bench's data
     (msmarco_like_vectors(3,201,821, 192, seed=501)) and its GPU-built graph
     (pm.build_graph(v, 32, 1.2, seed=502): kNN + robustPrune), its queries
-    (rng 503, 2 warm-up + 48 timed per session), 64 sessions (seeds 601 + i,
-    602 + i), each on its own context, in 2 lock-step teams of 32 with 16
+    (rng 503, 2 warm-up + 48 timed per session), 128 sessions (seeds 601 + i,
+    602 + i), each on its own context, in 4 lock-step teams of 32 with 16
     pooled workers, k = 100, step 20, parallel 3, and the bench's two calls
     of the serving loop.  Every session reaches its maintenance after query
-    44 (window 45, private-search.go:226-232) and the 64 clients are
+    44 (window 45, private-search.go:226-232) and the 128 clients are
     re-preprocessed as ONE launch set whose fold is ONE k_prep_fold_rot<1024>
     launch (CS 1,024: two chunks per staged block, 7 hints per lane) over all
-    64 clients' virtual hint groups.  Eight sessions from both teams are
+    128 clients' virtual hint groups.  Nine sessions from all four teams are
     replayed by independent oracle clients over all 50 queries
     (pir.go:303-352, 354-471; search.go:114-234): answers, graph counts and
     FinishedBatchNum / QueriesMadeInPartition / PrepCount equal."""
     import pacmann_amd as pm
     from pacmann_amd.synth import msmarco_like_vectors
-    N, DIM, K, S, G, NQ, WARM = 3_201_821, 192, 100, 64, 2, 50, 2
+    N, DIM, K, S, G, NQ, WARM = 3_201_821, 192, 100, 128, 4, 50, 2
     ctx0 = pm.Context(0)
     v = msmarco_like_vectors(N, DIM, seed=501)
     g, _ = pm.build_graph(v, 32, 1.2, seed=502, ctx=ctx0)
@@ -438,7 +438,7 @@ def test_search_msmarco_bench_exact_shape(oracle):
     assert n_fold == 1 and abs(fby / one - S) < 0.5, (n_fold, fby / one)
     assert tsum("host_fold_rot1024")[0] == 1 and tsum("host_fold_other")[0] == 0
     assert (mt > 0).all()
-    check = [0, 1, 17, 31, 32, 33, 50, 63]   # team 0: sessions 0-31, team 1: 32-63
+    check = [0, 1, 31, 32, 50, 64, 95, 96, 127]   # teams of 32: 0-31, 32-63, 64-95, 96-127
     got = {i: (sess[i].counts(), sess[i].PIR.stats()) for i in check}
     del sess, base, ctxs
 
