@@ -78,7 +78,13 @@ int pm_timing_enable(pm_ctx* ctx, int level);
  * automatic / 0 / 1; "match_part8": its one-wave-per-block form where PH % 8 ==
  * 0, 0 / 1; "match_resolve": k_match_resolve* for search-sized steps, 0 / 1 /
  * 2 (the general form).  -2 restores the environment's choice (PM_MATCH_PART,
- * PM_MATCH_PART8, PM_MATCH_RESOLVE).  PM_EINVAL for an unknown name. */
+ * PM_MATCH_PART8, PM_MATCH_RESOLVE).  "aes_bs": the preprocessing's PRF tables
+ * by the bitsliced VALU AES (1) or the T-table AES (0, default; -1: PM_AES_BS).
+ * "device_loop": the batched serving loop on the device (1 / 0; -1 automatic).
+ * "fault_drl_query" (tests): the device loop fails before queueing query
+ * `value` (-1 off); its sessions are then unusable (every later call on them
+ * returns PM_EINVAL: their host counters no longer match the device state).
+ * PM_EINVAL for an unknown name. */
 int pm_set_option(const char* name, int value);
 int pm_timing_reset(pm_ctx* ctx);
 /* Diagnostics: append one line "kernel,start_us,end_us,ctx" per timed launch
@@ -355,9 +361,14 @@ int  pm_rccl_create(int device, int nranks, int rank, const uint8_t* ids /* ntea
                     uint32_t nteams, pm_rccl** out);
 void pm_rccl_destroy(pm_rccl* r);
 int  pm_rccl_combine(void* user, uint32_t team, uint64_t* dev_words, uint64_t nwords, void* stream);
-/* Creation is bounded: the communicators are made nonblocking and polled for
- * at most pm_set_option("rccl_timeout_s") seconds (else PM_RCCL_TIMEOUT_S,
- * default 120); a rank whose peer never joins gets PM_ETIMEDOUT, not a hang.
+/* Creation is bounded, by one path: the teams' communicators are created
+ * nonblocking (ncclCommInitRankConfig, blocking = 0) inside ONE
+ * ncclGroupStart / ncclGroupEnd group, and each one's state is polled (with a
+ * sleep between polls) for at most pm_set_option("rccl_timeout_s") seconds
+ * (else PM_RCCL_TIMEOUT_S, default 120).  A rank whose peer never joins gets
+ * PM_ETIMEDOUT, not a hang.  Its communicators are aborted (ncclCommAbort), so
+ * no thread of the library stays inside RCCL.  An RCCL without the nonblocking
+ * API gives PM_EHIP.
  * pm_rccl_probe runs one 1-word all-reduce per team within the same bound and
  * checks that it sums to nranks; on failure the communicators are aborted.
  * Callers agree on the ranks' outcomes over another channel (a MIN of their

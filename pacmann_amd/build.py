@@ -18,7 +18,7 @@ CSRC = PKG / "csrc"
 LIB = PKG / "libpacmann.so"
 SOURCES = [CSRC / "pm_kernels.hip", CSRC / "pm_query.hip", CSRC / "pm_graph.hip", CSRC / "pm_shard.hip",
            CSRC / "pm_drl.hip", CSRC / "pm_engine.cpp"]
-HEADERS = [CSRC / "pm_internal.h", CSRC / "pm_aes.h", ROOT / "include" / "pacmann.h"]
+HEADERS = [CSRC / "pm_internal.h", CSRC / "pm_aes.h", CSRC / "pm_aes_bs.h", ROOT / "include" / "pacmann.h"]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = [

@@ -387,11 +387,15 @@ static std::atomic<int> g_device_loop{-1};
 // "rccl_timeout_s", else PM_RCCL_TIMEOUT_S, default 120 s): a rank whose peer
 // never joins returns PM_ETIMEDOUT instead of blocking inside RCCL.
 static std::atomic<int> g_rccl_timeout_s{-1};
+// fault seam (tests): run_batched_dev fails before queueing query n (-1: off)
+static std::atomic<int> g_fault_drl_query{-1};
 extern "C" int pm_set_option(const char* name, int value) {
   if (!name) return fail(PM_EINVAL, "NULL argument");
   if (!strcmp(name, "verify_records")) { g_verify_records.store(value < 0 ? 0 : value); return 0; }
   if (!strcmp(name, "rccl_timeout_s")) { g_rccl_timeout_s.store(value); return 0; }
   if (!strcmp(name, "device_loop")) { g_device_loop.store(value < 0 ? -1 : value); return 0; }
+  if (!strcmp(name, "fault_drl_query")) { g_fault_drl_query.store(value); return 0; }
+  if (!strcmp(name, "aes_bs")) { pmk::set_aes_bs(value); return 0; }
   if (pmk::set_option(name, value)) return fail(PM_EINVAL, std::string("unknown option ") + name);
   return 0;
 }
@@ -460,6 +464,7 @@ struct Engine {
   DevBuf zero16, parts_d, owned_d, tag, pp, parity, ridx, rval, hist, fqn, arena, tab, tabT, cur, done, gran;
   HostBuf parts_stage;   // pinned copy of [parts | owned parts] for the asynchronous upload (upload_parts_async)
   hipEvent_t stage_ev = nullptr;   // the last upload from parts_stage (the stage is rewritten only after it)
+  hipEvent_t order_ev = nullptr;   // upload_parts_async: the client's stream's queued work, waited for on the device
   uint32_t gran_words = 0;
   std::vector<uint32_t> owned_list;   // owned partitions in order (owned_d holds their PmPart)
   DevBuf qoffs, ans_srv;
@@ -476,6 +481,7 @@ struct Engine {
   ~Engine() {
     if (dev_ev) (void)hipEventDestroy(dev_ev);
     if (stage_ev) (void)hipEventDestroy(stage_ev);
+    if (order_ev) (void)hipEventDestroy(order_ev);
   }
   std::vector<PartHost> parts;
   uint32_t maxH = 0, maxPH = 0, maxSS = 0, maxRepl = 0, maxCS = 0, minCS = ~0u;
@@ -749,8 +755,15 @@ static int upload_parts(Engine* g) {
 // client's next preprocessing, after that synchronisation.
 static int upload_parts_async(Engine* g, hipStream_t st) {
   // the parts are read by kernels on the client's own stream too: anything still
-  // queued there finishes first (idle in batched serving: no wait)
-  if (g->ctx->stream != st && hipStreamQuery(g->ctx->stream) != hipSuccess) HIPCHK(hipStreamSynchronize(g->ctx->stream));
+  // queued there finishes before the copy overwrites them.  Ordered on the
+  // device (an event the copy's stream waits for), not by a host wait: in the
+  // device loop a team leader's stream is busy with the query just queued, and
+  // a host synchronisation there stalled the next teams' enqueueing
+  if (g->ctx->stream != st && hipStreamQuery(g->ctx->stream) != hipSuccess) {
+    if (!g->order_ev) HIPCHK(hipEventCreateWithFlags(&g->order_ev, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(g->order_ev, g->ctx->stream));
+    HIPCHK(hipStreamWaitEvent(st, g->order_ev, 0));
+  }
   const size_t no = g->owned_list.size();
   if (g->stage_ev) HIPCHK(hipEventSynchronize(g->stage_ev));   // the previous upload has left the stage
   else HIPCHK(hipEventCreateWithFlags(&g->stage_ev, hipEventDisableTiming));
@@ -1915,8 +1928,17 @@ struct pm_graph {
   std::vector<VD> heap, all;
   std::vector<std::pair<VD, uint32_t>> fs;
   Clock::time_point t_init;
+  // A device-loop call that failed after queueing work (run_batched_dev) leaves
+  // the session's host mirrors (FinishedBatchNum, QueriesMadeInPartition, the
+  // search and dummy streams) out of step with its device state; the session
+  // is then unusable and every later call on it fails with this reason.
+  std::string lost;
   ~pm_graph() { delete pir; }
 };
+static int check_session(const pm_graph* g) {
+  if (!g->lost.empty()) return fail(PM_EINVAL, "session state lost: " + g->lost);
+  return 0;
+}
 
 // PIRGraphInfo over one shard of the graph DB (multi-GPU private search,
 // SURVEY.md §8e): host vectors and graph as pm_graph_create, but only the
@@ -2219,6 +2241,7 @@ extern "C" int pm_graph_get_metadata(pm_graph* g, uint64_t* n, uint64_t* dim, ui
 extern "C" int pm_graph_get_vertex_info(pm_graph* g, const uint64_t* ids, uint64_t n, float* vecs, uint32_t* nbrs,
                                         uint8_t* ok, const float* query, float* dist) {
   if (!g || (n && !ids)) return fail(PM_EINVAL, "NULL argument");
+  CHK(check_session(g));
   if (dist && !query) return fail(PM_EINVAL, "dist needs a query");
   if (g->nshards > 1) return fail(PM_EINVAL, "a sharded graph searches through pm_search_loop_sharded (the shards' combine)");
   if (!g->nonprivate && !g->pir) return fail(PM_EINVAL, "graph not preprocessed");
@@ -2291,6 +2314,7 @@ static int search_knn_impl(pm_graph* g, const float* query, int k, int max_step,
                            int benchmarking, int64_t* ids_out, int64_t* steps_out);
 extern "C" int pm_search_knn(pm_graph* g, const float* query, int k, int max_step, int parallel,
                              int benchmarking, int64_t* ids_out, int64_t* steps_out) {
+  if (g) CHK(check_session(g));
   auto t = Clock::now();
   int r = search_knn_impl(g, query, k, max_step, parallel, benchmarking, ids_out, steps_out);
   g->ctx->host_add(HT_SEARCH_KNN, ms_since(t));
@@ -2433,6 +2457,7 @@ static int search_knn_impl(pm_graph* g, const float* query, int k, int max_step,
 // private-search.go:216-240
 extern "C" int pm_search_loop(pm_graph* g, const float* queries, uint64_t q, int k, int step, int parallel,
                               int benchmarking, int64_t* answers, double* online_s, double* maint_s) {
+  if (g) CHK(check_session(g));
   std::vector<int64_t> steps(k);
   double maint = 0;
   auto t0 = std::chrono::steady_clock::now();
@@ -2461,6 +2486,8 @@ extern "C" int pm_search_loop_sessions(pm_graph** gs, uint32_t S, const float* q
                                        int step, int parallel, int64_t* answers, double* wall_s,
                                        double* online_s, double* maint_s) {
   if (!gs || !S || (!queries && q) || (!answers && q)) return fail(PM_EINVAL, "NULL argument");
+  for (uint32_t i = 0; i < S; ++i)
+    if (gs[i]) CHK(check_session(gs[i]));
   for (uint32_t i = 0; i < S; ++i) {
     if (!gs[i]) return fail(PM_EINVAL, "NULL session");
     for (uint32_t j = 0; j < i; ++j)
@@ -4307,7 +4334,7 @@ static int drl_step(DrlTeam& T, const DrlShape& sh) {
   CHK(group_step_launch(G, S, sh.qn, T.nsub, ans_bytes, T.ans_st, T.ans_ev));
   for (size_t i = before; i < c->launches.size(); ++i)
     if (c->launches[i].name == "answer" || c->launches[i].name == "match_resolve" || c->launches[i].name == "hint_match")
-      T.tl.emplace_back(i, T.seq);
+      T.tl.emplace_back(i, T.seq - 1);   // the step the last BEGIN / MID round built (drl_round advanced seq)
   c->host_add(HT_DEV_STEPS, 0.0);
   return 0;
 }
@@ -4413,10 +4440,10 @@ static int drl_team_finish(DrlTeam& T, uint64_t q, int k, int64_t* answers) {
   return 0;
 }
 
-static int run_batched_dev(pm_graph** gs, uint32_t S, const float* queries, uint64_t q, int k, int step, int parallel,
-                           uint32_t NG, int64_t* answers, double* mt_out, const DrlShape& sh) {
+static int run_batched_dev_body(pm_graph** gs, uint32_t S, const float* queries, uint64_t q, int k, int step,
+                                int parallel, uint32_t NG, int64_t* answers, double* mt_out, const DrlShape& sh,
+                                std::vector<std::unique_ptr<DrlTeam>>& teams) {
   std::vector<StreamSwap> swaps(NG);   // (destroyed after the teams: drained, restored)
-  std::vector<std::unique_ptr<DrlTeam>> teams;
   struct Release {
     std::vector<std::unique_ptr<DrlTeam>>& t;
     ~Release() { for (auto& x : t) if (x->gs) team_release(x->gs, x->S); }
@@ -4463,6 +4490,7 @@ static int run_batched_dev(pm_graph** gs, uint32_t S, const float* queries, uint
     ~SetsRelease() { for (auto& x : v) { if (x.a) (void)hipEventDestroy(x.a); if (x.b) (void)hipEventDestroy(x.b); } }
   } sets_release{sets};
   for (uint64_t qi = 0; qi < q; ++qi) {
+    if ((int64_t)g_fault_drl_query.load() == (int64_t)qi) return fail(PM_EHIP, "injected fault (fault_drl_query)");
     CHK(drl_query_all(teams, sh, qi, q, step));
     // the harness's maintenance trigger (private-search.go:226-232) per session:
     // the triggered clients of every team as ONE launch set after the query
@@ -4531,12 +4559,30 @@ static int run_batched_dev(pm_graph** gs, uint32_t S, const float* queries, uint
   return 0;
 }
 
+// The device loop; on a failure after the teams started, their streams are
+// drained (nothing left running on the buffers being freed) and every session
+// is marked lost: its host mirrors were advanced for queries whose device state
+// was never read back.
+static int run_batched_dev(pm_graph** gs, uint32_t S, const float* queries, uint64_t q, int k, int step, int parallel,
+                           uint32_t NG, int64_t* answers, double* mt_out, const DrlShape& sh) {
+  std::vector<std::unique_ptr<DrlTeam>> teams;
+  const int rc = run_batched_dev_body(gs, S, queries, q, k, step, parallel, NG, answers, mt_out, sh, teams);
+  if (rc == 0) return 0;
+  const std::string why = pm_last_error();
+  for (auto& t : teams)
+    if (t && t->G.c) (void)hipStreamSynchronize(t->G.c->stream);
+  (void)hipDeviceSynchronize();
+  for (uint32_t i = 0; i < S; ++i) gs[i]->lost = "device loop failed: " + why;
+  return fail(rc, why);
+}
+
 extern "C" int pm_search_loop_batched(pm_graph** gs, uint32_t S, const float* queries, uint64_t q, int k, int step,
                                       int parallel, uint32_t ngroups, uint32_t nthreads, int64_t* answers,
                                       double* wall_s, double* online_s, double* maint_s) {
   if (!gs || !S || (!queries && q) || (!answers && q)) return fail(PM_EINVAL, "NULL argument");
   for (uint32_t i = 0; i < S; ++i) {
     if (!gs[i] || !gs[i]->pir || gs[i]->nonprivate) return fail(PM_EINVAL, "sessions must be preprocessed private graphs");
+    CHK(check_session(gs[i]));
     const Engine& a = gs[0]->pir->e;
     const Engine& b = gs[i]->pir->e;
     if (a.db.get() != b.db.get() || a.P != b.P || a.E != b.E || gs[i]->dim != gs[0]->dim || gs[i]->m != gs[0]->m ||
@@ -4616,7 +4662,9 @@ struct RcclApi {
   decltype(&ncclCommInitRankConfig) comm_init_rank_config = nullptr;
   decltype(&ncclCommGetAsyncError) get_async_error = nullptr;
   decltype(&ncclCommAbort) comm_abort = nullptr;
-  bool nonblocking() const { return comm_init_rank_config && get_async_error && comm_abort; }
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
+  bool nonblocking() const { return comm_init_rank_config && get_async_error && comm_abort && group_start && group_end; }
 };
 static const RcclApi& rccl_api() {
   static const RcclApi api = [] {
@@ -4633,6 +4681,8 @@ static const RcclApi& rccl_api() {
     a.comm_init_rank_config = (decltype(a.comm_init_rank_config))dlsym(a.h, "ncclCommInitRankConfig");
     a.get_async_error = (decltype(a.get_async_error))dlsym(a.h, "ncclCommGetAsyncError");
     a.comm_abort = (decltype(a.comm_abort))dlsym(a.h, "ncclCommAbort");
+    a.group_start = (decltype(a.group_start))dlsym(a.h, "ncclGroupStart");
+    a.group_end = (decltype(a.group_end))dlsym(a.h, "ncclGroupEnd");
     if (!a.get_unique_id || !a.comm_init_rank || !a.all_reduce || !a.comm_destroy || !a.error_string)
       a.err = "librccl.so.1 lacks an NCCL entry point";
     return a;
@@ -4674,11 +4724,13 @@ static ncclResult_t rccl_settle(const pm_rccl* r, ncclComm_t c, ncclResult_t res
   if (res != ncclInProgress || !r->nonblocking) return res;
   const auto t0 = Clock::now();
   ncclResult_t st = ncclInProgress;
-  while (st == ncclInProgress) {
+  for (uint64_t polls = 0;; ++polls) {
     if (rccl_api().get_async_error(c, &st) != ncclSuccess) return ncclInternalError;
-    if (st == ncclInProgress && std::chrono::duration<double>(Clock::now() - t0).count() > limit_s) return ncclInProgress;
+    if (st != ncclInProgress) return st;
+    if (std::chrono::duration<double>(Clock::now() - t0).count() > limit_s) return ncclInProgress;
+    // yield: RCCL's own proxy / init threads share the host cores with this poll
+    std::this_thread::sleep_for(std::chrono::microseconds(polls < 100 ? 10 : 200));
   }
-  return st;
 }
 
 extern "C" int pm_rccl_unique_id(uint8_t id[PM_RCCL_ID_BYTES]) {
@@ -4692,12 +4744,16 @@ extern "C" int pm_rccl_unique_id(uint8_t id[PM_RCCL_ID_BYTES]) {
   return 0;
 }
 
-// The teams' communicators, created within rccl_timeout_s(): the blocking
-// init runs on a helper thread the caller waits for with that bound, so a
-// rank whose peer failed (never joined) gets PM_ETIMEDOUT instead of a hang
-// (the helper stays blocked in RCCL and its handle is leaked, never used).
-// PM_RCCL_NONBLOCKING=1: ncclCommInitRankConfig with blocking = 0, polled, and
-// aborted on an error or the bound.
+// The teams' communicators, created within rccl_timeout_s() by ONE path (round
+// 6): nonblocking inits (ncclCommInitRankConfig, config.blocking = 0) issued
+// as one ncclGroupStart / ncclGroupEnd group -- NCCL's rule for several
+// communicators created by one thread; round 5's ungrouped nonblocking inits
+// never settled on the GPU box -- then each communicator's state polled with a
+// yield (ncclCommGetAsyncError, 10-200 us sleeps) until it settles or the bound
+// expires.  On an error or the bound every communicator is aborted
+// (ncclCommAbort: RCCL's own init work ends), so no thread of this library is
+// ever left inside RCCL; a rank whose peer never joined gets PM_ETIMEDOUT.
+// An RCCL without the nonblocking API is refused (PM_EHIP): callers fall back.
 static bool rccl_debug() {
   static const bool on = [] { const char* e = getenv("PM_RCCL_DEBUG"); return e && e[0] == '1'; }();
   return on;
@@ -4705,77 +4761,61 @@ static bool rccl_debug() {
 extern "C" int pm_rccl_create(int device, int nranks, int rank, const uint8_t* ids, uint32_t nteams, pm_rccl** out) {
   if (!ids || !out || nteams == 0 || nranks < 1 || rank < 0 || rank >= nranks) return fail(PM_EINVAL, "bad argument");
   *out = nullptr;
+  const double limit = rccl_timeout_s();
+  // fault seams (tests): this rank's create fails at once (it never joins), or
+  // its init never settles (the bounded wait runs out: PM_ETIMEDOUT after limit)
+  static const int fault = [] { const char* e = getenv("PM_FAULT_RCCL_CREATE"); return e ? atoi(e) : -1; }();
+  static const int fault_block = [] { const char* e = getenv("PM_FAULT_RCCL_BLOCK"); return e ? atoi(e) : -1; }();
+  if (fault == rank) return fail(PM_EHIP, "injected fault (PM_FAULT_RCCL_CREATE)");
+  if (fault_block == rank) {
+    const auto t0 = Clock::now();
+    while (std::chrono::duration<double>(Clock::now() - t0).count() <= limit)
+      std::this_thread::sleep_for(std::chrono::milliseconds(5));
+    return fail(PM_ETIMEDOUT, "RCCL communicators not ready after " + std::to_string((int)limit) +
+                                  " s (injected: PM_FAULT_RCCL_BLOCK)");
+  }
   const RcclApi& a = rccl_api();
   if (!a.err.empty()) return fail(PM_EHIP, "RCCL unavailable: " + a.err);
-  static const int fault = [] { const char* e = getenv("PM_FAULT_RCCL_CREATE"); return e ? atoi(e) : -1; }();
-  if (fault == rank) return fail(PM_EHIP, "injected fault (PM_FAULT_RCCL_CREATE)");   // tests: this rank never joins
+  if (!a.nonblocking()) return fail(PM_EHIP, "RCCL lacks the nonblocking init (ncclCommInitRankConfig / ncclCommAbort)");
   HIPCHK(hipSetDevice(device));
   std::unique_ptr<pm_rccl> r(new pm_rccl());
   r->device = device; r->nranks = nranks; r->rank = rank;
   r->comms.assign(nteams, nullptr);
-  const double limit = rccl_timeout_s();
-  if (rccl_debug()) fprintf(stderr, "[pm] rccl_create rank %d/%d teams %u nonblocking %d\n", rank, nranks, nteams, (int)a.nonblocking());
-  // The nonblocking form (ncclCommInitRankConfig, blocking = 0) is opt-in
-  // (PM_RCCL_NONBLOCKING=1): with the RCCL torch ships (2.26.6) polling a
-  // nonblocking communicator's state did not return on the GPU box; the
-  // default is the blocking init on a watched helper thread.
-  static const bool want_nb = [] { const char* e = getenv("PM_RCCL_NONBLOCKING"); return e && e[0] == '1'; }();
-  if (want_nb && a.nonblocking()) {
-    r->nonblocking = true;
-    for (uint32_t t = 0; t < nteams; ++t) {   // every rank issues the teams' inits in the same order
-      ncclUniqueId u;
-      memcpy(&u, ids + (size_t)t * PM_RCCL_ID_BYTES, sizeof u);
-      ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-      cfg.blocking = 0;
-      const ncclResult_t res = a.comm_init_rank_config(&r->comms[t], nranks, u, rank, &cfg);
-      if (res != ncclSuccess && res != ncclInProgress) {
-        r->abort_all();
-        return fail(PM_EHIP, std::string("ncclCommInitRankConfig: ") + a.error_string(res));
-      }
-    }
-    if (rccl_debug()) fprintf(stderr, "[pm] rccl_create: inits issued\n");
-    const auto t0 = Clock::now();
-    for (uint32_t t = 0; t < nteams; ++t) {
-      const double left = limit - std::chrono::duration<double>(Clock::now() - t0).count();
-      const ncclResult_t st = rccl_settle(r.get(), r->comms[t], ncclInProgress, std::max(0.0, left));
-      if (st == ncclInProgress) {
-        r->abort_all();
-        return fail(PM_ETIMEDOUT, "RCCL communicator " + std::to_string(t) + " not ready after " +
-                                      std::to_string((int)limit) + " s (a peer rank did not join)");
-      }
-      if (st != ncclSuccess) {
-        r->abort_all();
-        return fail(PM_EHIP, std::string("RCCL communicator init: ") + a.error_string(st));
-      }
-    }
-  } else {
-    struct Init { std::mutex mu; std::condition_variable cv; bool done = false; ncclResult_t res = ncclSuccess; };
-    auto st = std::make_shared<Init>();
-    std::vector<ncclComm_t>* comms = &r->comms;
-    std::vector<uint8_t> idv(ids, ids + (size_t)nteams * PM_RCCL_ID_BYTES);
-    std::thread th([st, comms, idv, nranks, rank, nteams, device] {
-      ncclResult_t res = hipSetDevice(device) == hipSuccess ? ncclSuccess : ncclUnhandledCudaError;
-      for (uint32_t t = 0; t < nteams && res == ncclSuccess; ++t) {
-        ncclUniqueId u;
-        memcpy(&u, idv.data() + (size_t)t * PM_RCCL_ID_BYTES, sizeof u);
-        res = rccl_api().comm_init_rank(&(*comms)[t], nranks, u, rank);
-      }
-      std::lock_guard<std::mutex> lk(st->mu);
-      st->done = true; st->res = res;
-      st->cv.notify_all();
-    });
-    std::unique_lock<std::mutex> lk(st->mu);
-    if (!st->cv.wait_for(lk, std::chrono::duration<double>(limit), [&] { return st->done; })) {
-      // the init thread stays blocked inside RCCL: it owns the handle from now on (leaked, never used)
-      th.detach();
-      (void)r.release();
-      return fail(PM_ETIMEDOUT, "RCCL communicator init not complete after " + std::to_string((int)limit) +
-                                    " s (a peer rank did not join)");
-    }
-    lk.unlock();
-    th.join();
-    if (st->res != ncclSuccess) return fail(PM_EHIP, std::string("ncclCommInitRank: ") + a.error_string(st->res));
+  r->nonblocking = true;
+  if (rccl_debug()) fprintf(stderr, "[pm] rccl_create rank %d/%d teams %u (grouped nonblocking inits)\n", rank, nranks, nteams);
+  // every rank issues the teams' inits in the same order, as one group
+  ncclResult_t gres = a.group_start();
+  for (uint32_t t = 0; t < nteams && (gres == ncclSuccess || gres == ncclInProgress); ++t) {
+    ncclUniqueId u;
+    memcpy(&u, ids + (size_t)t * PM_RCCL_ID_BYTES, sizeof u);
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    gres = a.comm_init_rank_config(&r->comms[t], nranks, u, rank, &cfg);
   }
+  const ncclResult_t eres = a.group_end();
+  if (rccl_debug()) fprintf(stderr, "[pm] rccl_create: group end %d (%s)\n", (int)eres, a.error_string(eres));
+  if ((gres != ncclSuccess && gres != ncclInProgress) || (eres != ncclSuccess && eres != ncclInProgress)) {
+    r->abort_all();
+    return fail(PM_EHIP, std::string("ncclCommInitRankConfig: ") +
+                             a.error_string(gres != ncclSuccess && gres != ncclInProgress ? gres : eres));
+  }
+  const auto t0 = Clock::now();
+  for (uint32_t t = 0; t < nteams; ++t) {
+    const double left = limit - std::chrono::duration<double>(Clock::now() - t0).count();
+    const ncclResult_t st = rccl_settle(r.get(), r->comms[t], ncclInProgress, std::max(0.0, left));
+    if (st == ncclInProgress) {
+      r->abort_all();
+      return fail(PM_ETIMEDOUT, "RCCL communicator " + std::to_string(t) + " not ready after " +
+                                    std::to_string((int)limit) + " s (a peer rank did not join)");
+    }
+    if (st != ncclSuccess) {
+      r->abort_all();
+      return fail(PM_EHIP, std::string("RCCL communicator init: ") + a.error_string(st));
+    }
+  }
+  if (rccl_debug())
+    fprintf(stderr, "[pm] rccl_create: %u communicators ready in %.3f s\n", nteams,
+            std::chrono::duration<double>(Clock::now() - t0).count());
   *out = r.release();
   return 0;
 }
@@ -4868,6 +4908,7 @@ extern "C" int pm_search_loop_sharded(pm_graph** gs, uint32_t S, const float* qu
   if (!gs || !S || (!queries && q) || (!answers && q)) return fail(PM_EINVAL, "NULL argument");
   for (uint32_t i = 0; i < S; ++i) {
     if (!gs[i] || !gs[i]->pir || gs[i]->nonprivate) return fail(PM_EINVAL, "sessions must be preprocessed private graphs");
+    CHK(check_session(gs[i]));
     const Engine& a = gs[0]->pir->e;
     const Engine& b = gs[i]->pir->e;
     if (a.db.get() != b.db.get() || a.P != b.P || a.E != b.E || gs[i]->dim != gs[0]->dim || gs[i]->m != gs[0]->m ||

@@ -300,6 +300,9 @@ using namespace pm;
 void prep_init(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxH, uint32_t maxRepl,
                uint32_t E, bool zero_state);
 void prep_offsets(hipStream_t st, const PmPart* dparts, int nparts, uint32_t maxH, uint32_t maxSS);
+// the PRF tables' AES form: 0 = T-table (k_prep_offsets, default), 1 = bitsliced on the
+// VALU (k_prep_offsets_bs, pm_aes_bs.h; profiles/r06/aes: 0.93x), -1 = PM_AES_BS's value
+void set_aes_bs(int v);
 // dparts: `clients` clients of each partition, partition-major (nparts = partitions x clients)
 // returns the fold kernel launched (FOLD_*)
 enum : int { FOLD_OTHER = 0, FOLD_ROT512 = 1, FOLD_ROT1024 = 2 };

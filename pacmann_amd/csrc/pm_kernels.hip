@@ -1,6 +1,8 @@
 // pm_kernels.hip — gfx950 kernels of the PianoPIR XOR fold / answer path and
 // the graphann distance path.  See DESIGN.md §5 for the roofline of each.
+#include <atomic>
 #include "pm_aes.h"
+#include "pm_aes_bs.h"
 #include "pm_internal.h"
 
 namespace pm {
@@ -116,6 +118,194 @@ __global__ void __launch_bounds__(kOffsBlock, PM_OFFS_PAIR ? 8 : 1) k_prep_offse
       __builtin_nontemporal_store(u32x4{t4.x, t4.y, t4.z, t4.w}, reinterpret_cast<u32x4*>(P.tabT + tabT_index(H, h, c0)));
     } else {
       *reinterpret_cast<uint4*>(P.tabT + tabT_index(H, h, c0)) = t4;
+    }
+  }
+}
+
+// Bitsliced form of k_prep_offsets (round 6, pm_aes_bs.h): the same tables
+// (tabT, cur, tab) bit for bit, the AES on the VALU instead of LDS T-table
+// lookups.  A lane owns 32 consecutive hints (one bitsliced block set) and one
+// tile group of 8 chunks; it evaluates the chunks in pairs, transposes each
+// pair's 2 x 16 output planes into 32 words (hint j: chunk c | chunk c+1 << 16,
+// i.e. one 4-B word of the hint's tabT tile) and stores them.  LDS holds only
+// the per-key setup (Te0 for rounds 1-2, the folded round constants, W's
+// planes): 2.7 KB.
+constexpr int kBsThreads = 256;
+#ifndef PM_BS_WAVES
+#define PM_BS_WAVES 2
+#endif
+__global__ void __launch_bounds__(kBsThreads, PM_BS_WAVES) k_prep_offsets_bs(const PmPart* __restrict__ parts) {
+  __shared__ uint32_t bs_te0[256];
+  __shared__ uint32_t bs_kx[32];
+  __shared__ uint32_t bs_wv[32][4];
+  __shared__ __attribute__((aligned(16))) uint32_t bs_wp[128];
+  __shared__ __attribute__((aligned(16))) uint32_t bs_stash[16 * kBsThreads];
+  __shared__ __attribute__((aligned(16))) uint32_t bs_kpl[kBsKplWords];
+  const PmPart& P = parts[blockIdx.y];
+  const uint32_t H = P.H, SS = P.SS, PH = P.PH;
+  const uint32_t nm = (H + 31) / 32, ng = (SS + 7) / 8;
+  if (blockIdx.x * kBsThreads >= nm * ng) return;   // block-uniform
+  bs_te0[threadIdx.x] = g_aes.te0[threadIdx.x];
+  __syncthreads();
+  bs_setup_a(bs_te0, P.rk, bs_kx, bs_wv);
+  __syncthreads();
+  bs_setup_b(bs_wv, bs_wp, bs_kx, bs_kpl);
+  __syncthreads();
+  const uint32_t task = blockIdx.x * kBsThreads + threadIdx.x;
+  if (task >= nm * ng) return;
+  const uint32_t m = task % nm, g = task / nm, h0 = 32 * m;
+  const uint32_t nb = P.log2CS, Qpc = P.Qpc;
+  const uint32_t keep = nb >= 16 ? 0xffffu : (1u << nb) - 1u;   // planes past log2(CS): masked off
+  auto lowmask = [](int n) { return n <= 0 ? 0u : n >= 32 ? ~0u : (1u << n) - 1u; };
+  // chunks in pairs: the first chunk's 16 planes wait in LDS (64 B per lane)
+  // while the second is evaluated, so one copy of the AES code serves both and
+  // no planes stay pinned in VGPRs across it
+  uint4* stash = reinterpret_cast<uint4*>(bs_stash) + threadIdx.x;
+#pragma unroll 1
+  for (uint32_t q = 0; q < 8; ++q) {
+    const uint32_t cc = 8 * g + q, c = cc & ~1u;
+    uint32_t T[32];
+    if (c < SS) {   // SetSize is a multiple of 4: a pair is whole
+      uint32_t o[16];
+      bs_prf16(bs_te0, P.rk, bs_kx, bs_wp, bs_kpl, m, cc, o);
+      // backup hints whose own chunk is cc (pir.go:332-334): kSkip (all 16 bits set)
+      const int lo = (int)(PH + cc * Qpc) - (int)h0, hi = lo + (int)Qpc;
+      const uint32_t own = lowmask(hi) & ~lowmask(lo);
+#pragma unroll
+      for (int b = 0; b < 16; ++b) o[b] = (((keep >> b) & 1u) ? o[b] : 0u) | own;
+      if ((q & 1) == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) stash[i * kBsThreads] = make_uint4(o[4 * i], o[4 * i + 1], o[4 * i + 2], o[4 * i + 3]);
+        continue;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint4 v = stash[i * kBsThreads];
+        T[4 * i] = v.x; T[4 * i + 1] = v.y; T[4 * i + 2] = v.z; T[4 * i + 3] = v.w;
+      }
+#pragma unroll
+      for (int b = 0; b < 16; ++b) T[16 + b] = o[b];
+      bs_transpose32(T);
+    } else {
+      if ((q & 1) == 0) continue;
+#pragma unroll
+      for (int j = 0; j < 32; ++j) T[j] = 0xffffffffu;   // tile padding past SetSize
+    }
+    // tag-major tiles: word (c & 7) / 2 of hint h0 + j's tile
+    uint32_t* tt = reinterpret_cast<uint32_t*>(P.tabT + tabT_index(H, h0, c));
+    if (h0 + 32 <= H) {
+#pragma unroll
+      for (int j = 0; j < 32; ++j) tt[4 * j] = T[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 32; ++j)
+        if (h0 + j < H) tt[4 * j] = T[j];
+    }
+    if (c >= SS) continue;
+    // 8-hint blocks of chunks c and c + 1 (cur: primary hints only; tab: every tag)
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb) {
+      const uint32_t hb = h0 + 8 * jb;
+      uint4 wlo, whi;
+      wlo.x = __builtin_amdgcn_perm(T[8 * jb + 1], T[8 * jb + 0], 0x05040100u);
+      wlo.y = __builtin_amdgcn_perm(T[8 * jb + 3], T[8 * jb + 2], 0x05040100u);
+      wlo.z = __builtin_amdgcn_perm(T[8 * jb + 5], T[8 * jb + 4], 0x05040100u);
+      wlo.w = __builtin_amdgcn_perm(T[8 * jb + 7], T[8 * jb + 6], 0x05040100u);
+      whi.x = __builtin_amdgcn_perm(T[8 * jb + 1], T[8 * jb + 0], 0x07060302u);
+      whi.y = __builtin_amdgcn_perm(T[8 * jb + 3], T[8 * jb + 2], 0x07060302u);
+      whi.z = __builtin_amdgcn_perm(T[8 * jb + 5], T[8 * jb + 4], 0x07060302u);
+      whi.w = __builtin_amdgcn_perm(T[8 * jb + 7], T[8 * jb + 6], 0x07060302u);
+      if (hb < PH) {
+        *reinterpret_cast<uint4*>(P.cur + cur_index(PH, P.curk, c, hb)) = wlo;
+        *reinterpret_cast<uint4*>(P.cur + cur_index(PH, P.curk, c + 1, hb)) = whi;
+      }
+      if (P.tab && hb < H) {
+        *reinterpret_cast<uint4*>(P.tab + (uint64_t)c * H + hb) = wlo;
+        *reinterpret_cast<uint4*>(P.tab + (uint64_t)(c + 1) * H + hb) = whi;
+      }
+    }
+  }
+}
+
+// Packed bitsliced form (pm_aes_bs.h, bs16_*): 16 tags per lane, 128 VGPRs,
+// four waves per SIMD.  Same tables as k_prep_offsets, bit for bit.
+__global__ void __launch_bounds__(kBsThreads, 4) k_prep_offsets_bs16(const PmPart* __restrict__ parts) {
+  __shared__ uint32_t bs_te0[256];
+  __shared__ uint32_t bs_kx[32];
+  __shared__ uint32_t bs_wv[32][4];
+  __shared__ __attribute__((aligned(16))) uint32_t bs_wp16[128];
+  __shared__ __attribute__((aligned(16))) uint32_t bs_kp16[kBs16Kpl];
+  __shared__ __attribute__((aligned(16))) uint32_t bs_stash[8 * kBsThreads];
+  const PmPart& P = parts[blockIdx.y];
+  const uint32_t H = P.H, SS = P.SS, PH = P.PH;
+  const uint32_t nm = (H + 15) / 16, ng = (SS + 7) / 8;
+  if (blockIdx.x * kBsThreads >= nm * ng) return;   // block-uniform
+  bs_te0[threadIdx.x] = g_aes.te0[threadIdx.x];
+  __syncthreads();
+  bs_setup_a(bs_te0, P.rk, bs_kx, bs_wv);
+  __syncthreads();
+  bs16_setup_b(bs_wv, bs_kx, bs_wp16, bs_kp16);
+  __syncthreads();
+  const uint32_t task = blockIdx.x * kBsThreads + threadIdx.x;
+  if (task >= nm * ng) return;
+  const uint32_t m = task % nm, g = task / nm, h0 = 16 * m;
+  const uint32_t nb = P.log2CS, Qpc = P.Qpc;
+  uint32_t keep[8];   // plane b keeps bit b (low half) and bit 8 + b (high half) below log2(CS)
+#pragma unroll
+  for (int b = 0; b < 8; ++b) keep[b] = ((uint32_t)b < nb ? 0xffffu : 0u) | ((uint32_t)(8 + b) < nb ? 0xffff0000u : 0u);
+  auto lowmask = [](int n) { return n <= 0 ? 0u : n >= 16 ? 0xffffu : (1u << n) - 1u; };
+  uint4* stash = reinterpret_cast<uint4*>(bs_stash) + threadIdx.x;
+#pragma unroll 1
+  for (uint32_t q = 0; q < 8; ++q) {
+    const uint32_t cc = 8 * g + q, c = cc & ~1u;
+    uint32_t W0[8], W1[8];
+    if (c < SS) {   // SetSize is a multiple of 4: a pair is whole
+      uint32_t o[8];
+      bs16_prf16(bs_te0, P.rk, bs_kx, bs_wp16, bs_kp16, m, cc, o);
+      // backup hints whose own chunk is cc (pir.go:332-334): kSkip (all 16 bits set)
+      const int lo = (int)(PH + cc * Qpc) - (int)h0, hi = lo + (int)Qpc;
+      const uint32_t own16 = lowmask(hi) & ~lowmask(lo), own = own16 | (own16 << 16);
+#pragma unroll
+      for (int b = 0; b < 8; ++b) o[b] = (o[b] & keep[b]) | own;
+      bs16_transpose(o);
+      if ((q & 1) == 0) {
+        stash[0] = make_uint4(o[0], o[1], o[2], o[3]);
+        stash[kBsThreads] = make_uint4(o[4], o[5], o[6], o[7]);
+        continue;
+      }
+      const uint4 v0 = stash[0], v1 = stash[kBsThreads];
+      W0[0] = v0.x; W0[1] = v0.y; W0[2] = v0.z; W0[3] = v0.w; W0[4] = v1.x; W0[5] = v1.y; W0[6] = v1.z; W0[7] = v1.w;
+#pragma unroll
+      for (int b = 0; b < 8; ++b) W1[b] = o[b];
+    } else {
+      if ((q & 1) == 0) continue;
+#pragma unroll
+      for (int b = 0; b < 8; ++b) W0[b] = W1[b] = 0xffffffffu;   // tile padding past SetSize
+    }
+    // W0 / W1[j'] = tag j' (low) | tag j' + 8 (high) at chunks c / c + 1
+    uint32_t* tt = reinterpret_cast<uint32_t*>(P.tabT + tabT_index(H, h0, c));
+    const uint32_t nj = min(16u, H - h0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if ((uint32_t)j < nj) tt[4 * j] = __builtin_amdgcn_perm(W1[j], W0[j], 0x05040100u);
+      if ((uint32_t)j + 8 < nj) tt[4 * (j + 8)] = __builtin_amdgcn_perm(W1[j], W0[j], 0x07060302u);
+    }
+    if (c >= SS) continue;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {   // 8-hint blocks: tags 0..7 (low halves), 8..15 (high)
+      const uint32_t sel = half ? 0x07060302u : 0x05040100u, hb = h0 + 8 * half;
+      const uint4 w0 = make_uint4(__builtin_amdgcn_perm(W0[1], W0[0], sel), __builtin_amdgcn_perm(W0[3], W0[2], sel),
+                                  __builtin_amdgcn_perm(W0[5], W0[4], sel), __builtin_amdgcn_perm(W0[7], W0[6], sel));
+      const uint4 w1 = make_uint4(__builtin_amdgcn_perm(W1[1], W1[0], sel), __builtin_amdgcn_perm(W1[3], W1[2], sel),
+                                  __builtin_amdgcn_perm(W1[5], W1[4], sel), __builtin_amdgcn_perm(W1[7], W1[6], sel));
+      if (hb < PH) {
+        *reinterpret_cast<uint4*>(P.cur + cur_index(PH, P.curk, c, hb)) = w0;
+        *reinterpret_cast<uint4*>(P.cur + cur_index(PH, P.curk, c + 1, hb)) = w1;
+      }
+      if (P.tab && hb < H) {
+        *reinterpret_cast<uint4*>(P.tab + (uint64_t)c * H + hb) = w0;
+        *reinterpret_cast<uint4*>(P.tab + (uint64_t)(c + 1) * H + hb) = w1;
+      }
     }
   }
 }
@@ -1069,9 +1259,28 @@ void prep_init(hipStream_t st, const PmPart* d, int np, uint32_t maxH, uint32_t 
   const uint32_t n = maxH > maxRepl ? maxH : maxRepl;
   hipLaunchKernelGGL(k_prep_init, dim3(cdiv(n, kBlock), np), dim3(kBlock), 0, st, d);
 }
-void prep_offsets(hipStream_t st, const PmPart* d, int np, uint32_t maxH, uint32_t maxSS) {
+void prep_offsets_tt(hipStream_t st, const PmPart* d, int np, uint32_t maxH, uint32_t maxSS) {
   hipLaunchKernelGGL(k_prep_offsets, dim3(cdiv(maxH, kOffsBlock), cdiv(maxSS, kOffsChunksPerBlock * kOffsTiles), np),
                      dim3(kOffsBlock), 0, st, d);
+}
+void prep_offsets_bs(hipStream_t st, const PmPart* d, int np, uint32_t maxH, uint32_t maxSS) {
+  hipLaunchKernelGGL(k_prep_offsets_bs, dim3(cdiv((uint64_t)cdiv(maxH, 32) * cdiv(maxSS, 8), kBsThreads), np),
+                     dim3(kBsThreads), 0, st, d);
+}
+void prep_offsets_bs16(hipStream_t st, const PmPart* d, int np, uint32_t maxH, uint32_t maxSS) {
+  hipLaunchKernelGGL(k_prep_offsets_bs16, dim3(cdiv((uint64_t)cdiv(maxH, 16) * cdiv(maxSS, 8), kBsThreads), np),
+                     dim3(kBsThreads), 0, st, d);
+}
+static std::atomic<int> g_aes_bs{-1};
+void set_aes_bs(int v) { g_aes_bs.store(v < 0 ? -1 : (v ? 1 : 0)); }
+bool prep_offsets_bitsliced() {
+  static const bool env = [] { const char* e = getenv("PM_AES_BS"); return e && e[0] == '1'; }();
+  const int v = g_aes_bs.load();
+  return v < 0 ? env : v == 1;
+}
+void prep_offsets(hipStream_t st, const PmPart* d, int np, uint32_t maxH, uint32_t maxSS) {
+  if (prep_offsets_bitsliced()) prep_offsets_bs(st, d, np, maxH, maxSS);
+  else prep_offsets_tt(st, d, np, maxH, maxSS);
 }
 bool fold_image_ok(uint32_t minCS, uint32_t maxCS, uint32_t E) {
   static const bool rot = [] { const char* e = getenv("PM_FOLD_ROT"); return !e || e[0] != '0'; }();

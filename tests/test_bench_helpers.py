@@ -52,16 +52,32 @@ def _run_watchdog(body: str):
 
 def test_watchdog_writes_the_partial_line_and_exits():
     """A stuck multi-rank block: the watchdog writes the one line (the blocks
-    marked unfinished) and ends the process, instead of a hang."""
+    marked unfinished, watchdog.fired) and ends the process with status 3,
+    instead of a hang."""
     rc, lines, dt = _run_watchdog(
         "out = {'metric': 'm', 'value': 1.0}\n"
         "wd = b.Watchdog(out, 0, 1, 0.3)\n"
         "time.sleep(30)\n"
         "print('not reached')\n")
-    assert rc == 0 and len(lines) == 1, (rc, lines)
+    assert rc == 3 and len(lines) == 1, (rc, lines)   # non-zero: the caller sees the hang
     assert lines[0]["value"] == 1.0
     assert "unfinished" in lines[0]["config3_bigann_100m"]["error"]
+    assert lines[0]["watchdog"] == {"fired": True, "budget_s": 0.3}   # the hang is reported in the line
     assert dt < 25
+
+
+def test_watchdog_snapshot_keeps_finished_blocks():
+    """Blocks finished before the budget expired (Watchdog.put, under the
+    watchdog's lock) are in the line; the one still running is marked."""
+    rc, lines, _ = _run_watchdog(
+        "out = {'metric': 'm', 'value': 3.0}\n"
+        "wd = b.Watchdog(out, 0, 1, 0.5)\n"
+        "wd.put('config3_bigann_100m', {'value': 7.0})\n"
+        "time.sleep(30)\n")
+    assert rc == 3 and len(lines) == 1, (rc, lines)
+    assert lines[0]["config3_bigann_100m"] == {"value": 7.0}
+    assert "unfinished" in lines[0]["config4_bigann_1b"]["error"]
+    assert lines[0]["watchdog"]["fired"] is True
 
 
 def test_watchdog_fire_before_the_budget():

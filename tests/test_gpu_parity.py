@@ -522,6 +522,55 @@ def test_search_device_loop_vs_host_loop(ctx, oracle, ngroups):
         assert c1[i] == o.counts(), i
 
 
+def test_device_loop_fault_marks_sessions_lost(ctx, oracle):
+    """A device-loop call that fails after queueing work: the
+    sessions' host mirrors (FinishedBatchNum, QueriesMadeInPartition, the
+    search streams) were advanced for the queued query while its device state
+    (dummy counters, FinishedQueryNum, localCache index, id stream) was never
+    read back.  Fault injected before query 1 (query 0 queued and running):
+    the call fails with the injected error, the teams' streams are drained,
+    and every later call on those sessions fails with "session state lost"
+    instead of reissuing dummy-counter values the server has seen.  Fresh
+    sessions of the same base still serve and equal the oracle."""
+    import pacmann_amd as pm
+    from pacmann_amd.synth import random_graph, sift_like_vectors
+    n = 16384
+    v = sift_like_vectors(n, 128, seed=171)
+    graph = random_graph(n, 32, seed=172)
+    rng = np.random.default_rng(173)
+    qs = np.stack([np.clip(np.rint(v[rng.integers(0, n, 3)] + rng.normal(0, 8, (3, 128))), 0, 255)
+                   .astype(np.float32) for _ in range(4)])
+    base = pm.PIRGraphInfo(v, graph, pir_seed=1, search_seed=2, ctx=pm.Context(0))
+    base.Preprocess()
+    pm.set_option("device_loop", 1)
+    try:
+        sess = [base.Session(180 + i, 190 + i) for i in range(4)]
+        for x in sess:
+            x.Preprocess()
+        pm.set_option("fault_drl_query", 1)
+        try:
+            with pytest.raises(RuntimeError, match="injected fault"):
+                pm.search_loop_batched(sess, qs, 10, 20, 3, 2, 4)
+        finally:
+            pm.set_option("fault_drl_query", -1)
+        with pytest.raises(RuntimeError, match="session state lost"):
+            pm.search_loop_batched(sess, qs, 10, 20, 3, 2, 4)
+        with pytest.raises(RuntimeError, match="session state lost"):
+            pm.search_loop_batched(sess[:1], qs[:1], 10, 20, 3, 1, 1)
+        seeds = [(280 + i, 290 + i) for i in range(2)]
+        fresh = [base.Session(p, s) for p, s in seeds]
+        for x in fresh:
+            x.Preprocess()
+        ans, _, _, _ = pm.search_loop_batched(fresh, qs[:2], 10, 20, 3, 1, 2)
+    finally:
+        pm.set_option("device_loop", -1)
+    for i, (p, s) in enumerate(seeds):
+        o = oracle.Graph(v, graph, pir_seed=p, search_seed=s)
+        o.Preprocess()
+        oa, _, _ = o.SearchLoop(qs[i], 10, 20, 3)
+        assert np.array_equal(ans[i], oa), i
+
+
 def test_search_sessions_batched_wide_entries(ctx, oracle):
     """Entries wider than the answer kernels' small row buffer: dim 500, m 16
     gives E = (2000 + 64) / 8 = 258 words, which passes k_answer_p's even-E

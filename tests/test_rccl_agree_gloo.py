@@ -62,17 +62,19 @@ def test_agreed_setup_one_rank_fails():
     assert res[0][2] == res[1][2] == "3", res
 
 
-def _rank_native(rank, world, port, out_dir):
+def _rank_native(rank, world, port, out_dir, fault="PM_FAULT_RCCL_CREATE", bound=10):
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     if rank == 1:
-        os.environ["PM_FAULT_RCCL_CREATE"] = "1"   # this rank's pm_rccl_create fails: it never joins
+        # PM_FAULT_RCCL_CREATE: this rank's pm_rccl_create fails at once (it never joins);
+        # PM_FAULT_RCCL_BLOCK: its init never settles, the bounded wait runs out
+        os.environ[fault] = "1"
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         import pacmann_amd as pm
         from pacmann_amd.shard import combiner_with_fallback
-        pm.set_option("rccl_timeout_s", 10)
+        pm.set_option("rccl_timeout_s", bound)
         t0 = time.perf_counter()
         comb, path, note = combiner_with_fallback([1000, 1000], device=0, prefer="native",
                                                   nccl_group_fn=lambda: None)
@@ -95,3 +97,23 @@ def test_native_combine_falls_back_when_a_rank_fails():
         assert res[r][2] == "30", res
         assert float(res[r][3]) < 60, res   # bounded: no rank waited for the one that never joined
     assert "injected fault" in res[1][1], res
+
+
+def test_native_combine_falls_back_when_a_rank_blocks():
+    """rank 1's communicator creation BLOCKS (its init never
+    settles: PM_FAULT_RCCL_BLOCK) instead of failing.  Its bounded wait ends
+    with PM_ETIMEDOUT after rccl_timeout_s (4 s here), rank 0 waits for it at
+    the agreement, both ranks fall back to the gloo combine and both processes
+    exit -- within the bound plus slack, with no thread left waiting."""
+    t0 = time.monotonic()
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_rank_native, args=(2, _free_port(), d, "PM_FAULT_RCCL_BLOCK", 4), nprocs=2, join=True)
+        res = [open(os.path.join(d, f"n{r}.txt")).read().split("|") for r in range(2)]
+    wall = time.monotonic() - t0
+    for r in range(2):
+        assert res[r][0] == "gloo", res
+        assert res[r][1].startswith("native RCCL combine unavailable"), res
+        assert res[r][2] == "30", res
+    assert "PM_FAULT_RCCL_BLOCK" in res[1][1] and "not ready after 4 s" in res[1][1], res
+    assert 3.5 < float(res[1][3]) < 30, res   # the blocked rank waited out its bound, no longer
+    assert wall < 90, wall                     # both processes exited (spawn joined them)
