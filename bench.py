@@ -357,6 +357,10 @@ def private_search_msmarco(local, args, with_cpu: bool):
         out["roofline_prep"] = {"bound": "lds", "kernel": "prep_fold", "achieved": round(ach, 1),
                                 "peak": LDS_B128_PEAK_GBS, "unit": "GB/s", "frac": round(ach / LDS_B128_PEAK_GBS, 4),
                                 "avg_ms": round(ms / n, 3), "launches": n, "alg_bytes_per_launch": by / n}
+    if "roofline" in out:   # the whole private query against its three ceilings
+        out["roofline"]["composite"] = composite_floor(kt, S2, MS_QUERIES, base.PIR, out["private_queries_per_s"],
+                                                       ss_r2=base.PIR.SubConfig(0)["SetSize"],
+                                                       entry_words=(MS_DIM + M) // 2)
     if with_cpu:   # the oracle replaying session 0's workload, one core
         cb = cpu_baseline(v, g, qs[0], MS_WARMUP, ans[0], ctx, 601, 602, k=MS_K)
         out["cpu_baseline"] = cb
@@ -775,7 +779,7 @@ def prf_roofline(entry, note, set_size=None):
                     "~2 VALU per lookup put the vector-issue ceiling at about the same rate"}
 
 
-def composite_floor(ktime, S, queries_per_session, pir, value_per_gpu, ss_r2=None):
+def composite_floor(ktime, S, queries_per_session, pir, value_per_gpu, ss_r2=None, entry_words=(DIM + M) // 2):
     """The whole private query's GPU floor: per session
     query, its answer bytes at HBM peak + its share of the maintenance fold's
     entry reads at the LDS ds_read_b128 aggregate + its share of the PRFs at the
@@ -793,7 +797,7 @@ def composite_floor(ktime, S, queries_per_session, pir, value_per_gpu, ss_r2=Non
     fbn_per_q = STEP * (PARALLEL * M // st["BatchSize"])
     cadence = -(-(st["SupportBatchNum"] - STEP * PARALLEL - 10) // fbn_per_q)   # queries between maintenances
     clients = max(1, round(fb / sum(((c["PrimaryHintNum"] + (c["SetSize"] - 1) * c["MaxQueryPerChunk"]) * c["SetSize"]
-                                      * ((DIM + M) // 2) * 8)
+                                      * entry_words * 8)
                                      for c in (pir.SubConfig(p) for p in range(st["PartitionNum"])))))
     ans_q = ab / (S * queries_per_session)
     fold_q = fb / clients / cadence

@@ -321,190 +321,4 @@ __device__ __forceinline__ void bs_transpose32(uint32_t (&a)[32]) {
 }
 
 
-// ---------------------------------------------------------------------------
-// Packed form (16 blocks per lane, two bytes per plane word): the same AES with
-// half the registers, so four waves per SIMD instead of two.  A lane holds the
-// tags 16 m .. 16 m + 15 at one chunk; plane word (pair pi, row r, bit b) has
-// bit b of byte (column pi, row r) of block j in bit j and bit b of byte
-// (column pi + 2, row r) in bit 16 + j.  A bitwise VALU operation then serves
-// two S-box bytes (or two MixColumns columns) at once, and ShiftRows becomes a
-// renaming plus a 16-bit rotation of four of the eight (pair, row) sets
-// (post (pi', r) = pre (pi' + r mod 2, r), halves swapped when pi' + r mod 4 >= 2).
-// Round 9 packs its eight useful bytes into four sets, round 10 its two into one.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t bs_rot16(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); }
-__device__ __forceinline__ uint32_t bs_lohi(uint32_t lo, uint32_t hi) {   // lo half of lo, hi half of hi
-  return __builtin_amdgcn_perm(hi, lo, 0x07060100u);
-}
-struct Bs16 { uint32_t s[2][4][8]; };   // [pair][row][bit]
-
-__device__ __forceinline__ void bs16_round(Bs16& S, const uint32_t* kpl) {   // kpl: 64 packed constant planes
-  uint32_t t[2][4][8];
-#pragma unroll
-  for (int pi = 0; pi < 2; ++pi)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bs_sbox(S.s[pi][r], t[pi][r], bs_kload(kpl + 8 * (4 * pi + r)));
-  // ShiftRows: post (0, r) <- (r & 1, r), halves swapped for r >= 2; post (1, r) <- ((r + 1) & 1, r),
-  // swapped for r = 1, 2
-#pragma unroll
-  for (int b = 0; b < 8; ++b) {
-    t[0][2][b] = bs_rot16(t[0][2][b]); t[1][3][b] = bs_rot16(t[1][3][b]);
-    t[0][1][b] = bs_rot16(t[0][1][b]); t[1][2][b] = bs_rot16(t[1][2][b]);
-  }
-#pragma unroll
-  for (int pp = 0; pp < 2; ++pp) {
-    const int q1 = (pp + 1) & 1;
-    uint32_t(&a0)[8] = t[pp][0];
-    uint32_t(&a1)[8] = t[q1][1];
-    uint32_t(&a2)[8] = t[pp][2];
-    uint32_t(&a3)[8] = t[q1][3];
-    // rows 0 and 2 need d01 and d23, rows 1 and 3 d12 and d30
-    uint32_t d01[8], d23[8];
-#pragma unroll
-    for (int b = 0; b < 8; ++b) { d01[b] = a0[b] ^ a1[b]; d23[b] = a2[b] ^ a3[b]; }
-    auto row = [&](const uint32_t (&di)[8], const uint32_t (&an)[8], const uint32_t (&dn)[8], uint32_t (&o)[8]) {
-      o[0] = bs_x3(di[7], an[0], dn[0]);
-      o[1] = bs_x3(di[0] ^ di[7], an[1], dn[1]);
-      o[2] = bs_x3(di[1], an[2], dn[2]);
-      o[3] = bs_x3(di[2] ^ di[7], an[3], dn[3]);
-      o[4] = bs_x3(di[3] ^ di[7], an[4], dn[4]);
-      o[5] = bs_x3(di[4], an[5], dn[5]);
-      o[6] = bs_x3(di[5], an[6], dn[6]);
-      o[7] = bs_x3(di[6], an[7], dn[7]);
-    };
-    row(d01, a1, d23, S.s[pp][0]);
-    row(d23, a3, d01, S.s[pp][2]);
-    uint32_t d12[8], d30[8];
-#pragma unroll
-    for (int b = 0; b < 8; ++b) { d12[b] = a1[b] ^ a2[b]; d30[b] = a3[b] ^ a0[b]; }
-    row(d12, a2, d30, S.s[pp][1]);
-    row(d30, a0, d12, S.s[pp][3]);
-  }
-}
-
-// Per-key LDS tables of the packed form (call with >= 256 threads after
-// bs_setup_a, whose wv rows 0..15 it reads; then synchronise):
-//   wp16[64 par + 8 (4 pi + r) + b]: W's packed planes for lanes of tag base 16 m, m % 2 = par
-//       (byte 4 of the block is (m & 1) << 7 | j << 3: W depends on m's parity)
-//   kp16[64 (rr) + 8 (4 pi + r) + b], rr = round - 3 = 0..5: packed constant planes
-//   kp16[384 + 8 k + b], k = 0..3: round 9's sets A (bytes 0 | 10), B (5 | 15), C (4 | 14), D (3 | 9)
-constexpr int kBs16Kpl = 384 + 32;
-__device__ __forceinline__ void bs16_setup_b(const uint32_t (*wv)[4], const uint32_t* kx, uint32_t* wp16,
-                                             uint32_t* kp16) {
-  const uint32_t t = threadIdx.x;
-  auto kbyte = [&](uint32_t rr, uint32_t col, uint32_t row) { return (kx[4 * rr + col] >> (8 * row)) & 0xffu; };
-  if (t < 128) {
-    const uint32_t par = t >> 6, set = (t >> 3) & 7, b = t & 7, pi = set >> 2, r = set & 3;
-    const uint32_t shl = 8 * r + b, j0 = 16 * par;
-    uint32_t pl = 0;
-#pragma unroll 4
-    for (uint32_t j = 0; j < 16; ++j) {
-      pl |= (((wv[j0 + j][pi] ^ wv[j0][pi]) >> shl) & 1u) << j;
-      pl |= (((wv[j0 + j][pi + 2] ^ wv[j0][pi + 2]) >> shl) & 1u) << (16 + j);
-    }
-    wp16[t] = pl;
-  }
-  for (uint32_t i = t; i < (uint32_t)kBs16Kpl; i += blockDim.x) {
-    const uint32_t b = i & 7;
-    uint32_t klo, khi;
-    if (i < 384) {
-      const uint32_t rr = i >> 6, set = (i >> 3) & 7, pi = set >> 2, r = set & 3;
-      klo = kbyte(rr, pi, r); khi = kbyte(rr, pi + 2, r);
-    } else {   // round 9 (rr 6): A = (0,0)|(2,2), B = (1,1)|(3,3), C = (1,0)|(3,2), D = (0,3)|(2,1)
-      const uint32_t k = (i - 384) >> 3;
-      const uint32_t cl = k == 0 ? 0 : k == 1 ? 1 : k == 2 ? 1 : 0, rl = k == 0 ? 0 : k == 1 ? 1 : k == 2 ? 0 : 3;
-      const uint32_t ch = k == 0 ? 2 : k == 1 ? 3 : k == 2 ? 3 : 2, rh = k == 0 ? 2 : k == 1 ? 3 : k == 2 ? 2 : 1;
-      klo = kbyte(6, cl, rl); khi = kbyte(6, ch, rh);
-    }
-    kp16[i] = (bs_kp(klo, b) & 0xffffu) | (bs_kp(khi, b) & 0xffff0000u);
-  }
-}
-
-// Packed output planes of lo16(PRF(16 m + j, x)) for j < 16: o[b] holds bit b
-// (low half) and bit 8 + b (high half) of tag j's value in bit j / 16 + j.
-__device__ __forceinline__ void bs16_prf16(const uint32_t* te0, const uint32_t* __restrict__ rk, const uint32_t* kx,
-                                           const uint32_t* wp16, const uint32_t* kp16, uint32_t m, uint32_t x,
-                                           uint32_t (&o)[8]) {
-  asm volatile("" ::: "memory");   // keep the LDS plane reads inside the caller's loop
-  uint32_t u[4];
-  bs_r12(te0, rk, x, m << 7, u);   // tag 16 m: w1 = 16 m << 3
-  Bs16 S;
-#pragma unroll
-  for (int pi = 0; pi < 2; ++pi)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const uint32_t* w = wp16 + 64 * (m & 1u) + 8 * (4 * pi + r);
-      const uint4 w0 = *reinterpret_cast<const uint4*>(w), w1 = *reinterpret_cast<const uint4*>(w + 4);
-      const uint32_t wl[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-#pragma unroll
-      for (int b = 0; b < 8; ++b) {
-        const uint32_t sh = 31 - (8 * r + b);
-        const uint32_t lo = (uint32_t)((int32_t)(u[pi] << sh) >> 31), hi = (uint32_t)((int32_t)(u[pi + 2] << sh) >> 31);
-        S.s[pi][r][b] = wl[b] ^ bs_lohi(lo, hi);
-      }
-    }
-#pragma unroll 1
-  for (int rr = 0; rr < 6; ++rr) bs16_round(S, kp16 + 64 * rr);   // rounds 3..8
-  // round 9: the eight useful bytes in four sets, S-boxes, MixColumns rows 0 (column 0) and 1 (column 1)
-  uint32_t A[8], B[8], C[8], D[8];
-#pragma unroll
-  for (int b = 0; b < 8; ++b) {
-    A[b] = bs_lohi(S.s[0][0][b], S.s[0][2][b]);   // bytes 0 | 10
-    B[b] = bs_lohi(S.s[1][1][b], S.s[1][3][b]);   // 5 | 15
-    C[b] = bs_lohi(S.s[1][0][b], S.s[1][2][b]);   // 4 | 14
-    D[b] = bs_lohi(S.s[0][3][b], S.s[0][1][b]);   // 3 | 9
-  }
-  uint32_t SA[8], SB[8], SC[8], SD[8];
-  bs_sbox(A, SA, bs_kload(kp16 + 384));
-  bs_sbox(B, SB, bs_kload(kp16 + 392));
-  bs_sbox(C, SC, bs_kload(kp16 + 400));
-  bs_sbox(D, SD, bs_kload(kp16 + 408));
-  // u00 = 2 (S0 ^ S5) ^ S5 ^ (S10 ^ S15) (low halves), u11 = 2 (S9 ^ S14) ^ S14 ^ (S3 ^ S4) (high halves)
-  uint32_t P1[8], P2[8], E[8];
-#pragma unroll
-  for (int b = 0; b < 8; ++b) {
-    P1[b] = bs_lohi(SA[b], SD[b]);                             // S0 | S9
-    P2[b] = bs_lohi(SB[b], SC[b]);                             // S5 | S14
-    E[b] = bs_rot16(bs_lohi(SD[b], SA[b])) ^ bs_rot16(bs_lohi(SC[b], SB[b]));   // S10 ^ S15 | S3 ^ S4
-  }
-  uint32_t d[8], uo[8];
-#pragma unroll
-  for (int b = 0; b < 8; ++b) d[b] = P1[b] ^ P2[b];
-  uo[0] = bs_x3(d[7], P2[0], E[0]);
-  uo[1] = bs_x3(d[0] ^ d[7], P2[1], E[1]);
-  uo[2] = bs_x3(d[1], P2[2], E[2]);
-  uo[3] = bs_x3(d[2] ^ d[7], P2[3], E[3]);
-  uo[4] = bs_x3(d[3] ^ d[7], P2[4], E[4]);
-  uo[5] = bs_x3(d[4], P2[5], E[5]);
-  uo[6] = bs_x3(d[5], P2[6], E[6]);
-  uo[7] = bs_x3(d[6], P2[7], E[7]);
-  // round 10: output bytes 0 | 1, with B's bytes 0 and 1 (x) folded into the constants
-  const uint32_t k10a = bs_kk(__builtin_amdgcn_readfirstlane(kx[28]) ^ (x & 0xffu));
-  const uint32_t k10b = bs_kk(__builtin_amdgcn_readfirstlane(kx[29]) ^ ((x >> 8) & 0xffu));
-  BsK K10;
-#pragma unroll
-  for (int b = 0; b < 8; ++b) K10.v[b] = (bs_kp(k10a, b) & 0xffffu) | (bs_kp(k10b, b) & 0xffff0000u);
-  bs_sbox(uo, o, K10);
-}
-
-// 16 x 16 bit transpose in the packed layout: w[b] = row b (low half) | row
-// 8 + b (high half), rows over tags j -> w[j'] = tag j' (low) | tag j' + 8 (high)
-__device__ __forceinline__ void bs16_transpose(uint32_t (&w)[8]) {
-#pragma unroll
-  for (int i = 0; i < 8; ++i) w[i] = __builtin_amdgcn_perm(w[i], w[i], 0x03010200u);   // swap bytes 1 and 2
-  auto stage = [&](int s, uint32_t msk) {
-#pragma unroll
-    for (int g = 0; g < 8; g += 2 * s)
-#pragma unroll
-      for (int i = g; i < g + s; ++i) {
-        const uint32_t t = ((w[i] >> s) ^ w[i + s]) & msk;
-        w[i + s] ^= t;
-        w[i] ^= t << s;
-      }
-  };
-  stage(4, 0x0f0f0f0fu);
-  stage(2, 0x33333333u);
-  stage(1, 0x55555555u);
-}
-
 }  // namespace pm

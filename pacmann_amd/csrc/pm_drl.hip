@@ -4,7 +4,7 @@
 // The host round of a lock-step team (pm_engine.cpp run_batched_pool: per
 // session the results' post-processing, GetVertexInfo's decode and success
 // count, SearchKNN's update and next batch, SimpleBatchPianoPIR.Query's
-// bucketing) as ONE launch of one 64-lane workgroup per session, so a team's
+// bucketing) as ONE launch of one kDrlThreads (256-thread) workgroup per session, so a team's
 // 20 rounds chain on its stream as [match + resolve, answer, round] with no
 // host round trip.  Same operations in the same order as the host restatement
 // (and the oracle), with Go's tie rules:

@@ -227,89 +227,6 @@ __global__ void __launch_bounds__(kBsThreads, PM_BS_WAVES) k_prep_offsets_bs(con
   }
 }
 
-// Packed bitsliced form (pm_aes_bs.h, bs16_*): 16 tags per lane, 128 VGPRs,
-// four waves per SIMD.  Same tables as k_prep_offsets, bit for bit.
-__global__ void __launch_bounds__(kBsThreads, 4) k_prep_offsets_bs16(const PmPart* __restrict__ parts) {
-  __shared__ uint32_t bs_te0[256];
-  __shared__ uint32_t bs_kx[32];
-  __shared__ uint32_t bs_wv[32][4];
-  __shared__ __attribute__((aligned(16))) uint32_t bs_wp16[128];
-  __shared__ __attribute__((aligned(16))) uint32_t bs_kp16[kBs16Kpl];
-  __shared__ __attribute__((aligned(16))) uint32_t bs_stash[8 * kBsThreads];
-  const PmPart& P = parts[blockIdx.y];
-  const uint32_t H = P.H, SS = P.SS, PH = P.PH;
-  const uint32_t nm = (H + 15) / 16, ng = (SS + 7) / 8;
-  if (blockIdx.x * kBsThreads >= nm * ng) return;   // block-uniform
-  bs_te0[threadIdx.x] = g_aes.te0[threadIdx.x];
-  __syncthreads();
-  bs_setup_a(bs_te0, P.rk, bs_kx, bs_wv);
-  __syncthreads();
-  bs16_setup_b(bs_wv, bs_kx, bs_wp16, bs_kp16);
-  __syncthreads();
-  const uint32_t task = blockIdx.x * kBsThreads + threadIdx.x;
-  if (task >= nm * ng) return;
-  const uint32_t m = task % nm, g = task / nm, h0 = 16 * m;
-  const uint32_t nb = P.log2CS, Qpc = P.Qpc;
-  uint32_t keep[8];   // plane b keeps bit b (low half) and bit 8 + b (high half) below log2(CS)
-#pragma unroll
-  for (int b = 0; b < 8; ++b) keep[b] = ((uint32_t)b < nb ? 0xffffu : 0u) | ((uint32_t)(8 + b) < nb ? 0xffff0000u : 0u);
-  auto lowmask = [](int n) { return n <= 0 ? 0u : n >= 16 ? 0xffffu : (1u << n) - 1u; };
-  uint4* stash = reinterpret_cast<uint4*>(bs_stash) + threadIdx.x;
-#pragma unroll 1
-  for (uint32_t q = 0; q < 8; ++q) {
-    const uint32_t cc = 8 * g + q, c = cc & ~1u;
-    uint32_t W0[8], W1[8];
-    if (c < SS) {   // SetSize is a multiple of 4: a pair is whole
-      uint32_t o[8];
-      bs16_prf16(bs_te0, P.rk, bs_kx, bs_wp16, bs_kp16, m, cc, o);
-      // backup hints whose own chunk is cc (pir.go:332-334): kSkip (all 16 bits set)
-      const int lo = (int)(PH + cc * Qpc) - (int)h0, hi = lo + (int)Qpc;
-      const uint32_t own16 = lowmask(hi) & ~lowmask(lo), own = own16 | (own16 << 16);
-#pragma unroll
-      for (int b = 0; b < 8; ++b) o[b] = (o[b] & keep[b]) | own;
-      bs16_transpose(o);
-      if ((q & 1) == 0) {
-        stash[0] = make_uint4(o[0], o[1], o[2], o[3]);
-        stash[kBsThreads] = make_uint4(o[4], o[5], o[6], o[7]);
-        continue;
-      }
-      const uint4 v0 = stash[0], v1 = stash[kBsThreads];
-      W0[0] = v0.x; W0[1] = v0.y; W0[2] = v0.z; W0[3] = v0.w; W0[4] = v1.x; W0[5] = v1.y; W0[6] = v1.z; W0[7] = v1.w;
-#pragma unroll
-      for (int b = 0; b < 8; ++b) W1[b] = o[b];
-    } else {
-      if ((q & 1) == 0) continue;
-#pragma unroll
-      for (int b = 0; b < 8; ++b) W0[b] = W1[b] = 0xffffffffu;   // tile padding past SetSize
-    }
-    // W0 / W1[j'] = tag j' (low) | tag j' + 8 (high) at chunks c / c + 1
-    uint32_t* tt = reinterpret_cast<uint32_t*>(P.tabT + tabT_index(H, h0, c));
-    const uint32_t nj = min(16u, H - h0);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if ((uint32_t)j < nj) tt[4 * j] = __builtin_amdgcn_perm(W1[j], W0[j], 0x05040100u);
-      if ((uint32_t)j + 8 < nj) tt[4 * (j + 8)] = __builtin_amdgcn_perm(W1[j], W0[j], 0x07060302u);
-    }
-    if (c >= SS) continue;
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {   // 8-hint blocks: tags 0..7 (low halves), 8..15 (high)
-      const uint32_t sel = half ? 0x07060302u : 0x05040100u, hb = h0 + 8 * half;
-      const uint4 w0 = make_uint4(__builtin_amdgcn_perm(W0[1], W0[0], sel), __builtin_amdgcn_perm(W0[3], W0[2], sel),
-                                  __builtin_amdgcn_perm(W0[5], W0[4], sel), __builtin_amdgcn_perm(W0[7], W0[6], sel));
-      const uint4 w1 = make_uint4(__builtin_amdgcn_perm(W1[1], W1[0], sel), __builtin_amdgcn_perm(W1[3], W1[2], sel),
-                                  __builtin_amdgcn_perm(W1[5], W1[4], sel), __builtin_amdgcn_perm(W1[7], W1[6], sel));
-      if (hb < PH) {
-        *reinterpret_cast<uint4*>(P.cur + cur_index(PH, P.curk, c, hb)) = w0;
-        *reinterpret_cast<uint4*>(P.cur + cur_index(PH, P.curk, c + 1, hb)) = w1;
-      }
-      if (P.tab && hb < H) {
-        *reinterpret_cast<uint4*>(P.tab + (uint64_t)c * H + hb) = w0;
-        *reinterpret_cast<uint4*>(P.tab + (uint64_t)(c + 1) * H + hb) = w1;
-      }
-    }
-  }
-}
-
 #ifndef PM_FOLD_NT
 #define PM_FOLD_NT 1   // k_prep_fold's (BIGANN's gather fold) row loads nontemporal: 221-222 -> 210-212 ms per
                        // 100M client = 0.83 of HBM peak (profiles/r05/ab/fold_nt_100m)
@@ -1265,10 +1182,6 @@ void prep_offsets_tt(hipStream_t st, const PmPart* d, int np, uint32_t maxH, uin
 }
 void prep_offsets_bs(hipStream_t st, const PmPart* d, int np, uint32_t maxH, uint32_t maxSS) {
   hipLaunchKernelGGL(k_prep_offsets_bs, dim3(cdiv((uint64_t)cdiv(maxH, 32) * cdiv(maxSS, 8), kBsThreads), np),
-                     dim3(kBsThreads), 0, st, d);
-}
-void prep_offsets_bs16(hipStream_t st, const PmPart* d, int np, uint32_t maxH, uint32_t maxSS) {
-  hipLaunchKernelGGL(k_prep_offsets_bs16, dim3(cdiv((uint64_t)cdiv(maxH, 16) * cdiv(maxSS, 8), kBsThreads), np),
                      dim3(kBsThreads), 0, st, d);
 }
 static std::atomic<int> g_aes_bs{-1};

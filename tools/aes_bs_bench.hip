@@ -1,8 +1,9 @@
-// aes_bs_bench.hip — the maintenance's PRF-table kernel in its three forms at
-// the serving shapes: k_prep_offsets (T-table AES in LDS, rounds 1-5) against
-// the bitsliced AES on the VALU (round 6, pm_aes_bs.h): k_prep_offsets_bs (32
-// blocks per lane, 256 VGPRs, 2 waves per SIMD) and k_prep_offsets_bs16 (16
-// blocks per lane, two bytes per plane word, 128 VGPRs, 4 waves per SIMD).
+// aes_bs_bench.hip — the maintenance's PRF-table kernel in its forms at the
+// serving shapes: k_prep_offsets (T-table AES in LDS, rounds 1-5) against the
+// bitsliced AES on the VALU (round 6, pm_aes_bs.h): k_prep_offsets_bs (32
+// blocks per lane, 256 VGPRs, 2 waves per SIMD).  The packed 16-block form
+// (k_prep_offsets_bs16, 128 VGPRs, 4 waves per SIMD) measured 0.85x and was
+// removed; it is in commit a8645fe (profiles/r06/aes/README.md).
 // All write every table (tabT, cur, and tab where given) for K clients x 16
 // partitions with their own keys; the outputs are compared word for word and
 // each launch is timed with HIP events (ABAB order, REPS rounds).
@@ -50,8 +51,8 @@ int main(int argc, char** argv) {
   const uint64_t per = tTw + cw + tw;
   printf("{\"shape\": \"%s\", \"clients\": %d, \"parts\": %d, \"H\": %u, \"SS\": %u, \"CS\": %u, \"curk\": %u, "
          "\"table_GB_per_variant\": %.2f}\n", S.name, K, np, H, S.SS, S.CS, curk, per * 2.0 * np / 1e9);
-  constexpr int NV = 3;
-  static const char* kname[NV] = {"k_prep_offsets", "k_prep_offsets_bs", "k_prep_offsets_bs16"};
+  constexpr int NV = 2;
+  static const char* kname[NV] = {"k_prep_offsets", "k_prep_offsets_bs"};
   uint16_t* buf[NV];
   for (int v = 0; v < NV; ++v) {
     CK(hipMalloc(&buf[v], per * 2 * np));
@@ -87,8 +88,7 @@ int main(int argc, char** argv) {
     for (int v = 0; v < NV; ++v) {
       CK(hipEventRecord(e0, 0));
       if (v == 0) pmk::prep_offsets_tt(0, dp[0], np, H, S.SS);
-      else if (v == 1) pmk::prep_offsets_bs(0, dp[1], np, H, S.SS);
-      else pmk::prep_offsets_bs16(0, dp[2], np, H, S.SS);
+      else pmk::prep_offsets_bs(0, dp[1], np, H, S.SS);
       CK(hipEventRecord(e1, 0));
       CK(hipEventSynchronize(e1));
       CK(hipGetLastError());
