@@ -893,9 +893,9 @@ class Watchdog:
     blocks marked, every rank exits.  fire() is called by the main thread when
     the blocks finished: False if the watchdog got there first."""
 
-    def __init__(self, out, rank, line_fd, budget_s):
+    def __init__(self, out, rank, line_fd, budget_s, keys=("config3_bigann_100m", "config4_bigann_1b")):
         import threading
-        self.out, self.rank, self.line_fd, self.budget_s = out, rank, line_fd, budget_s
+        self.out, self.rank, self.line_fd, self.budget_s, self.keys = out, rank, line_fd, budget_s, tuple(keys)
         self.lock = threading.Lock()
         self.done = False
         self.timer = threading.Timer(budget_s, self._expire) if budget_s > 0 else None
@@ -915,7 +915,7 @@ class Watchdog:
                 return
             self.done = True
             snap = dict(self.out)   # the blocks finished so far (each value is complete)
-        for key in ("config3_bigann_100m", "config4_bigann_1b"):
+        for key in self.keys:
             snap.setdefault(key, {"error": "unfinished: the run's multi-rank budget expired (watchdog)"})
         # the hang is reported in the line AND by the exit status (3): the
         # headline and single-GPU blocks in the line are complete and valid,
@@ -936,8 +936,8 @@ class Watchdog:
         return True
 
 
-def start_watchdog(out, rank, line_fd, budget_s):
-    return Watchdog(out, rank, line_fd, budget_s)
+def start_watchdog(out, rank, line_fd, budget_s, keys=("config3_bigann_100m", "config4_bigann_1b")):
+    return Watchdog(out, rank, line_fd, budget_s, keys)
 
 
 def cpu_baseline(v, g, q0, warmup, answers0, ctx, pir_seed, search_seed, k=K_TOP):
@@ -1035,6 +1035,9 @@ def main():
     ap.add_argument("--no-bigann", action="store_true", help="skip the BIGANN-100M / 1B batch-PIR blocks")
     ap.add_argument("--no-config0", action="store_true", help="skip the InnerProduct scan block")
     ap.add_argument("--big-sessions", type=int, default=0, help="cap on the BIGANN blocks' sessions per GPU")
+    ap.add_argument("--bigann-blocks", default="3,4",
+                    help="which BIGANN blocks run: configs[3] (100M) and/or configs[4] (1B), e.g. '3' for a "
+                         "multi-rank rehearsal on one GPU, where the 1B layout's shards do not fit")
     ap.add_argument("--big-groups", type=int, default=0, help="lock-step teams of the BIGANN blocks (0: BIG_GROUPS)")
     ap.add_argument("--combine", choices=["rccl", "torch-rccl", "gloo"], default="rccl",
                     help="collective of the sharded BIGANN rounds: rccl = the library's own RCCL communicators "
@@ -1459,7 +1462,9 @@ def main():
         # their budget, so a hang in a collective cannot lose the line.
         if rank == 0:
             progress("PARTIAL_LINE " + json.dumps(out))
-        wd = start_watchdog(out, rank, line_fd, args.bigann_budget_s)
+        want = {b.strip() for b in args.bigann_blocks.split(",")}
+        wd = start_watchdog(out, rank, line_fd, args.bigann_budget_s,
+                            keys=[k for k in ("config3_bigann_100m", "config4_bigann_1b") if k[6] in want])
         pm.set_option("rccl_timeout_s", 60)   # a peer that never joins costs 60 s, not the run
         prefer = {"rccl": "native", "torch-rccl": "torch-rccl", "gloo": "gloo"}[args.combine]
         memo = {}
@@ -1470,6 +1475,8 @@ def main():
             return memo["g"]
         for key, nm, n_entries in (("config3_bigann_100m", "BIGANN-100M-shaped (configs[3])", 100_000_000),
                                    ("config4_bigann_1b", "BIGANN-1B-shaped (configs[4])", 1_000_000_000)):
+            if key[6] not in want:
+                continue
             try:
                 progress(key)
                 lay = bigann_layout(key, ws, rank)
