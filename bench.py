@@ -184,23 +184,32 @@ def batch_pir_msmarco(ctx, with_cpu: bool):
     ctx.sync()
     prep = time.perf_counter() - t0
     rng = np.random.default_rng(78)
-    batches = rng.integers(0, C2_N, size=(C2_BATCHES + 20, C2_B)).astype(np.uint64)
+    batches = rng.integers(0, C2_N, size=(2 * C2_BATCHES + 10, C2_B)).astype(np.uint64)
     rows = db.reshape(C2_N, C2_E)
     for b in batches[:10]:   # warm-up
         g.Query(b)
     ctx.sync()
-    # the step kernels are timed over the timed batches themselves (events in
-    # their dispatch packets; no synchronisation added)
+
+    def query_pass(bs):
+        """The reference's loop (pir_test.go:245-262): Query, then check the
+        first response (zero or the entry).  Returns (seconds, mismatches)."""
+        t0 = time.perf_counter()
+        bad = 0
+        for b in bs:
+            resp, _ = g.Query(b)
+            r0 = resp[0]
+            bad += int(r0.any() and not np.array_equal(r0, rows[int(b[0])]))
+        ctx.sync()
+        return time.perf_counter() - t0, bad
+
+    # the throughput pass runs uninstrumented: events in the step's dispatch
+    # packet add ~8 us of launch time per batch (tools/batchpir_host.py), so
+    # the step kernel is timed over a second pass of fresh batches
+    support0 = g.SupportBatchNum
+    online, bad = query_pass(batches[10:10 + C2_BATCHES])
     ctx.timing_reset()
     ctx.timing(2)
-    t0 = time.perf_counter()
-    bad = 0
-    for b in batches[10:10 + C2_BATCHES]:
-        resp, _ = g.Query(b)
-        r0 = resp[0]   # the reference's check: the first response is zero or the entry
-        bad += int(r0.any() and not np.array_equal(r0, rows[int(b[0])]))
-    ctx.sync()
-    online = time.perf_counter() - t0
+    online_timed, bad_t = query_pass(batches[10 + C2_BATCHES:])
     ctx.timing(False)
     n, ms, by = ctx.timing_get("step")
     out = {"workload": "TestBatchPIRPerf shape (configs[2], MS-MARCO 3.2M): 3,201,821 x 896 B, BatchSize 32, "
@@ -208,7 +217,10 @@ def batch_pir_msmarco(ctx, with_cpu: bool):
            "preprocessing_s": round(prep, 6), "batches": C2_BATCHES,
            "batch_queries_per_s": round(C2_BATCHES / online, 1),
            "ids_per_s": round(C2_BATCHES * C2_B / online, 1), "ms_per_batch": round(online / C2_BATCHES * 1e3, 4),
-           "first_response_mismatches": bad}
+           "first_response_mismatches": bad + bad_t,
+           "kernel_timing_pass": {"batches": C2_BATCHES, "ms_per_batch": round(online_timed / C2_BATCHES * 1e3, 4),
+                                  "note": "a second pass of fresh batches with the step kernel's events on"},
+           "support_batch_num": support0, "finished_batch_num": g.FinishedBatchNum}
     if n:
         ach = (by / n) / (ms / n / 1e3) / 1e9
         out["roofline"] = {"bound": "hbm", "kernel": "step", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
@@ -223,27 +235,35 @@ def batch_pir_msmarco(ctx, with_cpu: bool):
     for c in clients[1:]:
         c.Preprocessing()
     grp = pm.BatchPIRGroup(clients)
-    gb = rng.integers(0, C2_N, size=(C2_BATCHES + 10, C2_CLIENTS, C2_B)).astype(np.uint64)
+    gb = rng.integers(0, C2_N, size=(2 * C2_BATCHES + 10, C2_CLIENTS, C2_B)).astype(np.uint64)
     for b in gb[:10]:
         grp.QueryWithMask(b)
     for c in clients:
         c.ctx.sync()
+
+    def group_pass(bs):
+        t0 = time.perf_counter()
+        bad = 0
+        for b in bs:
+            resp, ok = grp.QueryWithMask(b)
+            r0, ids0 = resp[:, 0], b[:, 0].astype(np.int64)   # every client's first response: zero or its entry
+            bad += int(((r0 != rows[ids0]).any(axis=1) & ok[:, 0]).sum() + (r0[~ok[:, 0]] != 0).any())
+        for c in clients:
+            c.ctx.sync()
+        return time.perf_counter() - t0, bad
+
+    # throughput uninstrumented, then the kernels timed over fresh rounds (as above)
+    gon, gbad = group_pass(gb[10:10 + C2_BATCHES])
     clients[0].ctx.timing_reset()
     clients[0].ctx.timing(2)   # the shared steps run on the first client's stream
-    t0 = time.perf_counter()
-    gbad = 0
-    for b in gb[10:]:
-        resp, ok = grp.QueryWithMask(b)
-        r0, ids0 = resp[:, 0], b[:, 0].astype(np.int64)   # every client's first response: zero or its entry
-        gbad += int(((r0 != rows[ids0]).any(axis=1) & ok[:, 0]).sum() + (r0[~ok[:, 0]] != 0).any())
-    for c in clients:
-        c.ctx.sync()
-    gon = time.perf_counter() - t0
+    gon_t, gbad_t = group_pass(gb[10 + C2_BATCHES:])
     clients[0].ctx.timing(False)
     out["clients_grouped"] = {"clients": C2_CLIENTS, "batches_per_client": C2_BATCHES,
                               "batch_queries_per_s": round(C2_CLIENTS * C2_BATCHES / gon, 1),
                               "ids_per_s": round(C2_CLIENTS * C2_BATCHES * C2_B / gon, 1),
-                              "ms_per_round": round(gon / C2_BATCHES * 1e3, 4), "first_response_mismatches": gbad}
+                              "ms_per_round": round(gon / C2_BATCHES * 1e3, 4),
+                              "first_response_mismatches": gbad + gbad_t,
+                              "kernel_timing_pass_ms_per_round": round(gon_t / C2_BATCHES * 1e3, 4)}
     n, ms, by = clients[0].ctx.timing_get("answer")
     if n:
         ach = (by / n) / (ms / n / 1e3) / 1e9

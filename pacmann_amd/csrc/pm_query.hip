@@ -41,6 +41,9 @@ constexpr int kAnsBlock = 512;
 #ifndef PM_ANSWER_NTLOAD
 #define PM_ANSWER_NTLOAD 0   // k_answer_p's row gather with nontemporal loads (streamed past the caches)
 #endif
+#ifndef PM_STEP_KG
+#define PM_STEP_KG 12   // k_step's answer role: rows per thread in flight together (configs[2]: 11 per thread)
+#endif
 #ifndef PM_ANSWER_KG
 #define PM_ANSWER_KG 6   // k_answer gather: rows per thread in flight together (no VGPR spill at 8 waves;
                          // alone 76.0-76.7 us vs 77.3 at 8 and 81-82 at 10, which spills 9 VGPRs)
@@ -1982,7 +1985,8 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, LDS& L)
         if (sl < nsl) {
           // every row load of a batch is issued before the first is consumed: the
           // gather is one HBM round trip per kG rows a thread reads, not one per 4
-          constexpr int kG = PM_ANSWER_KG;
+          // k_step (GRAN): one client's rows, a thread's whole share in one batch
+          constexpr int kG = GRAN ? PM_STEP_KG : PM_ANSWER_KG;
           typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
           for (uint32_t i0 = sl; i0 < P.SS; i0 += kG * nsl) {
             uint32_t rr[kG];   // partition rows (< 2^32): 32-bit, so the batch fits 64 VGPRs

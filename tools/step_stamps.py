@@ -28,14 +28,16 @@ def build():
     print(out)
 
 
-def run(steps=300):
+def run(steps=300, c2=False):
     import pacmann_amd as pm
-    N, E, B = 1_000_000, 80, 32
+    # default: SIFT1M-sized rounds of 96 ids; --c2: bench.py's configs[2]
+    # TestBatchPIRPerf shape (3,201,821 x 896 B, batches of 32 ids)
+    N, E, B, ids = (3_201_821, 112, 32, 32) if c2 else (1_000_000, 80, 32, 96)
     db = np.random.default_rng(0).integers(0, 2**64, size=N * E, dtype=np.uint64)
     g = pm.SimpleBatchPianoPIR(N, E * 8, B, db, 8, seed=1)
     g.Preprocessing()
     rng = np.random.default_rng(1)
-    for q in rng.integers(0, N, size=(steps, 96)).astype(np.uint64):
+    for q in rng.integers(0, N, size=(steps, ids)).astype(np.uint64):
         g.Query(q)
 
 
@@ -78,6 +80,6 @@ if __name__ == "__main__":
     if "--build" in sys.argv:
         build()
     if "--run" in sys.argv:
-        run()
+        run(c2="--c2" in sys.argv)
     if "--show" in sys.argv:
         show(sys.argv[sys.argv.index("--show") + 1])
