@@ -141,10 +141,12 @@ def make_queries(v, n, seed):
 
 
 def pmc_traffic(kernel_symbol: str, grid: int | None = None):
-    """HBM bytes per dispatch of `kernel_symbol` (of launches of `grid` threads
-    if given) from the newest committed rocprofv3 PMC summary (FETCH_SIZE x2
-    gfx950 correction + WRITE_SIZE, collected in separate --pmc passes of this
-    bench); None if absent."""
+    """Memory-side bytes per dispatch of `kernel_symbol` (of launches of `grid`
+    threads if given) from the newest committed rocprofv3 PMC summary
+    (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, collected in separate --pmc
+    passes of this bench); None if absent.  These count the L2's requests to
+    the fabric, Infinity Cache hits included (MI355X_MICROARCH.md): an upper
+    bound on HBM bytes."""
     best = None
     for f in sorted((ROOT / "profiles").glob("r*/pmc_summary.json")):
         k = json.loads(f.read_text()).get("kernels", {}).get(kernel_symbol)
