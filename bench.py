@@ -737,6 +737,62 @@ def inner_product_scan(ctx, with_cpu: bool):
     return out
 
 
+def ip_shard_rows(n, ws, rank):
+    """Rows [r0, r1) of the InnerProduct fill scanned by `rank` of `ws`
+    (the scan shards by rows)."""
+    return n * rank // ws, n * (rank + 1) // ws
+
+
+def ip_closed_form(r0, r1, d):
+    """sum_{r0 <= i < r1, j < d} (i + j) * j mod 2^32 (graphann_test.go:249-283's
+    fill v[i*D+j] = i+j, q[j] = j): rows [0, 1e8) at D = 128 give 1,178,525,696."""
+    n = r1 - r0
+    return ((r0 + r1 - 1) * n // 2 * (d * (d - 1) // 2) + n * ((d - 1) * d * (2 * d - 1) // 6)) % (1 << 32)
+
+
+def inner_product_scan_sharded(ctx, dist, rank, ws, local, nccl_group_fn):
+    """configs[0] over the job's ranks: rank r scans its rows of the 1e8-row
+    fill (ip_shard_rows; the same kernel, timed the same way, mean of 3), the
+    ranks' mod-2^32 sums are added by one all-reduce (over RCCL when the
+    agreed RCCL group exists, else gloo) and checked against the closed form;
+    scan time = the slowest rank's.  Total work fixed: strong scaling."""
+    import torch
+
+    import pacmann_amd as pm
+    r0, r1 = ip_shard_rows(C0_N, ws, rank)
+    runs = [pm.ip_bench(C0_N, C0_D, ctx, r0=r0, rows=r1 - r0) for _ in range(3)]
+    mine_ok = all(sm == ip_closed_form(r0, r1, C0_D) for sm, _ in runs)
+    ms_local = sum(m for _, m in runs) / len(runs)
+    grp = nccl_group_fn() if nccl_group_fn else None
+    sums = torch.tensor([sm for sm, _ in runs], dtype=torch.int64)
+    if grp is not None:   # the partial sums through RCCL (xGMI), like the reference's total
+        t = sums.to(f"cuda:{local}")
+        dist.all_reduce(t, group=grp)
+        total = t.cpu()
+    else:
+        dist.all_reduce(sums)
+        total = sums
+    ok = all((int(x) & 0xFFFFFFFF) == C0_SUM for x in total)
+    agg = torch.tensor([ms_local, float(mine_ok)], dtype=torch.float64)
+    mx, mn = agg.clone(), agg.clone()
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    dist.all_reduce(mn, op=dist.ReduceOp.MIN)
+    ms = float(mx[0])
+    nbytes = (r1 - r0) * C0_D * 4
+    ach = nbytes / (ms_local / 1e3) / 1e9
+    out = {"workload": "graphann_test.go InnerProduct bench (configs[0]): 1e8 x 128 uint32 rows v[i*D+j]=i+j, "
+                       f"q[j]=j, sum mod 2^32, rows sharded over {ws} GPUs",
+           "n_ranks": ws, "scaling": "strong", "shard_rows": r1 - r0,
+           "collective": "rccl" if grp is not None else "gloo",
+           "sum_ok": ok, "shard_sums_ok": bool(mn[1] == 1.0),
+           "scan_ms": round(ms, 4), "rows_per_s": round(C0_N / (ms / 1e3), 1),
+           "roofline": {"bound": "hbm", "kernel": "ip_scan", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": nbytes,
+                        "avg_ms": round(ms_local, 5), "launches": len(runs),
+                        "note": "rank 0's shard; scan_ms above is the slowest rank's"}}
+    return out
+
+
 def combine_probe(sess, qs, groups, args, local):
     """World 1: the sharded loop's two combine paths over a one-rank job, a
     few queries each on the block's sessions (results not in the block's
@@ -1505,17 +1561,20 @@ def main():
         del c0
         gc.collect()
     # BASELINE.json configs[3] (BIGANN-100M, sharded over the ranks) and
-    # configs[4] (BIGANN-1B in 8 shards): every rank takes part
-    if not args.no_bigann:
+    # configs[4] (BIGANN-1B in 8 shards), and with several ranks configs[0]
+    # sharded by rows: every rank takes part
+    ip_multi = ws > 1 and not args.no_config0
+    if not args.no_bigann or ip_multi:
         # The headline and the single-GPU blocks are complete: their line goes to
         # stderr now, and a watchdog writes the full line (the BIGANN blocks
         # marked unfinished) and ends the process if the blocks below overrun
         # their budget, so a hang in a collective cannot lose the line.
         if rank == 0:
             progress("PARTIAL_LINE " + json.dumps(out))
-        want = {b.strip() for b in args.bigann_blocks.split(",")}
+        want = set() if args.no_bigann else {b.strip() for b in args.bigann_blocks.split(",")}
         wd = start_watchdog(out, rank, line_fd, args.bigann_budget_s,
-                            keys=[k for k in ("config3_bigann_100m", "config4_bigann_1b") if k[6] in want])
+                            keys=(["config0_inner_product"] if ip_multi else []) +
+                                 [k for k in ("config3_bigann_100m", "config4_bigann_1b") if k[6] in want])
         pm.set_option("rccl_timeout_s", 60)   # a peer that never joins costs 60 s, not the run
         prefer = {"rccl": "native", "torch-rccl": "torch-rccl", "gloo": "gloo"}[args.combine]
         memo = {}
@@ -1524,6 +1583,15 @@ def main():
             if "g" not in memo:
                 memo["g"] = rccl_group(dist, local, out)
             return memo["g"]
+        if ip_multi:
+            try:
+                progress("config0 inner product, sharded by rows")
+                c0 = pm.Context(local)
+                wd.put("config0_inner_product", inner_product_scan_sharded(c0, dist, rank, ws, local, nccl_group_fn))
+                del c0
+                gc.collect()
+            except Exception as e:   # recorded, never fatal to the headline line
+                wd.put("config0_inner_product", {"error": f"{type(e).__name__}: {e}"})
         for key, nm, n_entries in (("config3_bigann_100m", "BIGANN-100M-shaped (configs[3])", 100_000_000),
                                    ("config4_bigann_1b", "BIGANN-1B-shaped (configs[4])", 1_000_000_000)):
             if key[6] not in want:

@@ -114,6 +114,11 @@ int pm_ip_batch(pm_ctx* ctx, const uint32_t* query, const uint32_t* rows, uint64
  * fills vectors[i*D+j] = i+j in HBM, query[j] = j, then sums the N row dot
  * products mod 2^32.  scan_ms = device time of the scan kernel alone. */
 int pm_ip_bench(pm_ctx* ctx, uint64_t N, uint64_t D, uint32_t* sum, double* scan_ms);
+/* The same scan over rows [r0, r0 + rows) of the N-row fill: one GPU's shard
+ * of the row-sharded scan (scans shard by rows, the mod-2^32
+ * partial sums add up to TestInnerProduct's sum).  r0 + rows <= N. */
+int pm_ip_bench_shard(pm_ctx* ctx, uint64_t N, uint64_t D, uint64_t r0, uint64_t rows, uint32_t* sum,
+                      double* scan_ms);
 
 /* ---- PianoPIR (pianopir/pir.go) --------------------------------------- */
 typedef struct {

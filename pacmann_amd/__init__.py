@@ -79,6 +79,7 @@ SIGNATURES = {
     "pm_l2_batch": (C.c_int, [vp, f32p, f32p, u64, u64, f32p]),
     "pm_ip_batch": (C.c_int, [vp, u32p, u32p, u64, u64, u32p, u32p]),
     "pm_ip_bench": (C.c_int, [vp, u64, u64, u32p, C.POINTER(dbl)]),
+    "pm_ip_bench_shard": (C.c_int, [vp, u64, u64, u64, u64, u32p, C.POINTER(dbl)]),
     "pm_pir_create": (C.c_int, [vp, u64, u64, u64p, u64, u64, C.POINTER(vp)]),
     "pm_pir_destroy": (None, [vp]),
     "pm_pir_preprocessing": (C.c_int, [vp]),
@@ -301,12 +302,17 @@ def ip_batch(query, rows, per_row: bool = True, ctx: Context | None = None):
     return (pr[: r.shape[0]] if per_row else None), s.value
 
 
-def ip_bench(N: int, D: int, ctx: Context | None = None):
-    """TestInnerProduct's scan fully on device; returns (sum, scan_ms)."""
+def ip_bench(N: int, D: int, ctx: Context | None = None, r0: int = 0, rows: int | None = None):
+    """TestInnerProduct's scan fully on device; returns (sum, scan_ms).  With
+    r0 / rows: only rows [r0, r0 + rows) of the N-row fill (one GPU's shard;
+    the shards' sums add up mod 2^32 to the whole scan's)."""
     ctx = ctx or default_context()
     s = C.c_uint32()
     ms = C.c_double()
-    _check(lib().pm_ip_bench(ctx.h, N, D, C.byref(s), C.byref(ms)))
+    if rows is None and r0 == 0:
+        _check(lib().pm_ip_bench(ctx.h, N, D, C.byref(s), C.byref(ms)))
+    else:
+        _check(lib().pm_ip_bench_shard(ctx.h, N, D, r0, N - r0 if rows is None else rows, C.byref(s), C.byref(ms)))
     return s.value, ms.value
 
 

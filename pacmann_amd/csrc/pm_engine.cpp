@@ -1837,7 +1837,18 @@ extern "C" int pm_ip_batch(pm_ctx* c, const uint32_t* q, const uint32_t* rows, u
   return 0;
 }
 extern "C" int pm_ip_bench(pm_ctx* c, uint64_t N, uint64_t D, uint32_t* sum, double* scan_ms) {
+  return pm_ip_bench_shard(c, N, D, 0, N, sum, scan_ms);
+}
+extern "C" int pm_ip_bench_shard(pm_ctx* c, uint64_t Ntot, uint64_t D, uint64_t r0, uint64_t N, uint32_t* sum,
+                                 double* scan_ms) {
+  if (!c) return fail(PM_EINVAL, "NULL context");
   if (D == 0 || D % 4 || D > 4096) return fail(PM_EINVAL, "D must be a multiple of 4 and <= 4096");
+  if (r0 > Ntot || N > Ntot - r0) return fail(PM_EINVAL, "shard rows past the fill's N");
+  if (N == 0) {   // an empty shard adds nothing
+    if (sum) *sum = 0;
+    if (scan_ms) *scan_ms = 0.0;
+    return 0;
+  }
   DevBuf dv, dq, ds;
   CHK(dv.reserve(N * D * 4)); CHK(dq.reserve(D * 4)); CHK(ds.reserve(4));
   std::vector<uint32_t> q(D);
@@ -1845,7 +1856,7 @@ extern "C" int pm_ip_bench(pm_ctx* c, uint64_t N, uint64_t D, uint32_t* sum, dou
   hipStream_t st = c->stream;
   HIPCHK(hipMemcpyAsync(dq.p, q.data(), D * 4, hipMemcpyHostToDevice, st));
   HIPCHK(hipMemsetAsync(ds.p, 0, 4, st));
-  pmk::ip_fill(st, dv.as<uint32_t>(), N, (uint32_t)D);
+  pmk::ip_fill(st, dv.as<uint32_t>(), N, (uint32_t)D, r0);
   hipEvent_t a, b;
   HIPCHK(hipEventCreate(&a)); HIPCHK(hipEventCreate(&b));
   HIPCHK(hipEventRecord(a, st));

@@ -366,7 +366,7 @@ void l2_rows(hipStream_t st, const float* rows, uint64_t row_stride_floats, uint
              const uint32_t* row_ids, const float* q, uint32_t dim, float* out, uint64_t seglen = 0);
 void ip_rows(hipStream_t st, const uint32_t* rows, uint64_t nrows, const uint32_t* q, uint32_t dim,
              uint32_t* per_row, uint32_t* sum);
-void ip_fill(hipStream_t st, uint32_t* rows, uint64_t N, uint32_t D);
+void ip_fill(hipStream_t st, uint32_t* rows, uint64_t N, uint32_t D, uint64_t r0 = 0);   // rows r0 .. r0 + N
 // Synthetic DB rows (pm_batchpir_create_synth): dst row i = global row r0 + i,
 // word w = sm64(sm64(db_seed + DOM_SYNTH_DB) ^ (r * E + w)).
 void db_synth(hipStream_t st, uint64_t* dst, uint64_t r0, uint64_t rows, uint32_t E, uint64_t db_seed);

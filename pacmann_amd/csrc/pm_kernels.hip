@@ -1118,11 +1118,12 @@ __global__ void __launch_bounds__(kBlock) k_ip_scan(const uint4* __restrict__ ro
   if ((threadIdx.x & 63) == 0) atomicAdd(sum, acc);
 }
 
-__global__ void __launch_bounds__(kBlock) k_ip_fill(uint4* __restrict__ rows, uint64_t n4, uint32_t dim) {
+__global__ void __launch_bounds__(kBlock) k_ip_fill(uint4* __restrict__ rows, uint64_t n4, uint32_t dim,
+                                                    uint64_t r0) {
   const uint64_t stride = (uint64_t)gridDim.x * kBlock;
   for (uint64_t f = (uint64_t)blockIdx.x * kBlock + threadIdx.x; f < n4; f += stride) {
     const uint64_t e = f * 4;
-    const uint32_t i = (uint32_t)(e / dim), j = (uint32_t)(e % dim);
+    const uint32_t i = (uint32_t)(r0 + e / dim), j = (uint32_t)(e % dim);   // global row (uint32 as in Go)
     rows[f] = make_uint4(i + j, i + j + 1, i + j + 2, i + j + 3);
   }
 }
@@ -1336,11 +1337,12 @@ void ip_rows(hipStream_t st, const uint32_t* rows, uint64_t nrows, const uint32_
   hipLaunchKernelGGL(k_ip_rows, dim3(cdiv(nrows * 16, kBlock)), dim3(kBlock), 0, st, rows, nrows, q, dim,
                      per_row, sum);
 }
-void ip_fill(hipStream_t st, uint32_t* rows, uint64_t N, uint32_t D) {
+void ip_fill(hipStream_t st, uint32_t* rows, uint64_t N, uint32_t D, uint64_t r0) {
   const uint64_t n4 = N * D / 4;
   unsigned grid = cdiv(n4, kBlock);
   if (grid > 256 * 16) grid = 256 * 16;
-  hipLaunchKernelGGL(k_ip_fill, dim3(grid), dim3(kBlock), 0, st, (uint4*)rows, n4, D);
+  if (grid == 0) return;
+  hipLaunchKernelGGL(k_ip_fill, dim3(grid), dim3(kBlock), 0, st, (uint4*)rows, n4, D, r0);
 }
 void db_synth(hipStream_t st, uint64_t* dst, uint64_t r0, uint64_t rows, uint32_t E, uint64_t db_seed) {
   const uint64_t nw = rows * E;

@@ -64,6 +64,21 @@ def test_bigann_rates_fields():
     assert r2["private_queries_per_s"] == round(2 * 18 * 36 / 0.25, 2)
 
 
+def test_ip_shards_closed_form():
+    """configs[0] sharded by rows (bench.ip_shard_rows / ip_closed_form): the
+    shards cover [0, N) once, and their mod-2^32 sums add up to
+    TestInnerProduct's 1,178,525,696 at N = 1e8, D = 128."""
+    b = _bench()
+    assert b.ip_closed_form(0, b.C0_N, b.C0_D) == b.C0_SUM == 1_178_525_696
+    for ws in (1, 2, 3, 4, 8):
+        spans = [b.ip_shard_rows(b.C0_N, ws, r) for r in range(ws)]
+        assert spans[0][0] == 0 and spans[-1][1] == b.C0_N
+        assert all(spans[i][1] == spans[i + 1][0] for i in range(ws - 1))
+        assert sum(b.ip_closed_form(r0, r1, b.C0_D) for r0, r1 in spans) % (1 << 32) == b.C0_SUM
+    # small case against the definition
+    assert b.ip_closed_form(3, 11, 8) == sum((i + j) * j for i in range(3, 11) for j in range(8)) % (1 << 32)
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -84,8 +99,12 @@ def _rank(rank, world, port, out_dir):
         g = groups[rank // 2]
         t = torch.tensor([1 << rank], dtype=torch.int64)
         dist.all_reduce(t, group=g)
+        # configs[0] over the world: this rank's shard sum, reduced like the bench's gloo path
+        r0, r1 = b.ip_shard_rows(b.C0_N, world, rank)
+        ip = torch.tensor([b.ip_closed_form(r0, r1, b.C0_D)], dtype=torch.int64)
+        dist.all_reduce(ip)
         with open(os.path.join(out_dir, f"r{rank}.txt"), "w") as f:
-            f.write(f"{lay['layout']}|{lay['shard']}|{lay['replica']}|{int(t.item())}")
+            f.write(f"{lay['layout']}|{lay['shard']}|{lay['replica']}|{int(t.item())}|{int(ip.item()) & 0xFFFFFFFF}")
     finally:
         dist.destroy_process_group()
 
@@ -98,3 +117,4 @@ def test_replica_groups_gloo_world4():
         assert res[r][:3] == ["4", str(r), "0"], res
         pair = (1 << (r & ~1)) | (1 << ((r & ~1) + 1))
         assert int(res[r][3]) == pair, res   # the group reduced over its own two ranks only
+        assert int(res[r][4]) == 1_178_525_696, res   # configs[0]'s shard sums over the world

@@ -101,6 +101,28 @@ def test_ip_bench_closed_form(ctx, oracle):
     assert s == oracle.inner_product_bench(1_000_000, 128, 8)
 
 
+@pytest.mark.parametrize("ws", [2, 3, 8])
+def test_ip_bench_shards(ctx, oracle, ws):
+    """The row-sharded scan (pm_ip_bench_shard, bench.py's configs[0] over N
+    ranks): each shard's sum equals its closed form and the oracle's scan of
+    the same rows, and the shards' sums add up mod 2^32 to the whole fill's."""
+    import pacmann_amd as pm
+    N, D = 1_000_003, 128
+    total = 0
+    for r in range(ws):
+        r0, r1 = N * r // ws, N * (r + 1) // ws
+        s, _ = pm.ip_bench(N, D, ctx, r0=r0, rows=r1 - r0)
+        assert s == (ip_closed_form(r1, D) - ip_closed_form(r0, D)) % 2**32, (ws, r)
+        if r == ws - 1:   # the last shard's rows materialised: the oracle's InnerProduct over them
+            rows = (np.arange(r0, r1, dtype=np.uint32)[:, None] + np.arange(D, dtype=np.uint32)[None, :])
+            assert s == oracle.inner_product_scan(rows, np.arange(D, dtype=np.uint32), 1)
+        total += s
+    assert total % 2**32 == ip_closed_form(N, D)
+    assert pm.ip_bench(N, D, ctx, r0=N, rows=0)[0] == 0   # an empty shard
+    with pytest.raises(RuntimeError, match="past the fill"):
+        pm.ip_bench(N, D, ctx, r0=N - 5, rows=10)
+
+
 @pytest.mark.slow
 def test_ip_bench_full_size(ctx):
     """graphann_test.go:249-283 at N=1e8, D=128 (51.2 GB in HBM)."""
