@@ -468,7 +468,7 @@ struct Engine {
   uint32_t gran_words = 0;
   std::vector<uint32_t> owned_list;   // owned partitions in order (owned_d holds their PmPart)
   DevBuf qoffs, ans_srv;
-  DevBuf subs_d, sb_d, bits, cand, meta, spec, res_d, ans, part_x, qvec, stamps;
+  DevBuf subs_d, sb_d, bits, cand, meta, spec, res_d, ans, part_x, qvec, stamps, helpg;
   std::vector<double> stamp_sum;   // PM_STAMPS builds: accumulated phase deltas
   uint64_t stamp_n = 0;
   uint32_t step_token = 0;         // PmStep::token of the last step
@@ -706,6 +706,9 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
     const size_t n = (size_t)kArgSubs * (8 + 64 + 2 * g->gran_words + 8) * 8;
     CHK(g->gran.reserve(n));
     HIPCHK(hipMemset(g->gran.p, 0, n));
+    const size_t nh = (size_t)kArgSubs * kStepHelpMax * kHelpGran * 8;   // the gather helpers' hand-offs
+    CHK(g->helpg.reserve(nh));
+    HIPCHK(hipMemset(g->helpg.p, 0, nh));
     CHK(g->err_h.reserve(64));
     memset(g->err_h.p, 0, 64);
   }
@@ -1237,8 +1240,17 @@ static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
   if (!c->no_fuse && !c->debug_sync && pmk::step_fused_ok(S, g->maxPH, max_per_part)) {
     S.cblk = 1;   // one match workgroup per sub-query
     S.no_guess = c->no_guess ? 1u : 0u;
+    // gather helpers where the launch still fits the 240 co-resident
+    // workgroups (one 1,024-thread workgroup per CU): configs[2]'s 32
+    // sub-queries over 16 partitions take PM_STEP_HELP (default 3) each; 0 disables
+    static const int help_env = [] { const char* e = getenv("PM_STEP_HELP"); return e ? atoi(e) : 3; }();
+    S.nhelp = 0;
+    if (help_env > 0 && (E & ~3ull) <= kHelpWords && g->helpg.p && 2 * nsub + g->P < 240)
+      S.nhelp = std::min<uint32_t>(std::min<uint32_t>(kStepHelpMax, (uint32_t)help_env),
+                                   (uint32_t)((240 - 2 * nsub - g->P) / nsub));
+    S.helpg = g->helpg.as<uint64_t>();
 #ifdef PM_STEP_STAMPS
-    const uint32_t grid = 2 * nsub + (uint32_t)g->P;
+    const uint32_t grid = 2 * nsub + (uint32_t)g->P + S.nhelp * nsub;
     CHK(g->stamps.reserve((uint64_t)grid * 8 * 8));
     HIPCHK(hipMemsetAsync(g->stamps.p, 0, (uint64_t)grid * 8 * 8, st));
     S.stamps = g->stamps.as<uint64_t>();

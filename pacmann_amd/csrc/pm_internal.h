@@ -198,6 +198,10 @@ struct alignas(16) PmOutHdr {
 #define PM_KARG_SUBS 112
 #endif
 constexpr uint32_t kArgSubs = PM_KARG_SUBS, kArgParts = PM_KARG_SUBS > 1 ? 32 : 1;
+// k_step gather helpers (PmStep::nhelp): at most kStepHelpMax per sub-query,
+// for entries of <= 256 gathered words; granules per helper: 2 x 256 partial
+// words + 8 guess fields
+constexpr uint32_t kStepHelpMax = 5, kHelpWords = 256, kHelpGran = 2 * kHelpWords + 8;
 struct PmStep {
   const PM_G PmPart* parts;
   const PM_G PmSub* subs_h;    // pinned host descriptor, read zero-copy by k_match
@@ -224,6 +228,11 @@ struct PmStep {
   PM_G uint64_t* specg;        // [kArgSubs][64] predicted re-evaluation values
   PM_G uint64_t* bitsg;        // [kArgSubs][words][2] match bits
   PM_G uint64_t* resg;         // [kArgSubs][8] resolution records
+  // k_step gather helpers: nhelp extra workgroups per sub-query each gather a
+  // range of the guessed set and hand over its partial XOR (granules: 2 per
+  // word of the partial, then the guess fields); 0 = none
+  PM_G uint64_t* helpg;        // [kArgSubs][kStepHelpMax][kHelpGran]
+  uint32_t nhelp;
   PM_G uint32_t* err_h;        // pinned host: set when a hand-off spin timed out        // [np] k_step: token of the step whose results the resolver published
   uint32_t words, E, dim, nsub, np, cblk;
   uint32_t np_live;            // partitions with at least one sub-query in this step

@@ -1867,6 +1867,140 @@ __device__ __forceinline__ uint32_t answer_mode(const PmRes& r) {
        : r.status == ST_DUMMY ? A_DUMMY : A_ZERO;
 }
 
+// The query set of (r, mode) for chunks [lo, hi) into qo (pir.go:363-371
+// dummy; :424-444 real): PRF row of the tag, program point and replacement
+// substituted.
+template <int NT>
+__device__ __forceinline__ void set_range(const PmPart& P, const PmSub& sub, const PmRes& r, uint32_t mode,
+                                          uint16_t* qo, uint32_t lo, uint32_t hi) {
+  const uint32_t tid = threadIdx.x, mask = P.CS - 1, lg = P.log2CS;
+  if (mode == A_FINAL || mode == A_CHAINED) {
+    const uint32_t pchunk = r.pp != kDefaultProgramPoint ? (r.pp >> lg) : kNone;
+    for (uint32_t i = lo + tid; i < hi; i += NT) {
+      uint32_t o = P.tabT[tabT_index(P.H, r.tag, i)];
+      if (i == pchunk) o = r.pp & mask;
+      if (i == r.chunk) o = P.ridx[r.chunk * P.Qpc + r.ing] & mask;
+      qo[i] = (uint16_t)o;
+    }
+  } else if (mode == A_DUMMY) {
+    for (uint32_t i = lo + tid; i < hi; i += NT)
+      qo[i] = (uint16_t)(hash4(P.seed, DOM_DUMMY, P.idx, sub.idx, i) & mask);
+  }
+}
+
+// The server XOR gather (HOT LOOP E) of the set's chunks [lo, hi) into
+// row.w[0..EX): every row load of a batch is issued before the first is
+// consumed, so the gather is one HBM round trip per kG rows a thread reads.
+template <int W, int NT, int kG, class RB>
+__device__ __forceinline__ void gather_range(const PmStep& S, const PmPart& P, const uint16_t* qo, uint64_t* red,
+                                             RB& row, uint32_t lo, uint32_t hi) {
+  const uint32_t tid = threadIdx.x, E = S.E, EX = E & ~3u, NSEG = EX / W;
+  const PM_G uint64_t* base = S.db + P.row0 * E;
+  for (uint32_t seg0 = 0; seg0 < NSEG; seg0 += NT) {
+    const uint32_t nseg = min(NSEG - seg0, (uint32_t)NT);
+    const uint32_t nsl = NT / nseg;
+    const uint32_t sl = tid / nseg, seg = seg0 + tid % nseg;
+    uint64_t a0 = 0, a1 = 0;
+    if (sl < nsl) {
+      typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+      for (uint32_t i0 = lo + sl; i0 < hi; i0 += kG * nsl) {
+        uint32_t rr[kG];   // partition rows (< 2^32): 32-bit, so the batch fits 64 VGPRs
+        // the batch's set offsets: unconditional LDS reads (clamped index),
+        // all in flight before one wait (a read inside each bounds branch
+        // waited for its own result before the next was issued)
+#pragma unroll
+        for (int u = 0; u < kG; ++u) rr[u] = qo[min(i0 + u * nsl, hi - 1)];
+#pragma unroll
+        for (int u = 0; u < kG; ++u) {
+          const uint32_t i = i0 + u * nsl;
+          rr[u] = i < hi ? i * P.CS + rr[u] : ~0u;
+        }
+        u64x2 x[kG];
+#pragma unroll
+        for (int u = 0; u < kG; ++u) {
+          x[u] = u64x2{0, 0};
+          if (rr[u] < P.N) {
+            const PM_G uint64_t* q = base + (uint64_t)rr[u] * E + (uint64_t)seg * W;
+            if (W == 2) x[u] = *reinterpret_cast<const PM_G u64x2*>(q);
+            else x[u].x = *q;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < kG; ++u) { a0 ^= x[u].x; a1 ^= x[u].y; }
+      }
+    }
+    red[tid * 2] = a0;
+    red[tid * 2 + 1] = a1;
+    __syncthreads();
+    if (tid < nseg) {
+      uint64_t x0 = 0, x1 = 0;
+      for (uint32_t k = 0; k < nsl; ++k) {
+        x0 ^= red[(k * nseg + tid) * 2];
+        x1 ^= red[(k * nseg + tid) * 2 + 1];
+      }
+      row.w[seg * W] = x0;
+      if (W == 2) row.w[seg * W + 1] = x1;
+    }
+    __syncthreads();
+  }
+}
+
+// k_step's guess of sub-query s's resolution (see answer_role): a dummy's set
+// needs none; a real one's first stale candidate over every hint (the match
+// role's predicate and state; one tag load per wave), with the in-chunk
+// index predicted from the chunk's QueryHistogram.  Whole workgroup (LDS:
+// L.f, L.red).  Returns the guessed answer mode (kNone: no guess).
+template <int NT, class LDS>
+__device__ __forceinline__ uint32_t step_guess(const PmStep& S, uint32_t s, const PmSub& sub, const PmPart& P, LDS& L,
+                                               PmRes& g) {
+  constexpr bool GRAN = true;   // (stamps)
+  (void)GRAN;
+  g = PmRes{kNone, 0, 0, 0, 0, 0, 0, 0};
+  if (S.no_guess) return kNone;
+  if (sub.kind == SUB_DUMMY) {
+    g.status = ST_DUMMY;
+    return A_DUMMY;
+  }
+  if (!(sub.kind == SUB_REAL && sub.idx < P.N)) return kNone;
+  const uint32_t tid = threadIdx.x, mask = P.CS - 1, lg = P.log2CS;
+  constexpr int HPT = kLdsPH / NT;   // k_step: PH <= kLdsPH
+  const uint32_t ch = (uint32_t)(sub.idx >> lg), off = (uint32_t)(sub.idx & mask);
+  const uint32_t wave = tid >> 6, lane = tid & 63;
+  uint32_t rv[HPT];
+  const PM_G uint16_t* crow = P.cur + cur_row(P.PH, P.curk, ch);   // match: value == offset (see match_role)
+#pragma unroll
+  for (int u = 0; u < HPT; ++u) rv[u] = u * NT + tid < P.PH ? crow[cur_row_off(P.curk, u * NT + tid)] : kNone;
+  const uint32_t h0k = wave == 0 ? P.hist[ch] : 0;
+  // per wave the lowest matching hint (lower u first: hints u*NT + tid)
+  uint32_t wh = kNone, wt = 0, wp = 0;
+#pragma unroll
+  for (int u = 0; u < HPT; ++u) {
+    const uint64_t bm = __ballot(rv[u] == off);
+    if (bm && wh == kNone) wh = u * NT + wave * 64 + (uint32_t)__builtin_ctzll(bm);
+  }
+  if (wh != kNone) { wt = P.tag[wh]; wp = P.pp[wh]; }
+  if (lane == 0) { L.f[wave] = wh; L.red[2 * wave] = wt; L.red[2 * wave + 1] = wp; }
+  if (wave == 0) {
+    const uint32_t pb0 = step_sb(S, sub.part), pn = step_sb(S, sub.part + 1) - pb0;
+    PmSub st;
+    bool validt;
+    const uint32_t sg0 = predict_ing(S, P, pb0, pn, s - pb0, ch, h0k, st, validt);
+    if (lane == 0) L.f[16] = sg0;
+  }
+  __syncthreads();
+  uint32_t c1 = kNone, t1 = 0, p1 = 0;
+  const uint32_t sg = L.f[16];
+  AS(0);
+  for (uint32_t w = 0; w < NT / 64; ++w)
+    if (L.f[w] < c1) { c1 = L.f[w]; t1 = (uint32_t)L.red[2 * w]; p1 = (uint32_t)L.red[2 * w + 1]; }
+  __syncthreads();
+  if (c1 != kNone && sg < P.Qpc && ch < P.SS) {
+    g = PmRes{ST_OK, c1, ch, sg, t1, p1, 0, 0};
+    return A_FINAL;
+  }
+  return kNone;
+}
+
 // One sub-query's answer (HOT LOOPs D + E, decode, outputs).  GRAN: inside
 // k_step.  There the answer starts before its partition's resolver is done:
 // a dummy sub-query's set does not depend on the resolution at all, and a
@@ -1882,7 +2016,7 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, LDS& L)
   uint64_t* const red = L.red;
   auto& row = L.row;
   const uint32_t tid = threadIdx.x;
-  const uint32_t E = S.E, EX = E & ~3u, NSEG = EX / W;
+  const uint32_t E = S.E, EX = E & ~3u;
   const PmSub sub = step_sub(S, s);
   const PmPart& P = S.parts[sub.part];
   PM_G uint64_t* const orow = S.rows_h + (uint64_t)s * E;
@@ -1894,7 +2028,6 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, LDS& L)
     S.stamps[(uint64_t)blockIdx.x * 8 + 6] = ((uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
                                              (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
 #endif
-  const uint32_t mask = P.CS - 1, lg = P.log2CS;
   // the search query the decoded row is scored against (L2): loaded now, in
   // flight with everything else, and put into LDS once the gather is done
   const float* const qq = P.qv ? P.qv : S.q;
@@ -1912,7 +2045,7 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, LDS& L)
   uint64_t e_rv = 0, e_bp = 0, e_pp = 0;
   uint32_t e_cur = kSkip;   // the refreshed hint's new search-row value at chunk tid (refresh_cur)
   // set expansion + gather into row.w[0..EX) and the decode operands for (r, mode)
-  auto gather = [&](const PmRes& r, uint32_t mode) {
+  auto gather = [&](const PmRes& r, uint32_t mode, uint32_t lo, uint32_t hi) {
     // a pre-expanded set goes to LDS before any later load is issued (its wait
     // then covers only the loads issued with the record)
     if (qpre && (mode == A_FINAL || mode == A_CHAINED) && tid < S.qw / 8)
@@ -1957,17 +2090,8 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, LDS& L)
     // ---- query set (pir.go:363-371 dummy; :424-444 real) -------------------
     if (qpre && (mode == A_FINAL || mode == A_CHAINED)) {
       // expanded by k_match_resolve_s: in LDS already (above)
-    } else if (mode == A_FINAL || mode == A_CHAINED) {
-      const uint32_t pchunk = r.pp != kDefaultProgramPoint ? (r.pp >> lg) : kNone;
-      for (uint32_t i = tid; i < P.SS; i += NT) {
-        uint32_t o = P.tabT[tabT_index(P.H, r.tag, i)];
-        if (i == pchunk) o = r.pp & mask;
-        if (i == r.chunk) o = P.ridx[r.chunk * P.Qpc + r.ing] & mask;
-        qo[i] = (uint16_t)o;
-      }
-    } else if (mode == A_DUMMY) {
-      for (uint32_t i = tid; i < P.SS; i += NT)
-        qo[i] = (uint16_t)(hash4(P.seed, DOM_DUMMY, P.idx, sub.idx, i) & mask);
+    } else {
+      set_range<NT>(P, sub, r, mode, qo, lo, hi);
     }
     STAMP_AT(stamp_wg && mode == A_FINAL, 49);
     __syncthreads();
@@ -1975,112 +2099,64 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, LDS& L)
     STAMP_AT(stamp_wg, 50);
     AST(2);
     // ---- server XOR gather (HOT LOOP E) into row.w[0..EX) ------------------
-    if (mode == A_FINAL || mode == A_CHAINED || mode == A_DUMMY) {
-      const PM_G uint64_t* base = S.db + P.row0 * E;
-      for (uint32_t seg0 = 0; seg0 < NSEG; seg0 += NT) {
-        const uint32_t nseg = min(NSEG - seg0, (uint32_t)NT);
-        const uint32_t nsl = NT / nseg;
-        const uint32_t sl = tid / nseg, seg = seg0 + tid % nseg;
-        uint64_t a0 = 0, a1 = 0;
-        if (sl < nsl) {
-          // every row load of a batch is issued before the first is consumed: the
-          // gather is one HBM round trip per kG rows a thread reads, not one per 4
-          // k_step (GRAN): one client's rows, a thread's whole share in one batch
-          constexpr int kG = GRAN ? PM_STEP_KG : PM_ANSWER_KG;
-          typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-          for (uint32_t i0 = sl; i0 < P.SS; i0 += kG * nsl) {
-            uint32_t rr[kG];   // partition rows (< 2^32): 32-bit, so the batch fits 64 VGPRs
-            // the batch's set offsets: unconditional LDS reads (clamped index),
-            // all in flight before one wait (a read inside each bounds branch
-            // waited for its own result before the next was issued)
-#pragma unroll
-            for (int u = 0; u < kG; ++u) rr[u] = qo[min(i0 + u * nsl, P.SS - 1)];
-#pragma unroll
-            for (int u = 0; u < kG; ++u) {
-              const uint32_t i = i0 + u * nsl;
-              rr[u] = i < P.SS ? i * P.CS + rr[u] : ~0u;
-            }
-            u64x2 x[kG];
-#pragma unroll
-            for (int u = 0; u < kG; ++u) {
-              x[u] = u64x2{0, 0};
-              if (rr[u] < P.N) {
-                const PM_G uint64_t* q = base + (uint64_t)rr[u] * E + (uint64_t)seg * W;
-                if (W == 2) x[u] = *reinterpret_cast<const PM_G u64x2*>(q);
-                else x[u].x = *q;
-              }
-            }
-#pragma unroll
-            for (int u = 0; u < kG; ++u) { a0 ^= x[u].x; a1 ^= x[u].y; }
-          }
-        }
-        red[tid * 2] = a0;
-        red[tid * 2 + 1] = a1;
-        __syncthreads();
-        if (tid < nseg) {
-          uint64_t x0 = 0, x1 = 0;
-          for (uint32_t k = 0; k < nsl; ++k) {
-            x0 ^= red[(k * nseg + tid) * 2];
-            x1 ^= red[(k * nseg + tid) * 2 + 1];
-          }
-          row.w[seg * W] = x0;
-          if (W == 2) row.w[seg * W + 1] = x1;
-        }
-        __syncthreads();
-      }
-    }
+    // (k_step, GRAN: one client's rows, a thread's whole share in one batch)
+    if (mode == A_FINAL || mode == A_CHAINED || mode == A_DUMMY)
+      gather_range<W, NT, GRAN ? PM_STEP_KG : PM_ANSWER_KG>(S, P, qo, red, row, lo, hi);
   };
   PmRes r;
   uint32_t mode;
   if (GRAN) {
     // ---- the guess (see above), from this sub-query's match record ---------
-    PmRes g{kNone, 0, 0, 0, 0, 0, 0, 0};
-    uint32_t gmode = kNone;
-    if (S.no_guess) {
-    } else if (sub.kind == SUB_DUMMY) {
-      g.status = ST_DUMMY;
-      gmode = A_DUMMY;
-    } else if (sub.kind == SUB_REAL && sub.idx < P.N) {
-      // first stale candidate, found here over every hint (the match role's
-      // predicate and state; one tag load and one PRF gather per hint), so
-      // the guess never waits for the match workgroup
-      constexpr int HPT = kLdsPH / NT;   // k_step: PH <= kLdsPH
-      const uint32_t ch = (uint32_t)(sub.idx >> lg), off = (uint32_t)(sub.idx & mask);
-      const uint32_t wave = tid >> 6, lane = tid & 63;
-      uint32_t rv[HPT];
-      const PM_G uint16_t* crow = P.cur + cur_row(P.PH, P.curk, ch);   // match: value == offset (see match_role)
+    PmRes g;
+    const uint32_t gmode = step_guess<NT>(S, s, sub, P, L, g);
+    // with gather helpers (S.nhelp) this workgroup gathers the set's first
+    // range only; the helpers' partials of the others are merged below
+    const bool helped = S.nhelp && (gmode == A_FINAL || gmode == A_DUMMY);
+    if (gmode != kNone) gather(g, gmode, 0, helped ? P.SS / (S.nhelp + 1) : P.SS);
+    // the helpers' partials, merged while the resolver still runs (a later
+    // redo overwrites row.w anyway).  Each helper's guess must be this one
+    // (the state it read may have been refreshed by then).  Every granule
+    // load of a thread is in flight before the first is checked.
+    bool help_ok = true;
+    if (helped) {
+      // one round trip: a thread's partial words of every helper and (lanes
+      // < nhelp) that helper's guess fields are all in flight before the
+      // first is checked; a granule not yet written is then polled
+      const PM_G uint64_t* const hbase = S.helpg + (uint64_t)s * kStepHelpMax * kHelpGran;
+      const uint32_t w = tid;   // EX <= kHelpWords <= NT: one word per thread
+      uint64_t v[2 * kStepHelpMax], fv[6];
 #pragma unroll
-      for (int u = 0; u < HPT; ++u) rv[u] = u * NT + tid < P.PH ? crow[cur_row_off(P.curk, u * NT + tid)] : kNone;
-      const uint32_t h0k = wave == 0 ? P.hist[ch] : 0;
-      // per wave the lowest matching hint (lower u first: hints u*NT + tid)
-      uint32_t wh = kNone, wt = 0, wp = 0;
-#pragma unroll
-      for (int u = 0; u < HPT; ++u) {
-        const uint64_t bm = __ballot(rv[u] == off);
-        if (bm && wh == kNone) wh = u * NT + wave * 64 + (uint32_t)__builtin_ctzll(bm);
+      for (uint32_t k = 0; k < kStepHelpMax; ++k) {
+        const bool ld = k < S.nhelp && w < EX;
+        v[2 * k] = ld ? ld64<true>(hbase + k * kHelpGran + 2 * w) : 0;
+        v[2 * k + 1] = ld ? ld64<true>(hbase + k * kHelpGran + 2 * w + 1) : 0;
       }
-      if (wh != kNone) { wt = P.tag[wh]; wp = P.pp[wh]; }
-      if (lane == 0) { L.f[wave] = wh; L.red[2 * wave] = wt; L.red[2 * wave + 1] = wp; }
-      if (wave == 0) {
-        const uint32_t pb0 = step_sb(S, sub.part), pn = step_sb(S, sub.part + 1) - pb0;
-        PmSub st;
-        bool validt;
-        const uint32_t sg0 = predict_ing(S, P, pb0, pn, s - pb0, ch, h0k, st, validt);
-        if (lane == 0) L.f[16] = sg0;
+      const PM_G uint64_t* const hf = hbase + (uint64_t)min(tid, kStepHelpMax - 1) * kHelpGran + 2 * kHelpWords;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) fv[i] = tid < S.nhelp ? ld64<true>(hf + i) : 0;
+      if (tid < S.nhelp) {
+        uint32_t f[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) f[i] = (uint32_t)(fv[i] >> 32) == S.token ? (uint32_t)fv[i] : get_g(hf + i, S);
+        L.f[8 + tid] = f[0] == gmode && (gmode == A_DUMMY || (f[1] == g.hit && f[2] == g.chunk && f[3] == g.ing &&
+                                                              f[4] == g.tag && f[5] == g.pp)) ? 1u : 0u;
       }
       __syncthreads();
-      uint32_t c1 = kNone, t1 = 0, p1 = 0;
-      const uint32_t sg = L.f[16];
-      AS(0);
-      for (uint32_t w = 0; w < NT / 64; ++w)
-        if (L.f[w] < c1) { c1 = L.f[w]; t1 = (uint32_t)L.red[2 * w]; p1 = (uint32_t)L.red[2 * w + 1]; }
-      __syncthreads();
-      if (c1 != kNone && sg < P.Qpc && ch < P.SS) {
-        g = PmRes{ST_OK, c1, ch, sg, t1, p1, 0, 0};
-        gmode = A_FINAL;
+      for (uint32_t k = 0; k < S.nhelp; ++k) help_ok = help_ok && L.f[8 + k] != 0;
+      if (help_ok && w < EX) {
+        uint64_t x = row.w[w];
+#pragma unroll
+        for (uint32_t k = 0; k < kStepHelpMax; ++k) {
+          if (k >= S.nhelp) break;
+          const PM_G uint64_t* hp = hbase + k * kHelpGran + 2 * w;
+          const uint32_t lo = (uint32_t)(v[2 * k] >> 32) == S.token ? (uint32_t)v[2 * k] : get_g(hp, S);
+          const uint32_t hi = (uint32_t)(v[2 * k + 1] >> 32) == S.token ? (uint32_t)v[2 * k + 1] : get_g(hp + 1, S);
+          x ^= (uint64_t)lo | ((uint64_t)hi << 32);
+        }
+        row.w[w] = x;
       }
+      __syncthreads();
     }
-    if (gmode != kNone) gather(g, gmode);
     TS(1);
     // ---- the resolver's record of this sub-query ----------------------------
     if (tid < G_RES) L.f[tid] = get_g(S.resg + (uint64_t)s * G_RES + tid, S);
@@ -2091,15 +2167,16 @@ __device__ __forceinline__ void answer_role(const PmStep& S, uint32_t s, LDS& L)
                       (mode == A_DUMMY || (r.hit == g.hit && r.chunk == g.chunk && r.ing == g.ing &&
                                            r.tag == g.tag && r.pp == g.pp));
     TS_SEEN(kept ? 1u : 0u);
-    if (!kept) {
+    const bool redo = !kept || !help_ok;
+    if (redo) {
       e_rv = e_bp = e_pp = 0;
-      gather(r, mode);
+      gather(r, mode, 0, P.SS);
     }
   } else {
     r = S.res[s];
     mode = answer_mode(r);
     AST(1);
-    gather(r, mode);
+    gather(r, mode, 0, P.SS);
   }
   const uint64_t dslot = (uint64_t)r.chunk * P.Qpc + r.ing;
   const uint64_t* rv = P.rval + dslot * E;
@@ -2658,6 +2735,35 @@ union StepLds {
   uint8_t one_per_cu[96 * 1024];
 };
 
+// A gather helper of sub-query s (k_step, S.nhelp > 0): the same guess as
+// the answer workgroup's, then range j (1..nhelp) of its set: set expansion,
+// rows, the partial XOR into granules (two per word), and the guess fields
+// the answer checks before it merges the partial.
+template <int W, int NT, class LDS>
+__device__ __forceinline__ void helper_role(const PmStep& S, uint32_t s, uint32_t j, LDS& L) {
+  const PmSub sub = step_sub(S, s);
+  const PmPart& P = S.parts[sub.part];
+  const uint32_t tid = threadIdx.x, EX = S.E & ~3u;
+  PmRes g;
+  const uint32_t gmode = step_guess<NT>(S, s, sub, P, L, g);
+  PM_G uint64_t* const out = S.helpg + ((uint64_t)s * kStepHelpMax + (j - 1)) * kHelpGran;
+  if (gmode == A_FINAL || gmode == A_DUMMY) {
+    const uint32_t n = S.nhelp + 1, lo = P.SS * j / n, hi = P.SS * (j + 1) / n;
+    set_range<NT>(P, sub, g, gmode, L.qo, lo, hi);
+    __syncthreads();
+    gather_range<W, NT, PM_STEP_KG>(S, P, L.qo, L.red, L.row, lo, hi);
+    for (uint32_t w = tid; w < EX; w += NT) {
+      const uint64_t x = L.row.w[w];
+      put_g(out + 2 * w, (uint32_t)x, S.token);
+      put_g(out + 2 * w + 1, (uint32_t)(x >> 32), S.token);
+    }
+  }
+  if (tid < 6) {
+    const uint32_t f = tid == 0 ? gmode : tid == 1 ? g.hit : tid == 2 ? g.chunk : tid == 3 ? g.ing : tid == 4 ? g.tag : g.pp;
+    put_g(out + 2 * kHelpWords + tid, f, S.token);
+  }
+}
+
 template <int W>
 __global__ void __launch_bounds__(kStepBlock) k_step(PmStep S) {
   __shared__ StepLds L;
@@ -2689,7 +2795,14 @@ __global__ void __launch_bounds__(kStepBlock) k_step(PmStep S) {
     finish_step<true>(S, L.a.row);
     return;
   }
-  answer_role<W, true, kStepBlock>(S, b - S.nsub - S.np, L.a);
+  const uint32_t hb = S.nsub + S.np;   // then nhelp x nsub helpers, then the answers
+  if (b < hb + S.nhelp * S.nsub) {
+    const uint32_t k = b - hb;
+    helper_role<W, kStepBlock>(S, k % S.nsub, 1 + k / S.nsub, L.a);
+    TS(2);
+    return;
+  }
+  answer_role<W, true, kStepBlock>(S, b - hb - S.nhelp * S.nsub, L.a);
   TS(2);
 }
 
@@ -2868,7 +2981,7 @@ bool step_fused_ok(const PmStep& S, uint32_t maxPH, uint32_t max_sub_per_part) {
 }
 void step_fused(hipStream_t st, const PmStep& S, PmEvents ev) {
   // S.cblk must be 1 (one match record per sub-query)
-  const dim3 grid(2 * S.nsub + S.np);
+  const dim3 grid(2 * S.nsub + S.np + S.nhelp * S.nsub);
   if (S.E % 2 == 0) PM_LAUNCH(ev, k_step<2>, grid, dim3(kStepBlock), st, S);
   else PM_LAUNCH(ev, k_step<1>, grid, dim3(kStepBlock), st, S);
 }

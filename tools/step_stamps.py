@@ -52,20 +52,23 @@ def show(fn):
         t, ms = t8[:grid * 4].reshape(grid, 4), t8[grid * 4:].reshape(grid, 4)
         t0 = t[:, 0][t[:, 0] > 0].min()
         rel = np.where(t[:, :3] > 0, t[:, :3].astype(np.int64) - t0, -1) * 10 / 1000.0   # us
-        m, r, a = rel[:nsub], rel[nsub:nsub + np_], rel[nsub + np_:]
+        a0 = grid - nsub   # answers last (after nhelp x nsub gather helpers, if any)
+        m, r, a = rel[:nsub], rel[nsub:nsub + np_], rel[a0:]
         live = r[:, 0] >= 0
-        seen = t[nsub + np_:, 3]
+        seen = t[a0:, 3]
         a_seen = ((seen >> 1).astype(np.int64) - int(t0)) * 0.01
         kept = (seen & 1).astype(bool)
-        arel = (ms[nsub + np_:, :2].astype(np.int64) - int(t0)) * 0.01
-        okr = ms[nsub + np_:, 0] > 0
-        rows.append([np.median(arel[okr, 0]), arel[okr, 0].max(), np.median(arel[okr, 1]), arel[okr, 1].max(),
+        arel = (ms[a0:, :2].astype(np.int64) - int(t0)) * 0.01
+        okr = ms[a0:, 0] > 0
+        hp = rel[nsub + np_:a0]   # gather helpers (start, -, end)
+        hl = [np.median(hp[:, 2]), hp[:, 2].max()] if len(hp) else [0.0, 0.0]
+        rows.append([*hl, np.median(arel[okr, 0]), arel[okr, 0].max(), np.median(arel[okr, 1]), arel[okr, 1].max(),
                      m[:, 0].max(), np.median(m[:, 1]), m[:, 1].max(),
                      np.median(r[live, 2]), r[live, 2].max(),
                      a[:, 1].max(), a_seen.max(), np.median((a[:, 2] - a_seen)[kept]) if kept.any() else 0,
                      np.median((a[:, 2] - a_seen)[~kept]) if (~kept).any() else 0, kept.mean(), a[:, 2].max()])
     rows = np.array(rows[10:])
-    names = ["answer median scan done", "answer last scan done", "answer median set done",
+    names = ["helper median end", "helper last end", "answer median scan done", "answer last scan done", "answer median set done",
              "answer last set done", "match last start", "match median role end", "match last role end",
              "resolver median end", "resolver last end", "answer last guess done",
              "answer last result seen", "answer after result, kept", "answer after result, redone",
