@@ -706,9 +706,6 @@ static int engine_create(pm_ctx* ctx, Engine* g, uint64_t N, uint64_t Ebytes, ui
     const size_t n = (size_t)kArgSubs * (8 + 64 + 2 * g->gran_words + 8) * 8;
     CHK(g->gran.reserve(n));
     HIPCHK(hipMemset(g->gran.p, 0, n));
-    const size_t nh = (size_t)kArgSubs * kStepHelpMax * kHelpGran * 8;   // the gather helpers' hand-offs
-    CHK(g->helpg.reserve(nh));
-    HIPCHK(hipMemset(g->helpg.p, 0, nh));
     CHK(g->err_h.reserve(64));
     memset(g->err_h.p, 0, 64);
   }
@@ -1245,9 +1242,14 @@ static int engine_step(Engine* g, const float* q_dev, uint32_t dim) {
     // sub-queries over 16 partitions take PM_STEP_HELP (default 3) each; 0 disables
     static const int help_env = [] { const char* e = getenv("PM_STEP_HELP"); return e ? atoi(e) : 3; }();
     S.nhelp = 0;
-    if (help_env > 0 && (E & ~3ull) <= kHelpWords && g->helpg.p && 2 * nsub + g->P < 240)
+    if (help_env > 0 && (E & ~3ull) <= kHelpWords && 2 * nsub + g->P < 240)
       S.nhelp = std::min<uint32_t>(std::min<uint32_t>(kStepHelpMax, (uint32_t)help_env),
                                    (uint32_t)((240 - 2 * nsub - g->P) / nsub));
+    if (S.nhelp && !g->helpg.p) {   // the helpers' hand-off granules, on first use (token 0 never marks a step)
+      const size_t nh = (size_t)kArgSubs * kStepHelpMax * kHelpGran * 8;
+      CHK(g->helpg.reserve(nh));
+      HIPCHK(hipMemsetAsync(g->helpg.p, 0, nh, st));
+    }
     S.helpg = g->helpg.as<uint64_t>();
 #ifdef PM_STEP_STAMPS
     const uint32_t grid = 2 * nsub + (uint32_t)g->P + S.nhelp * nsub;

@@ -201,7 +201,7 @@ constexpr uint32_t kArgSubs = PM_KARG_SUBS, kArgParts = PM_KARG_SUBS > 1 ? 32 : 
 // k_step gather helpers (PmStep::nhelp): at most kStepHelpMax per sub-query,
 // for entries of <= 256 gathered words; granules per helper: 2 x 256 partial
 // words + 8 guess fields
-constexpr uint32_t kStepHelpMax = 5, kHelpWords = 256, kHelpGran = 2 * kHelpWords + 8;
+constexpr uint32_t kStepHelpMax = 3, kHelpWords = 256, kHelpGran = 2 * kHelpWords + 8;
 struct PmStep {
   const PM_G PmPart* parts;
   const PM_G PmSub* subs_h;    // pinned host descriptor, read zero-copy by k_match
