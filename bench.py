@@ -174,6 +174,17 @@ C2_N, C2_E, C2_B, C2_BATCHES = 3_201_821, 112, 32, 300
 C2_CLIENTS = 32   # clients of the server answered together (one shared step per round)
 
 
+def step_grid_threads(nsub, npart):
+    """k_step's launch (pmk::step_fused) for nsub sub-queries over npart
+    partitions, in threads: match, resolve and answer workgroups plus the
+    gather helpers pm_engine.cpp engine_step adds while the launch fits 240
+    co-resident 1,024-thread workgroups (PM_STEP_HELP, default 3, at most 3)."""
+    cap = int(os.environ.get("PM_STEP_HELP", "3"))
+    base = 2 * nsub + npart
+    nhelp = min(3, max(cap, 0), (240 - base) // nsub) if base < 240 else 0
+    return (base + nhelp * nsub) * 1024
+
+
 def batch_pir_msmarco(ctx, with_cpu: bool):
     """Preprocessing time, then batch-query throughput, of the batch-PIR path at
     the configs[2] shape, with the step kernel's answer-bytes roofline."""
@@ -230,7 +241,7 @@ def batch_pir_msmarco(ctx, with_cpu: bool):
                            "launches": n, "alg_bytes_per_launch": by / n,
                            "note": "k_step of one 32-id batch (32 sub-queries over 16 partitions: latency-bound, "
                                    "one workgroup per sub-query gathers 196 rows); every launch of the timed batches"}
-        attach_traffic(out["roofline"], SYMBOLS["step"], (2 * C2_B + 16) * 1024)
+        attach_traffic(out["roofline"], SYMBOLS["step"], step_grid_threads(C2_B, 16))
     # C2_CLIENTS clients of the one server DB, every batch of all of them answered
     # together (pm_batchpir_group_*: one shared step per round)
     clients = [g] + [g.Client(1000 + i, pm.Context(0)) for i in range(C2_CLIENTS - 1)]

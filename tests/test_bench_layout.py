@@ -79,6 +79,16 @@ def test_ip_shards_closed_form():
     assert b.ip_closed_form(3, 11, 8) == sum((i + j) * j for i in range(3, 11) for j in range(8)) % (1 << 32)
 
 
+def test_step_grid_threads():
+    """bench.step_grid_threads restates pm_engine.cpp's k_step launch: the
+    configs[2] batch (32 sub-queries over 16 partitions) takes 3 gather helpers
+    per sub-query; a 96-sub-query search step has no room for any."""
+    b = _bench()
+    assert b.step_grid_threads(32, 16) == (64 + 16 + 96) * 1024
+    assert b.step_grid_threads(96, 16) == (192 + 16) * 1024
+    assert b.step_grid_threads(120, 16) == (240 + 16) * 1024
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
