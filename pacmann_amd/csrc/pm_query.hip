@@ -2720,13 +2720,15 @@ __global__ void __launch_bounds__(kGatherBlock, PM_GATHER_WAVES) k_gather(PmStep
 
 // ---- k_step: the step in one launch ---------------------------------------
 // Workgroups [0, nsub) match one sub-query each (all its hints), the next np
-// resolve one partition each, the last nsub answer one sub-query each.  Every
-// hand-off is a set of granules (put_g / get_g): a resolver polls its
-// partition's match records, an answer workgroup its own match record (for
-// its guess) and then its resolution record.  Dispatch is in workgroup order
-// and a role only waits for lower-numbered ones, so the lowest unfinished
-// workgroup can always run; at most 240 workgroups of 1024 threads whose LDS
-// admits one per CU, the envelope the hand-off forms are measured in.
+// resolve one partition each, then nhelp x nsub gather helpers (helper_role:
+// ranges 1..nhelp of each sub-query's guessed set), the last nsub answer one
+// sub-query each.  Every hand-off is a set of granules (put_g / get_g): a
+// resolver polls its partition's match records, an answer workgroup its
+// helpers' partials and then its resolution record.  Dispatch is in
+// workgroup order and a role only waits for lower-numbered ones (helpers wait
+// for none), so the lowest unfinished workgroup can always run; at most 240
+// workgroups of 1024 threads whose LDS admits one per CU, the envelope the
+// hand-off forms are measured in (the host sizes nhelp to stay inside it).
 constexpr int kStepBlock = 1024, kStepHPT = kLdsPH / kStepBlock;
 union StepLds {
   uint32_t s_cand[kStepBlock / 64][6];
